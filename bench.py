@@ -1,0 +1,131 @@
+#!/usr/bin/env python
+"""Headline benchmark: X-UNet training throughput on SRN-cars-shaped data.
+
+Metric (BASELINE.json): train imgs/sec for the whole node, SRN cars 64x64,
+global batch 128 (reference: ≈29.9 examples/s on 8x RTX 3090, README.md:39).
+One "example" = one 2-view training pair.
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Scaling is *strong* by default: the global batch stays 128 (the published
+config) and each of the N ranks trains on 128/N examples per step, so every
+point of the 1/2/4/8-GPU curve is the headline config itself.  Pass
+``--per_gpu_batch B`` for weak scaling (global = B*N).  Data are synthetic
+SRN-shaped batches generated on the device; weights are random-init at the
+full 136.7M-parameter architecture; every timed step is a complete
+forward + backward + gradient all-reduce + Adam update.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_EX_PER_S = 29.9  # 101,000 steps x 128 / 432,000 s on 8x RTX 3090
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--global_batch", type=int, default=128)
+    ap.add_argument("--per_gpu_batch", type=int, default=0, help="weak scaling: fixed per-GPU batch")
+    ap.add_argument("--micro_batch", type=int, default=-1, help="-1 = auto")
+    ap.add_argument("--imgsize", type=int, default=64)
+    ap.add_argument("--backend", default="auto")
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--bucket_mb", type=float, default=64.0)
+    ap.add_argument("--grad_dtype", default="fp32")
+    ap.add_argument("--profile", default="", help="write a torch.profiler kernel table (text) here")
+    args = ap.parse_args()
+
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup, barrier
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+
+    ctx = init_distributed("auto", timeout_s=900)
+    N = ctx.world
+    if args.gpus and args.gpus != N and ctx.rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={N}", file=sys.stderr)
+    if args.per_gpu_batch:
+        global_batch = args.per_gpu_batch * N
+        scaling = "weak"
+    else:
+        global_batch = args.global_batch
+        scaling = "strong"
+    local = global_batch // N
+    mb = args.micro_batch
+    if mb < 0:
+        mb = 0 if local <= 64 else 64
+    cfg = make_config(None, {"model.H": args.imgsize, "model.W": args.imgsize, "data.imgsize": args.imgsize,
+                             "global_batch": global_batch, "micro_batch": mb, "data.synthetic": True,
+                             "backend": args.backend, "dtype": args.dtype, "log_every": 0, "ckpt_every": 0,
+                             "dist.bucket_mb": args.bucket_mb, "dist.grad_dtype": args.grad_dtype})
+    trainer = Trainer(cfg, ctx)
+    data = SyntheticBatches(local, args.imgsize, ctx.device, seed=1234 + ctx.rank)
+    pool = [next(data) for _ in range(4)]
+
+    def sync():
+        if ctx.device.type == "cuda":
+            torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        trainer.train_step(*pool[i % len(pool)])
+    sync()
+    barrier()
+    sync()
+    prof = None
+    if args.profile:
+        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                  torch.profiler.ProfilerActivity.CUDA])
+        prof.__enter__()
+    t0 = time.perf_counter()
+    loss = None
+    for i in range(args.steps):
+        loss = trainer.train_step(*pool[i % len(pool)])
+    sync()
+    barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        if ctx.rank == 0:
+            with open(args.profile, "w") as f:
+                f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+    from distributed_3d_diffusion_pytorch_amd.parallel import all_reduce_max
+    dt = all_reduce_max(dt, ctx.device)
+    lv = float(loss) if loss is not None else float("nan")
+    ms = 1e3 * dt / max(args.steps, 1)
+    value = global_batch * args.steps / dt
+    if ctx.rank == 0:
+        from distributed_3d_diffusion_pytorch_amd.ops import use_hip
+        probe = torch.zeros(1, device=ctx.device)
+        out = {
+            "metric": f"train imgs/sec (whole node), SRN cars {args.imgsize}x{args.imgsize} bs{global_batch}",
+            "value": round(value, 3), "unit": "examples/s", "n_gpus": N, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": scaling,
+            "vs_baseline": round(value / BASELINE_EX_PER_S, 3) if args.imgsize == 64 else None,
+            "dtype": args.dtype, "data": "synthetic (on-device SRN-shaped batches, random-init weights)",
+            "config": {"model": "XUNet ch128 ch_mult(1,2,2,4) 136.7M params (3DiM, reference xunet.py)",
+                       "global_batch": global_batch, "seq_len": args.imgsize * args.imgsize,
+                       "image_size": args.imgsize, "per_gpu_batch": local, "micro_batch": mb or local,
+                       "parallelism": f"dp{N}",
+                       "backend": "hip" if (ctx.device.type == "cuda" and use_hip(probe)) else "torch"},
+            "final_loss": lv,
+        }
+        print(json.dumps(out), flush=True)
+    cleanup()
+
+
+if __name__ == "__main__":
+    main()

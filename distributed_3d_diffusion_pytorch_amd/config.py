@@ -1,0 +1,204 @@
+"""Typed configuration for the MI355X-native 3D-diffusion framework.
+
+The reference configures itself through hard-coded constants (`train.py:210-217`,
+`lightning/train.py:26-28`, `sampling.py:26,158`, `SRNdataset.py:44`) and
+`XUNet(**kwargs)` class-attribute overrides (`xunet.py:356-370`).  Here every
+knob lives in one dataclass tree with CLI overrides (``key.sub=value``) and
+named presets that mirror BASELINE.json's configs.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+from dataclasses import dataclass, field, fields, is_dataclass
+from typing import Any, Dict, List, Optional, Tuple
+
+
+@dataclass
+class ModelConfig:
+    """X-UNet hyper-parameters (defaults = `xunet.py:356-366`, ch=128 as every
+    reference entry point builds it: `train.py:229`, `sampling.py:51`)."""
+    H: int = 64
+    W: int = 64
+    ch: int = 128
+    ch_mult: Tuple[int, ...] = (1, 2, 2, 4)
+    emb_ch: int = 1024
+    num_res_blocks: int = 3
+    attn_resolutions: Tuple[int, ...] = (2, 3, 4)
+    attn_heads: int = 4
+    dropout: float = 0.1
+    use_pos_emb: bool = True
+    use_ref_pose_emb: bool = True
+    # Reference quirk D10: K is the 128^2 SRN intrinsic and is never rescaled.
+    rescale_intrinsics: bool = False
+
+
+@dataclass
+class DiffusionConfig:
+    logsnr_min: float = -20.0
+    logsnr_max: float = 20.0
+    loss_type: str = "l2"            # l2 | l1 | huber  (train.py:102-112)
+    cond_prob: float = 0.1           # CFG drop probability (train.py:95)
+    timesteps: int = 256             # sampler steps (sampling.py:129)
+    # D9: reference returns the mean (no noise) whenever logsnr_next == 0,
+    # which fires mid-trajectory at t=0.5.  Off = add noise on every step but
+    # the last one.
+    ref_sampler_quirk: bool = False
+
+
+@dataclass
+class DataConfig:
+    path: str = "./data/SRN/cars_train"
+    index: str = ""                  # pickle/json index {instance: [views]}; "" = scan
+    imgsize: int = 64
+    synthetic: bool = False          # on-device synthetic SRN-shaped batches
+    num_workers: int = 4
+    cache: str = ""                  # preprocessed uint8 cache (.npz dir), "" = PNG path
+    seed: int = 0
+
+
+@dataclass
+class OptimConfig:
+    lr: float = 1e-4
+    betas: Tuple[float, float] = (0.9, 0.99)
+    eps: float = 1e-8
+    weight_decay: float = 0.0
+    # D6: the paper warms up over 10M examples; the reference's DDP loop
+    # effectively uses none (last_step = num_epochs / batch_size).
+    warmup_examples: int = 0
+    use_cosine: bool = False         # lightning/diff3d.py:111-113
+    cosine_tmax: int = 300
+    ema_halflife_examples: float = 0.0   # D16 (documented, not implemented upstream)
+    grad_clip: float = 0.0
+
+
+@dataclass
+class DistConfig:
+    backend: str = "auto"            # auto -> nccl (RCCL) on GPU, gloo on CPU
+    bucket_mb: float = 64.0          # gradient bucket size (xGMI: see SURVEY 5.8)
+    first_bucket_mb: float = 4.0
+    grad_dtype: str = "fp32"         # fp32 | bf16 all-reduce payload
+    timeout_s: float = 600.0
+    checksum_every: int = 0          # cross-rank parameter checksum cadence
+
+
+@dataclass
+class TrainConfig:
+    model: ModelConfig = field(default_factory=ModelConfig)
+    diffusion: DiffusionConfig = field(default_factory=DiffusionConfig)
+    data: DataConfig = field(default_factory=DataConfig)
+    optim: OptimConfig = field(default_factory=OptimConfig)
+    dist: DistConfig = field(default_factory=DistConfig)
+    global_batch: int = 128
+    micro_batch: int = 0             # split each rank's batch into micro-batches (grad accumulation)
+    num_epochs: int = 10
+    max_steps: int = 0               # 0 = run num_epochs
+    log_every: int = 50
+    ckpt_every: int = 50
+    out_dir: str = ""
+    transfer: str = ""               # resume dir (reads <dir>/latest.pt)
+    dtype: str = "bf16"              # compute dtype on GPU: bf16 | fp32
+    backend: str = "auto"            # ops backend: auto | hip | torch
+    seed: int = 0
+    deterministic: bool = False
+    profile_steps: str = ""          # e.g. "10-12": torch.profiler window
+    graph: bool = False              # capture the step in a HIP graph
+
+
+PRESETS: Dict[str, Dict[str, Any]] = {
+    # BASELINE.json configs
+    "chairs32_cpu": {"model.H": 32, "model.W": 32, "data.imgsize": 32, "global_batch": 2,
+                     "dtype": "fp32", "backend": "torch"},
+    "cars64_1gpu_bf16": {"model.H": 64, "model.W": 64, "data.imgsize": 64, "global_batch": 16},
+    "cars64_8gpu": {"model.H": 64, "model.W": 64, "data.imgsize": 64, "global_batch": 128},
+    "cars128_8gpu": {"model.H": 128, "model.W": 128, "data.imgsize": 128, "global_batch": 128},
+    "sample256_bs64": {"model.H": 64, "model.W": 64, "data.imgsize": 64, "diffusion.timesteps": 256},
+}
+
+
+def _coerce(value: str, typ: Any, current: Any) -> Any:
+    if isinstance(current, bool):
+        return value.lower() in ("1", "true", "yes", "on")
+    if isinstance(current, int) and not isinstance(current, bool):
+        return int(value)
+    if isinstance(current, float):
+        return float(value)
+    if isinstance(current, tuple):
+        parts = [p for p in value.replace("(", "").replace(")", "").split(",") if p.strip()]
+        elem = type(current[0]) if current else float
+        return tuple(elem(p) for p in parts)
+    return value
+
+
+def apply_overrides(cfg: Any, overrides: Dict[str, Any]) -> Any:
+    """Apply ``{"a.b": value}`` overrides in place (strings are coerced)."""
+    for key, value in overrides.items():
+        obj = cfg
+        parts = key.split(".")
+        for p in parts[:-1]:
+            obj = getattr(obj, p)
+        cur = getattr(obj, parts[-1])
+        if isinstance(value, str) and not isinstance(cur, str):
+            value = _coerce(value, type(cur), cur)
+        setattr(obj, parts[-1], value)
+    return cfg
+
+
+def parse_kv(items: List[str]) -> Dict[str, str]:
+    out = {}
+    for it in items:
+        if "=" not in it:
+            raise ValueError(f"override must be key=value, got {it!r}")
+        k, v = it.split("=", 1)
+        out[k.strip()] = v.strip()
+    return out
+
+
+def make_config(preset: Optional[str] = None, overrides: Optional[Dict[str, Any]] = None) -> TrainConfig:
+    cfg = TrainConfig()
+    if preset:
+        if preset not in PRESETS:
+            raise KeyError(f"unknown preset {preset!r}; choose from {sorted(PRESETS)}")
+        apply_overrides(cfg, dict(PRESETS[preset]))
+    if overrides:
+        apply_overrides(cfg, overrides)
+    return cfg
+
+
+def to_dict(cfg: Any) -> Dict[str, Any]:
+    if is_dataclass(cfg):
+        return {f.name: to_dict(getattr(cfg, f.name)) for f in fields(cfg)}
+    if isinstance(cfg, tuple):
+        return list(cfg)
+    return cfg
+
+
+def from_dict(d: Dict[str, Any]) -> TrainConfig:
+    cfg = TrainConfig()
+    flat: Dict[str, Any] = {}
+
+    def walk(prefix: str, node: Any) -> None:
+        if isinstance(node, dict):
+            for k, v in node.items():
+                walk(f"{prefix}.{k}" if prefix else k, v)
+        else:
+            flat[prefix] = node
+
+    walk("", d)
+    for k, v in flat.items():
+        try:
+            obj = cfg
+            parts = k.split(".")
+            for p in parts[:-1]:
+                obj = getattr(obj, p)
+            cur = getattr(obj, parts[-1])
+            if isinstance(cur, tuple) and isinstance(v, list):
+                v = tuple(v)
+            setattr(obj, parts[-1], v)
+        except AttributeError:
+            continue
+    return cfg
+
+
+def dumps(cfg: TrainConfig) -> str:
+    return json.dumps(to_dict(cfg), indent=1, sort_keys=True)

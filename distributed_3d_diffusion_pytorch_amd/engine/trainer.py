@@ -1,0 +1,237 @@
+"""Training engine (reference: DDP loop `train.py:200-303`, Lightning module
+`lightning/diff3d.py:52-127`).
+
+One process per GPU.  Per step (no host synchronisation in the steady state):
+  1. diffusion forward on device: t~U[0,1), lambda(t), eps, z_t, CFG drop
+     (10 % of examples get noise instead of the conditioning view and zeroed
+     rays; `train.py:80-100`);
+  2. X-UNet forward/backward (HIP kernels on MI355X);
+  3. bucketed RCCL all-reduce launched from gradient hooks during backward,
+     drained before the optimizer;
+  4. one fused Adam launch (averaging folded in) + LR schedule.
+Rank 0 writes reference-named checkpoints atomically; losses are read back
+only every ``log_every`` steps.  Defects D1-D8 of the reference are fixed
+(see SURVEY 2.9).
+"""
+from __future__ import annotations
+
+import copy
+import math
+import os
+import time
+from typing import Dict, Iterator, Optional, Tuple
+
+import torch
+
+from .. import ops
+from ..config import TrainConfig, dumps, to_dict
+from ..diffusion import logsnr_schedule_cosine, q_sample, diffusion_loss
+from ..models import XUNet
+from ..parallel import (DistContext, FlatParams, GradReducer, get_context, check_replicas_in_sync)
+from ..utils import (save_checkpoint, load_checkpoint, load_model_weights, find_resume, MetricsLogger,
+                     StepTimer, train_flops_per_example, range_push, check_finite)
+from .optim import FusedAdam, ema_decay_for, warmup_lr
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+class Trainer:
+    def __init__(self, cfg: TrainConfig, ctx: Optional[DistContext] = None):
+        self.cfg = cfg
+        self.ctx = ctx or get_context()
+        dev = self.ctx.device
+        self.device = dev
+        if cfg.backend != "auto":
+            ops.set_backend(cfg.backend)
+        if cfg.deterministic:
+            torch.use_deterministic_algorithms(True, warn_only=True)
+        torch.manual_seed(cfg.seed)
+        self.model = XUNet(copy.deepcopy(cfg.model)).to(dev)
+        self.dtype = torch.bfloat16 if (dev.type == "cuda" and cfg.dtype == "bf16") else torch.float32
+        self.model.compute_dtype = self.dtype
+        self.flat = FlatParams(list(self.model.parameters()), device=dev)
+        W = self.ctx.world
+        if cfg.global_batch % W != 0:
+            raise ValueError(f"global_batch {cfg.global_batch} not divisible by world size {W}")
+        self.local_batch = cfg.global_batch // W
+        self.reducer = None
+        if W > 1:
+            self.reducer = GradReducer(self.flat, cfg.dist.bucket_mb, cfg.dist.first_bucket_mb, cfg.dist.grad_dtype)
+        oc = cfg.optim
+        self.optim = FusedAdam(self.flat, oc.lr, oc.betas, oc.eps, oc.weight_decay,
+                               ema_decay_for(cfg.global_batch, oc.ema_halflife_examples))
+        self.sched = None
+        if oc.use_cosine:
+            self.sched = torch.optim.lr_scheduler.CosineAnnealingLR(self.optim, T_max=oc.cosine_tmax)
+        self.warmup_steps = oc.warmup_examples / cfg.global_batch if oc.warmup_examples > 0 else 0.0
+        self.step = 0
+        self.epoch = 0
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(cfg.seed * 1000003 + self.ctx.rank + 1)
+        self.out_dir = cfg.out_dir or cfg.transfer or "runs/default"
+        self.logger = MetricsLogger(os.path.join(self.out_dir, "metrics.jsonl") if self.ctx.is_main else None)
+        self.fault_step = int(os.environ.get("D3D_FAULT_AT_STEP", "-1"))
+        self.fault_rank = int(os.environ.get("D3D_FAULT_RANK", "-1"))
+        if cfg.transfer:
+            self.resume(cfg.transfer)
+        if self.reducer is not None:
+            self.reducer.broadcast_params(0)
+
+    # ------------------------------------------------------------------
+    def resume(self, transfer: str) -> bool:
+        path = find_resume(transfer)
+        if path is None:
+            return False
+        ck = load_checkpoint(path, map_location="cpu")
+        load_model_weights(self.model, ck["model"])
+        if "optim" in ck:
+            self.optim.load_state_dict(ck["optim"])
+        self.step = int(ck.get("step", 0))
+        self.epoch = int(ck.get("epoch", -1)) + 1 if "epoch" in ck else 0
+        if "rng" in ck and ck["rng"] is not None and self.ctx.world == int(ck.get("world_size", 1)):
+            try:
+                self.gen.set_state(ck["rng"][self.ctx.rank].to(self.gen.get_state().device))
+            except Exception:
+                pass
+        return True
+
+    def save(self, name: str, epoch: Optional[int] = None) -> Optional[str]:
+        if not self.ctx.is_main:
+            return None
+        path = os.path.join(self.out_dir, name)
+        extra = {"config": to_dict(self.cfg), "world_size": self.ctx.world}
+        ema = self.optim.ema_state_dict(self.model)
+        if ema is not None:
+            extra["ema"] = {k: v.cpu() for k, v in ema.items()}
+        save_checkpoint(path, self.model, self.optim, self.step, epoch, extra)
+        return path
+
+    # ------------------------------------------------------------------
+    def diffusion_inputs(self, img, R, T, K):
+        """q_sample + CFG dropout (`train.py:80-100`), all on device."""
+        B = img.shape[0]
+        dev = img.device
+        x, z = img[:, 0].float(), img[:, 1].float()
+        t = torch.rand(B, generator=self.gen, device=dev)
+        dc = self.cfg.diffusion
+        logsnr = logsnr_schedule_cosine(t, logsnr_min=dc.logsnr_min, logsnr_max=dc.logsnr_max)
+        eps = torch.randn(z.shape, generator=self.gen, device=dev)
+        z_t = q_sample(z, logsnr, eps)
+        cond_mask = torch.rand(B, generator=self.gen, device=dev) > dc.cond_prob
+        x_cond = torch.where(cond_mask[:, None, None, None], x,
+                             torch.randn(x.shape, generator=self.gen, device=dev))
+        lam0 = logsnr_schedule_cosine(torch.zeros_like(logsnr), logsnr_min=dc.logsnr_min, logsnr_max=dc.logsnr_max)
+        batch = {"x": x_cond, "z": z_t, "logsnr": torch.stack([lam0, logsnr], 1), "R": R, "t": T, "K": K}
+        return batch, cond_mask, eps
+
+    def loss_fn(self, img, R, T, K) -> torch.Tensor:
+        batch, mask, eps = self.diffusion_inputs(img, R, T, K)
+        self.model.set_dropout_seed(self.step * self.ctx.world + self.ctx.rank)
+        eps_hat = self.model(batch, cond_mask=mask)
+        return diffusion_loss(eps, eps_hat, self.cfg.diffusion.loss_type)
+
+    def train_step(self, img, R, T, K) -> torch.Tensor:
+        if self.step == self.fault_step and self.ctx.rank == self.fault_rank:
+            os._exit(13)  # fault-injection hook for the failure-detection tests
+        g = self.optim.param_groups[0]
+        if self.sched is None:
+            g["lr"] = warmup_lr(self.step, self.warmup_steps, self.cfg.optim.lr)
+        self.model.train()
+        B = img.shape[0]
+        mb = self.cfg.micro_batch if 0 < self.cfg.micro_batch < B else B
+        chunks = [(s, min(s + mb, B)) for s in range(0, B, mb)]
+        total = None
+        with range_push("fwd_bwd"):
+            for ci, (s, e) in enumerate(chunks):
+                last_chunk = ci == len(chunks) - 1
+                ctx = self.reducer.no_sync() if (self.reducer is not None and not last_chunk) else _null()
+                with ctx:
+                    loss = self.loss_fn(img[s:e], R[s:e], T[s:e], K[s:e])
+                    (loss * ((e - s) / B)).backward() if len(chunks) > 1 else loss.backward()
+                l = loss.detach() * ((e - s) / B)
+                total = l if total is None else total + l
+        loss = total
+        if self.reducer is not None:
+            with range_push("allreduce_wait"):
+                self.reducer.finish()
+        with range_push("optimizer"):
+            self.optim.step(grad_scale=1.0 / self.ctx.world)
+            self.optim.zero_grad()
+        if self.sched is not None:
+            self.sched.step()
+        self.step += 1
+        ce = self.cfg.dist.checksum_every
+        if ce and self.step % ce == 0 and not check_replicas_in_sync(self.flat):
+            raise RuntimeError(f"data-parallel replicas diverged at step {self.step}")
+        return loss
+
+    # ------------------------------------------------------------------
+    def make_data(self) -> Tuple[Iterator, Optional[object], Optional[object]]:
+        dc = self.cfg.data
+        if dc.synthetic:
+            from ..data import SyntheticBatches
+            it = SyntheticBatches(self.local_batch, dc.imgsize, self.device,
+                                  seed=dc.seed * 7919 + self.ctx.rank)
+            return it, None, None
+        from ..data import SRNDataset, ShardSampler, MultiEpochsDataLoader
+        ds = SRNDataset("train", dc.path, dc.index, dc.imgsize, seed=dc.seed)
+        sampler = ShardSampler(len(ds), self.ctx.rank, self.ctx.world, shuffle=True, seed=dc.seed)
+        loader = MultiEpochsDataLoader(ds, batch_size=self.local_batch, sampler=sampler,
+                                       num_workers=dc.num_workers, drop_last=True,
+                                       pin_memory=self.device.type == "cuda")
+        return loader, ds, sampler
+
+    def _to_dev(self, batch):
+        return tuple(b.to(self.device, non_blocking=True) for b in batch)
+
+    def fit(self, steps_per_epoch: int = 0) -> Dict[str, float]:
+        cfg = self.cfg
+        data, ds, sampler = self.make_data()
+        timer = StepTimer(cfg.global_batch, train_flops_per_example(cfg.model.H), self.device)
+        timer.start()
+        last = {}
+        done = False
+        for epoch in range(self.epoch, cfg.num_epochs):
+            self.epoch = epoch
+            if sampler is not None:
+                sampler.set_epoch(epoch)
+                ds.set_epoch(epoch)
+            it = iter(data)
+            n = 0
+            while True:
+                if steps_per_epoch and n >= steps_per_epoch:
+                    break
+                try:
+                    batch = next(it)
+                except StopIteration:
+                    break
+                loss = self.train_step(*self._to_dev(batch))
+                timer.tick()
+                n += 1
+                if cfg.log_every and self.step % cfg.log_every == 0:
+                    lv = float(loss)
+                    check_finite(loss, self.step)
+                    rep = timer.report()
+                    last = {"step": self.step, "epoch": epoch, "loss": lv,
+                            "lr": self.optim.param_groups[0]["lr"], **rep}
+                    if self.ctx.is_main:
+                        print(f"[step {self.step}] loss {lv:.5f} {rep['examples_per_s']:.1f} ex/s "
+                              f"{rep['tflops']:.1f} TFLOP/s", flush=True)
+                        self.logger.log(**last)
+                    timer.start()
+                if cfg.ckpt_every and self.step % cfg.ckpt_every == 0:
+                    self.save("after_warmup.pt")
+                if cfg.max_steps and self.step >= cfg.max_steps:
+                    done = True
+                    break
+            self.save("latest.pt", epoch=epoch)
+            if done:
+                break
+        self.logger.close()
+        return last

@@ -1,0 +1,6 @@
+from .xunet import (XUNet, ResnetBlock, AttnBlock, AttnLayer, XUNetBlock, ConditioningProcessor, FiLM,
+                    GroupNorm, count_params)
+from .reference import reference_forward
+
+__all__ = ["XUNet", "ResnetBlock", "AttnBlock", "AttnLayer", "XUNetBlock", "ConditioningProcessor", "FiLM",
+           "GroupNorm", "count_params", "reference_forward"]

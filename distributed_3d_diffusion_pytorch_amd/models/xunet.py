@@ -1,0 +1,355 @@
+"""X-UNet denoiser (3DiM), MI355X-native NHWC execution.
+
+Capability parity with the reference X-UNet (`xunet.py:355-536`): identical
+module tree / parameter names / shapes / init (so `state_dict`s -- and the
+reference's Adam state, indexed by ``model.parameters()`` order -- load
+unchanged; Appendix A of SURVEY.md), identical math.  The execution is
+re-designed:
+
+* activations are ``[2B, H, W, C]`` (frames folded into the batch,
+  channels-last) in the compute dtype (bf16 on MI355X), parameters stay fp32
+  masters; every op goes through :mod:`..ops`, which dispatches to the gfx950
+  HIP kernels (implicit-GEMM MFMA conv3x3, fused GN/SiLU, fused GN+FiLM+dropout,
+  flash-style cross-view attention, on-device ray/posenc) or to the torch oracle;
+* camera rays are generated on device (the reference round-trips through numpy
+  on the host every forward, `xunet.py:311-318`);
+* ``silu(logsnr_emb + pose_emb_i)`` is computed once per resolution level and
+  shared by all FiLM layers of that level (the reference recomputes the SiLU in
+  every FiLM, `xunet.py:84`);
+* the output head runs on frame 1 only (the reference computes both frames and
+  discards frame 0, `xunet.py:535-536`).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..config import ModelConfig
+
+INV_SQRT2 = 1.0 / math.sqrt(2.0)
+
+
+class GroupNorm(nn.Module):
+    """GroupNorm(32) applied per (example, frame) image (`xunet.py:61-71`)."""
+
+    def __init__(self, num_groups: int = 32, num_channels: int = 64):
+        super().__init__()
+        self.gn = nn.GroupNorm(num_groups=num_groups, num_channels=num_channels)
+
+    def forward(self, h: torch.Tensor, silu: bool = False) -> torch.Tensor:
+        return ops.group_norm(h, self.gn.weight, self.gn.bias, self.gn.num_groups, self.gn.eps, silu)
+
+
+class FiLM(nn.Module):
+    """FiLM projection ``dense(silu(emb)) -> [scale | shift]`` (`xunet.py:74-87`).
+    ``forward`` takes the already-activated per-level embedding and returns the
+    packed ``[N, H, W, 2C]`` modulation; the modulation itself is fused into the
+    GroupNorm kernel (:func:`ops.gn_film`)."""
+
+    def __init__(self, features: int, emb_ch: int = 1024):
+        super().__init__()
+        self.features = features
+        self.dense = nn.Linear(emb_ch, 2 * features)
+
+    def forward(self, semb: torch.Tensor) -> torch.Tensor:
+        return ops.linear(semb, self.dense.weight, self.dense.bias)
+
+
+class ResnetBlock(nn.Module):
+    """BigGAN ResBlock over frames (`xunet.py:90-152`):
+    ``GN0 -> SiLU -> conv3x3 -> GN1 -> FiLM -> dropout -> conv3x3 (+ 1x1 skip)
+    -> /sqrt2 -> avgpool|nearest-up``."""
+
+    def __init__(self, in_features: int, out_features: Optional[int] = None, dropout: float = 0.0,
+                 resample: Optional[str] = None, emb_ch: int = 1024):
+        super().__init__()
+        out_features = in_features if out_features is None else out_features
+        self.in_features = in_features
+        self.features = out_features
+        self.dropout_p = float(dropout)
+        if resample not in (None, "up", "down"):
+            raise ValueError(resample)
+        self.resample = resample
+        # Registration order mirrors the reference so parameters() order (and
+        # therefore optimizer-state indices) is identical.
+        self.groupnorm0 = GroupNorm(num_channels=in_features)
+        self.groupnorm1 = GroupNorm(num_channels=out_features)
+        self.conv1 = nn.Conv2d(in_features, out_features, kernel_size=3, stride=1, padding=1)
+        self.film = FiLM(out_features, emb_ch)
+        self.conv2 = nn.Conv2d(out_features, out_features, kernel_size=3, stride=1, padding=1)
+        if in_features != out_features:
+            self.dense = nn.Conv2d(in_features, out_features, kernel_size=1)
+        nn.init.zeros_(self.conv2.weight)
+        self._seed_slot = 0
+
+    def forward(self, x: torch.Tensor, semb: torch.Tensor) -> torch.Tensor:
+        N, H, W, C = x.shape
+        assert C == self.in_features, (C, self.in_features)
+        h = self.groupnorm0(x, silu=True)
+        h = ops.conv3x3(h, self.conv1.weight, self.conv1.bias)
+        ss = self.film(semb)
+        h = ops.gn_film(h, self.groupnorm1.gn.weight, self.groupnorm1.gn.bias, ss,
+                        self.groupnorm1.gn.num_groups, self.groupnorm1.gn.eps,
+                        self.dropout_p, self.training, _next_seed(self))
+        if self.in_features != self.features:
+            skip = ops.linear(x, self.dense.weight, self.dense.bias)
+        else:
+            skip = x
+        h = ops.conv3x3(h, self.conv2.weight, self.conv2.bias, residual=skip, out_scale=INV_SQRT2)
+        if self.resample == "down":
+            h = ops.avgpool2(h)
+        elif self.resample == "up":
+            h = ops.upsample2(h)
+        return h
+
+
+class AttnLayer(nn.Module):
+    """Container of the reference's ``nn.MultiheadAttention`` parameters
+    (`xunet.py:154-177`): packed ``in_proj`` and ``out_proj``."""
+
+    def __init__(self, attn_heads: int = 4, in_channels: int = 32):
+        super().__init__()
+        self.in_channels = in_channels
+        self.attn_heads = attn_heads
+        self.attn = nn.MultiheadAttention(in_channels, attn_heads, batch_first=True)
+
+    def forward(self, hn: torch.Tensor, cross: bool) -> torch.Tensor:
+        N, L, C = hn.shape
+        qkv = ops.linear(hn, self.attn.in_proj_weight, self.attn.in_proj_bias)
+        a = ops.attention(qkv, self.attn_heads, cross)
+        return ops.linear(a, self.attn.out_proj.weight, self.attn.out_proj.bias)
+
+
+class AttnBlock(nn.Module):
+    """GN -> per-frame self / cross-frame MHA (shared weights for both frames)
+    -> zero-init 1x1 -> (h + x)/sqrt2 (`xunet.py:179-220`)."""
+
+    def __init__(self, attn_type: str, attn_heads: int = 4, in_channels: int = 32):
+        super().__init__()
+        if attn_type not in ("self", "cross"):
+            raise NotImplementedError(attn_type)
+        self.in_channels = in_channels
+        self.attn_type = attn_type
+        self.attn_heads = attn_heads
+        self.groupnorm = GroupNorm(num_channels=in_channels)
+        self.attn_layer = AttnLayer(attn_heads=attn_heads, in_channels=in_channels)
+        self.linear = nn.Conv2d(in_channels, in_channels, kernel_size=1)
+        nn.init.zeros_(self.linear.weight)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        N, H, W, C = x.shape
+        assert C == self.in_channels
+        hn = self.groupnorm(x).reshape(N, H * W, C)
+        o = self.attn_layer(hn, cross=(self.attn_type == "cross"))
+        y = ops.linear(o, self.linear.weight, self.linear.bias, residual=x.reshape(N, H * W, C),
+                       out_scale=INV_SQRT2)
+        return y.reshape(N, H, W, C)
+
+
+class XUNetBlock(nn.Module):
+    """ResnetBlock [+ self-attn + cross-attn] (`xunet.py:222-256`)."""
+
+    def __init__(self, in_channels: int, features: int, use_attn: bool = False, attn_heads: int = 4,
+                 dropout: float = 0.0, emb_ch: int = 1024):
+        super().__init__()
+        self.in_channels = in_channels
+        self.features = features
+        self.use_attn = use_attn
+        self.resnetblock = ResnetBlock(in_channels, features, dropout=dropout, emb_ch=emb_ch)
+        if use_attn:
+            self.attnblock_self = AttnBlock("self", attn_heads, features)
+            self.attnblock_cross = AttnBlock("cross", attn_heads, features)
+
+    def forward(self, x: torch.Tensor, semb: torch.Tensor) -> torch.Tensor:
+        assert x.shape[-1] == self.in_channels, (x.shape, self.in_channels)
+        h = self.resnetblock(x, semb)
+        if self.use_attn:
+            h = self.attnblock_self(h)
+            h = self.attnblock_cross(h)
+        return h
+
+
+class ConditioningProcessor(nn.Module):
+    """logSNR embedding MLP + camera-ray conditioning (`xunet.py:259-352`).
+
+    Returns the per-level activated embeddings ``silu(logsnr_emb + pose_emb_i)``
+    as ``[2B, H_i, W_i, emb_ch]`` tensors (the only form FiLM consumes)."""
+
+    D = 144
+
+    def __init__(self, emb_ch: int, H: int, W: int, num_resolutions: int, use_pos_emb: bool = True,
+                 use_ref_pose_emb: bool = True, rescale_intrinsics: bool = False):
+        super().__init__()
+        self.emb_ch = emb_ch
+        self.H, self.W = H, W
+        self.num_resolutions = num_resolutions
+        self.use_pos_emb = use_pos_emb
+        self.use_ref_pose_emb = use_ref_pose_emb
+        self.rescale_intrinsics = rescale_intrinsics
+        D = self.D
+        self.logsnr_emb_emb = nn.Sequential(nn.Linear(emb_ch, emb_ch), nn.SiLU(), nn.Linear(emb_ch, emb_ch))
+        if use_pos_emb:
+            self.pos_emb = nn.Parameter(torch.zeros(D, H, W))
+            nn.init.normal_(self.pos_emb, std=1.0 / np.sqrt(D))
+        if use_ref_pose_emb:
+            self.first_emb = nn.Parameter(torch.zeros(1, 1, D, 1, 1))
+            nn.init.normal_(self.first_emb, std=1.0 / np.sqrt(D))
+            self.other_emb = nn.Parameter(torch.zeros(1, 1, D, 1, 1))
+            nn.init.normal_(self.other_emb, std=1.0 / np.sqrt(D))
+        self.convs = nn.ModuleList([
+            nn.Conv2d(D, emb_ch, kernel_size=3, stride=2 ** i, padding=1) for i in range(num_resolutions)])
+
+    def logsnr_embedding(self, logsnr: torch.Tensor) -> torch.Tensor:
+        """[B, 2] logSNR -> [2B, emb_ch] fp32 (clip +-20, DDPM posenc x1000, MLP)."""
+        l = torch.clamp(logsnr.float(), -20.0, 20.0)
+        e = ops.posenc_ddpm(l, self.emb_ch, max_time=1.0)
+        l0, act, l1 = self.logsnr_emb_emb
+        e = l1(torch.nn.functional.silu(l0(e)))
+        return e.reshape(-1, self.emb_ch)
+
+    def forward(self, batch: Dict[str, torch.Tensor], cond_mask: torch.Tensor,
+                dtype: torch.dtype) -> List[torch.Tensor]:
+        B = batch["x"].shape[0]
+        assert cond_mask.shape == (B,), (cond_mask.shape, B)
+        logsnr_emb = self.logsnr_embedding(batch["logsnr"])
+        pose = ops.ray_posenc(batch["R"], batch["t"], batch["K"], self.H, self.W,
+                              cond_mask.to(batch["R"].device).bool(),
+                              self.pos_emb if self.use_pos_emb else None,
+                              self.first_emb if self.use_ref_pose_emb else None,
+                              self.other_emb if self.use_ref_pose_emb else None,
+                              rescale_from=128 if self.rescale_intrinsics else 0, out_dtype=dtype)
+        sembs = []
+        for i, conv in enumerate(self.convs):
+            e = ops.conv3x3(pose, conv.weight, conv.bias, stride=2 ** i, row_bias=logsnr_emb)
+            sembs.append(ops.silu(e))
+        return sembs
+
+
+class XUNet(nn.Module):
+    """The 2-frame X-UNet (`xunet.py:355-536`).  ``forward(batch, cond_mask=)``
+    takes the reference's batch dict ``{x, z: [B,3,H,W], logsnr: [B,2],
+    R: [B,2,3,3], t: [B,2,3], K: [B,3,3]}`` and returns eps-hat for frame 1,
+    ``[B,3,H,W]``."""
+
+    def __init__(self, cfg: Optional[ModelConfig] = None, **kwargs):
+        super().__init__()
+        cfg = cfg or ModelConfig()
+        for k, v in kwargs.items():
+            if not hasattr(cfg, k):
+                raise TypeError(f"unknown XUNet option {k}")
+            setattr(cfg, k, v)
+        self.cfg = cfg
+        self.H, self.W = cfg.H, cfg.W
+        self.ch = cfg.ch
+        self.ch_mult = tuple(cfg.ch_mult)
+        self.num_res_blocks = cfg.num_res_blocks
+        self.attn_resolutions = tuple(cfg.attn_resolutions)
+        L = len(self.ch_mult)
+        assert cfg.H % (2 ** (L - 1)) == 0 and cfg.W % (2 ** (L - 1)) == 0, \
+            f"image size must be a multiple of {2 ** (L - 1)}"
+        self.num_resolutions = L
+        self.compute_dtype: Optional[torch.dtype] = None
+
+        self.conditioningprocessor = ConditioningProcessor(
+            cfg.emb_ch, cfg.H, cfg.W, L, cfg.use_pos_emb, cfg.use_ref_pose_emb, cfg.rescale_intrinsics)
+        self.conv = nn.Conv2d(3, cfg.ch, kernel_size=3, stride=1, padding=1)
+        self.dim_in = [cfg.ch] + [cfg.ch * m for m in self.ch_mult[:-1]]
+        self.dim_out = [cfg.ch * m for m in self.ch_mult]
+        kw = dict(dropout=cfg.dropout, attn_heads=cfg.attn_heads, emb_ch=cfg.emb_ch)
+
+        self.xunetblocks = nn.ModuleList()
+        for i in range(L):
+            level = nn.ModuleList()
+            for j in range(cfg.num_res_blocks):
+                level.append(XUNetBlock(self.dim_in[i] if j == 0 else self.dim_out[i], self.dim_out[i],
+                                        use_attn=i in self.attn_resolutions, **kw))
+            if i != L - 1:
+                level.append(ResnetBlock(self.dim_out[i], self.dim_out[i], dropout=cfg.dropout,
+                                         resample="down", emb_ch=cfg.emb_ch))
+            self.xunetblocks.append(level)
+
+        self.middle = XUNetBlock(self.dim_out[-1], self.dim_out[-1], use_attn=L in self.attn_resolutions, **kw)
+
+        self.upsample = nn.ModuleDict()
+        for i in reversed(range(L)):
+            level = nn.ModuleList()
+            for j in range(cfg.num_res_blocks + 1):
+                if j == 0:
+                    prev_h = self.dim_out[i + 1] if i + 1 < L else self.dim_out[i]
+                    skip = self.dim_out[i]
+                elif j == cfg.num_res_blocks:
+                    prev_h, skip = self.dim_out[i], self.dim_in[i]
+                else:
+                    prev_h, skip = self.dim_out[i], self.dim_out[i]
+                level.append(XUNetBlock(prev_h + skip, self.dim_out[i], use_attn=i in self.attn_resolutions, **kw))
+            if i != 0:
+                level.append(ResnetBlock(self.dim_out[i], self.dim_out[i], dropout=cfg.dropout,
+                                         resample="up", emb_ch=cfg.emb_ch))
+            self.upsample[str(i)] = level
+
+        self.lastgn = GroupNorm(num_channels=cfg.ch)
+        self.lastconv = nn.Conv2d(cfg.ch, 3, kernel_size=3, stride=1, padding=1)
+        nn.init.zeros_(self.lastconv.weight)
+
+        # deterministic per-block dropout seed slots
+        for idx, m in enumerate(mm for mm in self.modules() if isinstance(mm, ResnetBlock)):
+            m._seed_slot = idx
+        self._dropout_seed = 0
+
+    # -- dropout seeding: every forward gets a fresh base seed (set by the
+    # trainer from its step counter) so HIP dropout masks are reproducible and
+    # regenerated (not stored) in backward.
+    def set_dropout_seed(self, seed: int) -> None:
+        for m in self.modules():
+            if isinstance(m, ResnetBlock):
+                m._base_seed = int(seed)
+
+    def forward(self, batch: Dict[str, torch.Tensor], *, cond_mask: torch.Tensor) -> torch.Tensor:
+        x, z = batch["x"], batch["z"]
+        B, C, H, W = x.shape
+        for key, v in batch.items():
+            assert v.shape[0] == B, f"{key} should have batch size {B}, not {v.shape[0]}"
+        assert cond_mask.shape[0] == B
+        assert (H, W) == (self.H, self.W), ((H, W), (self.H, self.W))
+        dt = self.compute_dtype or x.dtype
+
+        sembs = self.conditioningprocessor(batch, cond_mask, dt)
+        h = torch.stack([x, z], dim=1).reshape(2 * B, C, H, W).permute(0, 2, 3, 1).to(dt).contiguous()
+        h = ops.conv3x3(h, self.conv.weight, self.conv.bias)
+
+        L = self.num_resolutions
+        hs = [h]
+        for i in range(L):
+            for j in range(self.num_res_blocks):
+                h = self.xunetblocks[i][j](h, sembs[i])
+                hs.append(h)
+            if i != L - 1:
+                h = self.xunetblocks[i][-1](h, sembs[i])
+                hs.append(h)
+        h = self.middle(h, sembs[-1])
+        for i in reversed(range(L)):
+            level = self.upsample[str(i)]
+            for j in range(self.num_res_blocks + 1):
+                h = torch.cat([h, hs.pop()], dim=-1)
+                h = level[j](h, sembs[i])
+            if i != 0:
+                h = level[-1](h, sembs[i])
+        assert not hs
+        # only frame 1 (the target view) is returned by the reference
+        h1 = self.lastgn(h[1::2].contiguous(), silu=True)
+        out = ops.conv3x3(h1, self.lastconv.weight, self.lastconv.bias)
+        return out.permute(0, 3, 1, 2)
+
+
+def _next_seed(block: ResnetBlock) -> int:
+    base = getattr(block, "_base_seed", 0)
+    return (base * 1000003 + block._seed_slot * 7919 + 17) & 0x7FFFFFFF
+
+
+def count_params(model: nn.Module) -> int:
+    return sum(p.numel() for p in model.parameters())

@@ -1,0 +1,92 @@
+"""NHWC op set of the X-UNet, dispatched to hand-written HIP kernels (gfx950)
+or to the PyTorch reference composition.
+
+Every function here has identical semantics in both backends; the torch
+versions (``torch_impl``) are the numerics oracle used by the tests.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import torch_impl as _t
+from ._backend import use_hip, set_backend, load_library, library_error, lib_path
+
+_hip = None
+
+
+def _h():
+    global _hip
+    if _hip is None:
+        from . import hip_impl
+        _hip = hip_impl
+    return _hip
+
+
+def group_norm(x, weight, bias, groups: int = 32, eps: float = 1e-5, silu: bool = False):
+    if use_hip(x):
+        return _h().group_norm(x, weight, bias, groups, eps, silu)
+    return _t.group_norm(x, weight, bias, groups, eps, silu)
+
+
+def gn_film(x, weight, bias, ss, groups: int = 32, eps: float = 1e-5, dropout_p: float = 0.0,
+            training: bool = False, seed: int = 0):
+    if use_hip(x):
+        return _h().gn_film(x, weight, bias, ss, groups, eps, dropout_p, training, seed)
+    return _t.gn_film(x, weight, bias, ss, groups, eps, dropout_p, training, seed)
+
+
+def conv3x3(x, weight, bias, stride: int = 1, residual: Optional[torch.Tensor] = None,
+            out_scale: float = 1.0, row_bias: Optional[torch.Tensor] = None):
+    if use_hip(x):
+        return _h().conv3x3(x, weight, bias, stride, residual, out_scale, row_bias)
+    return _t.conv3x3(x, weight, bias, stride, residual, out_scale, row_bias)
+
+
+def linear(x, weight, bias, residual: Optional[torch.Tensor] = None, out_scale: float = 1.0):
+    if use_hip(x):
+        return _h().linear(x, weight, bias, residual, out_scale)
+    return _t.linear(x, weight, bias, residual, out_scale)
+
+
+def attention(qkv, heads: int, cross: bool):
+    if use_hip(qkv):
+        return _h().attention(qkv, heads, cross)
+    return _t.attention(qkv, heads, cross)
+
+
+def avgpool2(x):
+    if use_hip(x):
+        return _h().avgpool2(x)
+    return _t.avgpool2(x)
+
+
+def upsample2(x):
+    if use_hip(x):
+        return _h().upsample2(x)
+    return _t.upsample2(x)
+
+
+def silu(x):
+    if use_hip(x):
+        return _h().silu(x)
+    return _t.silu(x)
+
+
+def ray_posenc(R, t, K, H: int, W: int, cond_mask, pos_emb, first_emb, other_emb,
+               rescale_from: int = 0, out_dtype: torch.dtype = torch.float32):
+    if out_dtype == torch.bfloat16 and use_hip(R, any_dtype=True):
+        return _h().ray_posenc(R, t, K, H, W, cond_mask, pos_emb, first_emb, other_emb,
+                               rescale_from, out_dtype)
+    return _t.ray_posenc(R, t, K, H, W, cond_mask, pos_emb, first_emb, other_emb,
+                         rescale_from).to(out_dtype)
+
+
+posenc_ddpm = _t.posenc_ddpm
+camera_rays = _t.camera_rays
+posenc_nerf = _t.posenc_nerf
+
+__all__ = ["group_norm", "gn_film", "conv3x3", "linear", "attention", "avgpool2", "upsample2",
+           "silu", "ray_posenc", "posenc_ddpm", "camera_rays", "posenc_nerf", "set_backend",
+           "use_hip", "load_library", "library_error", "lib_path"]

@@ -1,0 +1,50 @@
+"""ctypes signatures of the C ABI exported by ``libd3d_hip.so``
+(sources in ``ops/csrc/*.hip``).  Pointers are passed as integers
+(``tensor.data_ptr()``), streams as the raw ``hipStream_t`` handle."""
+from __future__ import annotations
+
+import ctypes as C
+
+P = C.c_void_p
+I = C.c_int
+L = C.c_long
+F = C.c_float
+U64 = C.c_ulonglong
+IP = C.POINTER(C.c_int)
+
+SIGNATURES = {
+    # norm.hip
+    "d3d_gn_plan": [I, I, I, IP, IP],
+    "d3d_gn_stats": [P, I, I, I, I, F, P, P, P],
+    "d3d_gn_apply": [P, P, P, P, P, I, I, I, I, I, P],
+    "d3d_gn_film": [P, P, P, P, P, P, I, I, I, I, F, U64, P],
+    "d3d_gn_bwd": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, P],
+    # elementwise.hip
+    "d3d_silu": [P, P, L, P],
+    "d3d_dsilu": [P, P, P, L, P],
+    "d3d_avgpool2": [P, P, I, I, I, I, I, P],
+    "d3d_upsample2": [P, P, I, I, I, I, I, P],
+    "d3d_add_scale": [P, P, P, F, L, P],
+    "d3d_sampler_step": [P, P, P, P, P, I, I, F, F, F, F, F, I, U64, P],
+    "d3d_diffusion_fwd": [P, P, P, P, P, P, P, I, I, U64, P],
+    # adam.hip
+    "d3d_adam": [P, P, P, P, P, L, F, F, F, F, F, F, F, F, P],
+    # conv.hip
+    "d3d_conv3x3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, P],
+    "d3d_conv_wgrad_plan": [I, I, I, I, I, IP, IP],
+    "d3d_conv3x3_wgrad": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
+    "d3d_chansum": [P, P, P, P, I, I, I, I, P],
+    "d3d_pack_conv_weight": [P, P, I, I, I, I, I, P],
+    # rays.hip
+    "d3d_ray_posenc": [P, P, P, P, P, P, P, P, I, I, I, P],
+    # attention.hip
+    "d3d_attn_fwd": [P, P, P, I, I, I, I, I, F, P],
+    "d3d_attn_bwd": [P, P, P, P, P, P, P, I, I, I, I, I, F, P],
+}
+
+
+def declare(lib: C.CDLL) -> None:
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_int

@@ -1,0 +1,373 @@
+// Fused multi-head self / cross-view attention on gfx950 MFMA.
+//
+// Reference: AttnLayer / AttnBlock (xunet.py:154-220) -> nn.MultiheadAttention
+// with 4 heads, dispatched as bmm -> softmax -> bmm that MATERIALISES the
+// [B*4, L, L] probabilities (and head-averaged weights) for both frames and for
+// self and cross attention separately.
+//
+// Here one launch handles every (image, head, 64-query block) of a layer; the
+// key/value frame is n (self) or n^1 (cross: the two views of an example are
+// adjacent rows of the frame-folded batch).  Input is the packed in_proj
+// output qkv [N, L, 3C] (q | k | v, head h at columns h*D..h*D+D-1), output is
+// [N, L, C].  Nothing of size L x L ever leaves registers.
+//
+// Forward (flash, online softmax):  S^T = K Q^T is formed with keys on the
+// MFMA rows so that P^T lands in registers already laid out as the B operand
+// of O^T = V^T P^T (no LDS round trip for P); V^T fragments come from the
+// transpose read ds_read_b64_tr_b16 on a padded [key][D] LDS tile.  The key
+// order inside each 32-key MFMA step is permuted identically for both
+// operands (sum order is irrelevant), which is what makes the register reuse
+// and the conflict-free transpose reads line up.
+//
+// Backward (flash v2 recompute, one workgroup per 64-key block):
+// S = Q K^T and dP = dO V^T with KEYS on the lane, so P and dS are already the
+// A operands of dV = P^T dO and dK = dS^T Q; dQ = dS K goes through LDS once
+// and is accumulated across key blocks with fp32 atomics.
+#include "common.h"
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ s16x4 ds_tr(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+__device__ __forceinline__ bf16x8 tr8(const bf16* base, int stride, int r1, int r2, int col) {
+  s16x4 lo = ds_tr(base + r1 * stride + col);
+  s16x4 hi = ds_tr(base + r2 * stride + col);
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ bf16x8 pack8(f32x4 a, f32x4 b) {
+  bf16x8 r;
+  r[0] = (bf16)a[0]; r[1] = (bf16)a[1]; r[2] = (bf16)a[2]; r[3] = (bf16)a[3];
+  r[4] = (bf16)b[0]; r[5] = (bf16)b[1]; r[6] = (bf16)b[2]; r[7] = (bf16)b[3];
+  return r;
+}
+// swizzled [row][D] tile of 16-byte chunks for ds_read_b128 row reads
+template <int D>
+__device__ __forceinline__ int swz(int row, int chunk) {
+  return row * D + ((chunk ^ (row & 7)) << 3);
+}
+
+// ------------------------------------------------------------ forward ----
+template <int D>
+__global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                  float* __restrict__ lse, int L, int C, int heads, int cross,
+                                                  float scale) {
+  constexpr int VS = D + 16;                 // padded V row (tr reads)
+  constexpr int KC = D / 32;                 // 32-wide k chunks over head dim
+  constexpr int DT = D / 16;                 // 16-wide dv tiles
+  __shared__ __attribute__((aligned(16))) bf16 Ks[64 * D];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[64 * VS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int qblk = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int nkv = cross ? (n ^ 1) : n;
+  const int g = lane >> 4, fr = lane & 15;
+  const long C3 = 3L * C;
+  const int q = qblk * 64 + w * 16 + fr;
+  const bf16* qrow = qkv + ((long)n * L + q) * C3 + h * D;
+  bf16x8 qf[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) qf[kc] = *reinterpret_cast<const bf16x8*>(qrow + 32 * kc + 8 * g);
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const float sl2 = scale * LOG2E;
+  const int qq = (lane & 15) >> 2, pc = lane & 3;
+
+  for (int kb = 0; kb < L; kb += 64) {
+    // cooperative K/V block load
+    constexpr int CH = D / 8;  // chunks per row
+#pragma unroll
+    for (int i = 0; i < 64 * CH / 256; ++i) {
+      int idx = tid + i * 256;
+      int r = idx / CH, c = idx % CH;
+      const bf16* src = qkv + ((long)nkv * L + kb + r) * C3 + h * D + c * 8;
+      bf16x8 kv = *reinterpret_cast<const bf16x8*>(src + C);
+      bf16x8 vv = *reinterpret_cast<const bf16x8*>(src + 2 * C);
+      *reinterpret_cast<bf16x8*>(Ks + swz<D>(r, c)) = kv;
+      *reinterpret_cast<bf16x8*>(Vs + r * VS + c * 8) = vv;
+    }
+    __syncthreads();
+    f32x4 s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + swz<D>(16 * kt + fr, 4 * kc + g));
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[kc], s[kt], 0, 0, 0);
+      }
+    }
+    // online softmax over this block's 64 keys for query column q
+    float mb = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s[kt][i] *= sl2;
+        mb = fmaxf(mb, s[kt][i]);
+      }
+    mb = fmaxf(mb, __shfl_xor(mb, 16, 64));
+    mb = fmaxf(mb, __shfl_xor(mb, 32, 64));
+    float mn = fmaxf(m, mb);
+    float alpha = exp2f(m - mn);
+    float ls = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s[kt][i] = exp2f(s[kt][i] - mn);
+        ls += s[kt][i];
+      }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) o[t] *= alpha;
+    // O^T += V^T P^T, two 32-key steps
+#pragma unroll
+    for (int kc2 = 0; kc2 < 2; ++kc2) {
+      bf16x8 pb = pack8(s[2 * kc2], s[2 * kc2 + 1]);
+      int r1 = 32 * kc2 + 4 * g + qq, r2 = 32 * kc2 + 16 + 4 * g + qq;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        bf16x8 va = tr8(Vs, VS, r1, r2, 16 * t + 4 * pc);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  const float inv = 1.f / l;
+  bf16* orow = out + ((long)n * L + q) * C + h * D;
+#pragma unroll
+  for (int t = 0; t < DT; ++t) {
+    bf16x4 v4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v4[i] = (bf16)(o[t][i] * inv);
+    *reinterpret_cast<bf16x4*>(orow + 16 * t + 4 * g) = v4;
+  }
+  if (g == 0) lse[((long)n * heads + h) * L + q] = (m + log2f(l)) / LOG2E;
+}
+
+// ------------------------------------------------------- bwd preprocess --
+// Dv[n][h][q] = sum_d dO * O
+__global__ void attn_bwd_pre_k(const bf16* __restrict__ out, const bf16* __restrict__ dout, float* __restrict__ Dv,
+                               int N, int L, int C, int heads, int D) {
+  long total = (long)N * L * heads;
+  long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  int h = (int)(t % heads);
+  long r = t / heads;           // n*L + q
+  int q = (int)(r % L);
+  int n = (int)(r / L);
+  const bf16* o = out + r * C + h * D;
+  const bf16* d = dout + r * C + h * D;
+  float s = 0.f;
+  for (int k = 0; k < D; k += 8) {
+    f32x8 a = ld8(o + k), b = ld8(d + k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += a[j] * b[j];
+  }
+  Dv[((long)n * heads + h) * L + q] = s;
+}
+
+// --------------------------------------------------------------- backward --
+template <int D>
+__global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                  const float* __restrict__ lse, const float* __restrict__ Dv,
+                                                  float* __restrict__ dq_acc, bf16* __restrict__ dqkv, int L, int C,
+                                                  int heads, int cross, float scale) {
+  constexpr int KC = D / 32, DT = D / 16;
+  constexpr int TS = D + 16;      // padded rows: row reads + tr reads
+  constexpr int SS = 64 + 8;      // dS tile row stride (bf16)
+  __shared__ __attribute__((aligned(16))) bf16 Qs[32 * TS];
+  __shared__ __attribute__((aligned(16))) bf16 dOs[32 * TS];
+  __shared__ __attribute__((aligned(16))) bf16 Kt[64 * TS];
+  __shared__ __attribute__((aligned(16))) bf16 dSs[32 * SS];
+  __shared__ float lse_s[32], D_s[32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kblk = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int nkv = cross ? (n ^ 1) : n;
+  const int g = lane >> 4, fr = lane & 15, qq = (lane & 15) >> 2, pc = lane & 3;
+  const long C3 = 3L * C;
+  const int k0 = kblk * 64;
+  const float sl2 = scale * LOG2E;
+  constexpr int CH = D / 8;
+
+  // K tile of the block (for dQ) and this wave's K / V fragments (B operands)
+#pragma unroll
+  for (int i = 0; i < 64 * CH / 256; ++i) {
+    int idx = tid + i * 256;
+    int r = idx / CH, c = idx % CH;
+    *reinterpret_cast<bf16x8*>(Kt + r * TS + c * 8) =
+        *reinterpret_cast<const bf16x8*>(qkv + ((long)nkv * L + k0 + r) * C3 + C + h * D + c * 8);
+  }
+  const int key = k0 + 16 * w + fr;
+  const bf16* krow = qkv + ((long)nkv * L + key) * C3 + h * D;
+  bf16x8 kf[KC], vf[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    kf[kc] = *reinterpret_cast<const bf16x8*>(krow + C + 32 * kc + 8 * g);
+    vf[kc] = *reinterpret_cast<const bf16x8*>(krow + 2 * C + 32 * kc + 8 * g);
+  }
+  f32x4 dk[DT], dv[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) {
+    dk[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float* lse_nh = lse + ((long)n * heads + h) * L;
+  const float* D_nh = Dv + ((long)n * heads + h) * L;
+
+  for (int q0 = 0; q0 < L; q0 += 32) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < (32 * CH + 255) / 256; ++i) {
+      int idx = tid + i * 256;
+      if (idx < 32 * CH) {
+        int r = idx / CH, c = idx % CH;
+        long row = (long)n * L + q0 + r;
+        *reinterpret_cast<bf16x8*>(Qs + r * TS + c * 8) =
+            *reinterpret_cast<const bf16x8*>(qkv + row * C3 + h * D + c * 8);
+        *reinterpret_cast<bf16x8*>(dOs + r * TS + c * 8) =
+            *reinterpret_cast<const bf16x8*>(dout + row * C + h * D + c * 8);
+      }
+    }
+    if (tid < 32) {
+      lse_s[tid] = lse_nh[q0 + tid] * LOG2E;
+      D_s[tid] = D_nh[q0 + tid];
+    }
+    __syncthreads();
+    f32x4 p[2], ds[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        bf16x8 a = *reinterpret_cast<const bf16x8*>(Qs + (16 * qt + fr) * TS + 32 * kc + 8 * g);
+        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, kf[kc], s, 0, 0, 0);
+        bf16x8 b = *reinterpret_cast<const bf16x8*>(dOs + (16 * qt + fr) * TS + 32 * kc + 8 * g);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, vf[kc], dp, 0, 0, 0);
+      }
+      // rows: q = 16qt + 4g + i ; column (lane): key
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int qi = 16 * qt + 4 * g + i;
+        float pv = exp2f(s[i] * sl2 - lse_s[qi]);
+        p[qt][i] = pv;
+        ds[qt][i] = pv * (dp[i] - D_s[qi]);
+      }
+    }
+    // dV += P^T dO ; dK += dS^T Q  (k-slots permuted: q = {4g+j, 16+4g+j})
+    bf16x8 pa = pack8(p[0], p[1]);
+    bf16x8 dsa = pack8(ds[0], ds[1]);
+    int r1 = 4 * g + qq, r2 = 16 + 4 * g + qq;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      bf16x8 bo = tr8(dOs, TS, r1, r2, 16 * t + 4 * pc);
+      dv[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, bo, dv[t], 0, 0, 0);
+      bf16x8 bq = tr8(Qs, TS, r1, r2, 16 * t + 4 * pc);
+      dk[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsa, bq, dk[t], 0, 0, 0);
+    }
+    // dS -> LDS [32 q][64 keys] for dQ = dS K
+    // columns are stored in the permuted k-slot order of the tr-read K operand:
+    // key u of a 32-key chunk -> slot 8*(u/4)+u%4 (u<16), 8*((u-16)/4)+4+u%4
+    {
+      const int kl = 16 * w + fr, u = kl & 31;
+      const int col = (kl & 32) + (u < 16 ? 8 * (u >> 2) + (u & 3) : 8 * ((u - 16) >> 2) + 4 + (u & 3));
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dSs[(16 * qt + 4 * g + i) * SS + col] = (bf16)ds[qt][i];
+    }
+    __syncthreads();
+    // dQ tiles: 2 (q) x DT (d) tiles over 4 waves
+    for (int tt = w; tt < 2 * DT; tt += 4) {
+      int qt = tt / DT, t = tt % DT;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) {   // 64 keys = 2 x 32
+        bf16x8 a = *reinterpret_cast<const bf16x8*>(dSs + (16 * qt + fr) * SS + 32 * kc + 8 * g);
+        bf16x8 b = tr8(Kt, TS, 32 * kc + 4 * g + qq, 32 * kc + 16 + 4 * g + qq, 16 * t + 4 * pc);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+      }
+      // acc rows: q = 16qt + 4g + i, col d = 16t + fr ... (A rows = q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        long row = (long)n * L + q0 + 16 * qt + 4 * g + i;
+        atomicAdd(dq_acc + row * C + h * D + 16 * t + fr, acc[i] * scale);
+      }
+    }
+  }
+  // write dK, dV for this wave's 16 keys: dk[t][i] = dK[key = 4g+i][d = 16t+fr]
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      long row = (long)nkv * L + k0 + 16 * w + 4 * g + i;
+      dqkv[row * C3 + C + h * D + 16 * t + fr] = (bf16)(dk[t][i] * scale);
+      dqkv[row * C3 + 2 * C + h * D + 16 * t + fr] = (bf16)dv[t][i];
+    }
+}
+
+__global__ void dq_convert_k(const float* __restrict__ dq, bf16* __restrict__ dqkv, long rows, int C) {
+  long total = rows * C / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long r = (i * 8) / C;
+    int c = (int)((i * 8) % C);
+    st8(dqkv + r * 3L * C + c, ld8f(dq + i * 8));
+  }
+}
+
+}  // namespace
+
+// qkv: [N, L, 3C] bf16; out: [N, L, C] bf16; lse: [N, heads, L] fp32.
+// Requires L % 64 == 0, D = C/heads in {64, 128}.
+D3D_API int d3d_attn_fwd(const void* qkv, void* out, float* lse, int N, int L, int C, int heads, int cross,
+                         float scale, hipStream_t st) {
+  int D = C / heads;
+  dim3 grid(L / 64, heads, N);
+  if (D == 64)
+    hipLaunchKernelGGL(attn_fwd_k<64>, grid, dim3(256), 0, st, (const bf16*)qkv, (bf16*)out, lse, L, C, heads, cross,
+                       scale);
+  else if (D == 128)
+    hipLaunchKernelGGL(attn_fwd_k<128>, grid, dim3(256), 0, st, (const bf16*)qkv, (bf16*)out, lse, L, C, heads,
+                       cross, scale);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// dq_acc: [N, L, C] fp32 zero-initialised workspace; Dv: [N, heads, L] fp32
+// workspace; dqkv: [N, L, 3C] bf16 output (every element written).
+D3D_API int d3d_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* Dv,
+                         float* dq_acc, void* dqkv, int N, int L, int C, int heads, int cross, float scale,
+                         hipStream_t st) {
+  int D = C / heads;
+  long total = (long)N * L * heads;
+  hipLaunchKernelGGL(attn_bwd_pre_k, dim3((int)((total + 255) / 256)), dim3(256), 0, st, (const bf16*)out,
+                     (const bf16*)dout, Dv, N, L, C, heads, D);
+  dim3 grid(L / 64, heads, N);
+  if (D == 64)
+    hipLaunchKernelGGL(attn_bwd_k<64>, grid, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse, Dv, dq_acc,
+                       (bf16*)dqkv, L, C, heads, cross, scale);
+  else if (D == 128)
+    hipLaunchKernelGGL(attn_bwd_k<128>, grid, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse, Dv,
+                       dq_acc, (bf16*)dqkv, L, C, heads, cross, scale);
+  else
+    return (int)hipErrorInvalidValue;
+  long rows = (long)N * L;
+  long g = (rows * C / 8 + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(dq_convert_k, dim3((int)g), dim3(256), 0, st, dq_acc, (bf16*)dqkv, rows, C);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,92 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels of d3d_hip.
+//
+// Conventions:
+//   * activations are NHWC bf16 ([N, H, W, C], N = 2*B frame-interleaved);
+//   * parameters are fp32 masters, read directly by the kernels (or through a
+//     packed bf16 copy for the MFMA operands);
+//   * every launcher is `extern "C" int d3d_<op>(..., hipStream_t)` returning
+//     the hipError_t of the launch, so Python drives it via ctypes with the
+//     current torch stream (graph-capture safe: no allocation, no sync).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+#define D3D_API extern "C" __attribute__((visibility("default")))
+#define WAVE 64
+
+__device__ __forceinline__ f32x8 ld8(const bf16* p) {
+  return __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p), f32x8);
+}
+__device__ __forceinline__ void st8(bf16* p, f32x8 v) {
+  *reinterpret_cast<bf16x8*>(p) = __builtin_convertvector(v, bf16x8);
+}
+__device__ __forceinline__ f32x8 ld8f(const float* p) {
+  f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+  f32x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+__device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
+__device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float siluf_(float x) { return x * sigmoidf_(x); }
+// d/dx silu(x) = s * (1 + x * (1 - s))
+__device__ __forceinline__ float dsiluf_(float x) {
+  float s = sigmoidf_(x);
+  return s * (1.0f + x * (1.0f - s));
+}
+
+// Counter-based RNG for dropout masks: splitmix64 finalizer over
+// (seed, element index).  Stateless, so backward regenerates the mask.
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  return (uint32_t)(z >> 32);
+}
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
+  return (hash_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);
+}
+
+// Box-Muller normal from two counter-based uniforms.
+__device__ __forceinline__ float normal01(uint64_t seed, uint64_t idx) {
+  float u1 = ((hash_u32(seed, 2 * idx) >> 8) + 1) * (1.0f / 16777217.0f);
+  float u2 = (hash_u32(seed, 2 * idx + 1) >> 8) * (1.0f / 16777216.0f);
+  return sqrtf(-2.0f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Chan et al. parallel merge of (count, mean, M2) partial moments.
+struct Moments {
+  float n, mean, m2;
+};
+__device__ __forceinline__ Moments merge_moments(Moments a, Moments b) {
+  float n = a.n + b.n;
+  if (n <= 0.f) return a;
+  float d = b.mean - a.mean;
+  float fb = b.n / n;
+  Moments r;
+  r.n = n;
+  r.mean = a.mean + d * fb;
+  r.m2 = a.m2 + b.m2 + d * d * a.n * fb;
+  return r;
+}
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

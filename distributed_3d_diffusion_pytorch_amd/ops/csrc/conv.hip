@@ -1,0 +1,494 @@
+// 3x3 convolution (padding 1, stride s) as implicit GEMM on gfx950 MFMA.
+//
+// Replaces the 76 Conv2d(3x3) of the X-UNet (xunet.py:114-126,294-297,385,
+// 473): 54 % of the model FLOPs (+12 % for the strided conditioning convs).
+//
+// Forward / dgrad kernel (conv_igemm_k):
+//   D[co][pix] = sum_k Wp[co][k] * im2col(I)[k][pix],   k = (tap, ci)
+//   * A operand = packed weights [OC_pad][9][IC_pad] bf16 (K-contiguous rows),
+//     B operand = im2col gathered on the fly from NHWC input (each pixel's
+//     channels are contiguous, so an MFMA B fragment is one 16-byte load);
+//   * orientation puts PIXELS on the MFMA column (lane) and 4 consecutive
+//     output channels in each lane's accumulators, so the NHWC epilogue stores
+//     8 contiguous bytes per lane;
+//   * 128x128 block tile, BK=64 (one tap x 64 channels), 4 waves (2x2), each
+//     wave 64x64 = 4x4 v_mfma_f32_16x16x32_bf16 tiles, fp32 accumulate;
+//   * register-staged double-buffered LDS (global loads for step t+1 in
+//     flight while step t's MFMAs run), XOR-swizzled 128-byte LDS rows so the
+//     ds_read_b128 fragment reads are conflict-free;
+//   * zero-fill for padding / out-of-range taps / channel tails in the loader;
+//   * fused epilogue: + bias[co] + row_bias[image][co] (+ residual) * scale;
+//   * TRANS=true computes the input gradient of a strided conv
+//     (src = (o + 1 - k) / s when divisible) with weights packed [ci][tap][co].
+//
+// Weight gradient kernel (conv_wgrad_k):
+//   dW[co][(tap,ci)] = sum_pix dY[pix][co] * I[src(pix,tap)][ci]
+//   both operands have the reduction (pixel) axis as their SLOW memory axis,
+//   so tiles are stored pixel-major in LDS and MFMA fragments are read with
+//   the gfx950 transpose read ds_read_b64_tr_b16; rows are padded by 32 B and
+//   the pixel order inside a 32-pixel step is permuted identically for both
+//   operands so that every transpose read is bank-conflict free.  Split-K over
+//   pixels with fp32 partial slabs + a deterministic reduce kernel that also
+//   writes the OIHW layout of the parameter gradient.
+#include "common.h"
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+namespace {
+
+constexpr int BK = 64;
+
+template <int BM, int BN, bool TRANS>
+__global__ void __launch_bounds__(256, 2)
+conv_igemm_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
+             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int Nimg,
+             int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride, float scale) {
+  constexpr int WM = BM / 2, WN = BN / 2;       // 2x2 waves
+  constexpr int TM = WM / 16, TN = WN / 16;     // MFMA tiles per wave
+  constexpr int A_LD = BM * BK / 8 / 256;       // 16B loads per thread
+  constexpr int B_LD = BN * BK / 8 / 256;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * BK];
+  bf16* As = smem;
+  bf16* Bs = smem + 2 * BM * BK;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const long Mpix = (long)Nimg * OH * OW;
+  // XCD-aware remap: neighbouring pixel tiles (which share input rows and
+  // the whole weight panel) land on the same XCD's L2.
+  const int nbx = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    int q = nbx / 8, r = nbx % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const long n0 = (long)bid * BN;               // pixel tile start
+  const int m0 = blockIdx.y * BM;               // output-channel tile start
+  const int Kp = 9 * ICp;
+
+  // per-thread B rows (pixels): fixed over the K loop
+  const int cb = tid & 7;                        // 16B chunk within the BK row
+  int pn[B_LD], poh[B_LD], pow_[B_LD];
+  bool pvalid[B_LD];
+#pragma unroll
+  for (int i = 0; i < B_LD; ++i) {
+    long p = n0 + (tid >> 3) + i * 32;
+    pvalid[i] = p < Mpix;
+    long pp = pvalid[i] ? p : 0;
+    pow_[i] = (int)(pp % OW);
+    long t = pp / OW;
+    poh[i] = (int)(t % OH);
+    pn[i] = (int)(t / OH);
+  }
+
+  bf16x8 ra[A_LD], rb[B_LD];
+  const bf16x8 zero8 = {};
+  auto gload = [&](int kstep) {
+    const int tap = kstep / (ICp / BK);
+    const int c0 = (kstep % (ICp / BK)) * BK;
+    const int kh = tap / 3, kw = tap % 3;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      int r = (tid >> 3) + i * 32;
+      ra[i] = *reinterpret_cast<const bf16x8*>(Wp + (long)(m0 + r) * Kp + tap * ICp + c0 + cb * 8);
+    }
+    const int c = c0 + cb * 8;
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      int ih, iw;
+      bool ok = pvalid[i] && c < IC;
+      if (!TRANS) {
+        ih = poh[i] * stride + kh - 1;
+        iw = pow_[i] * stride + kw - 1;
+      } else {
+        int th = poh[i] + 1 - kh, tw = pow_[i] + 1 - kw;
+        ok = ok && th >= 0 && tw >= 0 && (th % stride) == 0 && (tw % stride) == 0;
+        ih = th / stride;
+        iw = tw / stride;
+      }
+      ok = ok && ih >= 0 && ih < IH && iw >= 0 && iw < IW;
+      rb[i] = ok ? *reinterpret_cast<const bf16x8*>(I + (((long)pn[i] * IH + ih) * IW + iw) * IC + c) : zero8;
+    }
+  };
+  auto swz = [](int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); };
+  auto swrite = [&](int buf) {
+    bf16* a = As + buf * BM * BK;
+    bf16* b = Bs + buf * BN * BK;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) *reinterpret_cast<bf16x8*>(a + swz((tid >> 3) + i * 32, cb)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) *reinterpret_cast<bf16x8*>(b + swz((tid >> 3) + i * 32, cb)) = rb[i];
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = Kp / BK;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) gload(ks + 1);
+    const bf16* a = As + buf * BM * BK;
+    const bf16* b = Bs + buf * BN * BK;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int row = wm * WM + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(a + swz(row, kk * 4 + fq));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int row = wn * WN + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(b + swz(row, kk * 4 + fq));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (ks + 1 < nk) swrite(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: D[co][pix] -> O[pix][co] (NHWC) ----
+  const int OHW = OH * OW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    long pix = n0 + wn * WN + j * 16 + fr;
+    if (pix >= Mpix) continue;
+    int img = (int)(pix / OHW);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int co = m0 + wm * WM + i * 16 + fq * 4;
+      if (co >= OC) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int c = co + e < OC ? co + e : OC - 1;
+        float t = acc[i][j][e] + (bias ? bias[c] : 0.f);
+        if (row_bias) t += row_bias[(long)img * OC + c];
+        v[e] = t;
+      }
+      bf16* dst = O + pix * ldo + co;
+      if (co + 3 < OC && (ldo & 3) == 0) {
+        if (res) {
+          bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + pix * ldo + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+        }
+        bf16x4 o4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o4[e] = (bf16)(v[e] * scale);
+        *reinterpret_cast<bf16x4*>(dst) = o4;
+      } else {
+        for (int e = 0; e < 4 && co + e < OC; ++e) {
+          float t = v[e];
+          if (res) t += (float)res[pix * ldo + co + e];
+          dst[e] = (bf16)(t * scale);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------ wgrad ------
+constexpr int WBK = 32;           // pixels per k-step
+constexpr int WPAD = 16;          // bf16 elements of row padding (32 B)
+
+__device__ __forceinline__ s16x4 ds_tr(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256, 2)
+conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __restrict__ ws, int Nimg, int IH,
+             int IW, int IC, int OH, int OW, int OC, int stride, int pix_per_split, int ncb) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int ALD = WBK * BM / 8 / 256, BLD = WBK * BN / 8 / 256;
+  constexpr int AS = BM + WPAD, BSt = BN + WPAD;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * WBK * (AS + BSt)];
+  bf16* As = smem;
+  bf16* Bs = smem + 2 * WBK * AS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tap = blockIdx.x / ncb;
+  const int ci0 = (blockIdx.x % ncb) * BN;
+  const int m0 = blockIdx.y * BM;
+  const int split = blockIdx.z;
+  const int kh = tap / 3, kw = tap % 3;
+  const long P = (long)Nimg * OH * OW;
+  const long p_begin = (long)split * pix_per_split;
+  const long p_end = p_begin + pix_per_split < P ? p_begin + pix_per_split : P;
+  const int OHW = OH * OW;
+  const bf16x8 zero8 = {};
+  constexpr int ACH = BM / 8, BCH = BN / 8;   // 16B chunks per row
+
+  bf16x8 ra[ALD], rb[BLD];
+  auto gload = [&](long p0) {
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) {
+      int idx = tid + i * 256;
+      int r = idx / ACH, c = (idx % ACH) * 8;
+      long p = p0 + r;
+      bool ok = p < p_end && m0 + c < OC;
+      ra[i] = ok ? *reinterpret_cast<const bf16x8*>(dY + p * OC + m0 + c) : zero8;
+    }
+#pragma unroll
+    for (int i = 0; i < BLD; ++i) {
+      int idx = tid + i * 256;
+      int r = idx / BCH, c = (idx % BCH) * 8;
+      long p = p0 + r;
+      bool ok = p < p_end && ci0 + c < IC;
+      int img = 0, oh = 0, ow = 0;
+      if (ok) {
+        img = (int)(p / OHW);
+        int rem = (int)(p % OHW);
+        oh = rem / OW;
+        ow = rem % OW;
+      }
+      int ih = oh * stride + kh - 1, iw = ow * stride + kw - 1;
+      ok = ok && ih >= 0 && ih < IH && iw >= 0 && iw < IW;
+      rb[i] = ok ? *reinterpret_cast<const bf16x8*>(I + (((long)img * IH + ih) * IW + iw) * IC + ci0 + c) : zero8;
+    }
+  };
+  auto swrite = [&](int buf) {
+    bf16* a = As + buf * WBK * AS;
+    bf16* b = Bs + buf * WBK * BSt;
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) {
+      int idx = tid + i * 256;
+      *reinterpret_cast<bf16x8*>(a + (idx / ACH) * AS + (idx % ACH) * 8) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BLD; ++i) {
+      int idx = tid + i * 256;
+      *reinterpret_cast<bf16x8*>(b + (idx / BCH) * BSt + (idx % BCH) * 8) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment addressing for ds_read_b64_tr_b16 (see header): group g = lane>>4,
+  // in-group lane i = 4q+p -> rows {4g+q, 16+4g+q}, columns 4p..4p+3.
+  const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
+  const int r1 = 4 * g + q, r2 = 16 + 4 * g + q;
+  const long nsteps = (p_end - p_begin + WBK - 1) / WBK;
+  if (nsteps > 0) {
+    gload(p_begin);
+    swrite(0);
+  }
+  __syncthreads();
+  for (long s = 0; s < nsteps; ++s) {
+    const int buf = (int)(s & 1);
+    if (s + 1 < nsteps) gload(p_begin + (s + 1) * WBK);
+    const bf16* a = As + buf * WBK * AS;
+    const bf16* b = Bs + buf * WBK * BSt;
+    bf16x8 af[TM], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int col = wm * WM + i * 16 + 4 * pc;
+      s16x4 lo = ds_tr(a + r1 * AS + col);
+      s16x4 hi = ds_tr(a + r2 * AS + col);
+      s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[i] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int col = wn * WN + j * 16 + 4 * pc;
+      s16x4 lo = ds_tr(b + r1 * BSt + col);
+      s16x4 hi = ds_tr(b + r2 * BSt + col);
+      s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bfr[j] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (s + 1 < nsteps) swrite(buf ^ 1);
+    __syncthreads();
+  }
+  // partial slab: ws[split][co][tap*IC + ci]
+  const int fr = lane & 15, fq = lane >> 4;
+  const long KW = 9L * IC;
+  float* slab = ws + (long)split * OC * KW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int ci = ci0 + wn * WN + j * 16 + fr;
+    if (ci >= IC) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < OC) slab[(long)(co + e) * KW + tap * IC + ci] = acc[i][j][e];
+    }
+  }
+}
+
+// sum the split slabs and write dW in OIHW fp32 layout (optionally accumulate)
+__global__ void wgrad_reduce_k(const float* __restrict__ ws, float* __restrict__ dW, int OC, int IC, int splits,
+                               int accumulate) {
+  long total = (long)OC * IC * 9;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    // t indexes the slab layout [co][tap][ci] (coalesced reads)
+    int ci = (int)(t % IC);
+    long r = t / IC;
+    int tap = (int)(r % 9);
+    int co = (int)(r / 9);
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += ws[(long)k * total + t];
+    long o = ((long)co * IC + ci) * 9 + tap;
+    dW[o] = accumulate ? dW[o] + s : s;
+  }
+}
+
+// per-image channel sums: block = 256 threads = 32 channel-vectors x 8 row lanes
+__global__ void chansum_k(const bf16* __restrict__ dy, float* __restrict__ part, int P, int C, int nchunks) {
+  const int img = blockIdx.y, chunk = blockIdx.z;
+  const int cv = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int rl = threadIdx.x >> 5;      // 0..7
+  __shared__ float red[8][32][8];
+  f32x8 s = {};
+  const int CV = C / 8;
+  if (cv < CV) {
+    int rows = (P + nchunks - 1) / nchunks;
+    int r0 = chunk * rows, r1 = min(P, r0 + rows);
+    for (int r = r0 + rl; r < r1; r += 8) s += ld8(dy + ((long)img * P + r) * C + cv * 8);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][threadIdx.x & 31][e] = s[e];
+  __syncthreads();
+  if (rl == 0 && cv < CV) {
+    for (int k = 1; k < 8; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += red[k][threadIdx.x & 31][e];
+    float* o = part + ((long)chunk * gridDim.y + img) * C + cv * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = s[e];
+  }
+}
+
+__global__ void chansum_final_k(const float* __restrict__ part, float* __restrict__ per_img, float* __restrict__ tot,
+                                int Nimg, int C, int nchunks) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float all = 0.f;
+  for (int n = 0; n < Nimg; ++n) {
+    float s = 0.f;
+    for (int k = 0; k < nchunks; ++k) s += part[((long)k * Nimg + n) * C + c];
+    if (per_img) per_img[(long)n * C + c] = s;
+    all += s;
+  }
+  if (tot) tot[c] = all;
+}
+
+// weight packing: OIHW fp32 -> [OCp][9][ICp] bf16 (forward) or
+//                              [ICp][9][OCp] bf16 (transposed, for dgrad)
+__global__ void pack_w_k(const float* __restrict__ w, bf16* __restrict__ out, int OC, int IC, int OCp, int ICp,
+                         int trans) {
+  long total = trans ? (long)ICp * 9 * OCp : (long)OCp * 9 * ICp;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    int co, ci, tap;
+    if (!trans) {
+      ci = (int)(t % ICp);
+      long r = t / ICp;
+      tap = (int)(r % 9);
+      co = (int)(r / 9);
+    } else {
+      co = (int)(t % OCp);
+      long r = t / OCp;
+      tap = (int)(r % 9);
+      ci = (int)(r / 9);
+    }
+    float v = (co < OC && ci < IC) ? w[((long)co * IC + ci) * 9 + tap] : 0.f;
+    out[t] = (bf16)v;
+  }
+}
+
+}  // namespace
+
+// ============================================================== C ABI =====
+// I: [N, IH, IW, IC] bf16 (IC % 8 == 0), Wp: packed [OCp][9][ICp] bf16 with
+// OCp % 128 == 0 and ICp % 64 == 0.  O: [N, OH, OW, ldo] bf16.
+D3D_API int d3d_conv3x3(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
+                        void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo,
+                        int stride, int trans, float scale, hipStream_t st) {
+  long Mpix = (long)N * OH * OW;
+  constexpr int BM = 128, BN = 128;
+  dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM));
+  if (trans)
+    hipLaunchKernelGGL((conv_igemm_k<BM, BN, true>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,
+                       row_bias, (const bf16*)res, (bf16*)O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, scale);
+  else
+    hipLaunchKernelGGL((conv_igemm_k<BM, BN, false>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,
+                       row_bias, (const bf16*)res, (bf16*)O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, scale);
+  return (int)hipGetLastError();
+}
+
+D3D_API int d3d_conv_wgrad_plan(int N, int OH, int OW, int OC, int IC, int* splits, int* pix_per_split) {
+  constexpr int BM = 128, BN = 128;
+  long P = (long)N * OH * OW;
+  int tiles = 9 * ((IC + BN - 1) / BN) * ((OC + BM - 1) / BM);
+  long want = (1024 + tiles - 1) / tiles;
+  long maxs = (P + 255) / 256;      // >= 256 pixels per split
+  if (want > maxs) want = maxs;
+  if (want < 1) want = 1;
+  long pps = (P + want - 1) / want;
+  pps = (pps + WBK - 1) / WBK * WBK;
+  *pix_per_split = (int)pps;
+  *splits = (int)((P + pps - 1) / pps);
+  return 0;
+}
+
+// dY: [N, OH, OW, OC] bf16 (OC % 8 == 0); I: [N, IH, IW, IC] bf16.
+// ws: [splits][OC][9*IC] fp32 workspace.  dW: OIHW fp32 [OC][IC][3][3].
+D3D_API int d3d_conv3x3_wgrad(const void* dY, const void* I, float* ws, float* dW, int N, int IH, int IW, int IC,
+                              int OH, int OW, int OC, int stride, int splits, int pix_per_split, int accumulate,
+                              hipStream_t st) {
+  constexpr int BM = 128, BN = 128;
+  int ncb = (IC + BN - 1) / BN;
+  dim3 grid(9 * ncb, (OC + BM - 1) / BM, splits);
+  hipLaunchKernelGGL((conv_wgrad_k<BM, BN>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
+                     IW, IC, OH, OW, OC, stride, pix_per_split, ncb);
+  long total = (long)OC * IC * 9;
+  long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(wgrad_reduce_k, dim3((int)g), dim3(256), 0, st, ws, dW, OC, IC, splits, accumulate);
+  return (int)hipGetLastError();
+}
+
+// per-image (optional) and total channel sums of dY [N, P, C] (C % 8 == 0).
+// part: workspace [nchunks][N][C] fp32.
+D3D_API int d3d_chansum(const void* dY, float* part, float* per_img, float* tot, int N, int P, int C, int nchunks,
+                        hipStream_t st) {
+  dim3 grid((C / 8 + 31) / 32, N, nchunks);
+  hipLaunchKernelGGL(chansum_k, grid, dim3(256), 0, st, (const bf16*)dY, part, P, C, nchunks);
+  hipLaunchKernelGGL(chansum_final_k, dim3((C + 255) / 256), dim3(256), 0, st, part, per_img, tot, N, C, nchunks);
+  return (int)hipGetLastError();
+}
+
+D3D_API int d3d_pack_conv_weight(const float* w, void* out, int OC, int IC, int OCp, int ICp, int trans,
+                                 hipStream_t st) {
+  long total = (long)OCp * 9 * ICp;
+  long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(pack_w_k, dim3((int)g), dim3(256), 0, st, w, (bf16*)out, OC, IC, OCp, ICp, trans);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,425 @@
+// GroupNorm family for NHWC bf16 activations on gfx950.
+//
+// Reference ops replaced: nn.GroupNorm(32, C) over the frame-folded batch
+// (xunet.py:61-71) x101, the SiLU after GN0/lastgn (xunet.py:140,535), the FiLM
+// modulation h*(1+scale)+shift (xunet.py:87) and Dropout(p=0.1)
+// (xunet.py:120).  Kernels:
+//   gn_stats   : per-(image, chunk) partial moments -> merged (Chan) -> mean/rstd
+//   gn_apply   : y = [silu](xhat*gamma+beta)
+//   gn_film    : y = dropout((xhat*gamma+beta)*(1+s)+t)          (one pass)
+//   gn_bwd_*   : fused backward; the FiLM variant also emits d[scale|shift]
+// Memory-bound: every pass moves 16-byte vectors (8 channels per lane); the
+// reductions never re-read the input in a second pass (partials in LDS,
+// tiny cross-chunk merge kernels).
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;        // threads per block for the chunked kernels
+
+struct Plan {
+  int tpr;      // threads per row (C/8)
+  int rpi;      // rows per iteration (NT / tpr)
+  int nchunks;  // chunks per image
+  int rows;     // rows per chunk (multiple of rpi)
+};
+
+Plan make_plan(int N, int P, int C) {
+  Plan p;
+  p.tpr = C / 8;
+  p.rpi = NT / p.tpr;
+  if (p.rpi < 1) p.rpi = 1;
+  int target_blocks = 2048;
+  int nch = (target_blocks + N - 1) / N;
+  int maxch = (P + p.rpi - 1) / p.rpi;
+  if (nch > maxch) nch = maxch;
+  // keep >= 4 rows per thread so the per-thread partials amortise the merge
+  int min_rows = 4 * p.rpi;
+  int maxch2 = (P + min_rows - 1) / min_rows;
+  if (nch > maxch2) nch = maxch2;
+  if (nch < 1) nch = 1;
+  int rows = (P + nch - 1) / nch;
+  rows = (rows + p.rpi - 1) / p.rpi * p.rpi;
+  p.rows = rows;
+  p.nchunks = (P + rows - 1) / rows;
+  return p;
+}
+
+// ---------------------------------------------------------------- stats ----
+__global__ void __launch_bounds__(NT) gn_stats_partial_k(const bf16* __restrict__ x, int P, int C, int G,
+                                                         int rows, int nchunks, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][C][3]
+  const int chunk = blockIdx.x, n = blockIdx.y;
+  const int tpr = C / 8, rpi = NT / tpr;
+  const int tid = threadIdx.x;
+  const int roff = tid / tpr, v = tid % tpr, c0 = v * 8;
+  const bool active = roff < rpi;
+  const int r0 = chunk * rows, r1 = min(P, r0 + rows);
+  float sh[8], s[8], q[8];
+  float cnt = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sh[j] = 0.f; s[j] = 0.f; q[j] = 0.f; }
+  if (active) {
+    const bf16* base = x + ((long)n * P) * C + c0;
+    int r = r0 + roff;
+    if (r < r1) {
+      f32x8 a = ld8(base + (long)r * C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sh[j] = a[j];
+      cnt = 1.f;
+      r += rpi;
+    }
+    for (; r < r1; r += rpi) {
+      f32x8 a = ld8(base + (long)r * C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = a[j] - sh[j];
+        s[j] += d;
+        q[j] += d * d;
+      }
+      cnt += 1.f;
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float* o = lds + ((roff * C) + c0 + j) * 3;
+      float m = cnt > 0.f ? s[j] / cnt : 0.f;
+      o[0] = cnt;
+      o[1] = sh[j] + m;
+      o[2] = fmaxf(q[j] - s[j] * m, 0.f);
+    }
+  }
+  __syncthreads();
+  const int Cg = C / G;
+  for (int g = tid; g < G; g += NT) {
+    Moments acc = {0.f, 0.f, 0.f};
+    for (int rr = 0; rr < rpi; ++rr)
+      for (int cc = 0; cc < Cg; ++cc) {
+        const float* o = lds + ((rr * C) + g * Cg + cc) * 3;
+        Moments b = {o[0], o[1], o[2]};
+        if (b.n > 0.f) acc = merge_moments(acc, b);
+      }
+    float* dst = part + (((long)n * nchunks + chunk) * G + g) * 2;
+    dst[0] = acc.mean;
+    dst[1] = acc.m2;
+  }
+}
+
+__global__ void gn_stats_final_k(const float* __restrict__ part, int N, int P, int G, int Cg, int rows,
+                                 int nchunks, float eps, float* __restrict__ stats) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * G) return;
+  int n = t / G, g = t % G;
+  Moments acc = {0.f, 0.f, 0.f};
+  for (int c = 0; c < nchunks; ++c) {
+    int r0 = c * rows, r1 = min(P, r0 + rows);
+    const float* p = part + (((long)n * nchunks + c) * G + g) * 2;
+    Moments b = {(float)((r1 - r0) * Cg), p[0], p[1]};
+    acc = merge_moments(acc, b);
+  }
+  float var = acc.m2 / acc.n;
+  stats[t * 2 + 0] = acc.mean;
+  stats[t * 2 + 1] = rsqrtf(fmaxf(var, 0.f) + eps);
+}
+
+// ---------------------------------------------------------------- apply ----
+template <bool SILU>
+__global__ void gn_apply_k(const bf16* __restrict__ x, const float* __restrict__ stats,
+                           const float* __restrict__ gamma, const float* __restrict__ beta, bf16* __restrict__ y,
+                           long nvec, int C, int Cg, int G, long PC) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    long e = i * 8;
+    int c0 = (int)(e % C);
+    int n = (int)(e / PC);
+    f32x8 a = ld8(x + e);
+    f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
+    f32x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int g = (c0 + j) / Cg;
+      float mean = stats[(n * G + g) * 2], rstd = stats[(n * G + g) * 2 + 1];
+      float h = (a[j] - mean) * rstd * gm[j] + bt[j];
+      o[j] = SILU ? siluf_(h) : h;
+    }
+    st8(y + e, o);
+  }
+}
+
+__global__ void gn_film_k(const bf16* __restrict__ x, const float* __restrict__ stats,
+                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                          const bf16* __restrict__ ss, bf16* __restrict__ y, long nvec, int C, int Cg, int G,
+                          long PC, float p_drop, uint64_t seed) {
+  const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    long e = i * 8;
+    int c0 = (int)(e % C);
+    long pix = e / C;
+    int n = (int)(e / PC);
+    f32x8 a = ld8(x + e);
+    f32x8 sc = ld8(ss + pix * 2 * C + c0);
+    f32x8 sf = ld8(ss + pix * 2 * C + C + c0);
+    f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
+    f32x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int g = (c0 + j) / Cg;
+      float mean = stats[(n * G + g) * 2], rstd = stats[(n * G + g) * 2 + 1];
+      float h = (a[j] - mean) * rstd * gm[j] + bt[j];
+      float z = h * (1.f + sc[j]) + sf[j];
+      if (p_drop > 0.f) z = (uniform01(seed, (uint64_t)(e + j)) < p_drop) ? 0.f : z * keep_scale;
+      o[j] = z;
+    }
+    st8(y + e, o);
+  }
+}
+
+// ------------------------------------------------------------- backward ----
+// MODE 0: plain GN, 1: GN+SiLU, 2: GN+FiLM(+dropout)
+template <int MODE>
+__device__ __forceinline__ void bwd_elem(float xv, float dyv, float mean, float rstd, float gm, float bt, float sc,
+                                         float& xhat, float& dA, float& dscale, float& dshift, float keepmul) {
+  xhat = (xv - mean) * rstd;
+  float h = xhat * gm + bt;
+  if (MODE == 0) {
+    dA = dyv;
+  } else if (MODE == 1) {
+    dA = dyv * dsiluf_(h);
+  } else {
+    float dz = dyv * keepmul;
+    dscale = dz * h;
+    dshift = dz;
+    dA = dz * (1.f + sc);
+  }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                      const bf16* __restrict__ ss, const float* __restrict__ stats,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      int P, int C, int G, int rows, int nchunks, float p_drop,
+                                                      uint64_t seed, bf16* __restrict__ dss,
+                                                      float* __restrict__ chan_part, float* __restrict__ grp_part) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][C][4]
+  const int chunk = blockIdx.x, n = blockIdx.y;
+  const int tpr = C / 8, rpi = NT / tpr;
+  const int tid = threadIdx.x;
+  const int roff = tid / tpr, v = tid % tpr, c0 = v * 8;
+  const bool active = roff < rpi;
+  const int r0 = chunk * rows, r1 = min(P, r0 + rows);
+  const int Cg = C / G;
+  const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  float dg[8], db[8], gs[8], gs2[8], mean[8], rstd[8];
+  f32x8 gm = {}, bt = {};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { dg[j] = db[j] = gs[j] = gs2[j] = 0.f; }
+  if (active) {
+    gm = ld8f(gamma + c0);
+    bt = ld8f(beta + c0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int g = (c0 + j) / Cg;
+      mean[j] = stats[(n * G + g) * 2];
+      rstd[j] = stats[(n * G + g) * 2 + 1];
+    }
+    for (int r = r0 + roff; r < r1; r += rpi) {
+      long pix = (long)n * P + r;
+      long e = pix * C + c0;
+      f32x8 xv = ld8(x + e), dv = ld8(dy + e);
+      f32x8 sc = {}, o_s, o_t;
+      if (MODE == 2) sc = ld8(ss + pix * 2 * C + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float keepmul = 1.f;
+        if (MODE == 2 && p_drop > 0.f) keepmul = (uniform01(seed, (uint64_t)(e + j)) < p_drop) ? 0.f : keep_scale;
+        float xhat, dA, dsc = 0.f, dsh = 0.f;
+        bwd_elem<MODE>(xv[j], dv[j], mean[j], rstd[j], gm[j], bt[j], sc[j], xhat, dA, dsc, dsh, keepmul);
+        o_s[j] = dsc;
+        o_t[j] = dsh;
+        dg[j] += dA * xhat;
+        db[j] += dA;
+        float dxh = dA * gm[j];
+        gs[j] += dxh;
+        gs2[j] += dxh * xhat;
+      }
+      if (MODE == 2) {
+        st8(dss + pix * 2 * C + c0, o_s);
+        st8(dss + pix * 2 * C + C + c0, o_t);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float* o = lds + ((roff * C) + c0 + j) * 4;
+      o[0] = dg[j];
+      o[1] = db[j];
+      o[2] = gs[j];
+      o[3] = gs2[j];
+    }
+  }
+  __syncthreads();
+  const long prow = (long)n * nchunks + chunk;
+  for (int c = tid; c < C; c += NT) {
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) {
+      const float* o = lds + ((rr * C) + c) * 4;
+      a += o[0];
+      b += o[1];
+    }
+    chan_part[(prow * C + c) * 2 + 0] = a;
+    chan_part[(prow * C + c) * 2 + 1] = b;
+  }
+  for (int g = tid; g < G; g += NT) {
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < rpi; ++rr)
+      for (int cc = 0; cc < Cg; ++cc) {
+        const float* o = lds + ((rr * C) + g * Cg + cc) * 4;
+        a += o[2];
+        b += o[3];
+      }
+    grp_part[(prow * G + g) * 2 + 0] = a;
+    grp_part[(prow * G + g) * 2 + 1] = b;
+  }
+}
+
+__global__ void gn_bwd_final_k(const float* __restrict__ chan_part, const float* __restrict__ grp_part, int N,
+                               int P, int C, int G, int nchunks, float* __restrict__ coef,
+                               float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < N * G) {
+    int n = t / G, g = t % G;
+    float a = 0.f, b = 0.f;
+    for (int c = 0; c < nchunks; ++c) {
+      const float* p = grp_part + (((long)n * nchunks + c) * G + g) * 2;
+      a += p[0];
+      b += p[1];
+    }
+    float inv = 1.f / (float)((long)P * (C / G));
+    coef[t * 2 + 0] = a * inv;
+    coef[t * 2 + 1] = b * inv;
+  }
+  if (t < C) {
+    float a = 0.f, b = 0.f;
+    long R = (long)N * nchunks;
+    for (long r = 0; r < R; ++r) {
+      a += chan_part[(r * C + t) * 2 + 0];
+      b += chan_part[(r * C + t) * 2 + 1];
+    }
+    dgamma[t] = a;
+    dbeta[t] = b;
+  }
+}
+
+template <int MODE>
+__global__ void gn_bwd_apply_k(const bf16* __restrict__ x, const bf16* __restrict__ dy, const bf16* __restrict__ ss,
+                               const float* __restrict__ stats, const float* __restrict__ coef,
+                               const float* __restrict__ gamma, const float* __restrict__ beta,
+                               bf16* __restrict__ dx, long nvec, int C, int Cg, int G, long PC, float p_drop,
+                               uint64_t seed) {
+  const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    long e = i * 8;
+    int c0 = (int)(e % C);
+    long pix = e / C;
+    int n = (int)(e / PC);
+    f32x8 xv = ld8(x + e), dv = ld8(dy + e);
+    f32x8 sc = {};
+    if (MODE == 2) sc = ld8(ss + pix * 2 * C + c0);
+    f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
+    f32x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int g = (c0 + j) / Cg;
+      float mean = stats[(n * G + g) * 2], rstd = stats[(n * G + g) * 2 + 1];
+      float c1 = coef[(n * G + g) * 2], c2 = coef[(n * G + g) * 2 + 1];
+      float keepmul = 1.f;
+      if (MODE == 2 && p_drop > 0.f) keepmul = (uniform01(seed, (uint64_t)(e + j)) < p_drop) ? 0.f : keep_scale;
+      float xhat, dA, dsc, dsh;
+      bwd_elem<MODE>(xv[j], dv[j], mean, rstd, gm[j], bt[j], sc[j], xhat, dA, dsc, dsh, keepmul);
+      float dxh = dA * gm[j];
+      o[j] = rstd * (dxh - c1 - xhat * c2);
+    }
+    st8(dx + e, o);
+  }
+}
+
+inline int ew_grid(long nvec) {
+  long g = (nvec + 255) / 256;
+  if (g > 256L * 16) g = 256L * 16;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+// =============================================================== C ABI ====
+D3D_API int d3d_gn_plan(int N, int P, int C, int* nchunks, int* rows) {
+  Plan p = make_plan(N, P, C);
+  *nchunks = p.nchunks;
+  *rows = p.rows;
+  return 0;
+}
+
+// stats: [N*G*2] fp32 (mean, rstd); part: workspace [N*nchunks*G*2]
+D3D_API int d3d_gn_stats(const void* x, int N, int P, int C, int G, float eps, float* part, float* stats,
+                         hipStream_t st) {
+  Plan p = make_plan(N, P, C);
+  size_t lds = (size_t)p.rpi * C * 3 * sizeof(float);
+  hipLaunchKernelGGL(gn_stats_partial_k, dim3(p.nchunks, N), dim3(NT), lds, st, (const bf16*)x, P, C, G, p.rows,
+                     p.nchunks, part);
+  hipLaunchKernelGGL(gn_stats_final_k, dim3(cdiv((long)N * G, 256)), dim3(256), 0, st, part, N, P, G, C / G,
+                     p.rows, p.nchunks, eps, stats);
+  return (int)hipGetLastError();
+}
+
+D3D_API int d3d_gn_apply(const void* x, const float* stats, const float* gamma, const float* beta, void* y, int N,
+                         int P, int C, int G, int silu, hipStream_t st) {
+  long nvec = (long)N * P * C / 8;
+  if (silu)
+    hipLaunchKernelGGL(gn_apply_k<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, stats, gamma, beta,
+                       (bf16*)y, nvec, C, C / G, G, (long)P * C);
+  else
+    hipLaunchKernelGGL(gn_apply_k<false>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, stats, gamma, beta,
+                       (bf16*)y, nvec, C, C / G, G, (long)P * C);
+  return (int)hipGetLastError();
+}
+
+D3D_API int d3d_gn_film(const void* x, const float* stats, const float* gamma, const float* beta, const void* ss,
+                        void* y, int N, int P, int C, int G, float p_drop, unsigned long long seed, hipStream_t st) {
+  long nvec = (long)N * P * C / 8;
+  hipLaunchKernelGGL(gn_film_k, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, stats, gamma, beta,
+                     (const bf16*)ss, (bf16*)y, nvec, C, C / G, G, (long)P * C, p_drop, (uint64_t)seed);
+  return (int)hipGetLastError();
+}
+
+// mode: 0 plain, 1 silu, 2 film.  Workspaces: chan_part [N*nchunks*C*2],
+// grp_part [N*nchunks*G*2], coef [N*G*2].  Outputs dx (bf16), dgamma/dbeta
+// (fp32 [C]) and, for mode 2, dss (bf16 [N,P,2C]).
+D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, const float* stats,
+                       const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
+                       unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
+                       float* grp_part, float* coef, hipStream_t st) {
+  Plan p = make_plan(N, P, C);
+  size_t lds = (size_t)p.rpi * C * 4 * sizeof(float);
+  dim3 g(p.nchunks, N);
+#define RED(M)                                                                                                    \
+  hipLaunchKernelGGL(gn_bwd_reduce_k<M>, g, dim3(NT), lds, st, (const bf16*)x, (const bf16*)dy, (const bf16*)ss, \
+                     stats, gamma, beta, P, C, G, p.rows, p.nchunks, p_drop, (uint64_t)seed, (bf16*)dss,          \
+                     chan_part, grp_part)
+  if (mode == 0) RED(0);
+  else if (mode == 1) RED(1);
+  else RED(2);
+#undef RED
+  int nt = N * G > C ? N * G : C;
+  hipLaunchKernelGGL(gn_bwd_final_k, dim3(cdiv(nt, 256)), dim3(256), 0, st, chan_part, grp_part, N, P, C, G,
+                     p.nchunks, coef, dgamma, dbeta);
+  long nvec = (long)N * P * C / 8;
+#define APP(M)                                                                                                  \
+  hipLaunchKernelGGL(gn_bwd_apply_k<M>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, (const bf16*)dy, \
+                     (const bf16*)ss, stats, coef, gamma, beta, (bf16*)dx, nvec, C, C / G, G, (long)P * C, p_drop, \
+                     (uint64_t)seed)
+  if (mode == 0) APP(0);
+  else if (mode == 1) APP(1);
+  else APP(2);
+#undef APP
+  return (int)hipGetLastError();
+}

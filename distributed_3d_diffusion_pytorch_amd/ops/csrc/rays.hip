@@ -1,0 +1,89 @@
+// On-device camera-ray conditioning input (reference: xunet.py:311-336).
+//
+// The reference builds rays with visu3d in numpy float64 on the HOST every
+// forward (a device->host->device round trip and sync), NeRF-encodes them,
+// masks them for unconditional examples and adds the learned pos / frame
+// embeddings.  This kernel fuses all of it and writes the bf16 NHWC
+// [2B, H, W, 144] tensor the conditioning convs consume:
+//   ch   0..2   ray origin (= camera position t)
+//   ch   3..47  sin(pos * 2^k), k=0..14, scale-major / xyz-minor
+//   ch  48..92  sin(pos * 2^k + pi/2)
+//   ch  93..95  ray direction R . normalize(K^-1 [u+.5, v+.5, 1])
+//   ch  96..119 sin(dir * 2^k), k=0..7
+//   ch 120..143 sin(dir * 2^k + pi/2)
+// then  * cond_mask[b]  + pos_emb[c][h][w]  + (frame ? other_emb : first_emb)[c].
+// The sin arguments reach 2^14 * |t|: they are formed exactly as the fp32
+// reference does (x*2^k, then +pi/2 in fp32) and use full-precision sinf.
+#include "common.h"
+
+namespace {
+constexpr int D = 144;
+
+__global__ void ray_posenc_k(const float* __restrict__ Rm, const float* __restrict__ tv,
+                             const float* __restrict__ Kinv, const uint8_t* __restrict__ mask,
+                             const float* __restrict__ pos_emb, const float* __restrict__ first_emb,
+                             const float* __restrict__ other_emb, bf16* __restrict__ out, int B, int H, int W) {
+  long total = (long)B * 2 * H * W * D;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c = (int)(i % D);
+    long pix = i / D;
+    int w = (int)(pix % W);
+    long t1 = pix / W;
+    int h = (int)(t1 % H);
+    int nf = (int)(t1 / H);       // n = 2*b + f
+    int b = nf >> 1, f = nf & 1;
+    float val = 0.f;
+    if (mask == nullptr || mask[b]) {
+      const float* R = Rm + (long)nf * 9;
+      const float* T = tv + (long)nf * 3;
+      float src[3];
+      int local;
+      bool is_pos = c < 93;
+      if (is_pos) {
+        src[0] = T[0]; src[1] = T[1]; src[2] = T[2];
+        local = c;
+      } else {
+        const float* Ki = Kinv + (long)b * 9;
+        float px = w + 0.5f, py = h + 0.5f;
+        float d0 = Ki[0] * px + Ki[1] * py + Ki[2];
+        float d1 = Ki[3] * px + Ki[4] * py + Ki[5];
+        float d2 = Ki[6] * px + Ki[7] * py + Ki[8];
+        float inv = rsqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+        d0 *= inv; d1 *= inv; d2 *= inv;
+        src[0] = R[0] * d0 + R[1] * d1 + R[2] * d2;
+        src[1] = R[3] * d0 + R[4] * d1 + R[5] * d2;
+        src[2] = R[6] * d0 + R[7] * d1 + R[8] * d2;
+        local = c - 93;
+      }
+      int nsc = is_pos ? 15 : 8;
+      if (local < 3) {
+        val = src[local];
+      } else {
+        int e = local - 3;
+        bool shifted = e >= nsc * 3;
+        if (shifted) e -= nsc * 3;
+        int k = e / 3, comp = e % 3;
+        float a = src[comp] * (float)(1 << k);
+        if (shifted) a = a + 1.5707963267948966f;
+        val = sinf(a);
+      }
+    }
+    if (pos_emb) val += pos_emb[((long)c * H + h) * W + w];
+    if (first_emb) val += (f ? other_emb[c] : first_emb[c]);
+    out[i] = (bf16)val;
+  }
+}
+}  // namespace
+
+// Rm: [2B,3,3] fp32 rotations, tv: [2B,3], Kinv: [B,3,3], mask: [B] uint8 or
+// null, pos_emb [144,H,W] / first_emb, other_emb [144] fp32 or null.
+D3D_API int d3d_ray_posenc(const float* Rm, const float* tv, const float* Kinv, const unsigned char* mask,
+                           const float* pos_emb, const float* first_emb, const float* other_emb, void* out, int B,
+                           int H, int W, hipStream_t st) {
+  long total = (long)B * 2 * H * W * D;
+  long g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(ray_posenc_k, dim3((int)g), dim3(256), 0, st, Rm, tv, Kinv, mask, pos_emb, first_emb,
+                     other_emb, (bf16*)out, B, H, W);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,493 @@
+"""Autograd bindings of the gfx950 HIP kernels (``libd3d_hip.so``).
+
+Every function takes/returns NHWC bf16 activations on the current HIP stream
+and fp32 master parameters; parameter gradients are produced in fp32.  No
+host synchronisation, no allocation inside the kernels (workspaces come from
+the torch caching allocator), so the whole step can be captured in a HIP
+graph.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from ._backend import load_library
+from . import torch_impl as _t
+
+_lib = load_library(required=True)
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _st() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _chk(rc: int, name: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with hipError {rc}")
+
+
+def _need_bf16(*ts):
+    for t in ts:
+        if t is not None and t.dtype != BF16:
+            raise TypeError(f"HIP kernels take bf16 activations, got {t.dtype}")
+
+
+def _up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+# --------------------------------------------------------------------------
+# weight caches (bf16 packed copies of fp32 master weights).  Invalidated by
+# the optimizer (epoch bump) and by any in-place update of the parameter.
+_EPOCH = [0]
+_WCACHE: Dict[Tuple, Tuple[Tuple, torch.Tensor]] = {}
+
+
+def invalidate_weight_cache() -> None:
+    _EPOCH[0] += 1
+    _WCACHE.clear()
+
+
+def _cached(p: torch.Tensor, kind: str, build):
+    if not isinstance(p, torch.nn.Parameter):
+        return build()      # temporaries (e.g. channel-padded stem/head weights)
+    key = (p.data_ptr(), kind, tuple(p.shape))
+    tok = (p._version, _EPOCH[0])
+    hit = _WCACHE.get(key)
+    if hit is not None and hit[0] == tok:
+        return hit[1]
+    v = build()
+    _WCACHE[key] = (tok, v)
+    return v
+
+
+def packed_conv_weight(w: torch.Tensor, trans: bool) -> torch.Tensor:
+    """OIHW fp32 -> [OCp][9][ICp] bf16 (trans: [ICp][9][OCp]) for the MFMA
+    kernel; row dims padded to 128 (block M), K chunks to 64 (BK)."""
+    OC, IC = w.shape[0], w.shape[1]
+
+    def build():
+        if not trans:
+            OCp, ICp = _up(OC, 128), _up(IC, 64)
+            out = torch.empty(OCp * 9 * ICp, dtype=BF16, device=w.device)
+        else:
+            OCp, ICp = _up(OC, 64), _up(IC, 128)
+            out = torch.empty(ICp * 9 * OCp, dtype=BF16, device=w.device)
+        _chk(_lib.d3d_pack_conv_weight(w.data_ptr(), out.data_ptr(), OC, IC, OCp, ICp, int(trans), _st()),
+             "pack_conv_weight")
+        return out
+    return _cached(w, "convT" if trans else "conv", build)
+
+
+def bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    return _cached(w, "bf16", lambda: w.detach().reshape(w.shape[0], -1).to(BF16))
+
+
+# ------------------------------------------------------------ GroupNorm ----
+def _gn_plan(N, P, C):
+    a, b = ctypes.c_int(), ctypes.c_int()
+    _lib.d3d_gn_plan(N, P, C, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def _gn_stats(x, G, eps):
+    N, H, W, C = x.shape
+    P = H * W
+    nch, _ = _gn_plan(N, P, C)
+    part = torch.empty(N * nch * G * 2, dtype=F32, device=x.device)
+    stats = torch.empty(N * G * 2, dtype=F32, device=x.device)
+    _chk(_lib.d3d_gn_stats(x.data_ptr(), N, P, C, G, eps, part.data_ptr(), stats.data_ptr(), _st()), "gn_stats")
+    return stats
+
+
+def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed):
+    N, H, W, C = x.shape
+    P = H * W
+    nch, _ = _gn_plan(N, P, C)
+    dev = x.device
+    dx = torch.empty_like(x)
+    dss = torch.empty_like(ss) if ss is not None else None
+    dg = torch.empty(C, dtype=F32, device=dev)
+    db = torch.empty(C, dtype=F32, device=dev)
+    cp = torch.empty(N * nch * C * 2, dtype=F32, device=dev)
+    gp = torch.empty(N * nch * G * 2, dtype=F32, device=dev)
+    coef = torch.empty(N * G * 2, dtype=F32, device=dev)
+    _chk(_lib.d3d_gn_bwd(mode, x.data_ptr(), dy.data_ptr(), _ptr(ss), stats.data_ptr(), w.data_ptr(), b.data_ptr(),
+                         N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), dg.data_ptr(), db.data_ptr(),
+                         cp.data_ptr(), gp.data_ptr(), coef.data_ptr(), _st()), "gn_bwd")
+    return dx, dss, dg, db
+
+
+class _GroupNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps, silu):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        stats = _gn_stats(x, groups, eps)
+        y = torch.empty_like(x)
+        _chk(_lib.d3d_gn_apply(x.data_ptr(), stats.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
+                               N, H * W, C, groups, int(silu), _st()), "gn_apply")
+        ctx.save_for_backward(x, weight, bias, stats)
+        ctx.cfg = (groups, 1 if silu else 0)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, stats = ctx.saved_tensors
+        G, mode = ctx.cfg
+        dx, _, dg, db = _gn_bwd(mode, x, dy.contiguous(), None, stats, w, b, G, 0.0, 0)
+        return dx, dg, db, None, None, None
+
+
+def group_norm(x, weight, bias, groups=32, eps=1e-5, silu=False):
+    _need_bf16(x)
+    return _GroupNorm.apply(x, weight, bias, groups, eps, silu)
+
+
+class _GNFiLM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, ss, groups, eps, p, seed):
+        x = x.contiguous()
+        ss = ss.contiguous()
+        N, H, W, C = x.shape
+        stats = _gn_stats(x, groups, eps)
+        y = torch.empty_like(x)
+        _chk(_lib.d3d_gn_film(x.data_ptr(), stats.data_ptr(), weight.data_ptr(), bias.data_ptr(), ss.data_ptr(),
+                              y.data_ptr(), N, H * W, C, groups, float(p), int(seed), _st()), "gn_film")
+        ctx.save_for_backward(x, weight, bias, ss, stats)
+        ctx.cfg = (groups, p, seed)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, ss, stats = ctx.saved_tensors
+        G, p, seed = ctx.cfg
+        dx, dss, dg, db = _gn_bwd(2, x, dy.contiguous(), ss, stats, w, b, G, p, seed)
+        return dx, dg, db, dss, None, None, None, None
+
+
+def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=False, seed=0):
+    _need_bf16(x, ss)
+    p = float(dropout_p) if training else 0.0
+    return _GNFiLM.apply(x, weight, bias, ss, groups, eps, p, int(seed) & 0x7FFFFFFFFFFFFFFF)
+
+
+# ----------------------------------------------------------------- conv ----
+def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale):
+    _chk(_lib.d3d_conv3x3(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
+                          IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), _st()), "conv3x3")
+
+
+def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride):
+    s, pps = ctypes.c_int(), ctypes.c_int()
+    _lib.d3d_conv_wgrad_plan(N, OH, OW, OC, IC, ctypes.byref(s), ctypes.byref(pps))
+    ws = torch.empty(s.value * OC * 9 * IC, dtype=F32, device=x.device)
+    dW = torch.empty(OC, IC, 3, 3, dtype=F32, device=x.device)
+    _chk(_lib.d3d_conv3x3_wgrad(g.data_ptr(), x.data_ptr(), ws.data_ptr(), dW.data_ptr(), N, H, W, IC, OH, OW, OC,
+                                stride, s.value, pps.value, 0, _st()), "conv3x3_wgrad")
+    return dW
+
+
+def _chansum(g, per_image: bool):
+    N, OH, OW, C = g.shape
+    P = OH * OW
+    nch = max(1, min(64, (2048 + N - 1) // N, (P + 63) // 64))
+    part = torch.empty(nch * N * C, dtype=F32, device=g.device)
+    per = torch.empty(N, C, dtype=F32, device=g.device) if per_image else None
+    tot = torch.empty(C, dtype=F32, device=g.device)
+    _chk(_lib.d3d_chansum(g.data_ptr(), part.data_ptr(), _ptr(per), tot.data_ptr(), N, P, C, nch, _st()), "chansum")
+    return per, tot
+
+
+class _Conv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias):
+        x = x.contiguous()
+        N, H, W, IC = x.shape
+        OC = weight.shape[0]
+        assert weight.shape[1] == IC and IC % 8 == 0 and OC % 8 == 0, (tuple(weight.shape), IC, OC)
+        OH = (H - 1) // stride + 1
+        OW = (W - 1) // stride + 1
+        wp = packed_conv_weight(weight, False)
+        out = torch.empty(N, OH, OW, OC, dtype=BF16, device=x.device)
+        res = residual.contiguous() if residual is not None else None
+        rb = row_bias.contiguous().float() if row_bias is not None else None
+        _conv_fwd(x, wp, bias, rb, res, out, N, H, W, IC, _up(IC, 64), OH, OW, OC, OC, stride, False, out_scale)
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (stride, out_scale, residual is not None, row_bias is not None, bias is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        stride, scale, has_res, has_rb, has_b = ctx.cfg
+        N, H, W, IC = x.shape
+        OC = weight.shape[0]
+        dy = dy.contiguous()
+        _, OH, OW, _ = dy.shape
+        if scale != 1.0:
+            g = torch.empty_like(dy)
+            _chk(_lib.d3d_add_scale(dy.data_ptr(), None, g.data_ptr(), float(scale), dy.numel(), _st()), "scale")
+        else:
+            g = dy
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = packed_conv_weight(weight, True)
+            dx = torch.empty_like(x)
+            _conv_fwd(g, wt, None, None, None, dx, N, OH, OW, OC, _up(OC, 64), H, W, IC, IC, stride, True, 1.0)
+        dW = _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride) if ctx.needs_input_grad[1] else None
+        per, tot = _chansum(g, has_rb) if (has_b or has_rb) else (None, None)
+        db = tot if (has_b and ctx.needs_input_grad[2]) else None
+        drb = per if has_rb else None
+        dres = g if has_res else None
+        return dx, dW, db, None, dres, None, drb
+
+
+def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=None):
+    _need_bf16(x, residual)
+    OC, IC = weight.shape[0], weight.shape[1]
+    if IC % 8 == 0 and OC % 8 == 0:
+        return _Conv3x3.apply(x, weight, bias, stride, residual, out_scale, row_bias)
+    # stem (IC=3) / head (OC=3): zero-pad channels to a multiple of 8 so every
+    # access stays 16-byte vectorised; the padding costs < 0.1 % of FLOPs.
+    ICe, OCe = _up(IC, 8), _up(OC, 8)
+    xe = F.pad(x, (0, ICe - IC)) if ICe != IC else x
+    we = F.pad(weight, (0, 0, 0, 0, 0, ICe - IC, 0, OCe - OC))
+    be = F.pad(bias, (0, OCe - OC)) if bias is not None else None
+    re = F.pad(residual, (0, OCe - OC)) if residual is not None else None
+    rbe = F.pad(row_bias, (0, OCe - OC)) if row_bias is not None else None
+    y = _Conv3x3.apply(xe, we, be, stride, re, out_scale, rbe)
+    return y[..., :OC].contiguous() if OCe != OC else y
+
+
+# --------------------------------------------------------------- linear ----
+def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    try:
+        return torch.mm(a, b, out_dtype=F32)
+    except (RuntimeError, TypeError):
+        return torch.mm(a, b).float()
+
+
+class _Linear(torch.autograd.Function):
+    """Per-pixel dense layer on hipBLASLt (plain library GEMM) with the
+    residual/scale epilogue done by a fused HIP elementwise kernel."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, out_scale):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        wb = bf16_weight(weight)
+        if bias is not None:
+            y = torch.addmm(bias.to(BF16), x2, wb.t())
+        else:
+            y = torch.mm(x2, wb.t())
+        if residual is not None or out_scale != 1.0:
+            r = residual.reshape(y.shape).contiguous() if residual is not None else None
+            _chk(_lib.d3d_add_scale(y.data_ptr(), _ptr(r), y.data_ptr(), float(out_scale), y.numel(), _st()),
+                 "add_scale")
+        ctx.save_for_backward(x2, weight)
+        ctx.cfg = (shp, out_scale, residual is not None, bias is not None)
+        return y.reshape(*shp[:-1], wb.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        shp, scale, has_res, has_b = ctx.cfg
+        g = dy.reshape(-1, dy.shape[-1])
+        if scale != 1.0:
+            gs = torch.empty_like(g)
+            _chk(_lib.d3d_add_scale(g.contiguous().data_ptr(), None, gs.data_ptr(), float(scale), g.numel(), _st()),
+                 "scale")
+            g = gs
+        wb = bf16_weight(weight)
+        dx = torch.mm(g, wb).reshape(shp) if ctx.needs_input_grad[0] else None
+        dW = _mm_f32(g.t(), x2).reshape(weight.shape) if ctx.needs_input_grad[1] else None
+        db = g.float().sum(0) if has_b and ctx.needs_input_grad[2] else None
+        dres = g.reshape(*shp[:-1], g.shape[-1]) if has_res else None
+        return dx, dW, db, dres, None
+
+
+def linear(x, weight, bias, residual=None, out_scale=1.0):
+    _need_bf16(x, residual)
+    return _Linear.apply(x, weight, bias, residual, out_scale)
+
+
+# ------------------------------------------------------------ attention ----
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, heads, cross):
+        qkv = qkv.contiguous()
+        N, L, C3 = qkv.shape
+        C = C3 // 3
+        out = torch.empty(N, L, C, dtype=BF16, device=qkv.device)
+        lse = torch.empty(N, heads, L, dtype=F32, device=qkv.device)
+        scale = 1.0 / math.sqrt(C // heads)
+        _chk(_lib.d3d_attn_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr(), N, L, C, heads, int(cross), scale,
+                               _st()), "attn_fwd")
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.cfg = (heads, cross, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        heads, cross, scale = ctx.cfg
+        N, L, C3 = qkv.shape
+        C = C3 // 3
+        dout = dout.contiguous()
+        Dv = torch.empty(N, heads, L, dtype=F32, device=qkv.device)
+        dq = torch.zeros(N, L, C, dtype=F32, device=qkv.device)
+        dqkv = torch.empty_like(qkv)
+        _chk(_lib.d3d_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), Dv.data_ptr(),
+                               dq.data_ptr(), dqkv.data_ptr(), N, L, C, heads, int(cross), scale, _st()), "attn_bwd")
+        return dqkv, None, None
+
+
+def attention(qkv, heads, cross):
+    _need_bf16(qkv)
+    N, L, C3 = qkv.shape
+    D = C3 // 3 // heads
+    if L % 64 != 0 or D not in (64, 128) or (cross and N % 2):
+        return _t.attention(qkv, heads, cross)  # tiny test shapes only
+    return _Attention.apply(qkv, heads, cross)
+
+
+# -------------------------------------------------------- elementwise ----
+class _SiLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        _chk(_lib.d3d_silu(x.data_ptr(), y.data_ptr(), x.numel(), _st()), "silu")
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        _chk(_lib.d3d_dsilu(x.data_ptr(), dy.contiguous().data_ptr(), dx.data_ptr(), x.numel(), _st()), "dsilu")
+        return dx
+
+
+def silu(x):
+    _need_bf16(x)
+    return _SiLU.apply(x)
+
+
+class _AvgPool2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        y = torch.empty(N, H // 2, W // 2, C, dtype=x.dtype, device=x.device)
+        _chk(_lib.d3d_avgpool2(x.data_ptr(), y.data_ptr(), N, H, W, C, 0, _st()), "avgpool2")
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C = ctx.shape
+        dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+        _chk(_lib.d3d_avgpool2(dy.contiguous().data_ptr(), dx.data_ptr(), N, H, W, C, 1, _st()), "avgpool2_bwd")
+        return dx
+
+
+class _Upsample2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        y = torch.empty(N, 2 * H, 2 * W, C, dtype=x.dtype, device=x.device)
+        _chk(_lib.d3d_upsample2(x.data_ptr(), y.data_ptr(), N, H, W, C, 0, _st()), "upsample2")
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C = ctx.shape
+        dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+        _chk(_lib.d3d_upsample2(dy.contiguous().data_ptr(), dx.data_ptr(), N, H, W, C, 1, _st()), "upsample2_bwd")
+        return dx
+
+
+def avgpool2(x):
+    _need_bf16(x)
+    return _AvgPool2.apply(x)
+
+
+def upsample2(x):
+    _need_bf16(x)
+    return _Upsample2.apply(x)
+
+
+# ------------------------------------------------------------- rays ------
+class _RayPosenc(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pos_emb, first_emb, other_emb, R, t, K, H, W, cond_mask, rescale_from):
+        B = R.shape[0]
+        Kd = K.to(torch.float64)
+        if rescale_from:
+            s = torch.tensor([W / rescale_from, H / rescale_from, 1.0], dtype=torch.float64, device=K.device)
+            Kd = Kd * s[None, :, None]
+        Kinv = torch.linalg.inv(Kd).float().contiguous()
+        Rf = R.float().reshape(B * 2, 9).contiguous()
+        tf = t.float().reshape(B * 2, 3).contiguous()
+        mask = cond_mask.to(torch.uint8).contiguous()
+        out = torch.empty(B * 2, H, W, 144, dtype=BF16, device=R.device)
+        pe = pos_emb.contiguous() if pos_emb is not None else None
+        fe = first_emb.reshape(-1).contiguous() if first_emb is not None else None
+        oe = other_emb.reshape(-1).contiguous() if other_emb is not None else None
+        _chk(_lib.d3d_ray_posenc(Rf.data_ptr(), tf.data_ptr(), Kinv.data_ptr(), mask.data_ptr(), _ptr(pe), _ptr(fe),
+                                 _ptr(oe), out.data_ptr(), B, H, W, _st()), "ray_posenc")
+        ctx.has = (pos_emb is not None, first_emb is not None)
+        ctx.B = B
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        has_pe, has_fe = ctx.has
+        B = ctx.B
+        N, H, W, D = g.shape
+        gf = g.float()
+        dpe = gf.sum(0).permute(2, 0, 1).contiguous() if has_pe else None
+        dfe = doe = None
+        if has_fe:
+            fsum = gf.reshape(B, 2, H * W, D).sum((0, 2))
+            dfe = fsum[0].reshape(1, 1, D, 1, 1)
+            doe = fsum[1].reshape(1, 1, D, 1, 1)
+        return dpe, dfe, doe, None, None, None, None, None, None, None
+
+
+def ray_posenc(R, t, K, H, W, cond_mask, pos_emb, first_emb, other_emb, rescale_from=0, out_dtype=BF16):
+    if out_dtype != BF16:
+        return _t.ray_posenc(R, t, K, H, W, cond_mask, pos_emb, first_emb, other_emb, rescale_from).to(out_dtype)
+    return _RayPosenc.apply(pos_emb, first_emb, other_emb, R, t, K, H, W, cond_mask, rescale_from)
+
+
+# ------------------------------------------------------------ optimizer --
+def adam_flat(p, g, m, v, ema, lr, b1, b2, eps, wd, step_size, bc2_sqrt, grad_scale, ema_decay):
+    _chk(_lib.d3d_adam(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(ema), p.numel(), b1, b2, eps, wd,
+                       step_size, bc2_sqrt, grad_scale, ema_decay, _st()), "adam")
+    invalidate_weight_cache()
+
+
+# ------------------------------------------------------------- sampler ---
+def sampler_step(z, eps_c, eps_u, w, alpha, sigma, alpha_n, c, var_sqrt, add_noise, seed):
+    b = z.shape[0]
+    D = z[0].numel()
+    out = torch.empty_like(z)
+    _chk(_lib.d3d_sampler_step(z.data_ptr(), eps_c.contiguous().data_ptr(), eps_u.contiguous().data_ptr(),
+                               w.float().contiguous().data_ptr(), out.data_ptr(), b, D, alpha, sigma, alpha_n, c,
+                               var_sqrt, int(add_noise), int(seed), _st()), "sampler_step")
+    return out

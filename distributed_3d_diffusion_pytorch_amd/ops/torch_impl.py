@@ -1,0 +1,194 @@
+"""Pure-PyTorch implementations of the NHWC op set.
+
+These are the numerics oracle for the HIP kernels (fp32 composition of the
+same op) and the CPU execution path.  Layout convention everywhere in the
+framework: activations are ``[N, H, W, C]`` with ``N = 2*B`` and the two views
+of an example adjacent (``n = 2*b + frame``), i.e. the reference's
+``[B, F=2, C, H, W]`` (`xunet.py:61-71`) folded frame-into-batch, channels-last.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+INV_SQRT2 = 1.0 / math.sqrt(2.0)
+
+
+def _cast(t: Optional[torch.Tensor], dtype: torch.dtype) -> Optional[torch.Tensor]:
+    if t is None:
+        return None
+    return t if t.dtype == dtype else t.to(dtype)
+
+
+def group_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, groups: int = 32,
+               eps: float = 1e-5, silu: bool = False) -> torch.Tensor:
+    """GroupNorm over each (example, frame) image; optional fused SiLU.
+    Matches ``nn.GroupNorm(32, C)`` on the frame-folded batch (`xunet.py:61-71`)."""
+    N, H, W, C = x.shape
+    xf = x.float().reshape(N, H * W, groups, C // groups)
+    mean = xf.mean(dim=(1, 3), keepdim=True)
+    var = xf.var(dim=(1, 3), unbiased=False, keepdim=True)
+    y = (xf - mean) * torch.rsqrt(var + eps)
+    y = y.reshape(N, H, W, C) * weight.float() + bias.float()
+    if silu:
+        y = F.silu(y)
+    return y.to(x.dtype)
+
+
+def dropout_mask(shape, p: float, seed: int, device) -> torch.Tensor:
+    g = torch.Generator(device="cpu")
+    g.manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
+    keep = (torch.rand(shape, generator=g) >= p).to(device)
+    return keep
+
+
+def gn_film(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, ss: torch.Tensor,
+            groups: int = 32, eps: float = 1e-5, dropout_p: float = 0.0,
+            training: bool = False, seed: int = 0) -> torch.Tensor:
+    """dropout(GN(x) * (1 + scale) + shift); ``ss = [scale | shift]`` on the
+    channel axis (FiLM, `xunet.py:74-87`; ResBlock ordering `xunet.py:140-146`)."""
+    C = x.shape[-1]
+    h = group_norm(x, weight, bias, groups, eps).float()
+    ssf = ss.float()
+    y = h * (1.0 + ssf[..., :C]) + ssf[..., C:]
+    if training and dropout_p > 0.0:
+        y = F.dropout(y, dropout_p, training=True)
+    return y.to(x.dtype)
+
+
+def conv3x3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int = 1,
+            residual: Optional[torch.Tensor] = None, out_scale: float = 1.0,
+            row_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """3x3 conv, padding 1, on NHWC.  Epilogue: + row_bias[n] (per image),
+    + residual, * out_scale."""
+    dt = x.dtype
+    y = F.conv2d(x.permute(0, 3, 1, 2), _cast(weight, dt), _cast(bias, dt), stride=stride, padding=1)
+    y = y.permute(0, 2, 3, 1)
+    if row_bias is not None:
+        y = y + row_bias.to(dt)[:, None, None, :]
+    if residual is not None:
+        y = y + residual
+    if out_scale != 1.0:
+        y = y * out_scale
+    return y.contiguous()
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+           residual: Optional[torch.Tensor] = None, out_scale: float = 1.0) -> torch.Tensor:
+    """Per-pixel dense layer (1x1 conv / nn.Linear) with fused residual epilogue."""
+    dt = x.dtype
+    w = weight.reshape(weight.shape[0], -1)
+    y = F.linear(x, _cast(w, dt), _cast(bias, dt))
+    if residual is not None:
+        y = y + residual
+    if out_scale != 1.0:
+        y = y * out_scale
+    return y
+
+
+def attention(qkv: torch.Tensor, heads: int, cross: bool) -> torch.Tensor:
+    """Multi-head attention within an example: queries of frame f attend to
+    keys/values of frame f (self) or frame 1-f (cross) (`xunet.py:202-211`).
+    ``qkv``: [N, L, 3C] (packed in_proj output).  Returns [N, L, C]."""
+    N, L, C3 = qkv.shape
+    C = C3 // 3
+    d = C // heads
+    q, k, v = qkv.split(C, dim=-1)
+    if cross:
+        perm = torch.arange(N, device=qkv.device) ^ 1
+        k = k[perm]
+        v = v[perm]
+    q = q.reshape(N, L, heads, d).transpose(1, 2)
+    k = k.reshape(N, L, heads, d).transpose(1, 2)
+    v = v.reshape(N, L, heads, d).transpose(1, 2)
+    s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * (1.0 / math.sqrt(d))
+    p = torch.softmax(s, dim=-1)
+    o = torch.matmul(p, v.float()).to(qkv.dtype)
+    return o.transpose(1, 2).reshape(N, L, C)
+
+
+def avgpool2(x: torch.Tensor) -> torch.Tensor:
+    N, H, W, C = x.shape
+    return x.reshape(N, H // 2, 2, W // 2, 2, C).float().mean(dim=(2, 4)).to(x.dtype)
+
+
+def upsample2(x: torch.Tensor) -> torch.Tensor:
+    N, H, W, C = x.shape
+    return x[:, :, None, :, None, :].expand(N, H, 2, W, 2, C).reshape(N, 2 * H, 2 * W, C)
+
+
+def silu(x: torch.Tensor) -> torch.Tensor:
+    return F.silu(x)
+
+
+def camera_rays(R: torch.Tensor, t: torch.Tensor, K: torch.Tensor, H: int, W: int,
+                rescale_from: int = 0):
+    """Per-pixel world rays of a pinhole camera (OpenCV convention, pixel
+    centres at +0.5), following visu3d's ``Camera.rays()`` as used in
+    `xunet.py:311-314`: ``pos = t``, ``dir = R @ normalize(K^-1 [u+.5, v+.5, 1])``.
+
+    R: [B,F,3,3] cam-to-world rotation, t: [B,F,3], K: [B,3,3].
+    Returns pos, dir: [B,F,H,W,3] in fp32 (computed in fp64).
+    """
+    dt = torch.float64
+    Rd, td, Kd = R.to(dt), t.to(dt), K.to(dt)
+    if rescale_from:
+        s = torch.tensor([W / rescale_from, H / rescale_from, 1.0], dtype=dt, device=K.device)
+        Kd = Kd * s[None, :, None]
+    dev = R.device
+    u = torch.arange(W, dtype=dt, device=dev) + 0.5
+    v = torch.arange(H, dtype=dt, device=dev) + 0.5
+    vv, uu = torch.meshgrid(v, u, indexing="ij")
+    pix = torch.stack([uu, vv, torch.ones_like(uu)], dim=-1)          # [H,W,3]
+    Kinv = torch.linalg.inv(Kd)                                        # [B,3,3]
+    d_cam = torch.einsum("bij,hwj->bhwi", Kinv, pix)                   # [B,H,W,3]
+    d_cam = d_cam / d_cam.norm(dim=-1, keepdim=True)
+    d_world = torch.einsum("bfij,bhwj->bfhwi", Rd, d_cam)              # [B,F,H,W,3]
+    B, Fr = R.shape[:2]
+    pos = td[:, :, None, None, :].expand(B, Fr, H, W, 3)
+    return pos.float(), d_world.float()
+
+
+def posenc_nerf(x: torch.Tensor, min_deg: int, max_deg: int) -> torch.Tensor:
+    """[x, sin(x*2^k), sin(x*2^k + pi/2)] with scale-major / xyz-minor packing
+    (`xunet.py:49-59`)."""
+    if min_deg == max_deg:
+        return x
+    scales = torch.tensor([2.0 ** i for i in range(min_deg, max_deg)], dtype=x.dtype, device=x.device)
+    xb = (x[..., None, :] * scales[:, None]).flatten(-2)
+    emb = torch.sin(torch.cat([xb, xb + math.pi / 2.0], dim=-1))
+    return torch.cat([x, emb], dim=-1)
+
+
+def posenc_ddpm(t: torch.Tensor, emb_ch: int, max_time: float = 1.0) -> torch.Tensor:
+    """DDPM sinusoidal embedding of (clipped) logSNR, t*1000/max_time
+    (`xunet.py:32-46`)."""
+    t = t.float() * (1000.0 / max_time)
+    half = emb_ch // 2
+    k = torch.arange(half, dtype=torch.float32, device=t.device)
+    freqs = torch.exp(k * (-math.log(10000.0) / (half - 1)))
+    arg = t[..., None] * freqs
+    return torch.cat([torch.sin(arg), torch.cos(arg)], dim=-1)
+
+
+def ray_posenc(R: torch.Tensor, t: torch.Tensor, K: torch.Tensor, H: int, W: int,
+               cond_mask: torch.Tensor, pos_emb: Optional[torch.Tensor],
+               first_emb: Optional[torch.Tensor], other_emb: Optional[torch.Tensor],
+               rescale_from: int = 0) -> torch.Tensor:
+    """144-channel camera conditioning input, NHWC frame-interleaved
+    [2B, H, W, 144] in fp32 (`xunet.py:311-336`): rays -> NeRF posenc (origins
+    deg 0..15, directions deg 0..8) -> zeroed for unconditional examples ->
+    + learned pos_emb[144,H,W] -> + per-frame embedding."""
+    pos, dirs = camera_rays(R, t, K, H, W, rescale_from)
+    emb = torch.cat([posenc_nerf(pos, 0, 15), posenc_nerf(dirs, 0, 8)], dim=-1)  # [B,2,H,W,144]
+    emb = torch.where(cond_mask.view(-1, 1, 1, 1, 1), emb, torch.zeros_like(emb))
+    if pos_emb is not None:
+        emb = emb + pos_emb.permute(1, 2, 0)[None, None]
+    if first_emb is not None:
+        fe = torch.cat([first_emb, other_emb], dim=1).reshape(1, 2, 1, 1, -1)
+        emb = emb + fe
+    B = emb.shape[0]
+    return emb.reshape(B * 2, H, W, emb.shape[-1])

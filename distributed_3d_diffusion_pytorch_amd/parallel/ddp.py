@@ -1,0 +1,155 @@
+"""Data-parallel gradient engine: bucketed RCCL all-reduce overlapped with
+backward.
+
+Reference behaviour: ``DDP(model)`` is constructed (`train.py:230-233`) but the
+loss is computed through the raw module (`train.py:275`), so the gradient
+all-reduce never fires and replicas diverge (D2); comm is ``gloo`` through host
+memory, and every step ends in a barrier (D8).
+
+Design here (MI355X, 8 GPUs on xGMI, 7 point-to-point links per GPU):
+
+* gradients are views of one flat fp32 buffer laid out in backward order
+  (:class:`.flat.FlatParams`), so a bucket is a contiguous slice that RCCL
+  reduces in place -- no flatten copies;
+* buckets default to 64 MiB with a small first bucket: big enough that RCCL's
+  rings over the 7 links each carry >=0.5 MiB chunks, few enough (≈9 over the
+  521 MiB model) that per-collective latency is negligible, and the small first
+  bucket starts communication early in backward;
+* each bucket is launched from a post-accumulate-grad hook the moment its last
+  gradient lands, on RCCL's own stream (``async_op``), so reduction overlaps the
+  rest of backward; ``finish()`` makes the compute stream wait on the handles;
+* averaging is folded into the optimizer (``grad_scale = 1/world``) -- no
+  separate divide pass; optional bf16 payload halves link traffic.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .flat import FlatParams
+
+
+class GradReducer:
+    def __init__(self, flat: FlatParams, bucket_mb: float = 64.0, first_bucket_mb: float = 4.0,
+                 grad_dtype: str = "fp32", group=None):
+        self.flat = flat
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.grad_dtype = torch.bfloat16 if grad_dtype == "bf16" else torch.float32
+        self.enabled = True
+        # buckets over the backward-ordered layout
+        self.buckets: List[dict] = []
+        cur: Optional[dict] = None
+        limit = first_bucket_mb * 2 ** 20
+        for i in flat.order:
+            s, e = flat.span(i)
+            if cur is None:
+                cur = {"start": s, "end": e, "params": [i]}
+            else:
+                cur["end"] = e
+                cur["params"].append(i)
+            if (cur["end"] - cur["start"]) * 4 >= limit:
+                self.buckets.append(cur)
+                cur = None
+                limit = bucket_mb * 2 ** 20
+        if cur is not None:
+            self.buckets.append(cur)
+        self.param_bucket = {}
+        for b, bk in enumerate(self.buckets):
+            for i in bk["params"]:
+                self.param_bucket[i] = b
+        self._pending = [0] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
+        self._works: List = []
+        self._tmp = {}
+        self._hooks = []
+        for i, p in enumerate(flat.params):
+            if p.requires_grad:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self.reset()
+
+    # ------------------------------------------------------------------
+    def reset(self) -> None:
+        for b, bk in enumerate(self.buckets):
+            self._pending[b] = sum(1 for i in bk["params"] if self.flat.params[i].requires_grad)
+            self._launched[b] = False
+        self._works = []
+
+    def _make_hook(self, i: int):
+        def hook(_p):
+            if not self.enabled or self.world == 1:
+                return
+            b = self.param_bucket[i]
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._launch(b)
+        return hook
+
+    def _launch(self, b: int) -> None:
+        if self._launched[b]:
+            return
+        self._launched[b] = True
+        bk = self.buckets[b]
+        view = self.flat.grad[bk["start"]: bk["end"]]
+        if self.grad_dtype == torch.float32:
+            self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+        else:
+            tmp = view.to(self.grad_dtype)
+            self._works.append((dist.all_reduce(tmp, group=self.group, async_op=True), tmp, view))
+
+    def finish(self) -> None:
+        """Launch any bucket whose gradients never arrived (unused params) and
+        make the current stream wait for every reduction."""
+        if self.world == 1 or not self.enabled:
+            self.reset()
+            return
+        for b in range(len(self.buckets)):
+            if not self._launched[b]:
+                self._launch(b)
+        for w, tmp, view in self._works:
+            w.wait()
+            if tmp is not None:
+                view.copy_(tmp)
+        self.reset()
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation: skip communication inside the block."""
+        prev = self.enabled
+        self.enabled = False
+        try:
+            yield
+        finally:
+            self.enabled = prev
+
+    def broadcast_params(self, src: int = 0) -> None:
+        if self.world > 1:
+            dist.broadcast(self.flat.data, src, group=self.group)
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def param_checksum(flat: FlatParams) -> torch.Tensor:
+    """Order-sensitive fp64 fingerprint of the flat parameters."""
+    d = flat.data.double()
+    w = torch.linspace(1.0, 2.0, d.numel(), dtype=torch.float64, device=d.device)
+    return torch.stack([d.sum(), (d * w).sum(), d.abs().max()])
+
+
+def check_replicas_in_sync(flat: FlatParams, group=None, rtol: float = 0.0) -> bool:
+    """Divergence detector (catches D2-class bugs): compares every rank's
+    fingerprint against rank 0's.  Returns True when all ranks agree."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return True
+    c = param_checksum(flat)
+    hi, lo = c.clone(), c.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    tol = rtol * hi.abs().clamp_min(1e-30)
+    return bool(((hi - lo).abs() <= tol).all().item())

@@ -1,0 +1,273 @@
+"""Numerics of every HIP kernel against the fp32 PyTorch composition of the
+same op (ops.torch_impl) on identical bf16-rounded inputs.  GPU only."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from distributed_3d_diffusion_pytorch_amd.ops import torch_impl as T  # noqa: E402
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+@pytest.fixture(scope="module")
+def H():
+    from distributed_3d_diffusion_pytorch_amd.ops import hip_impl
+    return hip_impl
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def leaf(t, dtype=None):
+    t = t.detach().clone()
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.requires_grad_(True)
+
+
+def run_both(fn_hip, fn_ref, inputs, grad_out):
+    """Run fwd+bwd of HIP op (bf16 inputs) and reference (fp32 copies)."""
+    xh = [leaf(x) for x in inputs]
+    xr = [leaf(x, torch.float32) if x.dtype == BF else leaf(x) for x in inputs]
+    yh = fn_hip(*xh)
+    yr = fn_ref(*xr)
+    yh.backward(grad_out.to(yh.dtype))
+    yr.backward(grad_out.float())
+    return yh, yr, [a.grad for a in xh], [b.grad for b in xr]
+
+
+@pytest.mark.parametrize("N,Hh,W,C,silu", [(4, 16, 16, 128, True), (2, 8, 8, 256, False), (3, 8, 8, 384, True),
+                                           (2, 4, 4, 1024, False), (2, 32, 32, 768, True)])
+def test_group_norm(H, N, Hh, W, C, silu):
+    torch.manual_seed(0)
+    x = (torch.randn(N, Hh, W, C, device=DEV) * 2 + 0.5).to(BF)
+    w = torch.randn(C, device=DEV) * 0.5 + 1
+    b = torch.randn(C, device=DEV) * 0.1
+    go = torch.randn(N, Hh, W, C, device=DEV)
+    yh, yr, gh, gr = run_both(lambda x, w, b: H.group_norm(x, w, b, 32, 1e-5, silu),
+                              lambda x, w, b: T.group_norm(x, w, b, 32, 1e-5, silu), [x, w, b], go)
+    assert rel(yh, yr) < 2e-2
+    assert rel(gh[0], gr[0]) < 3e-2
+    assert rel(gh[1], gr[1]) < 1e-2
+    assert rel(gh[2], gr[2]) < 1e-2
+
+
+@pytest.mark.parametrize("N,Hh,W,C", [(4, 16, 16, 128), (2, 8, 8, 512)])
+def test_gn_film(H, N, Hh, W, C):
+    torch.manual_seed(1)
+    x = torch.randn(N, Hh, W, C, device=DEV).to(BF)
+    w = torch.randn(C, device=DEV) * 0.5 + 1
+    b = torch.randn(C, device=DEV) * 0.1
+    ss = (torch.randn(N, Hh, W, 2 * C, device=DEV) * 0.5).to(BF)
+    go = torch.randn(N, Hh, W, C, device=DEV)
+    yh, yr, gh, gr = run_both(lambda x, w, b, ss: H.gn_film(x, w, b, ss, 32, 1e-5, 0.0, False, 0),
+                              lambda x, w, b, ss: T.gn_film(x, w, b, ss, 32, 1e-5, 0.0, False, 0), [x, w, b, ss], go)
+    assert rel(yh, yr) < 2e-2
+    for a, c in zip(gh, gr):
+        assert rel(a, c) < 3e-2
+
+
+def test_gn_film_dropout(H):
+    torch.manual_seed(2)
+    N, Hh, W, C, p = 2, 16, 16, 128, 0.1
+    x = torch.randn(N, Hh, W, C, device=DEV).to(BF)
+    w = torch.ones(C, device=DEV)
+    b = torch.zeros(C, device=DEV)
+    ss = torch.zeros(N, Hh, W, 2 * C, device=DEV).to(BF)
+    xh = leaf(x)
+    ssh = leaf(ss)
+    y = H.gn_film(xh, w, b, ssh, 32, 1e-5, p, True, 1234)
+    y0 = H.gn_film(x, w, b, ss, 32, 1e-5, 0.0, False, 0)
+    dropped = (y == 0) & (y0 != 0)
+    frac = dropped.float().mean().item()
+    assert abs(frac - p) < 0.01
+    kept = ~dropped
+    assert rel(y[kept], (y0 * (1 / (1 - p)))[kept]) < 1e-2
+    # same seed -> same mask; backward uses the regenerated mask
+    y2 = H.gn_film(x, w, b, ss, 32, 1e-5, p, True, 1234)
+    assert torch.equal(y, y2)
+    y.backward(torch.ones_like(y))
+    # d shift = dz = keep/(1-p)
+    dshift = ssh.grad[..., C:]
+    assert torch.equal(dshift == 0, dropped)
+
+
+CONV_SHAPES = [
+    # N, H, W, Cin, Cout, stride, residual, row_bias, scale
+    (4, 16, 16, 128, 128, 1, True, False, 1 / math.sqrt(2)),
+    (2, 8, 8, 256, 512, 1, False, False, 1.0),
+    (2, 8, 8, 512, 256, 1, True, False, 1 / math.sqrt(2)),
+    (2, 16, 16, 144, 256, 1, False, True, 1.0),
+    (2, 16, 16, 144, 256, 2, False, True, 1.0),
+    (2, 16, 16, 144, 128, 4, False, True, 1.0),
+    (2, 16, 16, 144, 128, 8, False, True, 1.0),
+    (2, 12, 20, 384, 128, 1, False, False, 1.0),
+    (2, 16, 16, 3, 128, 1, False, False, 1.0),     # stem
+    (2, 16, 16, 128, 3, 1, False, False, 1.0),     # head
+]
+
+
+@pytest.mark.parametrize("N,Hh,W,Ci,Co,s,res,rb,scale", CONV_SHAPES)
+def test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale):
+    torch.manual_seed(3)
+    x = torch.randn(N, Hh, W, Ci, device=DEV).to(BF)
+    w = torch.randn(Co, Ci, 3, 3, device=DEV) / math.sqrt(9 * Ci)
+    b = torch.randn(Co, device=DEV) * 0.1
+    OH, OW = (Hh - 1) // s + 1, (W - 1) // s + 1
+    r = torch.randn(N, OH, OW, Co, device=DEV).to(BF) if res else None
+    rbias = torch.randn(N, Co, device=DEV) if rb else None
+    go = torch.randn(N, OH, OW, Co, device=DEV)
+    ins = [x, w, b] + ([r] if res else []) + ([rbias] if rb else [])
+
+    def mk(fn):
+        def f(*a):
+            x, w, b = a[:3]
+            k = 3
+            rr = a[k] if res else None
+            k += int(res)
+            rbb = a[k] if rb else None
+            return fn(x, w, b, s, rr, scale, rbb)
+        return f
+
+    yh, yr, gh, gr = run_both(mk(H.conv3x3), mk(T.conv3x3), ins, go)
+    assert yh.shape == yr.shape
+    assert rel(yh, yr) < 2e-2
+    names = ["dx", "dw", "db", "dres", "drow"]
+    for i, (a, c) in enumerate(zip(gh, gr)):
+        assert a is not None and c is not None
+        assert rel(a, c) < 3e-2, (names[i], rel(a, c))
+
+
+def test_linear(H):
+    torch.manual_seed(4)
+    x = torch.randn(2, 64, 256, device=DEV).to(BF)
+    w = torch.randn(768, 256, device=DEV) / 16
+    b = torch.randn(768, device=DEV) * 0.1
+    r = torch.randn(2, 64, 768, device=DEV).to(BF)
+    go = torch.randn(2, 64, 768, device=DEV)
+    yh, yr, gh, gr = run_both(lambda x, w, b, r: H.linear(x, w, b, r, 0.7),
+                              lambda x, w, b, r: T.linear(x, w, b, r, 0.7), [x, w, b, r], go)
+    assert rel(yh, yr) < 2e-2
+    for a, c in zip(gh, gr):
+        assert rel(a, c) < 3e-2
+
+
+@pytest.mark.parametrize("N,L,C,cross", [(4, 256, 256, False), (4, 256, 256, True), (4, 64, 512, False),
+                                         (4, 64, 512, True), (2, 1024, 256, True)])
+def test_attention(H, N, L, C, cross):
+    torch.manual_seed(5)
+    qkv = torch.randn(N, L, 3 * C, device=DEV).to(BF)
+    go = torch.randn(N, L, C, device=DEV)
+    yh, yr, gh, gr = run_both(lambda q: H.attention(q, 4, cross), lambda q: T.attention(q, 4, cross), [qkv], go)
+    assert rel(yh, yr) < 2e-2
+    assert rel(gh[0], gr[0]) < 4e-2
+
+
+def test_attention_spiky(H):
+    """A key that dominates one query's softmax in a late key block forces the
+    online-softmax rescale branch."""
+    torch.manual_seed(6)
+    N, L, C = 2, 256, 256
+    qkv = torch.randn(N, L, 3 * C, device=DEV) * 0.3
+    qkv[:, 7, :C] = 2.0           # query 7
+    qkv[:, 200, C:2 * C] = 2.0    # key 200 (block 3)
+    qkv = qkv.to(BF)
+    yh = H.attention(qkv, 4, False)
+    yr = T.attention(qkv.float(), 4, False)
+    assert rel(yh, yr) < 2e-2
+
+
+def test_pool_upsample_silu(H):
+    torch.manual_seed(7)
+    x = torch.randn(2, 16, 16, 128, device=DEV).to(BF)
+    for fh, fr, oshape in [(H.avgpool2, T.avgpool2, (2, 8, 8, 128)), (H.upsample2, T.upsample2, (2, 32, 32, 128)),
+                           (H.silu, T.silu, (2, 16, 16, 128))]:
+        go = torch.randn(*oshape, device=DEV)
+        yh, yr, gh, gr = run_both(fh, fr, [x], go)
+        assert rel(yh, yr) < 1e-2
+        assert rel(gh[0], gr[0]) < 1e-2
+
+
+def test_ray_posenc(H):
+    from distributed_3d_diffusion_pytorch_amd.data.synthetic import random_orbit_poses
+    g = torch.Generator(device=DEV)
+    g.manual_seed(0)
+    B, Hh, W = 3, 16, 16
+    R, t = random_orbit_poses(2 * B, g, DEV)
+    R, t = R.reshape(B, 2, 3, 3), t.reshape(B, 2, 3)
+    K = torch.tensor([[131.25, 0, 64.0], [0, 131.25, 64.0], [0, 0, 1]], dtype=torch.float64, device=DEV)
+    K = K.expand(B, 3, 3)
+    mask = torch.tensor([True, False, True], device=DEV)
+    pe = torch.randn(144, Hh, W, device=DEV) * 0.1
+    fe = torch.randn(1, 1, 144, 1, 1, device=DEV) * 0.1
+    oe = torch.randn(1, 1, 144, 1, 1, device=DEV) * 0.1
+    yh = H.ray_posenc(R, t, K, Hh, W, mask, pe, fe, oe)
+    yr = T.ray_posenc(R, t, K, Hh, W, mask, pe, fe, oe)
+    assert (yh.float() - yr).abs().max().item() < 2e-2
+    # gradients of the learned embeddings
+    pe_, fe_, oe_ = leaf(pe), leaf(fe), leaf(oe)
+    pr_, fr_, or_ = leaf(pe), leaf(fe), leaf(oe)
+    go = torch.randn(2 * B, Hh, W, 144, device=DEV)
+    H.ray_posenc(R, t, K, Hh, W, mask, pe_, fe_, oe_).backward(go.to(BF))
+    T.ray_posenc(R, t, K, Hh, W, mask, pr_, fr_, or_).backward(go)
+    assert rel(pe_.grad, pr_.grad) < 1e-2
+    assert rel(fe_.grad, fr_.grad) < 1e-2
+    assert rel(oe_.grad, or_.grad) < 1e-2
+
+
+def test_adam_matches_torch(H):
+    from distributed_3d_diffusion_pytorch_amd.parallel.flat import FlatParams
+    from distributed_3d_diffusion_pytorch_amd.engine.optim import FusedAdam
+    torch.manual_seed(8)
+    ps = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in [(33, 7), (128,), (5, 5, 3)]]
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    flat = FlatParams(ps)
+    opt = FusedAdam(flat, lr=1e-2, betas=(0.9, 0.99))
+    topt = torch.optim.Adam(ref, lr=1e-2, betas=(0.9, 0.99))
+    for step in range(5):
+        grads = [torch.randn_like(p) for p in ps]
+        for p, g in zip(ps, grads):
+            p.grad.copy_(g)
+        for p, g in zip(ref, grads):
+            p.grad = g.clone()
+        opt.step()
+        topt.step()
+    for p, r in zip(ps, ref):
+        assert torch.allclose(p, r, atol=1e-6, rtol=1e-5)
+
+
+def test_model_hip_vs_torch_backend():
+    """Whole X-UNet forward+backward: HIP backend vs torch backend (bf16)."""
+    from distributed_3d_diffusion_pytorch_amd import ops
+    from distributed_3d_diffusion_pytorch_amd.models import XUNet
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    torch.manual_seed(9)
+    m = XUNet(H=32, W=32, ch=128).to(DEV)
+    with torch.no_grad():
+        for p in m.parameters():
+            if p.abs().sum() == 0:
+                p.normal_(0, 0.02)
+    m.compute_dtype = BF
+    m.eval()
+    img, R, t, K = next(SyntheticBatches(2, 32, DEV, seed=0))
+    batch = {"x": img[:, 0], "z": img[:, 1], "logsnr": torch.tensor([[20.0, 1.5], [20.0, -3.0]], device=DEV),
+             "R": R, "t": t, "K": K}
+    mask = torch.tensor([True, False], device=DEV)
+    outs, grads = [], []
+    for be in ("hip", "torch"):
+        ops.set_backend(be)
+        m.zero_grad(set_to_none=True)
+        y = m(batch, cond_mask=mask)
+        y.float().square().mean().backward()
+        outs.append(y.float())
+        grads.append(torch.cat([p.grad.flatten() for p in m.parameters()]))
+    ops.set_backend(None)
+    assert rel(outs[0], outs[1]) < 5e-2
+    cos = torch.nn.functional.cosine_similarity(grads[0], grads[1], dim=0).item()
+    assert cos > 0.98, cos
