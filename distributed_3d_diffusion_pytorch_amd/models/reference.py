@@ -93,12 +93,12 @@ def _xblock(sd, p, h, emb, use_attn, heads):
     return h
 
 
-@torch.no_grad()
-def reference_forward(sd: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cond_mask: torch.Tensor,
+def reference_forward_grad(sd: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cond_mask: torch.Tensor,
                       ch_mult=(1, 2, 2, 4), num_res_blocks=3, attn_resolutions=(2, 3, 4), attn_heads=4,
                       emb_ch=1024, rescale_from: int = 0) -> torch.Tensor:
     """Eval-mode (no dropout) fp32 forward of the reference X-UNet."""
-    sd = {k[7:] if k.startswith("module.") else k: v.float() for k, v in sd.items()}
+    sd = {k[7:] if k.startswith("module.") else k: v if v.dtype == torch.float32 else v.float()
+          for k, v in sd.items()}
     x, z = batch["x"].float(), batch["z"].float()
     B, _, H, W = x.shape
     L = len(ch_mult)
@@ -136,3 +136,9 @@ def reference_forward(sd: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor
             h = _resblock(sd, f"upsample.{i}.{num_res_blocks + 1}", h, embs[i], "up")
     h = F.silu(_gn(sd, "lastgn", h))
     return _conv(sd, "lastconv", h)[:, 1]
+
+
+@torch.no_grad()
+def reference_forward(sd, batch, cond_mask, **kw) -> torch.Tensor:
+    """Eval-mode (no dropout) fp32 forward of the reference X-UNet (no grad)."""
+    return reference_forward_grad(sd, batch, cond_mask, **kw)

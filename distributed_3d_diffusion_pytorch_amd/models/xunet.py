@@ -212,20 +212,39 @@ class ConditioningProcessor(nn.Module):
         e = l1(torch.nn.functional.silu(l0(e)))
         return e.reshape(-1, self.emb_ch)
 
+    def learned_embedding_image(self, dtype: torch.dtype) -> Optional[torch.Tensor]:
+        """The learned part of the 144-ch conditioning input, identical for
+        every example of a given frame: ``[2, H, W, 144]`` with image f =
+        pos_emb + (first_emb if f == 0 else other_emb) (`xunet.py:333-336`)."""
+        e = None
+        if self.use_pos_emb:
+            e = self.pos_emb.permute(1, 2, 0)[None].expand(2, self.H, self.W, self.D)
+        if self.use_ref_pose_emb:
+            fe = torch.cat([self.first_emb, self.other_emb], dim=1).reshape(2, 1, 1, self.D)
+            e = fe.expand(2, self.H, self.W, self.D) if e is None else e + fe
+        return None if e is None else e.to(dtype).contiguous()
+
     def forward(self, batch: Dict[str, torch.Tensor], cond_mask: torch.Tensor,
                 dtype: torch.dtype) -> List[torch.Tensor]:
         B = batch["x"].shape[0]
         assert cond_mask.shape == (B,), (cond_mask.shape, B)
         logsnr_emb = self.logsnr_embedding(batch["logsnr"])
-        pose = ops.ray_posenc(batch["R"], batch["t"], batch["K"], self.H, self.W,
-                              cond_mask.to(batch["R"].device).bool(),
-                              self.pos_emb if self.use_pos_emb else None,
-                              self.first_emb if self.use_ref_pose_emb else None,
-                              self.other_emb if self.use_ref_pose_emb else None,
+        # Data-dependent part: NeRF-encoded camera rays (masked), no gradient.
+        rays = ops.ray_posenc(batch["R"], batch["t"], batch["K"], self.H, self.W,
+                              cond_mask.to(batch["R"].device).bool(), None, None, None,
                               rescale_from=128 if self.rescale_intrinsics else 0, out_dtype=dtype)
+        # Convolution is linear, so conv(rays + emb) = conv(rays) + conv(emb):
+        # the learned term is convolved once per FRAME (2 images) and added as
+        # a batch-broadcast residual.  Its input gradient (for pos_emb /
+        # first_emb / other_emb) is then a 2-image transposed conv instead of a
+        # per-example one.
+        emb_img = self.learned_embedding_image(dtype)
         sembs = []
         for i, conv in enumerate(self.convs):
-            e = ops.conv3x3(pose, conv.weight, conv.bias, stride=2 ** i, row_bias=logsnr_emb)
+            s = 2 ** i
+            e_emb = ops.conv3x3(emb_img, conv.weight, None, stride=s) if emb_img is not None else None
+            e = ops.conv3x3(rays, conv.weight, conv.bias, stride=s, row_bias=logsnr_emb, residual=e_emb,
+                            res_period=2 if e_emb is not None else 0)
             sembs.append(ops.silu(e))
         return sembs
 

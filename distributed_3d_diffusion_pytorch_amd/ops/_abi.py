@@ -30,10 +30,11 @@ SIGNATURES = {
     # adam.hip
     "d3d_adam": [P, P, P, P, P, L, F, F, F, F, F, F, F, F, P],
     # conv.hip
-    "d3d_conv3x3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, P],
+    "d3d_conv3x3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P],
     "d3d_conv_wgrad_plan": [I, I, I, I, I, IP, IP],
     "d3d_conv3x3_wgrad": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
     "d3d_chansum": [P, P, P, P, I, I, I, I, P],
+    "d3d_colsum": [P, L, I, P, P, P, I, P],
     "d3d_pack_conv_weight": [P, P, I, I, I, I, I, P],
     # rays.hip
     "d3d_ray_posenc": [P, P, P, P, P, P, P, P, I, I, I, P],

@@ -32,6 +32,9 @@
 //   writes the OIHW layout of the parameter gradient.
 #include "common.h"
 
+D3D_API int d3d_colsum(const float* in, long R, int Cc, float* part, float* out, float* out_odd, int accumulate,
+                       hipStream_t st);
+
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -44,7 +47,8 @@ template <int BM, int BN, bool TRANS>
 __global__ void __launch_bounds__(256, 2)
 conv_igemm_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
              const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int Nimg,
-             int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride, float scale) {
+             int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride, float scale,
+             int res_nmod) {
   constexpr int WM = BM / 2, WN = BN / 2;       // 2x2 waves
   constexpr int TM = WM / 16, TN = WN / 16;     // MFMA tiles per wave
   constexpr int A_LD = BM * BK / 8 / 256;       // 16B loads per thread
@@ -181,9 +185,12 @@ conv_igemm_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const floa
         v[e] = t;
       }
       bf16* dst = O + pix * ldo + co;
+      // residual row: same pixel, or (image % res_nmod) for a residual that is
+      // broadcast over the batch (per-frame conditioning term)
+      const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
       if (co + 3 < OC && (ldo & 3) == 0) {
         if (res) {
-          bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + pix * ldo + co);
+          bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
         }
@@ -194,7 +201,7 @@ conv_igemm_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const floa
       } else {
         for (int e = 0; e < 4 && co + e < OC; ++e) {
           float t = v[e];
-          if (res) t += (float)res[pix * ldo + co + e];
+          if (res) t += (float)res[rpix * ldo + co + e];
           dst[e] = (bf16)(t * scale);
         }
       }
@@ -385,18 +392,14 @@ __global__ void chansum_k(const bf16* __restrict__ dy, float* __restrict__ part,
   }
 }
 
-__global__ void chansum_final_k(const float* __restrict__ part, float* __restrict__ per_img, float* __restrict__ tot,
-                                int Nimg, int C, int nchunks) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float all = 0.f;
-  for (int n = 0; n < Nimg; ++n) {
-    float s = 0.f;
-    for (int k = 0; k < nchunks; ++k) s += part[((long)k * Nimg + n) * C + c];
-    if (per_img) per_img[(long)n * C + c] = s;
-    all += s;
-  }
-  if (tot) tot[c] = all;
+__global__ void chansum_img_k(const float* __restrict__ part, float* __restrict__ per_img, int Nimg, int C,
+                              int nchunks) {
+  long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (t >= (long)Nimg * C) return;
+  int n = (int)(t / C), c = (int)(t % C);
+  float s = 0.f;
+  for (int k = 0; k < nchunks; ++k) s += part[((long)k * Nimg + n) * C + c];
+  per_img[t] = s;
 }
 
 // weight packing: OIHW fp32 -> [OCp][9][ICp] bf16 (forward) or
@@ -429,16 +432,18 @@ __global__ void pack_w_k(const float* __restrict__ w, bf16* __restrict__ out, in
 // OCp % 128 == 0 and ICp % 64 == 0.  O: [N, OH, OW, ldo] bf16.
 D3D_API int d3d_conv3x3(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
                         void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo,
-                        int stride, int trans, float scale, hipStream_t st) {
+                        int stride, int trans, float scale, int res_nmod, hipStream_t st) {
   long Mpix = (long)N * OH * OW;
   constexpr int BM = 128, BN = 128;
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM));
   if (trans)
     hipLaunchKernelGGL((conv_igemm_k<BM, BN, true>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,
-                       row_bias, (const bf16*)res, (bf16*)O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, scale);
+                       row_bias, (const bf16*)res, (bf16*)O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, scale,
+                       res_nmod);
   else
     hipLaunchKernelGGL((conv_igemm_k<BM, BN, false>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,
-                       row_bias, (const bf16*)res, (bf16*)O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, scale);
+                       row_bias, (const bf16*)res, (bf16*)O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, scale,
+                       res_nmod);
   return (int)hipGetLastError();
 }
 
@@ -475,12 +480,16 @@ D3D_API int d3d_conv3x3_wgrad(const void* dY, const void* I, float* ws, float* d
 }
 
 // per-image (optional) and total channel sums of dY [N, P, C] (C % 8 == 0).
-// part: workspace [nchunks][N][C] fp32.
+// part: workspace [(nchunks + 1) * N * C + 64 * C] fp32.
 D3D_API int d3d_chansum(const void* dY, float* part, float* per_img, float* tot, int N, int P, int C, int nchunks,
                         hipStream_t st) {
   dim3 grid((C / 8 + 31) / 32, N, nchunks);
   hipLaunchKernelGGL(chansum_k, grid, dim3(256), 0, st, (const bf16*)dY, part, P, C, nchunks);
-  hipLaunchKernelGGL(chansum_final_k, dim3((C + 255) / 256), dim3(256), 0, st, part, per_img, tot, N, C, nchunks);
+  // per-image sums (written into per_img, or into the part tail when the
+  // caller only wants totals), then a parallel column sum over images
+  float* pi = per_img ? per_img : part + (long)nchunks * N * C;
+  hipLaunchKernelGGL(chansum_img_k, dim3(cdiv((long)N * C, 256)), dim3(256), 0, st, part, pi, N, C, nchunks);
+  if (tot) d3d_colsum(pi, N, C, part + (long)(nchunks + 1) * N * C, tot, nullptr, 0, st);
   return (int)hipGetLastError();
 }
 

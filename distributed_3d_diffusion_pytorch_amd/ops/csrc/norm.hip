@@ -13,6 +13,9 @@
 // tiny cross-chunk merge kernels).
 #include "common.h"
 
+D3D_API int d3d_colsum(const float* in, long R, int Cc, float* part, float* out, float* out_odd, int accumulate,
+                       hipStream_t st);
+
 namespace {
 
 constexpr int NT = 256;        // threads per block for the chunked kernels
@@ -281,32 +284,20 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
   }
 }
 
-__global__ void gn_bwd_final_k(const float* __restrict__ chan_part, const float* __restrict__ grp_part, int N,
-                               int P, int C, int G, int nchunks, float* __restrict__ coef,
-                               float* __restrict__ dgamma, float* __restrict__ dbeta) {
+__global__ void gn_bwd_coef_k(const float* __restrict__ grp_part, int N, int P, int C, int G, int nchunks,
+                              float* __restrict__ coef) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < N * G) {
-    int n = t / G, g = t % G;
-    float a = 0.f, b = 0.f;
-    for (int c = 0; c < nchunks; ++c) {
-      const float* p = grp_part + (((long)n * nchunks + c) * G + g) * 2;
-      a += p[0];
-      b += p[1];
-    }
-    float inv = 1.f / (float)((long)P * (C / G));
-    coef[t * 2 + 0] = a * inv;
-    coef[t * 2 + 1] = b * inv;
+  if (t >= N * G) return;
+  int n = t / G, g = t % G;
+  float a = 0.f, b = 0.f;
+  for (int c = 0; c < nchunks; ++c) {
+    const float* p = grp_part + (((long)n * nchunks + c) * G + g) * 2;
+    a += p[0];
+    b += p[1];
   }
-  if (t < C) {
-    float a = 0.f, b = 0.f;
-    long R = (long)N * nchunks;
-    for (long r = 0; r < R; ++r) {
-      a += chan_part[(r * C + t) * 2 + 0];
-      b += chan_part[(r * C + t) * 2 + 1];
-    }
-    dgamma[t] = a;
-    dbeta[t] = b;
-  }
+  float inv = 1.f / (float)((long)P * (C / G));
+  coef[t * 2 + 0] = a * inv;
+  coef[t * 2 + 1] = b * inv;
 }
 
 template <int MODE>
@@ -392,7 +383,7 @@ D3D_API int d3d_gn_film(const void* x, const float* stats, const float* gamma, c
 }
 
 // mode: 0 plain, 1 silu, 2 film.  Workspaces: chan_part [N*nchunks*C*2],
-// grp_part [N*nchunks*G*2], coef [N*G*2].  Outputs dx (bf16), dgamma/dbeta
+// grp_part [N*nchunks*G*2 + 64*2*C] (tail = column-sum partials), coef [N*G*2].  Outputs dx (bf16), dgamma/dbeta
 // (fp32 [C]) and, for mode 2, dss (bf16 [N,P,2C]).
 D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, const float* stats,
                        const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
@@ -409,9 +400,12 @@ D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, 
   else if (mode == 1) RED(1);
   else RED(2);
 #undef RED
-  int nt = N * G > C ? N * G : C;
-  hipLaunchKernelGGL(gn_bwd_final_k, dim3(cdiv(nt, 256)), dim3(256), 0, st, chan_part, grp_part, N, P, C, G,
-                     p.nchunks, coef, dgamma, dbeta);
+  hipLaunchKernelGGL(gn_bwd_coef_k, dim3(cdiv((long)N * G, 256)), dim3(256), 0, st, grp_part, N, P, C, G,
+                     p.nchunks, coef);
+  // dgamma/dbeta: chan_part is [N*nchunks][C][2] -> column sums over 2C
+  // interleaved columns (coef's workspace is reused after the apply kernel
+  // has been enqueued? no: use the tail of chan_part's allocation instead)
+  d3d_colsum(chan_part, (long)N * p.nchunks, 2 * C, grp_part + (long)N * p.nchunks * G * 2, dgamma, dbeta, 0, st);
   long nvec = (long)N * P * C / 8;
 #define APP(M)                                                                                                  \
   hipLaunchKernelGGL(gn_bwd_apply_k<M>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, (const bf16*)dy, \

@@ -120,7 +120,7 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed):
     dg = torch.empty(C, dtype=F32, device=dev)
     db = torch.empty(C, dtype=F32, device=dev)
     cp = torch.empty(N * nch * C * 2, dtype=F32, device=dev)
-    gp = torch.empty(N * nch * G * 2, dtype=F32, device=dev)
+    gp = torch.empty(N * nch * G * 2 + 64 * 2 * C, dtype=F32, device=dev)
     coef = torch.empty(N * G * 2, dtype=F32, device=dev)
     _chk(_lib.d3d_gn_bwd(mode, x.data_ptr(), dy.data_ptr(), _ptr(ss), stats.data_ptr(), w.data_ptr(), b.data_ptr(),
                          N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), dg.data_ptr(), db.data_ptr(),
@@ -183,9 +183,9 @@ def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=Fa
 
 
 # ----------------------------------------------------------------- conv ----
-def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale):
+def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale, res_nmod=0):
     _chk(_lib.d3d_conv3x3(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
-                          IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), _st()), "conv3x3")
+                          IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), _st()), "conv3x3")
 
 
 def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride):
@@ -202,7 +202,7 @@ def _chansum(g, per_image: bool):
     N, OH, OW, C = g.shape
     P = OH * OW
     nch = max(1, min(64, (2048 + N - 1) // N, (P + 63) // 64))
-    part = torch.empty(nch * N * C, dtype=F32, device=g.device)
+    part = torch.empty((nch + 1) * N * C + 64 * C, dtype=F32, device=g.device)
     per = torch.empty(N, C, dtype=F32, device=g.device) if per_image else None
     tot = torch.empty(C, dtype=F32, device=g.device)
     _chk(_lib.d3d_chansum(g.data_ptr(), part.data_ptr(), _ptr(per), tot.data_ptr(), N, P, C, nch, _st()), "chansum")
@@ -211,7 +211,7 @@ def _chansum(g, per_image: bool):
 
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias):
+    def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias, res_period):
         x = x.contiguous()
         N, H, W, IC = x.shape
         OC = weight.shape[0]
@@ -222,15 +222,16 @@ class _Conv3x3(torch.autograd.Function):
         out = torch.empty(N, OH, OW, OC, dtype=BF16, device=x.device)
         res = residual.contiguous() if residual is not None else None
         rb = row_bias.contiguous().float() if row_bias is not None else None
-        _conv_fwd(x, wp, bias, rb, res, out, N, H, W, IC, _up(IC, 64), OH, OW, OC, OC, stride, False, out_scale)
+        _conv_fwd(x, wp, bias, rb, res, out, N, H, W, IC, _up(IC, 64), OH, OW, OC, OC, stride, False, out_scale,
+                  res_period)
         ctx.save_for_backward(x, weight)
-        ctx.cfg = (stride, out_scale, residual is not None, row_bias is not None, bias is not None)
+        ctx.cfg = (stride, out_scale, residual is not None, row_bias is not None, bias is not None, res_period)
         return out
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        stride, scale, has_res, has_rb, has_b = ctx.cfg
+        stride, scale, has_res, has_rb, has_b, res_period = ctx.cfg
         N, H, W, IC = x.shape
         OC = weight.shape[0]
         dy = dy.contiguous()
@@ -249,15 +250,18 @@ class _Conv3x3(torch.autograd.Function):
         per, tot = _chansum(g, has_rb) if (has_b or has_rb) else (None, None)
         db = tot if (has_b and ctx.needs_input_grad[2]) else None
         drb = per if has_rb else None
-        dres = g if has_res else None
-        return dx, dW, db, None, dres, None, drb
+        dres = None
+        if has_res:
+            dres = g if not res_period else \
+                g.reshape(N // res_period, res_period, *g.shape[1:]).float().sum(0).to(g.dtype)
+        return dx, dW, db, None, dres, None, drb, None
 
 
-def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=None):
+def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=None, res_period=0):
     _need_bf16(x, residual)
     OC, IC = weight.shape[0], weight.shape[1]
     if IC % 8 == 0 and OC % 8 == 0:
-        return _Conv3x3.apply(x, weight, bias, stride, residual, out_scale, row_bias)
+        return _Conv3x3.apply(x, weight, bias, stride, residual, out_scale, row_bias, res_period)
     # stem (IC=3) / head (OC=3): zero-pad channels to a multiple of 8 so every
     # access stays 16-byte vectorised; the padding costs < 0.1 % of FLOPs.
     ICe, OCe = _up(IC, 8), _up(OC, 8)
@@ -266,7 +270,7 @@ def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=No
     be = F.pad(bias, (0, OCe - OC)) if bias is not None else None
     re = F.pad(residual, (0, OCe - OC)) if residual is not None else None
     rbe = F.pad(row_bias, (0, OCe - OC)) if row_bias is not None else None
-    y = _Conv3x3.apply(xe, we, be, stride, re, out_scale, rbe)
+    y = _Conv3x3.apply(xe, we, be, stride, re, out_scale, rbe, res_period)
     return y[..., :OC].contiguous() if OCe != OC else y
 
 

@@ -61,15 +61,18 @@ def gn_film(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, ss: torch
 
 def conv3x3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int = 1,
             residual: Optional[torch.Tensor] = None, out_scale: float = 1.0,
-            row_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+            row_bias: Optional[torch.Tensor] = None, res_period: int = 0) -> torch.Tensor:
     """3x3 conv, padding 1, on NHWC.  Epilogue: + row_bias[n] (per image),
-    + residual, * out_scale."""
+    + residual (broadcast as residual[n % res_period] when res_period > 0),
+    * out_scale."""
     dt = x.dtype
     y = F.conv2d(x.permute(0, 3, 1, 2), _cast(weight, dt), _cast(bias, dt), stride=stride, padding=1)
     y = y.permute(0, 2, 3, 1)
     if row_bias is not None:
         y = y + row_bias.to(dt)[:, None, None, :]
     if residual is not None:
+        if res_period:
+            residual = residual.repeat(y.shape[0] // res_period, 1, 1, 1)
         y = y + residual
     if out_scale != 1.0:
         y = y * out_scale

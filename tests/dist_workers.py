@@ -1,0 +1,78 @@
+"""Multi-process worker bodies for test_distributed.py (spawned ranks read
+RANK/WORLD_SIZE from the environment like torchrun workers)."""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+TINY_OV = {"model.ch": 32, "model.emb_ch": 64, "model.H": 16, "model.W": 16, "data.imgsize": 16,
+           "dtype": "fp32", "backend": "torch", "log_every": 0, "ckpt_every": 0, "data.synthetic": True,
+           "dist.timeout_s": 20.0}
+
+
+def reducer_matches_manual_average(out_dir, bucket_mb):
+    from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup, FlatParams, GradReducer
+    from helpers import tiny_model, tiny_batch
+    ctx = init_distributed("gloo", 60, use_gpu=False)
+    m = tiny_model(seed=0).eval()      # no dropout: both passes must be identical
+    flat = FlatParams(list(m.parameters()))
+    red = GradReducer(flat, bucket_mb=bucket_mb, first_bucket_mb=bucket_mb / 4)
+    assert len(red.buckets) >= 1
+    b = tiny_batch(2, seed=10 + ctx.rank)       # different data per rank
+    cm = torch.tensor([True, ctx.rank == 0])
+    # local gradient without communication
+    with red.no_sync():
+        m(b, cond_mask=cm).square().mean().backward()
+    local = flat.grad.clone()
+    flat.zero_grad()
+    red.reset()
+    # reduced gradient through the bucketed hooks
+    m(b, cond_mask=cm).square().mean().backward()
+    red.finish()
+    summed = flat.grad.clone()
+    ref = local.clone()
+    dist.all_reduce(ref)
+    ok = torch.allclose(summed, ref, atol=1e-6, rtol=1e-5)
+    with open(os.path.join(out_dir, f"r{ctx.rank}.txt"), "w") as f:
+        f.write(f"{int(ok)} {len(red.buckets)}")
+    cleanup()
+
+
+def trainer_in_sync(out_dir):
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup, check_replicas_in_sync
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    ctx = init_distributed("gloo", 60, use_gpu=False)
+    cfg = make_config(None, dict(TINY_OV, **{"global_batch": 4, "out_dir": out_dir, "dist.checksum_every": 1}))
+    tr = Trainer(cfg, ctx)
+    data = SyntheticBatches(tr.local_batch, 16, "cpu", seed=ctx.rank)
+    for _ in range(3):
+        tr.train_step(*next(data))
+    ok = check_replicas_in_sync(tr.flat)
+    tr.save("latest.pt", epoch=0)
+    with open(os.path.join(out_dir, f"sync{ctx.rank}.txt"), "w") as f:
+        f.write(str(int(ok)))
+    cleanup()
+
+
+def fault_injection(out_dir):
+    os.environ["D3D_FAULT_AT_STEP"] = "1"
+    os.environ["D3D_FAULT_RANK"] = "1"
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    ctx = init_distributed("gloo", 10, use_gpu=False)
+    cfg = make_config(None, dict(TINY_OV, **{"global_batch": 4, "out_dir": out_dir, "dist.timeout_s": 10.0}))
+    tr = Trainer(cfg, ctx)
+    data = SyntheticBatches(tr.local_batch, 16, "cpu", seed=ctx.rank)
+    for _ in range(4):
+        tr.train_step(*next(data))
+    # only reached if the dead peer went unnoticed
+    with open(os.path.join(out_dir, f"survived{ctx.rank}.txt"), "w") as f:
+        f.write("1")

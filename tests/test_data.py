@@ -1,0 +1,78 @@
+import os
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_3d_diffusion_pytorch_amd.data import (SRNDataset, ShardSampler, MultiEpochsDataLoader,
+                                                       write_synthetic_srn, load_index, split_ids)
+
+
+@pytest.fixture(scope="module")
+def srn_root(tmp_path_factory):
+    root = str(tmp_path_factory.mktemp("srn"))
+    write_synthetic_srn(root, num_instances=10, num_views=5, size=32, seed=0)
+    return root
+
+
+def test_split_is_reference_deterministic(srn_root):
+    idx = load_index(os.path.join(srn_root, "index.pkl"))
+    tr, va = split_ids(list(idx), "train"), split_ids(list(idx), "val")
+    assert len(tr) == 9 and len(va) == 1 and not set(tr) & set(va)
+    import random
+    allv = sorted(idx)
+    random.seed(0)
+    random.shuffle(allv)
+    assert tr == allv[:9]                  # SRNdataset.py:50-57
+
+
+def test_item(srn_root):
+    ds = SRNDataset("train", srn_root, os.path.join(srn_root, "index.json"), imgsize=16)
+    imgs, R, T, K = ds[0]
+    assert imgs.shape == (2, 3, 16, 16) and imgs.dtype == np.float32
+    assert imgs.min() >= -1 and imgs.max() <= 1
+    assert R.shape == (2, 3, 3) and T.shape == (2, 3) and K.shape == (3, 3)
+    assert abs(K[0, 0] - 131.25 * 32 / 128) < 1e-4       # K not rescaled to imgsize (D10)
+    assert np.allclose(R[0] @ R[0].T, np.eye(3), atol=1e-6)
+
+
+def test_scan_index_matches_pickle(srn_root):
+    a = SRNDataset("train", srn_root, "", imgsize=16)
+    b = SRNDataset("train", srn_root, os.path.join(srn_root, "index.pkl"), imgsize=16)
+    assert a.ids == b.ids
+
+
+def test_safe_unpickler_refuses_code(tmp_path):
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("echo pwned",))
+    p = tmp_path / "evil.pkl"
+    p.write_bytes(pickle.dumps({"x": Evil()}))
+    with pytest.raises(pickle.UnpicklingError):
+        load_index(str(p))
+
+
+def test_shard_sampler_disjoint_covering():
+    n, world = 23, 4
+    shards = []
+    for r in range(world):
+        s = ShardSampler(n, r, world, shuffle=True, seed=3)
+        s.set_epoch(2)
+        shards.append(list(s))
+    assert all(len(x) == len(shards[0]) for x in shards)
+    allidx = sum(shards, [])
+    assert set(allidx) == set(range(n))
+    s0 = ShardSampler(n, 0, world, seed=3)
+    s0.set_epoch(1)
+    assert list(s0) != shards[0]           # reshuffled per epoch
+
+
+def test_loader(srn_root):
+    ds = SRNDataset("train", srn_root, "", imgsize=16)
+    dl = MultiEpochsDataLoader(ds, batch_size=4, sampler=ShardSampler(len(ds), 0, 1), num_workers=2)
+    for _ in range(2):
+        batches = list(dl)
+        assert len(batches) == 2
+        img, R, T, K = batches[0]
+        assert img.shape == (4, 2, 3, 16, 16) and R.dtype == torch.float64 and K.shape == (4, 3, 3)
