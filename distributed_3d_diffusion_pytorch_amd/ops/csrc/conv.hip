@@ -43,7 +43,7 @@ namespace {
 
 constexpr int BK = 64;
 
-template <int BM, int BN, bool TRANS>
+template <int BM, int BN, bool TRANS, int TAPS>
 __global__ void __launch_bounds__(256, 2)
 conv_igemm_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
              const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int Nimg,
@@ -70,7 +70,7 @@ conv_igemm_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const floa
   }
   const long n0 = (long)bid * BN;               // pixel tile start
   const int m0 = blockIdx.y * BM;               // output-channel tile start
-  const int Kp = 9 * ICp;
+  const int Kp = TAPS * ICp;
 
   // per-thread B rows (pixels): fixed over the K loop
   const int cb = tid & 7;                        // 16B chunk within the BK row
@@ -90,9 +90,9 @@ conv_igemm_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const floa
   bf16x8 ra[A_LD], rb[B_LD];
   const bf16x8 zero8 = {};
   auto gload = [&](int kstep) {
-    const int tap = kstep / (ICp / BK);
-    const int c0 = (kstep % (ICp / BK)) * BK;
-    const int kh = tap / 3, kw = tap % 3;
+    const int tap = TAPS == 9 ? kstep / (ICp / BK) : 0;
+    const int c0 = (TAPS == 9 ? kstep % (ICp / BK) : kstep) * BK;
+    const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;   // 1x1 == centre tap
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       int r = (tid >> 3) + i * 32;
@@ -217,7 +217,7 @@ __device__ __forceinline__ s16x4 ds_tr(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int TAPS>
 __global__ void __launch_bounds__(256, 2)
 conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __restrict__ ws, int Nimg, int IH,
              int IW, int IC, int OH, int OW, int OC, int stride, int pix_per_split, int ncb) {
@@ -230,11 +230,11 @@ conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __r
   bf16* Bs = smem + 2 * WBK * AS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tap = blockIdx.x / ncb;
+  const int tap = blockIdx.x / ncb;                 // 0 when TAPS == 1
   const int ci0 = (blockIdx.x % ncb) * BN;
   const int m0 = blockIdx.y * BM;
   const int split = blockIdx.z;
-  const int kh = tap / 3, kw = tap % 3;
+  const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
   const long P = (long)Nimg * OH * OW;
   const long p_begin = (long)split * pix_per_split;
   const long p_end = p_begin + pix_per_split < P ? p_begin + pix_per_split : P;
@@ -333,7 +333,7 @@ conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __r
   }
   // partial slab: ws[split][co][tap*IC + ci]
   const int fr = lane & 15, fq = lane >> 4;
-  const long KW = 9L * IC;
+  const long KW = (long)TAPS * IC;
   float* slab = ws + (long)split * OC * KW;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -351,17 +351,17 @@ conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __r
 
 // sum the split slabs and write dW in OIHW fp32 layout (optionally accumulate)
 __global__ void wgrad_reduce_k(const float* __restrict__ ws, float* __restrict__ dW, int OC, int IC, int splits,
-                               int accumulate) {
-  long total = (long)OC * IC * 9;
+                               int accumulate, int taps) {
+  long total = (long)OC * IC * taps;
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
     // t indexes the slab layout [co][tap][ci] (coalesced reads)
     int ci = (int)(t % IC);
     long r = t / IC;
-    int tap = (int)(r % 9);
-    int co = (int)(r / 9);
+    int tap = (int)(r % taps);
+    int co = (int)(r / taps);
     float s = 0.f;
     for (int k = 0; k < splits; ++k) s += ws[(long)k * total + t];
-    long o = ((long)co * IC + ci) * 9 + tap;
+    long o = ((long)co * IC + ci) * taps + tap;
     dW[o] = accumulate ? dW[o] + s : s;
   }
 }
@@ -405,22 +405,22 @@ __global__ void chansum_img_k(const float* __restrict__ part, float* __restrict_
 // weight packing: OIHW fp32 -> [OCp][9][ICp] bf16 (forward) or
 //                              [ICp][9][OCp] bf16 (transposed, for dgrad)
 __global__ void pack_w_k(const float* __restrict__ w, bf16* __restrict__ out, int OC, int IC, int OCp, int ICp,
-                         int trans) {
-  long total = trans ? (long)ICp * 9 * OCp : (long)OCp * 9 * ICp;
+                         int trans, int taps) {
+  long total = trans ? (long)ICp * taps * OCp : (long)OCp * taps * ICp;
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
     int co, ci, tap;
     if (!trans) {
       ci = (int)(t % ICp);
       long r = t / ICp;
-      tap = (int)(r % 9);
-      co = (int)(r / 9);
+      tap = (int)(r % taps);
+      co = (int)(r / taps);
     } else {
       co = (int)(t % OCp);
       long r = t / OCp;
-      tap = (int)(r % 9);
-      ci = (int)(r / 9);
+      tap = (int)(r % taps);
+      ci = (int)(r / taps);
     }
-    float v = (co < OC && ci < IC) ? w[((long)co * IC + ci) * 9 + tap] : 0.f;
+    float v = (co < OC && ci < IC) ? w[((long)co * IC + ci) * taps + tap] : 0.f;
     out[t] = (bf16)v;
   }
 }
@@ -428,29 +428,39 @@ __global__ void pack_w_k(const float* __restrict__ w, bf16* __restrict__ out, in
 }  // namespace
 
 // ============================================================== C ABI =====
-// I: [N, IH, IW, IC] bf16 (IC % 8 == 0), Wp: packed [OCp][9][ICp] bf16 with
-// OCp % 128 == 0 and ICp % 64 == 0.  O: [N, OH, OW, ldo] bf16.
-D3D_API int d3d_conv3x3(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
-                        void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo,
-                        int stride, int trans, float scale, int res_nmod, hipStream_t st) {
+// I: [N, IH, IW, IC] bf16 (IC % 8 == 0), Wp: packed [OCp][taps][ICp] bf16 with
+// OCp % 128 == 0 and ICp % 64 == 0.  O: [N, OH, OW, ldo] bf16.  taps = 9 (3x3)
+// or 1 (1x1 / per-pixel linear).
+D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
+                     void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
+                     int trans, float scale, int res_nmod, int taps, hipStream_t st) {
   long Mpix = (long)N * OH * OW;
   constexpr int BM = 128, BN = 128;
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM));
-  if (trans)
-    hipLaunchKernelGGL((conv_igemm_k<BM, BN, true>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,
-                       row_bias, (const bf16*)res, (bf16*)O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, scale,
-                       res_nmod);
-  else
-    hipLaunchKernelGGL((conv_igemm_k<BM, BN, false>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,
-                       row_bias, (const bf16*)res, (bf16*)O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, scale,
-                       res_nmod);
+#define LAUNCH(TR, TP)                                                                                             \
+  hipLaunchKernelGGL((conv_igemm_k<BM, BN, TR, TP>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias, \
+                     row_bias, (const bf16*)res, (bf16*)O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, scale,      \
+                     res_nmod)
+  if (taps == 9) {
+    if (trans) LAUNCH(true, 9); else LAUNCH(false, 9);
+  } else {
+    if (trans) LAUNCH(true, 1); else LAUNCH(false, 1);
+  }
+#undef LAUNCH
   return (int)hipGetLastError();
 }
 
-D3D_API int d3d_conv_wgrad_plan(int N, int OH, int OW, int OC, int IC, int* splits, int* pix_per_split) {
+D3D_API int d3d_conv3x3(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
+                        void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo,
+                        int stride, int trans, float scale, int res_nmod, hipStream_t st) {
+  return d3d_conv(I, Wp, bias, row_bias, res, O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans, scale,
+                  res_nmod, 9, st);
+}
+
+D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps, int* splits, int* pix_per_split) {
   constexpr int BM = 128, BN = 128;
   long P = (long)N * OH * OW;
-  int tiles = 9 * ((IC + BN - 1) / BN) * ((OC + BM - 1) / BM);
+  int tiles = taps * ((IC + BN - 1) / BN) * ((OC + BM - 1) / BM);
   long want = (1024 + tiles - 1) / tiles;
   long maxs = (P + 255) / 256;      // >= 256 pixels per split
   if (want > maxs) want = maxs;
@@ -462,21 +472,35 @@ D3D_API int d3d_conv_wgrad_plan(int N, int OH, int OW, int OC, int IC, int* spli
   return 0;
 }
 
+D3D_API int d3d_conv_wgrad_plan(int N, int OH, int OW, int OC, int IC, int* splits, int* pix_per_split) {
+  return d3d_conv_wgrad_plan2(N, OH, OW, OC, IC, 9, splits, pix_per_split);
+}
+
 // dY: [N, OH, OW, OC] bf16 (OC % 8 == 0); I: [N, IH, IW, IC] bf16.
-// ws: [splits][OC][9*IC] fp32 workspace.  dW: OIHW fp32 [OC][IC][3][3].
+// ws: [splits][OC][taps*IC] fp32 workspace.  dW: [OC][IC][taps] fp32 (OIHW).
+D3D_API int d3d_conv_wgrad(const void* dY, const void* I, float* ws, float* dW, int N, int IH, int IW, int IC, int OH,
+                           int OW, int OC, int stride, int splits, int pix_per_split, int accumulate, int taps,
+                           hipStream_t st) {
+  constexpr int BM = 128, BN = 128;
+  int ncb = (IC + BN - 1) / BN;
+  dim3 grid(taps * ncb, (OC + BM - 1) / BM, splits);
+  if (taps == 9)
+    hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 9>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
+                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb);
+  else
+    hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 1>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
+                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb);
+  long total = (long)OC * IC * taps;
+  long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(wgrad_reduce_k, dim3((int)g), dim3(256), 0, st, ws, dW, OC, IC, splits, accumulate, taps);
+  return (int)hipGetLastError();
+}
+
 D3D_API int d3d_conv3x3_wgrad(const void* dY, const void* I, float* ws, float* dW, int N, int IH, int IW, int IC,
                               int OH, int OW, int OC, int stride, int splits, int pix_per_split, int accumulate,
                               hipStream_t st) {
-  constexpr int BM = 128, BN = 128;
-  int ncb = (IC + BN - 1) / BN;
-  dim3 grid(9 * ncb, (OC + BM - 1) / BM, splits);
-  hipLaunchKernelGGL((conv_wgrad_k<BM, BN>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
-                     IW, IC, OH, OW, OC, stride, pix_per_split, ncb);
-  long total = (long)OC * IC * 9;
-  long g = (total + 255) / 256;
-  if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(wgrad_reduce_k, dim3((int)g), dim3(256), 0, st, ws, dW, OC, IC, splits, accumulate);
-  return (int)hipGetLastError();
+  return d3d_conv_wgrad(dY, I, ws, dW, N, IH, IW, IC, OH, OW, OC, stride, splits, pix_per_split, accumulate, 9, st);
 }
 
 // per-image (optional) and total channel sums of dY [N, P, C] (C % 8 == 0).
@@ -493,11 +517,16 @@ D3D_API int d3d_chansum(const void* dY, float* part, float* per_img, float* tot,
   return (int)hipGetLastError();
 }
 
-D3D_API int d3d_pack_conv_weight(const float* w, void* out, int OC, int IC, int OCp, int ICp, int trans,
-                                 hipStream_t st) {
-  long total = (long)OCp * 9 * ICp;
+D3D_API int d3d_pack_weight(const float* w, void* out, int OC, int IC, int OCp, int ICp, int trans, int taps,
+                            hipStream_t st) {
+  long total = (long)OCp * taps * ICp;
   long g = (total + 255) / 256;
   if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(pack_w_k, dim3((int)g), dim3(256), 0, st, w, (bf16*)out, OC, IC, OCp, ICp, trans);
+  hipLaunchKernelGGL(pack_w_k, dim3((int)g), dim3(256), 0, st, w, (bf16*)out, OC, IC, OCp, ICp, trans, taps);
   return (int)hipGetLastError();
+}
+
+D3D_API int d3d_pack_conv_weight(const float* w, void* out, int OC, int IC, int OCp, int ICp, int trans,
+                                 hipStream_t st) {
+  return d3d_pack_weight(w, out, OC, IC, OCp, ICp, trans, 9, st);
 }

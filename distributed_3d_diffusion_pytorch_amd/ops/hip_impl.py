@@ -71,22 +71,26 @@ def _cached(p: torch.Tensor, kind: str, build):
     return v
 
 
-def packed_conv_weight(w: torch.Tensor, trans: bool) -> torch.Tensor:
-    """OIHW fp32 -> [OCp][9][ICp] bf16 (trans: [ICp][9][OCp]) for the MFMA
-    kernel; row dims padded to 128 (block M), K chunks to 64 (BK)."""
+def packed_weight(w: torch.Tensor, trans: bool, taps: int = 9) -> torch.Tensor:
+    """[OC, IC(, kh, kw)] fp32 -> [OCp][taps][ICp] bf16 (trans: [ICp][taps][OCp])
+    for the MFMA kernels; GEMM-M dims padded to 128 (block M), K chunks to 64."""
     OC, IC = w.shape[0], w.shape[1]
 
     def build():
         if not trans:
             OCp, ICp = _up(OC, 128), _up(IC, 64)
-            out = torch.empty(OCp * 9 * ICp, dtype=BF16, device=w.device)
+            out = torch.empty(OCp * taps * ICp, dtype=BF16, device=w.device)
         else:
             OCp, ICp = _up(OC, 64), _up(IC, 128)
-            out = torch.empty(ICp * 9 * OCp, dtype=BF16, device=w.device)
-        _chk(_lib.d3d_pack_conv_weight(w.data_ptr(), out.data_ptr(), OC, IC, OCp, ICp, int(trans), _st()),
-             "pack_conv_weight")
+            out = torch.empty(ICp * taps * OCp, dtype=BF16, device=w.device)
+        _chk(_lib.d3d_pack_weight(w.data_ptr(), out.data_ptr(), OC, IC, OCp, ICp, int(trans), taps, _st()),
+             "pack_weight")
         return out
-    return _cached(w, "convT" if trans else "conv", build)
+    return _cached(w, f"pack{taps}{'T' if trans else ''}", build)
+
+
+def packed_conv_weight(w: torch.Tensor, trans: bool) -> torch.Tensor:
+    return packed_weight(w, trans, 9)
 
 
 def bf16_weight(w: torch.Tensor) -> torch.Tensor:
@@ -183,18 +187,19 @@ def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=Fa
 
 
 # ----------------------------------------------------------------- conv ----
-def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale, res_nmod=0):
-    _chk(_lib.d3d_conv3x3(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
-                          IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), _st()), "conv3x3")
+def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale, res_nmod=0,
+              taps=9):
+    _chk(_lib.d3d_conv(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
+                       IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), taps, _st()), "conv")
 
 
-def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride):
+def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9):
     s, pps = ctypes.c_int(), ctypes.c_int()
-    _lib.d3d_conv_wgrad_plan(N, OH, OW, OC, IC, ctypes.byref(s), ctypes.byref(pps))
-    ws = torch.empty(s.value * OC * 9 * IC, dtype=F32, device=x.device)
-    dW = torch.empty(OC, IC, 3, 3, dtype=F32, device=x.device)
-    _chk(_lib.d3d_conv3x3_wgrad(g.data_ptr(), x.data_ptr(), ws.data_ptr(), dW.data_ptr(), N, H, W, IC, OH, OW, OC,
-                                stride, s.value, pps.value, 0, _st()), "conv3x3_wgrad")
+    _lib.d3d_conv_wgrad_plan2(N, OH, OW, OC, IC, taps, ctypes.byref(s), ctypes.byref(pps))
+    ws = torch.empty(s.value * OC * taps * IC, dtype=F32, device=x.device)
+    dW = torch.empty(OC, IC, taps, dtype=F32, device=x.device)
+    _chk(_lib.d3d_conv_wgrad(g.data_ptr(), x.data_ptr(), ws.data_ptr(), dW.data_ptr(), N, H, W, IC, OH, OW, OC,
+                             stride, s.value, pps.value, 0, taps, _st()), "conv_wgrad")
     return dW
 
 
@@ -209,29 +214,37 @@ def _chansum(g, per_image: bool):
     return per, tot
 
 
-class _Conv3x3(torch.autograd.Function):
+class _Conv(torch.autograd.Function):
+    """Implicit-GEMM conv (taps=9: 3x3 pad 1 stride s; taps=1: per-pixel
+    linear) with fused bias / per-image bias / residual / scale epilogue.
+    Backward: input grad via the same kernel in transposed mode, weight grad
+    via the split-K transpose-read kernel, bias grads via channel sums."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias, res_period):
+    def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias, res_period, taps):
         x = x.contiguous()
         N, H, W, IC = x.shape
         OC = weight.shape[0]
         assert weight.shape[1] == IC and IC % 8 == 0 and OC % 8 == 0, (tuple(weight.shape), IC, OC)
-        OH = (H - 1) // stride + 1
-        OW = (W - 1) // stride + 1
-        wp = packed_conv_weight(weight, False)
+        if taps == 9:
+            OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+        else:
+            assert stride == 1
+            OH, OW = H, W
+        wp = packed_weight(weight, False, taps)
         out = torch.empty(N, OH, OW, OC, dtype=BF16, device=x.device)
         res = residual.contiguous() if residual is not None else None
         rb = row_bias.contiguous().float() if row_bias is not None else None
         _conv_fwd(x, wp, bias, rb, res, out, N, H, W, IC, _up(IC, 64), OH, OW, OC, OC, stride, False, out_scale,
-                  res_period)
+                  res_period, taps)
         ctx.save_for_backward(x, weight)
-        ctx.cfg = (stride, out_scale, residual is not None, row_bias is not None, bias is not None, res_period)
+        ctx.cfg = (stride, out_scale, residual is not None, row_bias is not None, bias is not None, res_period, taps)
         return out
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        stride, scale, has_res, has_rb, has_b, res_period = ctx.cfg
+        stride, scale, has_res, has_rb, has_b, res_period, taps = ctx.cfg
         N, H, W, IC = x.shape
         OC = weight.shape[0]
         dy = dy.contiguous()
@@ -243,25 +256,33 @@ class _Conv3x3(torch.autograd.Function):
             g = dy
         dx = None
         if ctx.needs_input_grad[0]:
-            wt = packed_conv_weight(weight, True)
+            wt = packed_weight(weight, True, taps)
             dx = torch.empty_like(x)
-            _conv_fwd(g, wt, None, None, None, dx, N, OH, OW, OC, _up(OC, 64), H, W, IC, IC, stride, True, 1.0)
-        dW = _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride) if ctx.needs_input_grad[1] else None
-        per, tot = _chansum(g, has_rb) if (has_b or has_rb) else (None, None)
+            _conv_fwd(g, wt, None, None, None, dx, N, OH, OW, OC, _up(OC, 64), H, W, IC, IC, stride, True, 1.0, 0,
+                      taps)
+        dW = None
+        if ctx.needs_input_grad[1]:
+            dW = _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps).reshape(weight.shape)
+        if has_b or has_rb:
+            # 1x1 "images" are rows of one big image for the channel sums
+            gg = g if (taps == 9 or has_rb) else g.reshape(1, N * OH * OW, 1, OC)
+            per, tot = _chansum(gg, has_rb)
+        else:
+            per, tot = None, None
         db = tot if (has_b and ctx.needs_input_grad[2]) else None
         drb = per if has_rb else None
         dres = None
         if has_res:
             dres = g if not res_period else \
                 g.reshape(N // res_period, res_period, *g.shape[1:]).float().sum(0).to(g.dtype)
-        return dx, dW, db, None, dres, None, drb, None
+        return dx, dW, db, None, dres, None, drb, None, None
 
 
 def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=None, res_period=0):
     _need_bf16(x, residual)
     OC, IC = weight.shape[0], weight.shape[1]
     if IC % 8 == 0 and OC % 8 == 0:
-        return _Conv3x3.apply(x, weight, bias, stride, residual, out_scale, row_bias, res_period)
+        return _Conv.apply(x, weight, bias, stride, residual, out_scale, row_bias, res_period, 9)
     # stem (IC=3) / head (OC=3): zero-pad channels to a multiple of 8 so every
     # access stays 16-byte vectorised; the padding costs < 0.1 % of FLOPs.
     ICe, OCe = _up(IC, 8), _up(OC, 8)
@@ -270,7 +291,7 @@ def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=No
     be = F.pad(bias, (0, OCe - OC)) if bias is not None else None
     re = F.pad(residual, (0, OCe - OC)) if residual is not None else None
     rbe = F.pad(row_bias, (0, OCe - OC)) if row_bias is not None else None
-    y = _Conv3x3.apply(xe, we, be, stride, re, out_scale, rbe, res_period)
+    y = _Conv.apply(xe, we, be, stride, re, out_scale, rbe, res_period, 9)
     return y[..., :OC].contiguous() if OCe != OC else y
 
 
@@ -322,8 +343,18 @@ class _Linear(torch.autograd.Function):
 
 
 def linear(x, weight, bias, residual=None, out_scale=1.0):
+    """Per-pixel dense layer on the MFMA implicit-GEMM kernel (1-tap mode):
+    fused bias + residual + scale epilogue, split-K weight gradient."""
     _need_bf16(x, residual)
-    return _Linear.apply(x, weight, bias, residual, out_scale)
+    shp = x.shape
+    IC, OC = shp[-1], weight.shape[0]
+    if IC % 8 or OC % 8:
+        return _Linear.apply(x, weight, bias, residual, out_scale)
+    rows = x.numel() // IC
+    x4 = x.reshape(rows, 1, 1, IC)
+    r4 = residual.reshape(rows, 1, 1, OC) if residual is not None else None
+    y = _Conv.apply(x4, weight, bias, 1, r4, out_scale, None, 0, 1)
+    return y.reshape(*shp[:-1], OC)
 
 
 # ------------------------------------------------------------ attention ----
