@@ -106,6 +106,9 @@ conv_igemm_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const floa
       if (!TRANS) {
         ih = poh[i] * stride + kh - 1;
         iw = pow_[i] * stride + kw - 1;
+      } else if (stride == 1) {      // wave-uniform: no integer division in the common case
+        ih = poh[i] + 1 - kh;
+        iw = pow_[i] + 1 - kw;
       } else {
         int th = poh[i] + 1 - kh, tw = pow_[i] + 1 - kw;
         ok = ok && th >= 0 && tw >= 0 && (th % stride) == 0 && (tw % stride) == 0;

@@ -94,6 +94,8 @@ def packed_conv_weight(w: torch.Tensor, trans: bool) -> torch.Tensor:
 
 
 def bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    if w.dim() == 1:
+        return _cached(w, "bf16", lambda: w.detach().to(BF16))
     return _cached(w, "bf16", lambda: w.detach().reshape(w.shape[0], -1).to(BF16))
 
 
@@ -313,7 +315,7 @@ class _Linear(torch.autograd.Function):
         x2 = x.reshape(-1, shp[-1])
         wb = bf16_weight(weight)
         if bias is not None:
-            y = torch.addmm(bias.to(BF16), x2, wb.t())
+            y = torch.addmm(bf16_weight(bias), x2, wb.t())
         else:
             y = torch.mm(x2, wb.t())
         if residual is not None or out_scale != 1.0:
@@ -335,26 +337,34 @@ class _Linear(torch.autograd.Function):
                  "scale")
             g = gs
         wb = bf16_weight(weight)
+        OC, IC = g.shape[-1], x2.shape[-1]
+        rows = g.shape[0]
         dx = torch.mm(g, wb).reshape(shp) if ctx.needs_input_grad[0] else None
-        dW = _mm_f32(g.t(), x2).reshape(weight.shape) if ctx.needs_input_grad[1] else None
-        db = g.float().sum(0) if has_b and ctx.needs_input_grad[2] else None
-        dres = g.reshape(*shp[:-1], g.shape[-1]) if has_res else None
+        dW = db = None
+        if IC % 8 == 0 and OC % 8 == 0:
+            g = g.contiguous()
+            if ctx.needs_input_grad[1]:
+                dW = _wgrad(g.reshape(rows, 1, 1, OC), x2.contiguous().reshape(rows, 1, 1, IC), OC, IC, rows, 1, 1,
+                            1, 1, 1, 1).reshape(weight.shape)
+            if has_b and ctx.needs_input_grad[2]:
+                db = _chansum(g.reshape(1, rows, 1, OC), False)[1]
+        else:
+            if ctx.needs_input_grad[1]:
+                dW = _mm_f32(g.t(), x2).reshape(weight.shape)
+            if has_b and ctx.needs_input_grad[2]:
+                db = g.float().sum(0)
+        dres = g.reshape(*shp[:-1], OC) if has_res else None
         return dx, dW, db, dres, None
 
 
 def linear(x, weight, bias, residual=None, out_scale=1.0):
-    """Per-pixel dense layer on the MFMA implicit-GEMM kernel (1-tap mode):
-    fused bias + residual + scale epilogue, split-K weight gradient."""
+    """Per-pixel dense layer.  Forward and input-gradient are plain GEMMs on
+    hipBLASLt (≈1 PF/s on these shapes); the weight gradient -- a GEMM whose
+    reduction runs over every pixel of the batch (K up to 5e5), where
+    hipBLASLt drops to 45-240 TF/s -- uses the split-K MFMA kernel, and the
+    bias / residual epilogues are fused HIP kernels."""
     _need_bf16(x, residual)
-    shp = x.shape
-    IC, OC = shp[-1], weight.shape[0]
-    if IC % 8 or OC % 8:
-        return _Linear.apply(x, weight, bias, residual, out_scale)
-    rows = x.numel() // IC
-    x4 = x.reshape(rows, 1, 1, IC)
-    r4 = residual.reshape(rows, 1, 1, OC) if residual is not None else None
-    y = _Conv.apply(x4, weight, bias, 1, r4, out_scale, None, 0, 1)
-    return y.reshape(*shp[:-1], OC)
+    return _Linear.apply(x, weight, bias, residual, out_scale)
 
 
 # ------------------------------------------------------------ attention ----
