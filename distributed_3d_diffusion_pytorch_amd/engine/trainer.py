@@ -63,6 +63,19 @@ class Trainer:
         self.reducer = None
         if W > 1:
             self.reducer = GradReducer(self.flat, cfg.dist.bucket_mb, cfg.dist.first_bucket_mb, cfg.dist.grad_dtype)
+        # Direct gradient sink: HIP weight-gradient kernels deposit straight
+        # into the flat gradient buffer (no AccumulateGrad adds) and report
+        # completion to the bucketed reducer themselves.
+        self.sink = None
+        if dev.type == "cuda" and self.dtype == torch.bfloat16 and cfg.backend != "torch" and \
+                os.environ.get("D3D_GRAD_SINK", "1") == "1":
+            from ..ops.gradsink import SINK
+            views = [self.flat.view(self.flat.grad, i) for i in range(len(self.flat.params))]
+            notify = self.reducer.mark_ready if self.reducer is not None else None
+            SINK.attach(self.flat.params, views, notify)
+            if self.reducer is not None:
+                self.reducer.sink = SINK
+            self.sink = SINK
         oc = cfg.optim
         self.optim = FusedAdam(self.flat, oc.lr, oc.betas, oc.eps, oc.weight_decay,
                                ema_decay_for(cfg.global_batch, oc.ema_halflife_examples))
@@ -143,6 +156,8 @@ class Trainer:
         if self.sched is None:
             g["lr"] = warmup_lr(self.step, self.warmup_steps, self.cfg.optim.lr)
         self.model.train()
+        if self.sink is not None:
+            self.sink.reset()
         B = img.shape[0]
         mb = self.cfg.micro_batch if 0 < self.cfg.micro_batch < B else B
         chunks = [(s, min(s + mb, B)) for s in range(0, B, mb)]

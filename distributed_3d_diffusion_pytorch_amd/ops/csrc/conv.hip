@@ -212,6 +212,174 @@ conv_igemm_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const floa
   }
 }
 
+// ---------------------------------------------------- glds pipeline ------
+// Same GEMM as conv_igemm_k, but operand tiles go global -> LDS directly
+// (global_load_lds_dwordx4: no VGPR staging, no ds_write), double-buffered
+// with a COUNTED vmcnt so the next tile's DMA stays in flight across the raw
+// s_barrier while the current tile's MFMAs run.  LDS images are lane-linear
+// per wave instruction (8 rows x 128 B = 1 KiB); the XOR swizzle lives in the
+// per-lane SOURCE address (lane L of an instruction loads logical chunk
+// (L%8)^(L/8) of its row), read back with the same swizzle -> conflict-free
+// ds_read_b128.  Padding / out-of-range taps read from a 16-byte zero page.
+template <int TAPS, bool TRANS>
+__global__ void __launch_bounds__(256, 2)
+conv_glds_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
+            const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
+            const bf16* __restrict__ zero16, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC,
+            int ldo, int stride, float scale, int res_nmod) {
+  constexpr int BM = 128, BN = 128, BKk = 64;
+  constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
+  constexpr int STAGE = (BM + BN) * BKk;           // elements per stage
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
+  typedef __attribute__((address_space(3))) void lds_void;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const long Mpix = (long)Nimg * OH * OW;
+  const int nbx = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    int q = nbx / 8, r = nbx % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const long n0 = (long)bid * BN;
+  const int m0 = blockIdx.y * BM;
+  const int Kp = TAPS * ICp;
+
+  // glds lane mapping: wave w issues instructions i=0..3 covering rows
+  // (w*4+i)*8 .. +7 of each tile; lane L -> row +L/8, logical chunk (L%8)^(L/8)
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;
+  int prow[4];
+  int pn[4], poh[4], pw[4];
+  bool pval[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    prow[i] = (wave * 4 + i) * 8 + lrow;
+    long p = n0 + prow[i];
+    pval[i] = p < Mpix;
+    long pp = pval[i] ? p : 0;
+    pw[i] = (int)(pp % OW);
+    long t = pp / OW;
+    poh[i] = (int)(t % OH);
+    pn[i] = (int)(t / OH);
+  }
+  const bf16* wrow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) wrow[i] = Wp + (long)(m0 + prow[i]) * Kp + lchunk * 8;
+
+  auto issue = [&](int kstep, int stage) {
+    const int tap = TAPS == 9 ? kstep / (ICp / BKk) : 0;
+    const int c0 = (TAPS == 9 ? kstep % (ICp / BKk) : kstep) * BKk;
+    const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
+    bf16* sA = smem + stage * STAGE;
+    bf16* sB = sA + BM * BKk;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(wrow[i] + tap * ICp + c0),
+                                       (lds_void*)(sA + (wave * 4 + i) * 8 * BKk), 16, 0, 0);
+    const int c = c0 + lchunk * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int ih, iw;
+      bool ok = pval[i] && c < IC;
+      if (!TRANS) {
+        ih = poh[i] * stride + kh - 1;
+        iw = pw[i] * stride + kw - 1;
+      } else if (stride == 1) {
+        ih = poh[i] + 1 - kh;
+        iw = pw[i] + 1 - kw;
+      } else {
+        int th = poh[i] + 1 - kh, tw = pw[i] + 1 - kw;
+        ok = ok && th >= 0 && tw >= 0 && (th % stride) == 0 && (tw % stride) == 0;
+        ih = th / stride;
+        iw = tw / stride;
+      }
+      ok = ok && ih >= 0 && ih < IH && iw >= 0 && iw < IW;
+      const bf16* src = ok ? I + (((long)pn[i] * IH + ih) * IW + iw) * IC + c : zero16;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sB + (wave * 4 + i) * 8 * BKk), 16, 0, 0);
+    }
+  };
+  auto swz = [](int row, int chunk) { return row * BKk + ((chunk ^ (row & 7)) << 3); };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = Kp / BKk;
+  const int fr = lane & 15, fq = lane >> 4;
+  issue(0, 0);
+  for (int ks = 0; ks < nk; ++ks) {
+    const int st = ks & 1;
+    if (ks + 1 < nk) {
+      issue(ks + 1, st ^ 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // retire stage st, keep st^1 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const bf16* a = smem + st * STAGE;
+    const bf16* b = a + BM * BKk;
+#pragma unroll
+    for (int kk = 0; kk < BKk / 32; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a + swz(wm * WM + i * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(b + swz(wn * WN + j * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                             // stage st free for reuse
+  }
+
+  const int OHW = OH * OW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    long pix = n0 + wn * WN + j * 16 + fr;
+    if (pix >= Mpix) continue;
+    int img = (int)(pix / OHW);
+    const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int co = m0 + wm * WM + i * 16 + fq * 4;
+      if (co >= OC) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int cc = co + e < OC ? co + e : OC - 1;
+        float t = acc[i][j][e] + (bias ? bias[cc] : 0.f);
+        if (row_bias) t += row_bias[(long)img * OC + cc];
+        v[e] = t;
+      }
+      bf16* dst = O + pix * ldo + co;
+      if (co + 3 < OC && (ldo & 3) == 0) {
+        if (res) {
+          bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+        }
+        bf16x4 o4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o4[e] = (bf16)(v[e] * scale);
+        *reinterpret_cast<bf16x4*>(dst) = o4;
+      } else {
+        for (int e = 0; e < 4 && co + e < OC; ++e) {
+          float t = v[e];
+          if (res) t += (float)res[rpix * ldo + co + e];
+          dst[e] = (bf16)(t * scale);
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------ wgrad ------
 constexpr int WBK = 32;           // pixels per k-step
 constexpr int WPAD = 16;          // bf16 elements of row padding (32 B)
@@ -223,7 +391,8 @@ __device__ __forceinline__ s16x4 ds_tr(const bf16* p) {
 template <int BM, int BN, int TAPS>
 __global__ void __launch_bounds__(256, 2)
 conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __restrict__ ws, int Nimg, int IH,
-             int IW, int IC, int OH, int OW, int OC, int stride, int pix_per_split, int ncb) {
+             int IW, int IC, int OH, int OW, int OC, int stride, int pix_per_split, int ncb,
+             float* __restrict__ bws) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int ALD = WBK * BM / 8 / 256, BLD = WBK * BN / 8 / 256;
@@ -304,11 +473,20 @@ conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __r
     swrite(0);
   }
   __syncthreads();
+  // fused bias gradient: the first (tap, ci) block column of every split also
+  // sums its dY tile over pixels (thread -> column tid%BM, rows half tid/BM)
+  const bool do_bias = bws != nullptr && blockIdx.x == 0;
+  float bacc = 0.f;
   for (long s = 0; s < nsteps; ++s) {
     const int buf = (int)(s & 1);
     if (s + 1 < nsteps) gload(p_begin + (s + 1) * WBK);
     const bf16* a = As + buf * WBK * AS;
     const bf16* b = Bs + buf * WBK * BSt;
+    if (do_bias) {
+      const int col = tid % BM, r0 = (tid / BM) * (WBK * BM / 256);
+#pragma unroll
+      for (int r = 0; r < WBK * BM / 256; ++r) bacc += (float)a[(r0 + r) * AS + col];
+    }
     bf16x8 af[TM], bfr[TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -334,6 +512,10 @@ conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __r
     if (s + 1 < nsteps) swrite(buf ^ 1);
     __syncthreads();
   }
+  if (do_bias) {
+    const int col = tid % BM, half = tid / BM;
+    if (m0 + col < OC) bws[((long)split * (256 / BM) + half) * OC + m0 + col] = bacc;
+  }
   // partial slab: ws[split][co][tap*IC + ci]
   const int fr = lane & 15, fq = lane >> 4;
   const long KW = (long)TAPS * IC;
@@ -354,8 +536,16 @@ conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __r
 
 // sum the split slabs and write dW in OIHW fp32 layout (optionally accumulate)
 __global__ void wgrad_reduce_k(const float* __restrict__ ws, float* __restrict__ dW, int OC, int IC, int splits,
-                               int accumulate, int taps) {
+                               int accumulate, int taps, const float* __restrict__ bws, float* __restrict__ db,
+                               int brows) {
   long total = (long)OC * IC * taps;
+  if (db) {
+    for (long c = blockIdx.x * (long)blockDim.x + threadIdx.x; c < OC; c += (long)gridDim.x * blockDim.x) {
+      float s = 0.f;
+      for (int k = 0; k < brows; ++k) s += bws[(long)k * OC + c];
+      db[c] = accumulate ? db[c] + s : s;
+    }
+  }
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
     // t indexes the slab layout [co][tap][ci] (coalesced reads)
     int ci = (int)(t % IC);
@@ -434,12 +624,34 @@ __global__ void pack_w_k(const float* __restrict__ w, bf16* __restrict__ out, in
 // I: [N, IH, IW, IC] bf16 (IC % 8 == 0), Wp: packed [OCp][taps][ICp] bf16 with
 // OCp % 128 == 0 and ICp % 64 == 0.  O: [N, OH, OW, ldo] bf16.  taps = 9 (3x3)
 // or 1 (1x1 / per-pixel linear).
+static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline
+static const bf16* g_zero16 = nullptr;
+
+D3D_API int d3d_set_conv_impl(int impl, const void* zero16) {
+  g_conv_impl = impl;
+  if (zero16) g_zero16 = (const bf16*)zero16;
+  return 0;
+}
+
 D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
                      void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
                      int trans, float scale, int res_nmod, int taps, hipStream_t st) {
   long Mpix = (long)N * OH * OW;
   constexpr int BM = 128, BN = 128;
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM));
+  if (g_conv_impl == 1 && g_zero16) {
+#define GLDS(TP, TR)                                                                                             \
+  hipLaunchKernelGGL((conv_glds_k<TP, TR>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,        \
+                     row_bias, (const bf16*)res, (bf16*)O, g_zero16, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, \
+                     scale, res_nmod)
+    if (taps == 9) {
+      if (trans) GLDS(9, true); else GLDS(9, false);
+    } else {
+      if (trans) GLDS(1, true); else GLDS(1, false);
+    }
+#undef GLDS
+    return (int)hipGetLastError();
+  }
 #define LAUNCH(TR, TP)                                                                                             \
   hipLaunchKernelGGL((conv_igemm_k<BM, BN, TR, TP>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias, \
                      row_bias, (const bf16*)res, (bf16*)O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, scale,      \
@@ -481,23 +693,36 @@ D3D_API int d3d_conv_wgrad_plan(int N, int OH, int OW, int OC, int IC, int* spli
 
 // dY: [N, OH, OW, OC] bf16 (OC % 8 == 0); I: [N, IH, IW, IC] bf16.
 // ws: [splits][OC][taps*IC] fp32 workspace.  dW: [OC][IC][taps] fp32 (OIHW).
-D3D_API int d3d_conv_wgrad(const void* dY, const void* I, float* ws, float* dW, int N, int IH, int IW, int IC, int OH,
-                           int OW, int OC, int stride, int splits, int pix_per_split, int accumulate, int taps,
-                           hipStream_t st) {
+// ws: [splits][OC][taps*IC] + (db ? 2*splits*OC : 0) fp32 workspace.
+// dW (and db when non-null) are written (accumulate=0) or added to
+// (accumulate=1) -- the latter lets kernels deposit straight into the flat
+// gradient buffer across micro-batches.
+D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW, float* db, int N, int IH, int IW,
+                            int IC, int OH, int OW, int OC, int stride, int splits, int pix_per_split, int accumulate,
+                            int taps, hipStream_t st) {
   constexpr int BM = 128, BN = 128;
   int ncb = (IC + BN - 1) / BN;
   dim3 grid(taps * ncb, (OC + BM - 1) / BM, splits);
+  long total = (long)OC * IC * taps;
+  float* bws = db ? ws + (long)splits * total : nullptr;
   if (taps == 9)
     hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 9>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
-                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb);
+                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws);
   else
     hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 1>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
-                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb);
-  long total = (long)OC * IC * taps;
+                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws);
   long g = (total + 255) / 256;
   if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(wgrad_reduce_k, dim3((int)g), dim3(256), 0, st, ws, dW, OC, IC, splits, accumulate, taps);
+  hipLaunchKernelGGL(wgrad_reduce_k, dim3((int)g), dim3(256), 0, st, ws, dW, OC, IC, splits, accumulate, taps, bws,
+                     db, splits * (256 / BM));
   return (int)hipGetLastError();
+}
+
+D3D_API int d3d_conv_wgrad(const void* dY, const void* I, float* ws, float* dW, int N, int IH, int IW, int IC, int OH,
+                           int OW, int OC, int stride, int splits, int pix_per_split, int accumulate, int taps,
+                           hipStream_t st) {
+  return d3d_conv_wgrad2(dY, I, ws, dW, nullptr, N, IH, IW, IC, OH, OW, OC, stride, splits, pix_per_split,
+                         accumulate, taps, st);
 }
 
 D3D_API int d3d_conv3x3_wgrad(const void* dY, const void* I, float* ws, float* dW, int N, int IH, int IW, int IC,

@@ -385,10 +385,10 @@ D3D_API int d3d_gn_film(const void* x, const float* stats, const float* gamma, c
 // mode: 0 plain, 1 silu, 2 film.  Workspaces: chan_part [N*nchunks*C*2],
 // grp_part [N*nchunks*G*2 + 64*2*C] (tail = column-sum partials), coef [N*G*2].  Outputs dx (bf16), dgamma/dbeta
 // (fp32 [C]) and, for mode 2, dss (bf16 [N,P,2C]).
-D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, const float* stats,
-                       const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
-                       unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
-                       float* grp_part, float* coef, hipStream_t st) {
+D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss, const float* stats,
+                        const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
+                        unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
+                        float* grp_part, float* coef, int accumulate, hipStream_t st) {
   Plan p = make_plan(N, P, C);
   size_t lds = (size_t)p.rpi * C * 4 * sizeof(float);
   dim3 g(p.nchunks, N);
@@ -405,7 +405,8 @@ D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, 
   // dgamma/dbeta: chan_part is [N*nchunks][C][2] -> column sums over 2C
   // interleaved columns (coef's workspace is reused after the apply kernel
   // has been enqueued? no: use the tail of chan_part's allocation instead)
-  d3d_colsum(chan_part, (long)N * p.nchunks, 2 * C, grp_part + (long)N * p.nchunks * G * 2, dgamma, dbeta, 0, st);
+  d3d_colsum(chan_part, (long)N * p.nchunks, 2 * C, grp_part + (long)N * p.nchunks * G * 2, dgamma, dbeta,
+             accumulate, st);
   long nvec = (long)N * P * C / 8;
 #define APP(M)                                                                                                  \
   hipLaunchKernelGGL(gn_bwd_apply_k<M>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, (const bf16*)dy, \
@@ -416,4 +417,12 @@ D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, 
   else APP(2);
 #undef APP
   return (int)hipGetLastError();
+}
+
+D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, const float* stats,
+                       const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
+                       unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
+                       float* grp_part, float* coef, hipStream_t st) {
+  return d3d_gn_bwd2(mode, x, dy, ss, stats, gamma, beta, N, P, C, G, p_drop, seed, dx, dss, dgamma, dbeta,
+                     chan_part, grp_part, coef, 0, st);
 }

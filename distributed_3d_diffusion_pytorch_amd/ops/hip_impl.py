@@ -17,10 +17,32 @@ import torch.nn.functional as F
 
 from ._backend import load_library
 from . import torch_impl as _t
+from .gradsink import SINK
 
 _lib = load_library(required=True)
 BF16 = torch.bfloat16
 F32 = torch.float32
+
+_ZERO_PAGE: Dict[int, torch.Tensor] = {}
+
+
+def set_conv_impl(impl: str) -> None:
+    """'glds' (default: direct-to-LDS pipelined MFMA kernel) or 'reg'
+    (register-staged variant, kept for A/B measurements)."""
+    dev = torch.cuda.current_device()
+    if dev not in _ZERO_PAGE:
+        _ZERO_PAGE[dev] = torch.zeros(64, dtype=BF16, device="cuda")
+    _chk(_lib.d3d_set_conv_impl(1 if impl == "glds" else 0, _ZERO_PAGE[dev].data_ptr()), "set_conv_impl")
+
+
+_IMPL_SET = [False]
+
+
+def _ensure_impl():
+    if not _IMPL_SET[0]:
+        import os
+        set_conv_impl(os.environ.get("D3D_CONV_IMPL", "glds"))
+        _IMPL_SET[0] = True
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -123,14 +145,20 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed):
     dev = x.device
     dx = torch.empty_like(x)
     dss = torch.empty_like(ss) if ss is not None else None
-    dg = torch.empty(C, dtype=F32, device=dev)
-    db = torch.empty(C, dtype=F32, device=dev)
+    tg, tb = SINK.target(w), SINK.target(b)
+    direct = tg is not None and tb is not None
+    dg = tg if direct else torch.empty(C, dtype=F32, device=dev)
+    db = tb if direct else torch.empty(C, dtype=F32, device=dev)
     cp = torch.empty(N * nch * C * 2, dtype=F32, device=dev)
     gp = torch.empty(N * nch * G * 2 + 64 * 2 * C, dtype=F32, device=dev)
     coef = torch.empty(N * G * 2, dtype=F32, device=dev)
-    _chk(_lib.d3d_gn_bwd(mode, x.data_ptr(), dy.data_ptr(), _ptr(ss), stats.data_ptr(), w.data_ptr(), b.data_ptr(),
-                         N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), dg.data_ptr(), db.data_ptr(),
-                         cp.data_ptr(), gp.data_ptr(), coef.data_ptr(), _st()), "gn_bwd")
+    _chk(_lib.d3d_gn_bwd2(mode, x.data_ptr(), dy.data_ptr(), _ptr(ss), stats.data_ptr(), w.data_ptr(),
+                          b.data_ptr(), N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), dg.data_ptr(),
+                          db.data_ptr(), cp.data_ptr(), gp.data_ptr(), coef.data_ptr(), int(direct), _st()), "gn_bwd")
+    if direct:
+        SINK.done(w)
+        SINK.done(b)
+        return dx, dss, None, None
     return dx, dss, dg, db
 
 
@@ -145,6 +173,8 @@ class _GroupNorm(torch.autograd.Function):
                                N, H * W, C, groups, int(silu), _st()), "gn_apply")
         ctx.save_for_backward(x, weight, bias, stats)
         ctx.cfg = (groups, 1 if silu else 0)
+        SINK.use(weight, ctx.needs_input_grad[1])
+        SINK.use(bias, ctx.needs_input_grad[2])
         return y
 
     @staticmethod
@@ -172,6 +202,8 @@ class _GNFiLM(torch.autograd.Function):
                               y.data_ptr(), N, H * W, C, groups, float(p), int(seed), _st()), "gn_film")
         ctx.save_for_backward(x, weight, bias, ss, stats)
         ctx.cfg = (groups, p, seed)
+        SINK.use(weight, ctx.needs_input_grad[1])
+        SINK.use(bias, ctx.needs_input_grad[2])
         return y
 
     @staticmethod
@@ -191,18 +223,25 @@ def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=Fa
 # ----------------------------------------------------------------- conv ----
 def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale, res_nmod=0,
               taps=9):
+    _ensure_impl()
     _chk(_lib.d3d_conv(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
                        IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), taps, _st()), "conv")
 
 
-def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9):
+def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9, want_bias=False, dW=None, db=None, accumulate=False):
+    """Split-K weight gradient (+ fused bias column sums).  Writes into the
+    given dW/db (accumulating when asked) or into fresh fp32 tensors."""
     s, pps = ctypes.c_int(), ctypes.c_int()
     _lib.d3d_conv_wgrad_plan2(N, OH, OW, OC, IC, taps, ctypes.byref(s), ctypes.byref(pps))
-    ws = torch.empty(s.value * OC * taps * IC, dtype=F32, device=x.device)
-    dW = torch.empty(OC, IC, taps, dtype=F32, device=x.device)
-    _chk(_lib.d3d_conv_wgrad(g.data_ptr(), x.data_ptr(), ws.data_ptr(), dW.data_ptr(), N, H, W, IC, OH, OW, OC,
-                             stride, s.value, pps.value, 0, taps, _st()), "conv_wgrad")
-    return dW
+    extra = 2 * s.value * OC if (want_bias or db is not None) else 0
+    ws = torch.empty(s.value * OC * taps * IC + extra, dtype=F32, device=x.device)
+    if dW is None:
+        dW = torch.empty(OC, IC, taps, dtype=F32, device=x.device)
+    if want_bias and db is None:
+        db = torch.empty(OC, dtype=F32, device=x.device)
+    _chk(_lib.d3d_conv_wgrad2(g.data_ptr(), x.data_ptr(), ws.data_ptr(), dW.data_ptr(), _ptr(db), N, H, W, IC, OH,
+                              OW, OC, stride, s.value, pps.value, int(accumulate), taps, _st()), "conv_wgrad")
+    return dW, db
 
 
 def _chansum(g, per_image: bool):
@@ -241,6 +280,9 @@ class _Conv(torch.autograd.Function):
                   res_period, taps)
         ctx.save_for_backward(x, weight)
         ctx.cfg = (stride, out_scale, residual is not None, row_bias is not None, bias is not None, res_period, taps)
+        ctx.bias_param = bias
+        SINK.use(weight, ctx.needs_input_grad[1])
+        SINK.use(bias, ctx.needs_input_grad[2])
         return out
 
     @staticmethod
@@ -262,17 +304,38 @@ class _Conv(torch.autograd.Function):
             dx = torch.empty_like(x)
             _conv_fwd(g, wt, None, None, None, dx, N, OH, OW, OC, _up(OC, 64), H, W, IC, IC, stride, True, 1.0, 0,
                       taps)
-        dW = None
-        if ctx.needs_input_grad[1]:
-            dW = _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps).reshape(weight.shape)
-        if has_b or has_rb:
-            # 1x1 "images" are rows of one big image for the channel sums
-            gg = g if (taps == 9 or has_rb) else g.reshape(1, N * OH * OW, 1, OC)
-            per, tot = _chansum(gg, has_rb)
-        else:
-            per, tot = None, None
-        db = tot if (has_b and ctx.needs_input_grad[2]) else None
-        drb = per if has_rb else None
+        bias = ctx.bias_param
+        need_w, need_b = ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]
+        dW = db = drb = None
+        tw = SINK.target(weight) if need_w else None
+        tb = SINK.target(bias) if need_b else None
+        if has_rb:
+            # per-image bias gradient (conditioning convs) -> channel sums
+            per, tot = _chansum(g, True)
+            drb = per
+            if need_b:
+                if tb is not None:
+                    tb.add_(tot)
+                    SINK.done(bias)
+                else:
+                    db = tot
+            need_b = False
+        if need_w:
+            direct = tw is not None and (not need_b or tb is not None)
+            if direct:
+                _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, dW=tw.view(OC, IC, taps),
+                       db=tb if need_b else None, accumulate=True)
+                SINK.done(weight)
+                if need_b:
+                    SINK.done(bias)
+            else:
+                dW, db2 = _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, want_bias=need_b)
+                dW = dW.reshape(weight.shape)
+                if need_b:
+                    db = db2
+        elif need_b:
+            gg = g if taps == 9 else g.reshape(1, N * OH * OW, 1, OC)
+            db = _chansum(gg, False)[1]
         dres = None
         if has_res:
             dres = g if not res_period else \
@@ -324,6 +387,10 @@ class _Linear(torch.autograd.Function):
                  "add_scale")
         ctx.save_for_backward(x2, weight)
         ctx.cfg = (shp, out_scale, residual is not None, bias is not None)
+        ctx.bias_param = bias
+        if shp[-1] % 8 == 0 and wb.shape[0] % 8 == 0:
+            SINK.use(weight, ctx.needs_input_grad[1])
+            SINK.use(bias, ctx.needs_input_grad[2])
         return y.reshape(*shp[:-1], wb.shape[0])
 
     @staticmethod
@@ -341,13 +408,24 @@ class _Linear(torch.autograd.Function):
         rows = g.shape[0]
         dx = torch.mm(g, wb).reshape(shp) if ctx.needs_input_grad[0] else None
         dW = db = None
-        if IC % 8 == 0 and OC % 8 == 0:
+        bias = ctx.bias_param
+        need_w, need_b = ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]
+        if IC % 8 == 0 and OC % 8 == 0 and need_w:
             g = g.contiguous()
-            if ctx.needs_input_grad[1]:
-                dW = _wgrad(g.reshape(rows, 1, 1, OC), x2.contiguous().reshape(rows, 1, 1, IC), OC, IC, rows, 1, 1,
-                            1, 1, 1, 1).reshape(weight.shape)
-            if has_b and ctx.needs_input_grad[2]:
-                db = _chansum(g.reshape(1, rows, 1, OC), False)[1]
+            g4, x4 = g.reshape(rows, 1, 1, OC), x2.contiguous().reshape(rows, 1, 1, IC)
+            tw = SINK.target(weight)
+            tb = SINK.target(bias) if need_b else None
+            if tw is not None and (not need_b or tb is not None):
+                _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, dW=tw.view(OC, IC, 1), db=tb, accumulate=True)
+                SINK.done(weight)
+                if need_b:
+                    SINK.done(bias)
+            else:
+                dW, db = _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, want_bias=need_b)
+                dW = dW.reshape(weight.shape)
+        elif IC % 8 == 0 and OC % 8 == 0:
+            if need_b:
+                db = _chansum(g.contiguous().reshape(1, rows, 1, OC), False)[1]
         else:
             if ctx.needs_input_grad[1]:
                 dW = _mm_f32(g.t(), x2).reshape(weight.shape)

@@ -61,6 +61,7 @@ class GradReducer:
         for b, bk in enumerate(self.buckets):
             for i in bk["params"]:
                 self.param_bucket[i] = b
+        self.sink = None            # ops.gradsink.GradSink delivering kernel-deposited grads
         self._pending = [0] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
         self._works: List = []
@@ -79,14 +80,21 @@ class GradReducer:
         self._works = []
 
     def _make_hook(self, i: int):
-        def hook(_p):
-            if not self.enabled or self.world == 1:
-                return
-            b = self.param_bucket[i]
-            self._pending[b] -= 1
-            if self._pending[b] == 0:
-                self._launch(b)
+        def hook(p):
+            if self.sink is not None and self.sink.was_used(p):
+                return          # the sink reports this parameter itself
+            self.mark_ready(i)
         return hook
+
+    def mark_ready(self, i: int) -> None:
+        """Parameter i's gradient is complete in the flat buffer (called by the
+        autograd hook, or by the HIP gradient sink for kernel-deposited grads)."""
+        if not self.enabled or self.world == 1:
+            return
+        b = self.param_bucket[i]
+        self._pending[b] -= 1
+        if self._pending[b] == 0:
+            self._launch(b)
 
     def _launch(self, b: int) -> None:
         if self._launched[b]:

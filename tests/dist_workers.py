@@ -76,3 +76,48 @@ def fault_injection(out_dir):
     # only reached if the dead peer went unnoticed
     with open(os.path.join(out_dir, f"survived{ctx.rank}.txt"), "w") as f:
         f.write("1")
+
+
+def gpu_sink_reducer(out_dir):
+    """Two ranks sharing one GPU over gloo: HIP kernels + direct gradient sink +
+    bucketed reducer must equal the manual all-reduce of plain autograd grads."""
+    import torch
+    from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup, FlatParams, GradReducer
+    from distributed_3d_diffusion_pytorch_amd.ops.gradsink import SINK
+    from distributed_3d_diffusion_pytorch_amd.models import XUNet
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    ctx = init_distributed("gloo", 120, use_gpu=True)
+    torch.manual_seed(0)
+    m = XUNet(H=32, W=32, ch=128).cuda().eval()
+    with torch.no_grad():
+        for p in m.parameters():
+            if p.abs().sum() == 0:
+                p.normal_(0, 0.02)
+    m.compute_dtype = torch.bfloat16
+    flat = FlatParams(list(m.parameters()))
+    red = GradReducer(flat, bucket_mb=8.0, first_bucket_mb=1.0)
+    img, R, t, K = next(SyntheticBatches(2, 32, "cuda", seed=ctx.rank))
+    batch = {"x": img[:, 0], "z": img[:, 1], "logsnr": torch.tensor([[20.0, 1.0], [20.0, -2.0]], device="cuda"),
+             "R": R, "t": t, "K": K}
+    mask = torch.tensor([True, False], device="cuda")
+    # reference: plain autograd grads, manual all-reduce
+    with red.no_sync():
+        m(batch, cond_mask=mask).float().square().mean().backward()
+    ref = flat.grad.clone()
+    torch.distributed.all_reduce(ref)
+    flat.zero_grad()
+    red.reset()
+    # sink path
+    views = [flat.view(flat.grad, i) for i in range(len(flat.params))]
+    SINK.attach(flat.params, views, red.mark_ready)
+    red.sink = SINK
+    SINK.reset()
+    m(batch, cond_mask=mask).float().square().mean().backward()
+    red.finish()
+    got = flat.grad.clone()
+    SINK.detach()
+    cos = torch.nn.functional.cosine_similarity(got, ref, dim=0).item()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    with open(os.path.join(out_dir, f"g{ctx.rank}.txt"), "w") as f:
+        f.write(f"{cos} {rel}")
+    cleanup()

@@ -271,3 +271,14 @@ def test_model_hip_vs_torch_backend():
     assert rel(outs[0], outs[1]) < 5e-2
     cos = torch.nn.functional.cosine_similarity(grads[0], grads[1], dim=0).item()
     assert cos > 0.98, cos
+
+
+def test_grad_sink_and_reducer_two_ranks_one_gpu(tmp_path):
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import dist_workers as W
+    from distributed_3d_diffusion_pytorch_amd.parallel import spawn
+    spawn(W.gpu_sink_reducer, 2, (str(tmp_path),))
+    for r in range(2):
+        cos, rel = map(float, open(tmp_path / f"g{r}.txt").read().split())
+        assert cos > 0.9999 and rel < 1e-2, (r, cos, rel)

@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64, help="examples (frame batch N = 2*batch)")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--torch", action="store_true", help="also time the torch composition")
+    ap.add_argument("--only_glds_check", action="store_true")
     a = ap.parse_args()
     dev = "cuda"
     N = 2 * a.batch
@@ -76,9 +77,12 @@ def main():
         y = torch.empty(N, OH, OH, Co, dtype=BF, device=dev)
         g = torch.randn(N, OH, OH, Co, device=dev).to(BF)
         if "conv" in ops:
-            rep("conv_fwd", shp, "hip", timeit(lambda: H._conv_fwd(x, wp, b, None, None, y, N, Hh, Hh, Ci,
-                                                                    H._up(Ci, 64), OH, OH, Co, Co, s, False, 1.0),
-                                               a.iters), fl)
+            for impl in ("reg", "glds"):
+                H.set_conv_impl(impl)
+                rep("conv_fwd", shp, "hip-" + impl,
+                    timeit(lambda: H._conv_fwd(x, wp, b, None, None, y, N, Hh, Hh, Ci, H._up(Ci, 64), OH, OH, Co, Co,
+                                               s, False, 1.0), a.iters), fl)
+            H.set_conv_impl("glds")
             if a.torch:
                 wb, bb = w.to(BF), b.to(BF)
                 xc = x.permute(0, 3, 1, 2)
@@ -87,9 +91,12 @@ def main():
         if "dgrad" in ops and s == 1:
             wt = H.packed_weight(w, True, 9)
             dx = torch.empty_like(x)
-            rep("conv_dgrad", shp, "hip", timeit(lambda: H._conv_fwd(g, wt, None, None, None, dx, N, OH, OH, Co,
-                                                                      H._up(Co, 64), Hh, Hh, Ci, Ci, s, True, 1.0),
-                                                 a.iters), fl)
+            for impl in ("reg", "glds"):
+                H.set_conv_impl(impl)
+                rep("conv_dgrad", shp, "hip-" + impl,
+                    timeit(lambda: H._conv_fwd(g, wt, None, None, None, dx, N, OH, OH, Co, H._up(Co, 64), Hh, Hh, Ci,
+                                               Ci, s, True, 1.0), a.iters), fl)
+            H.set_conv_impl("glds")
         if "wgrad" in ops:
             rep("conv_wgrad", shp, "hip", timeit(lambda: H._wgrad(g, x, Co, Ci, N, Hh, Hh, OH, OH, s, 9), a.iters), fl)
     if "linear" in ops:
