@@ -45,7 +45,13 @@ def main() -> None:
     ap.add_argument("--bucket_mb", type=float, default=64.0)
     ap.add_argument("--grad_dtype", default="fp32")
     ap.add_argument("--profile", default="", help="write a torch.profiler kernel table (text) here")
+    ap.add_argument("--mode", default="train", choices=["train", "sample"],
+                    help="sample: 256-step stochastic-conditioning CFG sampling wall-clock (BASELINE config 5)")
+    ap.add_argument("--sample_batch", type=int, default=64)
+    ap.add_argument("--timesteps", type=int, default=256)
     args = ap.parse_args()
+    if args.mode == "sample":
+        return bench_sample(args)
 
     from distributed_3d_diffusion_pytorch_amd.config import make_config
     from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup, barrier
@@ -125,6 +131,50 @@ def main() -> None:
         }
         print(json.dumps(out), flush=True)
     cleanup()
+
+
+def bench_sample(args) -> None:
+    """Wall-clock of generating one novel view with the 256-step CFG ancestral
+    sampler and stochastic conditioning (sampling.py:129-155) for a batch of
+    `sample_batch` chains on one GPU (random-init weights, synthetic poses)."""
+    from distributed_3d_diffusion_pytorch_amd.models import XUNet
+    from distributed_3d_diffusion_pytorch_amd.engine import DiffusionSampler, RecordEntry
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    from distributed_3d_diffusion_pytorch_amd import ops
+    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    if args.backend != "auto":
+        ops.set_backend(args.backend)
+    torch.manual_seed(0)
+    S = args.imgsize
+    model = XUNet(H=S, W=S, ch=128).to(dev)
+    model.compute_dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    model.eval()
+    b = args.sample_batch
+    img, R, T, K = next(SyntheticBatches(b, S, dev, seed=0))
+    record = [RecordEntry(img[:, 0].contiguous(), R[0, 0].float(), T[0, 0].float()),
+              RecordEntry(img[:, 1].contiguous(), R[0, 1].float(), T[0, 1].float())]
+    w = torch.arange(b, dtype=torch.float32) % 8
+    smp = DiffusionSampler(model, args.timesteps, seed=0, device=dev)
+    # warmup: a few steps through the same code path
+    warm = DiffusionSampler(model, max(2, args.warmup), seed=1, device=dev)
+    warm.sample(record, R[1, 0].float(), T[1, 0].float(), K[0].float(), w)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = smp.sample(record, R[1, 0].float(), T[1, 0].float(), K[0].float(), w)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+
+    res = {"metric": f"256-step sample wall-clock, stochastic conditioning, bs{b}, {S}x{S}", "value": round(dt, 3),
+           "unit": "s", "n_gpus": 1, "steps": args.timesteps, "warmup": args.warmup,
+           "ms_per_step": round(1e3 * dt / args.timesteps, 3), "higher_is_better": False, "scaling": "none",
+           "vs_baseline": None, "dtype": "bf16", "data": "synthetic poses/images, random-init weights",
+           "config": {"model": "XUNet ch128 136.7M", "global_batch": b, "cfg_batch": 2 * b, "image_size": S,
+                      "parallelism": "single"},
+           "achieved_tflops": round(2 * b * 235.9e9 * (S / 64.0) ** 2 * args.timesteps / dt / 1e12, 1),
+           "finite": bool(torch.isfinite(out).all())}
+    print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -40,6 +40,8 @@ class DiffusionSampler:
         self.device = device or next(model.parameters()).device
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
+        self._cpu_gen = torch.Generator()
+        self._cpu_gen.manual_seed(seed + 1)
         self.choice_rng = random.Random(seed)
         lam, lam_next = sampler_logsnrs(timesteps, logsnr_min, logsnr_max)
         self.lam, self.lam_next = lam.tolist(), lam_next.tolist()
@@ -64,11 +66,22 @@ class DiffusionSampler:
     def step(self, z, x_cond, R, T, K, w, k: int):
         lam, lam_next = self.lam[k], self.lam_next[k]
         eps_c, eps_u = self.denoise_eps(x_cond, z, R, T, K, lam)
-        mean, var = cfg_posterior(z, eps_c, eps_u, w, torch.tensor(lam), torch.tensor(lam_next))
         if self.ref_quirk:
             add_noise = lam_next != 0.0
         else:
             add_noise = k < self.T - 1
+        from .. import ops
+        if z.is_cuda and ops.use_hip(z, any_dtype=True):
+            # fused on-device CFG combine + x0 clamp + posterior + noise
+            # (the reference does this on the CPU, two host syncs per step)
+            import math
+            from ..ops import hip_impl
+            c = -math.expm1(lam - lam_next)
+            sig = lambda x: 1.0 / (1.0 + math.exp(-x))  # noqa: E731
+            seed = int(torch.randint(0, 2 ** 62, (1,), generator=self._cpu_gen).item())
+            return hip_impl.sampler_step(z.contiguous(), eps_c, eps_u, w, math.sqrt(sig(lam)), math.sqrt(sig(-lam)),
+                                         math.sqrt(sig(lam_next)), c, math.sqrt(sig(-lam_next) * c), add_noise, seed)
+        mean, var = cfg_posterior(z, eps_c, eps_u, w, torch.tensor(lam), torch.tensor(lam_next))
         if not add_noise:
             return mean
         return mean + var.sqrt() * torch.randn(z.shape, generator=self.gen, device=z.device)

@@ -42,6 +42,7 @@ SIGNATURES = {
     "d3d_conv_wgrad": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "d3d_pack_weight": [P, P, I, I, I, I, I, I, P],
     "d3d_set_conv_impl": [I, P],
+    "d3d_pack_all": [P, I, P],
     "d3d_conv_wgrad2": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     # rays.hip
     "d3d_ray_posenc": [P, P, P, P, P, P, P, P, I, I, I, P],

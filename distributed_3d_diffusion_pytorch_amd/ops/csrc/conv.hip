@@ -618,7 +618,47 @@ __global__ void pack_w_k(const float* __restrict__ w, bf16* __restrict__ out, in
   }
 }
 
+// Batched weight refresh: one launch re-derives every cached bf16 operand
+// (packed conv/linear weights and plain casts) from the fp32 masters after the
+// optimizer step.  blockIdx.y selects the descriptor.
+struct PackDesc {
+  const float* src;
+  bf16* dst;
+  int OC, IC, OCp, ICp, taps, mode;     // mode 0: pack, 1: transposed pack, 2: cast (OC elements)
+};
+
+__global__ void pack_all_k(const PackDesc* __restrict__ descs) {
+  const PackDesc d = descs[blockIdx.y];
+  long total = d.mode == 2 ? (long)d.OC : (long)d.OCp * d.taps * d.ICp;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    if (d.mode == 2) {
+      d.dst[t] = (bf16)d.src[t];
+      continue;
+    }
+    int co, ci, tap;
+    if (d.mode == 0) {
+      ci = (int)(t % d.ICp);
+      long r = t / d.ICp;
+      tap = (int)(r % d.taps);
+      co = (int)(r / d.taps);
+    } else {
+      co = (int)(t % d.OCp);
+      long r = t / d.OCp;
+      tap = (int)(r % d.taps);
+      ci = (int)(r / d.taps);
+    }
+    float v = (co < d.OC && ci < d.IC) ? d.src[((long)co * d.IC + ci) * d.taps + tap] : 0.f;
+    d.dst[t] = (bf16)v;
+  }
+}
+
 }  // namespace
+
+D3D_API int d3d_pack_all(const void* descs, int n, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(pack_all_k, dim3(64, n), dim3(256), 0, st, (const PackDesc*)descs);
+  return (int)hipGetLastError();
+}
 
 // ============================================================== C ABI =====
 // I: [N, IH, IW, IC] bf16 (IC % 8 == 0), Wp: packed [OCp][taps][ICp] bf16 with

@@ -69,18 +69,24 @@ def _up(x: int, m: int) -> int:
 
 
 # --------------------------------------------------------------------------
-# weight caches (bf16 packed copies of fp32 master weights).  Invalidated by
-# the optimizer (epoch bump) and by any in-place update of the parameter.
+# bf16 operand cache of the fp32 master weights.  Every entry keeps a
+# descriptor; after the optimizer step ``refresh_weights()`` re-derives ALL
+# entries in one kernel launch (instead of ~500 lazy per-layer packs).  Any
+# other in-place change of a parameter bumps its version and rebuilds that
+# entry alone.
 _EPOCH = [0]
-_WCACHE: Dict[Tuple, Tuple[Tuple, torch.Tensor]] = {}
+_WCACHE: Dict[Tuple, list] = {}          # key -> [tok, tensor, desc_tuple]
+_DESC_TABLE = [None, 0, -1]              # device tensor, count, revision
+_REV = [0]
 
 
 def invalidate_weight_cache() -> None:
     _EPOCH[0] += 1
     _WCACHE.clear()
+    _REV[0] += 1
 
 
-def _cached(p: torch.Tensor, kind: str, build):
+def _cached(p: torch.Tensor, kind: str, build, desc=None):
     if not isinstance(p, torch.nn.Parameter):
         return build()      # temporaries (e.g. channel-padded stem/head weights)
     key = (p.data_ptr(), kind, tuple(p.shape))
@@ -89,8 +95,36 @@ def _cached(p: torch.Tensor, kind: str, build):
     if hit is not None and hit[0] == tok:
         return hit[1]
     v = build()
-    _WCACHE[key] = (tok, v)
+    _WCACHE[key] = [tok, v, (p, desc)]
+    _REV[0] += 1
     return v
+
+
+def refresh_weights() -> None:
+    """After an optimizer update of the master weights: one launch repacks
+    every cached operand; cache tokens advance to the new epoch."""
+    _EPOCH[0] += 1
+    if not _WCACHE:
+        return
+    if _DESC_TABLE[2] != _REV[0]:
+        import numpy as np
+        rows = []
+        for key, (tok, t, (p, desc)) in _WCACHE.items():
+            if desc is None:
+                continue
+            OC, IC, OCp, ICp, taps, mode = desc
+            rows.append((p.data_ptr(), t.data_ptr(), OC, IC, OCp, ICp, taps, mode))
+        dt = np.dtype([("src", np.uint64), ("dst", np.uint64), ("OC", np.int32), ("IC", np.int32),
+                       ("OCp", np.int32), ("ICp", np.int32), ("taps", np.int32), ("mode", np.int32)])
+        arr = np.array(rows, dtype=dt)
+        host = torch.from_numpy(arr.view(np.uint8).copy())
+        _DESC_TABLE[0] = host.to("cuda", non_blocking=False)
+        _DESC_TABLE[1] = len(rows)
+        _DESC_TABLE[2] = _REV[0]
+    _chk(_lib.d3d_pack_all(_DESC_TABLE[0].data_ptr(), _DESC_TABLE[1], _st()), "pack_all")
+    for ent in _WCACHE.values():
+        p = ent[2][0]
+        ent[0] = (p._version, _EPOCH[0])
 
 
 def packed_weight(w: torch.Tensor, trans: bool, taps: int = 9) -> torch.Tensor:
@@ -108,7 +142,11 @@ def packed_weight(w: torch.Tensor, trans: bool, taps: int = 9) -> torch.Tensor:
         _chk(_lib.d3d_pack_weight(w.data_ptr(), out.data_ptr(), OC, IC, OCp, ICp, int(trans), taps, _st()),
              "pack_weight")
         return out
-    return _cached(w, f"pack{taps}{'T' if trans else ''}", build)
+    if not trans:
+        desc = (OC, IC, _up(OC, 128), _up(IC, 64), taps, 0)
+    else:   # kernel-side names: rows = IC (padded 128), K = OC (padded 64)
+        desc = (OC, IC, _up(OC, 64), _up(IC, 128), taps, 1)
+    return _cached(w, f"pack{taps}{'T' if trans else ''}", build, desc)
 
 
 def packed_conv_weight(w: torch.Tensor, trans: bool) -> torch.Tensor:
@@ -116,9 +154,10 @@ def packed_conv_weight(w: torch.Tensor, trans: bool) -> torch.Tensor:
 
 
 def bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    desc = (w.numel(), 1, 1, 1, 1, 2)
     if w.dim() == 1:
-        return _cached(w, "bf16", lambda: w.detach().to(BF16))
-    return _cached(w, "bf16", lambda: w.detach().reshape(w.shape[0], -1).to(BF16))
+        return _cached(w, "bf16", lambda: w.detach().to(BF16), desc)
+    return _cached(w, "bf16", lambda: w.detach().reshape(w.shape[0], -1).to(BF16), desc)
 
 
 # ------------------------------------------------------------ GroupNorm ----
@@ -602,7 +641,7 @@ def ray_posenc(R, t, K, H, W, cond_mask, pos_emb, first_emb, other_emb, rescale_
 def adam_flat(p, g, m, v, ema, lr, b1, b2, eps, wd, step_size, bc2_sqrt, grad_scale, ema_decay):
     _chk(_lib.d3d_adam(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(ema), p.numel(), b1, b2, eps, wd,
                        step_size, bc2_sqrt, grad_scale, ema_decay, _st()), "adam")
-    invalidate_weight_cache()
+    refresh_weights()
 
 
 # ------------------------------------------------------------- sampler ---

@@ -282,3 +282,22 @@ def test_grad_sink_and_reducer_two_ranks_one_gpu(tmp_path):
     for r in range(2):
         cos, rel = map(float, open(tmp_path / f"g{r}.txt").read().split())
         assert cos > 0.9999 and rel < 1e-2, (r, cos, rel)
+
+
+def test_sampler_step_matches_posterior(H):
+    from distributed_3d_diffusion_pytorch_amd.diffusion import cfg_posterior
+    torch.manual_seed(11)
+    z = torch.randn(4, 3, 16, 16, device=DEV)
+    ec, eu = torch.randn_like(z), torch.randn_like(z)
+    w = torch.tensor([0.0, 1.0, 3.0, 7.0], device=DEV)
+    lam, lamn = 0.7, 1.9
+    c = -math.expm1(lam - lamn)
+    sig = lambda x: 1 / (1 + math.exp(-x))  # noqa: E731
+    out = H.sampler_step(z, ec, eu, w, math.sqrt(sig(lam)), math.sqrt(sig(-lam)), math.sqrt(sig(lamn)), c,
+                         math.sqrt(sig(-lamn) * c), False, 0)
+    mean, var = cfg_posterior(z, ec, eu, w, torch.tensor(lam), torch.tensor(lamn))
+    assert torch.allclose(out, mean, atol=1e-5, rtol=1e-5)
+    noisy = H.sampler_step(z, ec, eu, w, math.sqrt(sig(lam)), math.sqrt(sig(-lam)), math.sqrt(sig(lamn)), c,
+                           math.sqrt(sig(-lamn) * c), True, 123)
+    nz = (noisy - mean) / var.sqrt()
+    assert abs(nz.mean().item()) < 0.05 and abs(nz.std().item() - 1) < 0.05
