@@ -114,7 +114,7 @@ def main() -> None:
     value = global_batch * args.steps / dt
     if ctx.rank == 0:
         from distributed_3d_diffusion_pytorch_amd.ops import use_hip
-        probe = torch.zeros(1, device=ctx.device)
+        probe = torch.zeros(1, device=ctx.device, dtype=torch.bfloat16)
         out = {
             "metric": f"train imgs/sec (whole node), SRN cars {args.imgsize}x{args.imgsize} bs{global_batch}",
             "value": round(value, 3), "unit": "examples/s", "n_gpus": N, "steps": args.steps,

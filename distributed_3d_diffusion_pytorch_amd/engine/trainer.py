@@ -194,8 +194,11 @@ class Trainer:
             it = SyntheticBatches(self.local_batch, dc.imgsize, self.device,
                                   seed=dc.seed * 7919 + self.ctx.rank)
             return it, None, None
-        from ..data import SRNDataset, ShardSampler, MultiEpochsDataLoader
-        ds = SRNDataset("train", dc.path, dc.index, dc.imgsize, seed=dc.seed)
+        from ..data import SRNDataset, ShardSampler, MultiEpochsDataLoader, CachedSRNDataset
+        if dc.cache:
+            ds = CachedSRNDataset("train", dc.cache, seed=dc.seed)
+        else:
+            ds = SRNDataset("train", dc.path, dc.index, dc.imgsize, seed=dc.seed)
         sampler = ShardSampler(len(ds), self.ctx.rank, self.ctx.world, shuffle=True, seed=dc.seed)
         loader = MultiEpochsDataLoader(ds, batch_size=self.local_batch, sampler=sampler,
                                        num_workers=dc.num_workers, drop_last=True,
@@ -226,6 +229,7 @@ class Trainer:
                     batch = next(it)
                 except StopIteration:
                     break
+                self._profile_hook(self.step)
                 loss = self.train_step(*self._to_dev(batch))
                 timer.tick()
                 n += 1
@@ -248,5 +252,30 @@ class Trainer:
             self.save("latest.pt", epoch=epoch)
             if done:
                 break
+        self._profile_hook(None)
         self.logger.close()
         return last
+
+    _prof = None
+
+    def _profile_hook(self, step) -> None:
+        """``profile_steps="a-b"``: torch.profiler (roctracer) over steps [a, b);
+        rank 0 writes <out_dir>/profile_rank0.txt (kernel table)."""
+        spec = self.cfg.profile_steps
+        if not spec:
+            return
+        a, b = (int(v) for v in spec.split("-"))
+        if step is not None and step == a and self._prof is None:
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if self.device.type == "cuda":
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self._prof = torch.profiler.profile(activities=acts)
+            self._prof.__enter__()
+        elif self._prof is not None and (step is None or step >= b):
+            self._prof.__exit__(None, None, None)
+            if self.ctx.is_main:
+                os.makedirs(self.out_dir, exist_ok=True)
+                with open(os.path.join(self.out_dir, f"profile_rank{self.ctx.rank}.txt"), "w") as f:
+                    key = "cuda_time_total" if self.device.type == "cuda" else "cpu_time_total"
+                    f.write(self._prof.key_averages().table(sort_by=key, row_limit=80))
+            self._prof = None

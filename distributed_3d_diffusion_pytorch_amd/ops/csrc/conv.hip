@@ -392,7 +392,7 @@ template <int BM, int BN, int TAPS>
 __global__ void __launch_bounds__(256, 2)
 conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __restrict__ ws, int Nimg, int IH,
              int IW, int IC, int OH, int OW, int OC, int stride, int pix_per_split, int ncb,
-             float* __restrict__ bws) {
+             float* __restrict__ bws, int lw, int lh) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int ALD = WBK * BM / 8 / 256, BLD = WBK * BN / 8 / 256;
@@ -432,10 +432,17 @@ conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __r
       bool ok = p < p_end && ci0 + c < IC;
       int img = 0, oh = 0, ow = 0;
       if (ok) {
-        img = (int)(p / OHW);
-        int rem = (int)(p % OHW);
-        oh = rem / OW;
-        ow = rem % OW;
+        if (lw >= 0) {                 // power-of-two spatial dims: shifts, no division
+          ow = (int)(p & (OW - 1));
+          long t = p >> lw;
+          oh = (int)(t & (OH - 1));
+          img = (int)(t >> lh);
+        } else {
+          img = (int)(p / OHW);
+          int rem = (int)(p % OHW);
+          oh = rem / OW;
+          ow = rem % OW;
+        }
       }
       int ih = oh * stride + kh - 1, iw = ow * stride + kw - 1;
       ok = ok && ih >= 0 && ih < IH && iw >= 0 && iw < IW;
@@ -552,8 +559,16 @@ __global__ void wgrad_reduce_k(const float* __restrict__ ws, float* __restrict__
     long r = t / IC;
     int tap = (int)(r % taps);
     int co = (int)(r / taps);
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += ws[(long)k * total + t];
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int k = 0;
+    for (; k + 4 <= splits; k += 4) {      // 4 independent loads in flight
+      s0 += ws[(long)k * total + t];
+      s1 += ws[(long)(k + 1) * total + t];
+      s2 += ws[(long)(k + 2) * total + t];
+      s3 += ws[(long)(k + 3) * total + t];
+    }
+    for (; k < splits; ++k) s0 += ws[(long)k * total + t];
+    float s = (s0 + s1) + (s2 + s3);
     long o = ((long)co * IC + ci) * taps + tap;
     dW[o] = accumulate ? dW[o] + s : s;
   }
@@ -656,7 +671,7 @@ __global__ void pack_all_k(const PackDesc* __restrict__ descs) {
 
 D3D_API int d3d_pack_all(const void* descs, int n, hipStream_t st) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(pack_all_k, dim3(64, n), dim3(256), 0, st, (const PackDesc*)descs);
+  hipLaunchKernelGGL(pack_all_k, dim3(512, n), dim3(256), 0, st, (const PackDesc*)descs);
   return (int)hipGetLastError();
 }
 
@@ -716,8 +731,10 @@ D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps
   constexpr int BM = 128, BN = 128;
   long P = (long)N * OH * OW;
   int tiles = taps * ((IC + BN - 1) / BN) * ((OC + BM - 1) / BM);
-  long want = (1024 + tiles - 1) / tiles;
-  long maxs = (P + 255) / 256;      // >= 256 pixels per split
+  // ~2 blocks per CU (the kernel's occupancy) and >= 1024 pixels per split:
+  // every extra split costs a full fp32 OCxK slab of write + reduce traffic
+  long want = (512 + tiles - 1) / tiles;
+  long maxs = (P + 1023) / 1024;
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
   long pps = (P + want - 1) / want;
@@ -745,14 +762,17 @@ D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW,
   dim3 grid(taps * ncb, (OC + BM - 1) / BM, splits);
   long total = (long)OC * IC * taps;
   float* bws = db ? ws + (long)splits * total : nullptr;
+  auto lg2 = [](int v) { int l = 0; while ((1 << l) < v) ++l; return (1 << l) == v ? l : -1; };
+  int lw = lg2(OW), lh = lg2(OH);
+  if (lw < 0 || lh < 0) lw = lh = -1;
   if (taps == 9)
     hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 9>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
-                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws);
+                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh);
   else
     hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 1>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
-                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws);
+                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh);
   long g = (total + 255) / 256;
-  if (g > 4096) g = 4096;
+  if (g > 8192) g = 8192;
   hipLaunchKernelGGL(wgrad_reduce_k, dim3((int)g), dim3(256), 0, st, ws, dW, OC, IC, splits, accumulate, taps, bws,
                      db, splits * (256 / BM));
   return (int)hipGetLastError();
