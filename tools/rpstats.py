@@ -1,0 +1,41 @@
+#!/usr/bin/env python
+"""Summarise a rocprofv3 rocpd database (kernel trace): per-kernel-name total
+time, calls, avg, and grid size buckets.  ``python tools/rpstats.py run_results.db [--steps K]``"""
+import argparse
+import sqlite3
+from collections import defaultdict
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--steps", type=int, default=0, help="divide totals by K (per-step ms)")
+    ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--grid", action="store_true", help="split rows by grid size")
+    a = ap.parse_args()
+    db = sqlite3.connect(a.db)
+    cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
+    name_col = "kernel_name" if "kernel_name" in cols else "name"
+    gx = "grid_x" if "grid_x" in cols else None
+    q = f"select {name_col}, start, end" + (f", {gx}, grid_y, grid_z, workgroup_x" if gx else "") + " from kernels"
+    agg = defaultdict(lambda: [0.0, 0])
+    t0, t1 = None, None
+    for r in db.execute(q):
+        nm = r[0]
+        short = nm.replace("(anonymous namespace)::", "").split("(")[0][:100]
+        if a.grid and gx:
+            short += f"  grid={r[3] // max(r[6], 1)}x{r[4]}x{r[5]}"
+        dur = (r[2] - r[1]) * 1e-6
+        agg[short][0] += dur
+        agg[short][1] += 1
+        t0 = r[1] if t0 is None else min(t0, r[1])
+        t1 = r[2] if t1 is None else max(t1, r[2])
+    tot = sum(v[0] for v in agg.values())
+    div = a.steps or 1
+    print(f"kernel time total {tot / div:.2f} ms{'/step' if a.steps else ''}  ({len(agg)} kernels)")
+    for k, (t, n) in sorted(agg.items(), key=lambda kv: -kv[1][0])[: a.top]:
+        print(f"{t / div:9.3f} ms {100 * t / tot:5.1f}%  {n / div:8.1f} calls  {1e3 * t / n:9.1f} us  {k}")
+
+
+if __name__ == "__main__":
+    main()
