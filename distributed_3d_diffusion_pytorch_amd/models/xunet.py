@@ -92,7 +92,9 @@ class ResnetBlock(nn.Module):
         assert C == self.in_features, (C, self.in_features)
         h = self.groupnorm0(x, silu=True)
         h = ops.conv3x3(h, self.conv1.weight, self.conv1.bias)
-        ss = self.film(semb)
+        ss = self.__dict__.pop("_ss", None)     # precomputed by the level-batched FiLM
+        if ss is None:
+            ss = self.film(semb)
         h = ops.gn_film(h, self.groupnorm1.gn.weight, self.groupnorm1.gn.bias, ss,
                         self.groupnorm1.gn.num_groups, self.groupnorm1.gn.eps,
                         self.dropout_p, self.training, _next_seed(self))
@@ -319,6 +321,22 @@ class XUNet(nn.Module):
         for idx, m in enumerate(mm for mm in self.modules() if isinstance(mm, ResnetBlock)):
             m._seed_slot = idx
         self._dropout_seed = 0
+        self.batch_film = True
+
+    def _film_groups(self):
+        """ResnetBlocks grouped by the conditioning level whose embedding
+        their FiLM consumes (mirrors the routing in forward)."""
+        if self.__dict__.get("_fg") is None:
+            L = self.num_resolutions
+            groups = [[] for _ in range(L)]
+            for i in range(L):
+                for blk in self.xunetblocks[i]:
+                    groups[i].append(blk.resnetblock if isinstance(blk, XUNetBlock) else blk)
+                for blk in self.upsample[str(i)]:
+                    groups[i].append(blk.resnetblock if isinstance(blk, XUNetBlock) else blk)
+            groups[L - 1].append(self.middle.resnetblock)
+            self.__dict__["_fg"] = groups
+        return self.__dict__["_fg"]
 
     # -- dropout seeding: every forward gets a fresh base seed (set by the
     # trainer from its step counter) so HIP dropout masks are reproducible and
@@ -338,6 +356,15 @@ class XUNet(nn.Module):
         dt = self.compute_dtype or x.dtype
 
         sembs = self.conditioningprocessor(batch, cond_mask, dt)
+        if self.batch_film:
+            # every FiLM projection of a level reads the same embedding: run
+            # them as one GEMM per level (ops.film_batch) and hand each
+            # ResnetBlock its modulation slice
+            for i, blocks in enumerate(self._film_groups()):
+                outs = ops.film_batch(sembs[i], [b.film.dense.weight for b in blocks],
+                                      [b.film.dense.bias for b in blocks])
+                for b, o in zip(blocks, outs):
+                    b.__dict__["_ss"] = o
         h = torch.stack([x, z], dim=1).reshape(2 * B, C, H, W).permute(0, 2, 3, 1).to(dt).contiguous()
         h = ops.conv3x3(h, self.conv.weight, self.conv.bias)
 

@@ -50,6 +50,12 @@ def linear(x, weight, bias, residual: Optional[torch.Tensor] = None, out_scale: 
     return _t.linear(x, weight, bias, residual, out_scale)
 
 
+def film_batch(semb, weights, biases):
+    if use_hip(semb):
+        return _h().film_batch(semb, weights, biases)
+    return _t.film_batch(semb, weights, biases)
+
+
 def attention(qkv, heads: int, cross: bool):
     if use_hip(qkv):
         return _h().attention(qkv, heads, cross)
@@ -87,6 +93,6 @@ posenc_ddpm = _t.posenc_ddpm
 camera_rays = _t.camera_rays
 posenc_nerf = _t.posenc_nerf
 
-__all__ = ["group_norm", "gn_film", "conv3x3", "linear", "attention", "avgpool2", "upsample2",
+__all__ = ["group_norm", "gn_film", "conv3x3", "linear", "film_batch", "attention", "avgpool2", "upsample2",
            "silu", "ray_posenc", "posenc_ddpm", "camera_rays", "posenc_nerf", "set_backend",
            "use_hip", "load_library", "library_error", "lib_path"]

@@ -17,9 +17,9 @@ SIGNATURES = {
     "d3d_gn_plan": [I, I, I, IP, IP],
     "d3d_gn_stats": [P, I, I, I, I, F, P, P, P],
     "d3d_gn_apply": [P, P, P, P, P, I, I, I, I, I, P],
-    "d3d_gn_film": [P, P, P, P, P, P, I, I, I, I, F, U64, P],
+    "d3d_gn_film": [P, P, P, P, P, P, I, I, I, I, F, U64, I, P],
     "d3d_gn_bwd": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, P],
-    "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, P],
+    "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P],
     # elementwise.hip
     "d3d_silu": [P, P, L, P],
     "d3d_dsilu": [P, P, P, L, P],
@@ -43,6 +43,7 @@ SIGNATURES = {
     "d3d_pack_weight": [P, P, I, I, I, I, I, I, P],
     "d3d_set_conv_impl": [I, P],
     "d3d_pack_all": [P, I, P],
+    "d3d_conv_wgrad_seg": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "d3d_conv_wgrad2": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     # rays.hip
     "d3d_ray_posenc": [P, P, P, P, P, P, P, P, I, I, I, P],

@@ -574,6 +574,61 @@ __global__ void wgrad_reduce_k(const float* __restrict__ ws, float* __restrict__
   }
 }
 
+// Segmented variant: the OC rows of one GEMM belong to several parameters
+// (a level-batched FiLM projection: OC = sum of 2C_i).  Row co of segment s
+// lands in w[s] + (co - row0[s]) * IC * taps (+ bias in b[s]); the segment table
+// travels as a kernel argument, so one launch scatters into every parameter's
+// gradient view (no temporary dW, no per-parameter copies).
+constexpr int kMaxSegs = 16;
+struct WSegs {
+  int n;
+  int row0[kMaxSegs + 1];
+  float* w[kMaxSegs];
+  float* b[kMaxSegs];
+};
+
+__device__ __forceinline__ int seg_of(const WSegs& sg, int co) {
+  int s = 0;
+  while (s + 1 < sg.n && co >= sg.row0[s + 1]) ++s;
+  return s;
+}
+
+__global__ void wgrad_reduce_seg_k(const float* __restrict__ ws, int OC, int IC, int splits, int accumulate,
+                                   int taps, const float* __restrict__ bws, int brows, WSegs sg) {
+  long total = (long)OC * IC * taps;
+  if (bws) {
+    for (long c = blockIdx.x * (long)blockDim.x + threadIdx.x; c < OC; c += (long)gridDim.x * blockDim.x) {
+      float s = 0.f;
+      for (int k = 0; k < brows; ++k) s += bws[(long)k * OC + c];
+      int g = seg_of(sg, (int)c);
+      float* d = sg.b[g];
+      if (d) {
+        d += c - sg.row0[g];
+        *d = accumulate ? *d + s : s;
+      }
+    }
+  }
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    int ci = (int)(t % IC);
+    long r = t / IC;
+    int tap = (int)(r % taps);
+    int co = (int)(r / taps);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int k = 0;
+    for (; k + 4 <= splits; k += 4) {
+      s0 += ws[(long)k * total + t];
+      s1 += ws[(long)(k + 1) * total + t];
+      s2 += ws[(long)(k + 2) * total + t];
+      s3 += ws[(long)(k + 3) * total + t];
+    }
+    for (; k < splits; ++k) s0 += ws[(long)k * total + t];
+    float s = (s0 + s1) + (s2 + s3);
+    int g = seg_of(sg, co);
+    float* d = sg.w[g] + (((long)(co - sg.row0[g]) * IC + ci) * taps + tap);
+    *d = accumulate ? *d + s : s;
+  }
+}
+
 // per-image channel sums: block = 256 threads = 32 channel-vectors x 8 row lanes
 __global__ void chansum_k(const bf16* __restrict__ dy, float* __restrict__ part, int P, int C, int nchunks) {
   const int img = blockIdx.y, chunk = blockIdx.z;
@@ -775,6 +830,45 @@ D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW,
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL(wgrad_reduce_k, dim3((int)g), dim3(256), 0, st, ws, dW, OC, IC, splits, accumulate, taps, bws,
                      db, splits * (256 / BM));
+  return (int)hipGetLastError();
+}
+
+// Weight gradient of a GEMM whose output rows are split over nseg parameters
+// (row0[s] = first row of segment s, ascending; wdst[s] / bdst[s] = that
+// parameter's dW / db, bdst entries may be null).  ws as for d3d_conv_wgrad2
+// plus 2*splits*OC floats when any bdst is non-null.
+D3D_API int d3d_conv_wgrad_seg(const void* dY, const void* I, float* ws, int N, int IH, int IW, int IC, int OH,
+                               int OW, int OC, int stride, int splits, int pix_per_split, int accumulate, int taps,
+                               int nseg, const int* row0, float* const* wdst, float* const* bdst, hipStream_t st) {
+  constexpr int BM = 128, BN = 128;
+  if (nseg < 1 || nseg > kMaxSegs) return (int)hipErrorInvalidValue;
+  WSegs sg{};
+  sg.n = nseg;
+  bool any_b = false;
+  for (int i = 0; i < nseg; ++i) {
+    sg.row0[i] = row0[i];
+    sg.w[i] = wdst[i];
+    sg.b[i] = bdst ? bdst[i] : nullptr;
+    any_b = any_b || sg.b[i];
+  }
+  sg.row0[nseg] = OC;
+  int ncb = (IC + BN - 1) / BN;
+  dim3 grid(taps * ncb, (OC + BM - 1) / BM, splits);
+  long total = (long)OC * IC * taps;
+  float* bws = any_b ? ws + (long)splits * total : nullptr;
+  auto lg2 = [](int v) { int l = 0; while ((1 << l) < v) ++l; return (1 << l) == v ? l : -1; };
+  int lw = lg2(OW), lh = lg2(OH);
+  if (lw < 0 || lh < 0) lw = lh = -1;
+  if (taps == 9)
+    hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 9>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
+                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh);
+  else
+    hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 1>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
+                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh);
+  long g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(wgrad_reduce_seg_k, dim3((int)g), dim3(256), 0, st, ws, OC, IC, splits, accumulate, taps, bws,
+                     splits * (256 / BM), sg);
   return (int)hipGetLastError();
 }
 

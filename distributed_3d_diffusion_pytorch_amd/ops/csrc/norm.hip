@@ -152,7 +152,7 @@ __global__ void gn_apply_k(const bf16* __restrict__ x, const float* __restrict__
 __global__ void gn_film_k(const bf16* __restrict__ x, const float* __restrict__ stats,
                           const float* __restrict__ gamma, const float* __restrict__ beta,
                           const bf16* __restrict__ ss, bf16* __restrict__ y, long nvec, int C, int Cg, int G,
-                          long PC, float p_drop, uint64_t seed) {
+                          long PC, float p_drop, uint64_t seed, int ssld) {
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
     long e = i * 8;
@@ -160,8 +160,8 @@ __global__ void gn_film_k(const bf16* __restrict__ x, const float* __restrict__ 
     long pix = e / C;
     int n = (int)(e / PC);
     f32x8 a = ld8(x + e);
-    f32x8 sc = ld8(ss + pix * 2 * C + c0);
-    f32x8 sf = ld8(ss + pix * 2 * C + C + c0);
+    f32x8 sc = ld8(ss + pix * ssld + c0);
+    f32x8 sf = ld8(ss + pix * ssld + C + c0);
     f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
     f32x8 o;
 #pragma unroll
@@ -202,7 +202,8 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       int P, int C, int G, int rows, int nchunks, float p_drop,
                                                       uint64_t seed, bf16* __restrict__ dss,
-                                                      float* __restrict__ chan_part, float* __restrict__ grp_part) {
+                                                      float* __restrict__ chan_part, float* __restrict__ grp_part,
+                                                      int ssld) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][C][4]
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int tpr = C / 8, rpi = NT / tpr;
@@ -230,7 +231,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
       long e = pix * C + c0;
       f32x8 xv = ld8(x + e), dv = ld8(dy + e);
       f32x8 sc = {}, o_s, o_t;
-      if (MODE == 2) sc = ld8(ss + pix * 2 * C + c0);
+      if (MODE == 2) sc = ld8(ss + pix * ssld + c0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float keepmul = 1.f;
@@ -246,8 +247,8 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
         gs2[j] += dxh * xhat;
       }
       if (MODE == 2) {
-        st8(dss + pix * 2 * C + c0, o_s);
-        st8(dss + pix * 2 * C + C + c0, o_t);
+        st8(dss + pix * ssld + c0, o_s);
+        st8(dss + pix * ssld + C + c0, o_t);
       }
     }
 #pragma unroll
@@ -305,7 +306,7 @@ __global__ void gn_bwd_apply_k(const bf16* __restrict__ x, const bf16* __restric
                                const float* __restrict__ stats, const float* __restrict__ coef,
                                const float* __restrict__ gamma, const float* __restrict__ beta,
                                bf16* __restrict__ dx, long nvec, int C, int Cg, int G, long PC, float p_drop,
-                               uint64_t seed) {
+                               uint64_t seed, int ssld) {
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
     long e = i * 8;
@@ -314,7 +315,7 @@ __global__ void gn_bwd_apply_k(const bf16* __restrict__ x, const bf16* __restric
     int n = (int)(e / PC);
     f32x8 xv = ld8(x + e), dv = ld8(dy + e);
     f32x8 sc = {};
-    if (MODE == 2) sc = ld8(ss + pix * 2 * C + c0);
+    if (MODE == 2) sc = ld8(ss + pix * ssld + c0);
     f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
     f32x8 o;
 #pragma unroll
@@ -374,11 +375,15 @@ D3D_API int d3d_gn_apply(const void* x, const float* stats, const float* gamma, 
   return (int)hipGetLastError();
 }
 
+// ss: [N, P, ssld] bf16 with scale at channel c and shift at C + c (ssld >= 2C;
+// ssld > 2C when ss is a column slice of a level-batched FiLM projection).
 D3D_API int d3d_gn_film(const void* x, const float* stats, const float* gamma, const float* beta, const void* ss,
-                        void* y, int N, int P, int C, int G, float p_drop, unsigned long long seed, hipStream_t st) {
+                        void* y, int N, int P, int C, int G, float p_drop, unsigned long long seed, int ssld,
+                        hipStream_t st) {
   long nvec = (long)N * P * C / 8;
   hipLaunchKernelGGL(gn_film_k, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, stats, gamma, beta,
-                     (const bf16*)ss, (bf16*)y, nvec, C, C / G, G, (long)P * C, p_drop, (uint64_t)seed);
+                     (const bf16*)ss, (bf16*)y, nvec, C, C / G, G, (long)P * C, p_drop, (uint64_t)seed,
+                     ssld ? ssld : 2 * C);
   return (int)hipGetLastError();
 }
 
@@ -388,14 +393,15 @@ D3D_API int d3d_gn_film(const void* x, const float* stats, const float* gamma, c
 D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss, const float* stats,
                         const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
                         unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
-                        float* grp_part, float* coef, int accumulate, hipStream_t st) {
+                        float* grp_part, float* coef, int accumulate, int ssld, hipStream_t st) {
   Plan p = make_plan(N, P, C);
+  if (ssld == 0) ssld = 2 * C;
   size_t lds = (size_t)p.rpi * C * 4 * sizeof(float);
   dim3 g(p.nchunks, N);
 #define RED(M)                                                                                                    \
   hipLaunchKernelGGL(gn_bwd_reduce_k<M>, g, dim3(NT), lds, st, (const bf16*)x, (const bf16*)dy, (const bf16*)ss, \
                      stats, gamma, beta, P, C, G, p.rows, p.nchunks, p_drop, (uint64_t)seed, (bf16*)dss,          \
-                     chan_part, grp_part)
+                     chan_part, grp_part, ssld)
   if (mode == 0) RED(0);
   else if (mode == 1) RED(1);
   else RED(2);
@@ -411,7 +417,7 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
 #define APP(M)                                                                                                  \
   hipLaunchKernelGGL(gn_bwd_apply_k<M>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, (const bf16*)dy, \
                      (const bf16*)ss, stats, coef, gamma, beta, (bf16*)dx, nvec, C, C / G, G, (long)P * C, p_drop, \
-                     (uint64_t)seed)
+                     (uint64_t)seed, ssld)
   if (mode == 0) APP(0);
   else if (mode == 1) APP(1);
   else APP(2);
@@ -424,5 +430,5 @@ D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, 
                        unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
                        float* grp_part, float* coef, hipStream_t st) {
   return d3d_gn_bwd2(mode, x, dy, ss, stats, gamma, beta, N, P, C, G, p_drop, seed, dx, dss, dgamma, dbeta,
-                     chan_part, grp_part, coef, 0, st);
+                     chan_part, grp_part, coef, 0, 0, st);
 }

@@ -177,13 +177,14 @@ def _gn_stats(x, G, eps):
     return stats
 
 
-def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed):
+def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0):
     N, H, W, C = x.shape
     P = H * W
     nch, _ = _gn_plan(N, P, C)
     dev = x.device
     dx = torch.empty_like(x)
-    dss = torch.empty_like(ss) if ss is not None else None
+    if dss is None and ss is not None:
+        dss = torch.empty_like(ss)
     tg, tb = SINK.target(w), SINK.target(b)
     direct = tg is not None and tb is not None
     dg = tg if direct else torch.empty(C, dtype=F32, device=dev)
@@ -193,7 +194,8 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed):
     coef = torch.empty(N * G * 2, dtype=F32, device=dev)
     _chk(_lib.d3d_gn_bwd2(mode, x.data_ptr(), dy.data_ptr(), _ptr(ss), stats.data_ptr(), w.data_ptr(),
                           b.data_ptr(), N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), dg.data_ptr(),
-                          db.data_ptr(), cp.data_ptr(), gp.data_ptr(), coef.data_ptr(), int(direct), _st()), "gn_bwd")
+                          db.data_ptr(), cp.data_ptr(), gp.data_ptr(), coef.data_ptr(), int(direct), int(ssld), _st()),
+         "gn_bwd")
     if direct:
         SINK.done(w)
         SINK.done(b)
@@ -229,18 +231,30 @@ def group_norm(x, weight, bias, groups=32, eps=1e-5, silu=False):
     return _GroupNorm.apply(x, weight, bias, groups, eps, silu)
 
 
+def _ss_layout(ss: torch.Tensor, C: int):
+    """Row stride of a FiLM modulation [N,H,W,2C]: 2C when contiguous, or the
+    parent width when ss is a channel slice of a level-batched projection."""
+    N, H, W, C2 = ss.shape
+    ld = ss.stride(2)
+    if C2 == 2 * C and ss.stride(3) == 1 and ss.stride(1) == W * ld and ss.stride(0) == H * W * ld and ld >= C2:
+        return ss, ld
+    return ss.contiguous(), 2 * C
+
+
 class _GNFiLM(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, ss, groups, eps, p, seed):
         x = x.contiguous()
-        ss = ss.contiguous()
         N, H, W, C = x.shape
+        slot = getattr(ss, "_d3d_slot", None)
+        ss, ld = _ss_layout(ss, C)
         stats = _gn_stats(x, groups, eps)
         y = torch.empty_like(x)
         _chk(_lib.d3d_gn_film(x.data_ptr(), stats.data_ptr(), weight.data_ptr(), bias.data_ptr(), ss.data_ptr(),
-                              y.data_ptr(), N, H * W, C, groups, float(p), int(seed), _st()), "gn_film")
+                              y.data_ptr(), N, H * W, C, groups, float(p), int(seed), ld, _st()), "gn_film")
         ctx.save_for_backward(x, weight, bias, ss, stats)
-        ctx.cfg = (groups, p, seed)
+        ctx.cfg = (groups, p, seed, ld)
+        ctx.slot = slot if ld != 2 * C or slot is not None else None
         SINK.use(weight, ctx.needs_input_grad[1])
         SINK.use(bias, ctx.needs_input_grad[2])
         return y
@@ -248,8 +262,15 @@ class _GNFiLM(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, b, ss, stats = ctx.saved_tensors
-        G, p, seed = ctx.cfg
-        dx, dss, dg, db = _gn_bwd(2, x, dy.contiguous(), ss, stats, w, b, G, p, seed)
+        G, p, seed, ld = ctx.cfg
+        dss = None
+        if ctx.slot is not None and ctx.needs_input_grad[3]:
+            # write d(scale|shift) straight into the level's shared dY buffer
+            # so the batched FiLM backward runs one GEMM with no gather
+            holder, off = ctx.slot
+            dss = holder.grad_slice(off, x.shape[-1])
+            ld = holder.width
+        dx, dss, dg, db = _gn_bwd(2, x, dy.contiguous(), ss, stats, w, b, G, p, seed, dss=dss, ssld=ld)
         return dx, dg, db, dss, None, None, None, None
 
 
@@ -472,6 +493,122 @@ class _Linear(torch.autograd.Function):
                 db = g.float().sum(0)
         dres = g.reshape(*shp[:-1], OC) if has_res else None
         return dx, dW, db, dres, None
+
+
+class _FiLMSlot:
+    """Shared gradient buffer of one level-batched FiLM projection: each
+    GN-FiLM backward deposits its d(scale|shift) into its column slice."""
+
+    def __init__(self, shape, width, device):
+        self.shape, self.width, self.device = tuple(shape), width, device
+        self.buf = None
+
+    def grad_slice(self, off: int, C: int) -> torch.Tensor:
+        if self.buf is None:
+            self.buf = torch.empty(*self.shape, self.width, dtype=BF16, device=self.device)
+        return self.buf[..., off: off + 2 * C]
+
+
+class _FiLMBatch(torch.autograd.Function):
+    """All FiLM projections that read one level's conditioning embedding
+    (`xunet.py:74-87`, one ``nn.Linear(emb_ch, 2C)`` per ResnetBlock) as ONE
+    GEMM ``[P, emb_ch] x [emb_ch, sum 2C_i]``: the 1024-channel embedding is
+    read once instead of once per block, and in backward the input gradient is
+    one GEMM over the concatenated d(scale|shift) -- no per-block [P, 1024]
+    partial products and no autograd accumulation adds.  The weight gradient
+    is one split-K MFMA launch whose reduction scatters rows into each block's
+    parameter gradient."""
+
+    @staticmethod
+    def forward(ctx, semb, slot, n, *wb):
+        Ws, Bs = wb[:n], wb[n:]
+        shp = semb.shape
+        K = shp[-1]
+        x2 = semb.reshape(-1, K)
+        wcat = torch.cat([bf16_weight(w) for w in Ws], 0)
+        bcat = torch.cat([bf16_weight(b) for b in Bs], 0)
+        y = torch.addmm(bcat, x2, wcat.t()).view(*shp[:-1], wcat.shape[0])
+        ctx.save_for_backward(x2, wcat)
+        ctx.n, ctx.slot, ctx.shp = n, slot, shp
+        ctx.params = (Ws, Bs)
+        ctx.widths = [w.shape[0] for w in Ws]
+        for i, (w, b) in enumerate(zip(Ws, Bs)):
+            SINK.use(w, ctx.needs_input_grad[3 + i])
+            SINK.use(b, ctx.needs_input_grad[3 + n + i])
+        outs, off = [], 0
+        for wd in ctx.widths:
+            outs.append(y[..., off: off + wd])
+            off += wd
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        x2, wcat = ctx.saved_tensors
+        n, slot, shp = ctx.n, ctx.slot, ctx.shp
+        S = wcat.shape[0]
+        buf = slot.buf
+        offs = [0]
+        for wd in ctx.widths:
+            offs.append(offs[-1] + wd)
+        ok = buf is not None
+        if ok:
+            for g, o in zip(gs, offs):
+                if g is None or g.data_ptr() != buf.data_ptr() + 2 * o or g.stride(-2) != S:
+                    ok = False
+                    break
+        if ok:
+            dy = buf.view(-1, S)
+        else:
+            dy = torch.zeros(x2.shape[0], S, dtype=BF16, device=x2.device)
+            for g, o, wd in zip(gs, offs, ctx.widths):
+                if g is not None:
+                    dy[:, o: o + wd].copy_(g.reshape(-1, wd))
+        slot.buf = None
+        dx = torch.mm(dy, wcat).view(shp) if ctx.needs_input_grad[0] else None
+        Ws, Bs = ctx.params
+        rows, K = x2.shape
+        grads_w, grads_b = [None] * n, [None] * n
+        need_w = any(ctx.needs_input_grad[3: 3 + n])
+        if need_w:
+            tw = [SINK.target(w) for w in Ws]
+            tb = [SINK.target(b) for b in Bs]
+            direct = all(t is not None for t in tw + tb)
+            if not direct:
+                tw = [torch.zeros(w.shape, dtype=F32, device=x2.device) for w in Ws]
+                tb = [torch.zeros(b.shape, dtype=F32, device=x2.device) for b in Bs]
+            sp, pps = ctypes.c_int(), ctypes.c_int()
+            _lib.d3d_conv_wgrad_plan2(rows, 1, 1, S, K, 1, ctypes.byref(sp), ctypes.byref(pps))
+            ws = torch.empty(sp.value * S * K + 2 * sp.value * S, dtype=F32, device=x2.device)
+            row0 = (ctypes.c_int * n)(*offs[:n])
+            wd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tw])
+            bd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tb])
+            _chk(_lib.d3d_conv_wgrad_seg(dy.data_ptr(), x2.data_ptr(), ws.data_ptr(), rows, 1, 1, K, 1, 1, S, 1,
+                                         sp.value, pps.value, 1, 1, n, row0, wd, bd, _st()), "film_wgrad")
+            if direct:
+                for w, b in zip(Ws, Bs):
+                    SINK.done(w)
+                    SINK.done(b)
+            else:
+                grads_w = [t.view(w.shape) for t, w in zip(tw, Ws)]
+                grads_b = tb
+        return (dx, None, None, *grads_w, *grads_b)
+
+
+def film_batch(semb, weights, biases):
+    """Level-batched FiLM projections -> tuple of ``[N,H,W,2C_i]`` modulations
+    (column slices of one GEMM output; GN-FiLM reads them strided)."""
+    _need_bf16(semb)
+    K = semb.shape[-1]
+    widths = [w.shape[0] for w in weights]
+    if K % 8 or any(wd % 8 for wd in widths) or len(weights) > 16:
+        return tuple(linear(semb, w, b) for w, b in zip(weights, biases))
+    slot = _FiLMSlot(semb.shape[:-1], sum(widths), semb.device)
+    outs = _FiLMBatch.apply(semb.contiguous(), slot, len(weights), *weights, *biases)
+    off = 0
+    for o, wd in zip(outs, widths):
+        o._d3d_slot = (slot, off)
+        off += wd
+    return outs
 
 
 def linear(x, weight, bias, residual=None, out_scale=1.0):

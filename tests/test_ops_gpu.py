@@ -301,3 +301,39 @@ def test_sampler_step_matches_posterior(H):
                            math.sqrt(sig(-lamn) * c), True, 123)
     nz = (noisy - mean) / var.sqrt()
     assert abs(nz.mean().item()) < 0.05 and abs(nz.std().item() - 1) < 0.05
+
+
+@pytest.mark.parametrize("chans", [[128, 128, 256], [512, 512]])
+def test_film_batch_with_gn_film(H, chans):
+    """Level-batched FiLM projection feeding strided GN-FiLM: forward, the
+    shared d(scale|shift) buffer and the segmented weight-gradient scatter
+    against per-block fp32 linears."""
+    torch.manual_seed(0)
+    N, Hh, K = 4, 8, 1024
+    semb = (torch.randn(N, Hh, Hh, K, device=DEV)).to(BF)
+    Ws = [torch.randn(2 * c, K, device=DEV) / 32 for c in chans]
+    Bs = [torch.randn(2 * c, device=DEV) * 0.1 for c in chans]
+    xs = [torch.randn(N, Hh, Hh, c, device=DEV).to(BF) for c in chans]
+    gam = [torch.rand(c, device=DEV) + 0.5 for c in chans]
+    bet = [torch.randn(c, device=DEV) * 0.1 for c in chans]
+    gos = [torch.randn(N, Hh, Hh, c, device=DEV) for c in chans]
+
+    def run(hip):
+        s = leaf(semb) if hip else leaf(semb, torch.float32)
+        ws = [leaf(w) for w in Ws]
+        bs = [leaf(b) for b in Bs]
+        if hip:
+            sss = H.film_batch(s, ws, bs)
+        else:
+            sss = [T.linear(s, w, b) for w, b in zip(ws, bs)]
+        loss = 0
+        for x, g, b, ss, go in zip(xs, gam, bet, sss, gos):
+            xx = x if hip else x.float()
+            y = (H if hip else T).gn_film(xx, g, b, ss, 32, 1e-5, 0.0, False, 0)
+            loss = loss + (y.float() * go).sum()
+        loss.backward()
+        return [s.grad] + [w.grad for w in ws] + [b.grad for b in bs]
+
+    gh, gr = run(True), run(False)
+    for a, b in zip(gh, gr):
+        assert rel(a, b) < 3e-2, rel(a, b)
