@@ -155,6 +155,8 @@ class Trainer:
         g = self.optim.param_groups[0]
         if self.sched is None:
             g["lr"] = warmup_lr(self.step, self.warmup_steps, self.cfg.optim.lr)
+        if self.cfg.graph and self.device.type == "cuda" and self.sink is not None:
+            return self._graph_train_step(img, R, T, K)
         self.model.train()
         if self.sink is not None:
             self.sink.reset()
@@ -178,6 +180,25 @@ class Trainer:
         with range_push("optimizer"):
             self.optim.step(grad_scale=1.0 / self.ctx.world)
             self.optim.zero_grad()
+        if self.sched is not None:
+            self.sched.step()
+        self.step += 1
+        ce = self.cfg.dist.checksum_every
+        if ce and self.step % ce == 0 and not check_replicas_in_sync(self.flat):
+            raise RuntimeError(f"data-parallel replicas diverged at step {self.step}")
+        return loss
+
+    _graphed = None
+
+    def _graph_train_step(self, img, R, T, K) -> torch.Tensor:
+        """Same step, replayed from captured HIP graphs (engine/graphs.py)."""
+        from .graphs import GraphedTrainStep
+        B = img.shape[0]
+        mb = self.cfg.micro_batch if 0 < self.cfg.micro_batch < B else B
+        if self._graphed is None or self._graphed.mb != mb:
+            self._graphed = GraphedTrainStep(self, mb, (img, R, T, K))
+        self.model.train()
+        loss = self._graphed.step(img, R, T, K)
         if self.sched is not None:
             self.sched.step()
         self.step += 1

@@ -17,9 +17,9 @@ SIGNATURES = {
     "d3d_gn_plan": [I, I, I, IP, IP],
     "d3d_gn_stats": [P, I, I, I, I, F, P, P, P],
     "d3d_gn_apply": [P, P, P, P, P, I, I, I, I, I, P],
-    "d3d_gn_film": [P, P, P, P, P, P, I, I, I, I, F, U64, I, P],
+    "d3d_gn_film": [P, P, P, P, P, P, I, I, I, I, F, U64, I, P, P],
     "d3d_gn_bwd": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, P],
-    "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P],
+    "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P],
     # elementwise.hip
     "d3d_silu": [P, P, L, P],
     "d3d_dsilu": [P, P, P, L, P],
@@ -30,6 +30,7 @@ SIGNATURES = {
     "d3d_diffusion_fwd": [P, P, P, P, P, P, P, I, I, U64, P],
     # adam.hip
     "d3d_adam": [P, P, P, P, P, L, F, F, F, F, F, F, F, F, P],
+    "d3d_adam_dev": [P, P, P, P, P, L, P, P],
     # conv.hip
     "d3d_conv3x3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P],
     "d3d_conv_wgrad_plan": [I, I, I, I, I, IP, IP],

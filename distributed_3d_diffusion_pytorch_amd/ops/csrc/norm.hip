@@ -152,7 +152,8 @@ __global__ void gn_apply_k(const bf16* __restrict__ x, const float* __restrict__
 __global__ void gn_film_k(const bf16* __restrict__ x, const float* __restrict__ stats,
                           const float* __restrict__ gamma, const float* __restrict__ beta,
                           const bf16* __restrict__ ss, bf16* __restrict__ y, long nvec, int C, int Cg, int G,
-                          long PC, float p_drop, uint64_t seed, int ssld) {
+                          long PC, float p_drop, uint64_t seed, int ssld, const uint64_t* __restrict__ seed_dev) {
+  if (seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;   // graph replays: per-step seed lives on the device
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
     long e = i * 8;
@@ -203,7 +204,8 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
                                                       int P, int C, int G, int rows, int nchunks, float p_drop,
                                                       uint64_t seed, bf16* __restrict__ dss,
                                                       float* __restrict__ chan_part, float* __restrict__ grp_part,
-                                                      int ssld) {
+                                                      int ssld, const uint64_t* __restrict__ seed_dev) {
+  if (seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][C][4]
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int tpr = C / 8, rpi = NT / tpr;
@@ -306,7 +308,8 @@ __global__ void gn_bwd_apply_k(const bf16* __restrict__ x, const bf16* __restric
                                const float* __restrict__ stats, const float* __restrict__ coef,
                                const float* __restrict__ gamma, const float* __restrict__ beta,
                                bf16* __restrict__ dx, long nvec, int C, int Cg, int G, long PC, float p_drop,
-                               uint64_t seed, int ssld) {
+                               uint64_t seed, int ssld, const uint64_t* __restrict__ seed_dev) {
+  if (seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
     long e = i * 8;
@@ -379,11 +382,11 @@ D3D_API int d3d_gn_apply(const void* x, const float* stats, const float* gamma, 
 // ssld > 2C when ss is a column slice of a level-batched FiLM projection).
 D3D_API int d3d_gn_film(const void* x, const float* stats, const float* gamma, const float* beta, const void* ss,
                         void* y, int N, int P, int C, int G, float p_drop, unsigned long long seed, int ssld,
-                        hipStream_t st) {
+                        const void* seed_dev, hipStream_t st) {
   long nvec = (long)N * P * C / 8;
   hipLaunchKernelGGL(gn_film_k, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, stats, gamma, beta,
                      (const bf16*)ss, (bf16*)y, nvec, C, C / G, G, (long)P * C, p_drop, (uint64_t)seed,
-                     ssld ? ssld : 2 * C);
+                     ssld ? ssld : 2 * C, (const uint64_t*)seed_dev);
   return (int)hipGetLastError();
 }
 
@@ -393,7 +396,8 @@ D3D_API int d3d_gn_film(const void* x, const float* stats, const float* gamma, c
 D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss, const float* stats,
                         const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
                         unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
-                        float* grp_part, float* coef, int accumulate, int ssld, hipStream_t st) {
+                        float* grp_part, float* coef, int accumulate, int ssld, const void* seed_dev,
+                        hipStream_t st) {
   Plan p = make_plan(N, P, C);
   if (ssld == 0) ssld = 2 * C;
   size_t lds = (size_t)p.rpi * C * 4 * sizeof(float);
@@ -401,7 +405,7 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
 #define RED(M)                                                                                                    \
   hipLaunchKernelGGL(gn_bwd_reduce_k<M>, g, dim3(NT), lds, st, (const bf16*)x, (const bf16*)dy, (const bf16*)ss, \
                      stats, gamma, beta, P, C, G, p.rows, p.nchunks, p_drop, (uint64_t)seed, (bf16*)dss,          \
-                     chan_part, grp_part, ssld)
+                     chan_part, grp_part, ssld, (const uint64_t*)seed_dev)
   if (mode == 0) RED(0);
   else if (mode == 1) RED(1);
   else RED(2);
@@ -417,7 +421,7 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
 #define APP(M)                                                                                                  \
   hipLaunchKernelGGL(gn_bwd_apply_k<M>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, (const bf16*)dy, \
                      (const bf16*)ss, stats, coef, gamma, beta, (bf16*)dx, nvec, C, C / G, G, (long)P * C, p_drop, \
-                     (uint64_t)seed, ssld)
+                     (uint64_t)seed, ssld, (const uint64_t*)seed_dev)
   if (mode == 0) APP(0);
   else if (mode == 1) APP(1);
   else APP(2);
@@ -430,5 +434,5 @@ D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, 
                        unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
                        float* grp_part, float* coef, hipStream_t st) {
   return d3d_gn_bwd2(mode, x, dy, ss, stats, gamma, beta, N, P, C, G, p_drop, seed, dx, dss, dgamma, dbeta,
-                     chan_part, grp_part, coef, 0, 0, st);
+                     chan_part, grp_part, coef, 0, 0, nullptr, st);
 }

@@ -160,6 +160,17 @@ def bf16_weight(w: torch.Tensor) -> torch.Tensor:
     return _cached(w, "bf16", lambda: w.detach().reshape(w.shape[0], -1).to(BF16), desc)
 
 
+# Per-step dropout seed on the device (graph replay: a captured kernel cannot
+# see a new Python seed, so the mask kernels add this device word to their
+# baked seed).  None in eager mode.
+_SEED_DEV = [None]
+
+
+def set_device_seed(t: Optional[torch.Tensor]) -> None:
+    assert t is None or (t.dtype == torch.int64 and t.is_cuda and t.numel() >= 1)
+    _SEED_DEV[0] = t
+
+
 # ------------------------------------------------------------ GroupNorm ----
 def _gn_plan(N, P, C):
     a, b = ctypes.c_int(), ctypes.c_int()
@@ -194,8 +205,8 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0):
     coef = torch.empty(N * G * 2, dtype=F32, device=dev)
     _chk(_lib.d3d_gn_bwd2(mode, x.data_ptr(), dy.data_ptr(), _ptr(ss), stats.data_ptr(), w.data_ptr(),
                           b.data_ptr(), N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), dg.data_ptr(),
-                          db.data_ptr(), cp.data_ptr(), gp.data_ptr(), coef.data_ptr(), int(direct), int(ssld), _st()),
-         "gn_bwd")
+                          db.data_ptr(), cp.data_ptr(), gp.data_ptr(), coef.data_ptr(), int(direct), int(ssld),
+                          _ptr(_SEED_DEV[0]) if mode == 2 else None, _st()), "gn_bwd")
     if direct:
         SINK.done(w)
         SINK.done(b)
@@ -251,7 +262,8 @@ class _GNFiLM(torch.autograd.Function):
         stats = _gn_stats(x, groups, eps)
         y = torch.empty_like(x)
         _chk(_lib.d3d_gn_film(x.data_ptr(), stats.data_ptr(), weight.data_ptr(), bias.data_ptr(), ss.data_ptr(),
-                              y.data_ptr(), N, H * W, C, groups, float(p), int(seed), ld, _st()), "gn_film")
+                              y.data_ptr(), N, H * W, C, groups, float(p), int(seed), ld, _ptr(_SEED_DEV[0]), _st()),
+             "gn_film")
         ctx.save_for_backward(x, weight, bias, ss, stats)
         ctx.cfg = (groups, p, seed, ld)
         ctx.slot = slot if ld != 2 * C or slot is not None else None
@@ -731,15 +743,30 @@ def upsample2(x):
 
 
 # ------------------------------------------------------------- rays ------
+def _inv3x3(m: torch.Tensor) -> torch.Tensor:
+    """Batched 3x3 inverse by the adjugate: pure elementwise kernels, no
+    host synchronisation (torch.linalg.inv reads its error flags back to the
+    host, which a graph capture forbids)."""
+    a, b, c = m[:, 0, 0], m[:, 0, 1], m[:, 0, 2]
+    d, e, f = m[:, 1, 0], m[:, 1, 1], m[:, 1, 2]
+    g, h, i = m[:, 2, 0], m[:, 2, 1], m[:, 2, 2]
+    A, B_, C = e * i - f * h, -(d * i - f * g), d * h - e * g
+    det = a * A + b * B_ + c * C
+    adj = torch.stack([A, -(b * i - c * h), b * f - c * e,
+                       B_, a * i - c * g, -(a * f - c * d),
+                       C, -(a * h - b * g), a * e - b * d], 1).reshape(-1, 3, 3)
+    return adj / det[:, None, None]
+
+
+
 class _RayPosenc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, pos_emb, first_emb, other_emb, R, t, K, H, W, cond_mask, rescale_from):
         B = R.shape[0]
         Kd = K.to(torch.float64)
         if rescale_from:
-            s = torch.tensor([W / rescale_from, H / rescale_from, 1.0], dtype=torch.float64, device=K.device)
-            Kd = Kd * s[None, :, None]
-        Kinv = torch.linalg.inv(Kd).float().contiguous()
+            Kd = torch.cat([Kd[:, 0:1] * (W / rescale_from), Kd[:, 1:2] * (H / rescale_from), Kd[:, 2:3]], 1)
+        Kinv = _inv3x3(Kd).float().contiguous()
         Rf = R.float().reshape(B * 2, 9).contiguous()
         tf = t.float().reshape(B * 2, 3).contiguous()
         mask = cond_mask.to(torch.uint8).contiguous()
@@ -778,6 +805,14 @@ def ray_posenc(R, t, K, H, W, cond_mask, pos_emb, first_emb, other_emb, rescale_
 def adam_flat(p, g, m, v, ema, lr, b1, b2, eps, wd, step_size, bc2_sqrt, grad_scale, ema_decay):
     _chk(_lib.d3d_adam(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(ema), p.numel(), b1, b2, eps, wd,
                        step_size, bc2_sqrt, grad_scale, ema_decay, _st()), "adam")
+    refresh_weights()
+
+
+def adam_flat_dev(p, g, m, v, ema, hp):
+    """Adam with its per-step hyper-parameters read from the device block
+    ``hp`` (graph-replay form; see d3d_adam_dev)."""
+    _chk(_lib.d3d_adam_dev(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(ema), p.numel(),
+                           hp.data_ptr(), _st()), "adam_dev")
     refresh_weights()
 
 
