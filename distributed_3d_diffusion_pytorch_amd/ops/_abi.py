@@ -38,7 +38,8 @@ SIGNATURES = {
     "d3d_chansum": [P, P, P, P, I, I, I, I, P],
     "d3d_colsum": [P, L, I, P, P, P, I, P],
     "d3d_pack_conv_weight": [P, P, I, I, I, I, I, P],
-    "d3d_conv": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P],
+    "d3d_conv": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P],
+    "d3d_conv_plan": [I, I, I, I, I, I],
     "d3d_conv_wgrad_plan2": [I, I, I, I, I, I, IP, IP],
     "d3d_conv_wgrad": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "d3d_pack_weight": [P, P, I, I, I, I, I, I, P],

@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(256, 2)
 conv_glds_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
             const bf16* __restrict__ zero16, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC,
-            int ldo, int stride, float scale, int res_nmod) {
+            int ldo, int stride, float scale, int res_nmod, float* __restrict__ part) {
   constexpr int BM = 128, BN = 128, BKk = 64;
   constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
   constexpr int STAGE = (BM + BN) * BKk;           // elements per stage
@@ -308,13 +308,18 @@ conv_glds_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = Kp / BKk;
+  // split-K (small grids): blockIdx.z owns k-steps [k0, k1) and writes an
+  // fp32 partial slab; conv_splitk_epi_k sums the slabs and applies the epilogue
+  const int nk_all = Kp / BKk;
+  const int k0 = (int)((long)blockIdx.z * nk_all / gridDim.z);
+  const int k1 = (int)((long)(blockIdx.z + 1) * nk_all / gridDim.z);
+  const int nk = k1 - k0;
   const int fr = lane & 15, fq = lane >> 4;
-  issue(0, 0);
+  issue(k0, 0);
   for (int ks = 0; ks < nk; ++ks) {
     const int st = ks & 1;
     if (ks + 1 < nk) {
-      issue(ks + 1, st ^ 1);
+      issue(k0 + ks + 1, st ^ 1);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // retire stage st, keep st^1 in flight
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -340,6 +345,21 @@ conv_glds_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   }
 
   const int OHW = OH * OW;
+  if (part) {
+    float* slab = part + (long)blockIdx.z * Mpix * OC;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      long pix = n0 + wn * WN + j * 16 + fr;
+      if (pix >= Mpix) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int co = m0 + wm * WM + i * 16 + fq * 4;
+        if (co >= OC) continue;
+        *reinterpret_cast<f32x4*>(slab + pix * OC + co) = acc[i][j];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     long pix = n0 + wn * WN + j * 16 + fr;
@@ -377,6 +397,39 @@ conv_glds_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
         }
       }
     }
+  }
+}
+
+// split-K epilogue: O[pix][co] = (sum_s part[s][pix][co] + bias + row_bias
+// (+ residual)) * scale, 4 channels per thread (OC % 4 == 0).
+__global__ void conv_splitk_epi_k(const float* __restrict__ part, int nsplit, long Mpix, int OC, int OHW,
+                                  const float* __restrict__ bias, const float* __restrict__ row_bias,
+                                  const bf16* __restrict__ res, int res_nmod, bf16* __restrict__ O, int ldo,
+                                  float scale) {
+  const long nv = Mpix * (OC / 4);
+  const long slab = Mpix * OC;
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nv; v += (long)gridDim.x * blockDim.x) {
+    long pix = v / (OC / 4);
+    int co = (int)(v % (OC / 4)) * 4;
+    f32x4 a = *reinterpret_cast<const f32x4*>(part + pix * OC + co);
+    for (int sp = 1; sp < nsplit; ++sp) a += *reinterpret_cast<const f32x4*>(part + sp * slab + pix * OC + co);
+    int img = (int)(pix / OHW);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = a[e] + (bias ? bias[co + e] : 0.f);
+      if (row_bias) t += row_bias[(long)img * OC + co + e];
+      a[e] = t;
+    }
+    if (res) {
+      const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
+      bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] += (float)r4[e];
+    }
+    bf16x4 o4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o4[e] = (bf16)(a[e] * scale);
+    *reinterpret_cast<bf16x4*>(O + pix * ldo + co) = o4;
   }
 }
 
@@ -743,23 +796,49 @@ D3D_API int d3d_set_conv_impl(int impl, const void* zero16) {
   return 0;
 }
 
+// Split-K factor for the forward / dgrad GEMM: grids far below the 2 blocks
+// per CU the kernel runs at (the 8x8 / 16x16 levels at small per-GPU batch:
+// 64-128 blocks on 256 CUs) split their K = taps x IC reduction so the chip
+// fills; >= 6 k-steps per split keeps the pipeline prologue amortised.
+D3D_API int d3d_conv_plan(int N, int OH, int OW, int OC, int ICp, int taps) {
+  constexpr int BM = 128, BN = 128;
+  long Mpix = (long)N * OH * OW;
+  long blocks = ((Mpix + BN - 1) / BN) * ((OC + BM - 1) / BM);
+  int nk = taps * ICp / 64;
+  if (blocks >= 384 || (OC & 3) || g_conv_impl != 1) return 1;
+  long want = (512 + blocks - 1) / blocks;
+  long maxs = nk / 6;
+  if (want > maxs) want = maxs;
+  if (want > 16) want = 16;
+  return want < 2 ? 1 : (int)want;
+}
+
 D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
                      void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
-                     int trans, float scale, int res_nmod, int taps, hipStream_t st) {
+                     int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, hipStream_t st) {
   long Mpix = (long)N * OH * OW;
   constexpr int BM = 128, BN = 128;
-  dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM));
+  if (nsplit < 1 || !ws || g_conv_impl != 1) nsplit = 1;
+  dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM), (unsigned)nsplit);
   if (g_conv_impl == 1 && g_zero16) {
+    float* part = nsplit > 1 ? ws : nullptr;
 #define GLDS(TP, TR)                                                                                             \
   hipLaunchKernelGGL((conv_glds_k<TP, TR>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,        \
                      row_bias, (const bf16*)res, (bf16*)O, g_zero16, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, \
-                     scale, res_nmod)
+                     scale, res_nmod, part)
     if (taps == 9) {
       if (trans) GLDS(9, true); else GLDS(9, false);
     } else {
       if (trans) GLDS(1, true); else GLDS(1, false);
     }
 #undef GLDS
+    if (part) {
+      long nv = Mpix * (OC / 4);
+      long g = (nv + 255) / 256;
+      if (g > 4096) g = 4096;
+      hipLaunchKernelGGL(conv_splitk_epi_k, dim3((unsigned)g), dim3(256), 0, st, part, nsplit, Mpix, OC, OH * OW,
+                         bias, row_bias, (const bf16*)res, res_nmod, (bf16*)O, ldo, scale);
+    }
     return (int)hipGetLastError();
   }
 #define LAUNCH(TR, TP)                                                                                             \
@@ -779,7 +858,7 @@ D3D_API int d3d_conv3x3(const void* I, const void* Wp, const float* bias, const 
                         void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo,
                         int stride, int trans, float scale, int res_nmod, hipStream_t st) {
   return d3d_conv(I, Wp, bias, row_bias, res, O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans, scale,
-                  res_nmod, 9, st);
+                  res_nmod, 9, nullptr, 1, st);
 }
 
 D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps, int* splits, int* pix_per_split) {
@@ -789,7 +868,7 @@ D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps
   // ~2 blocks per CU (the kernel's occupancy) and >= 1024 pixels per split:
   // every extra split costs a full fp32 OCxK slab of write + reduce traffic
   long want = (512 + tiles - 1) / tiles;
-  long maxs = (P + 1023) / 1024;
+  long maxs = (P + 255) / 256;       // small reductions (8x8 level at small batch): fill the chip first
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
   long pps = (P + want - 1) / want;

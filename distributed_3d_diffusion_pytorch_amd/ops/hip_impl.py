@@ -296,8 +296,11 @@ def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=Fa
 def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale, res_nmod=0,
               taps=9):
     _ensure_impl()
+    ns = _lib.d3d_conv_plan(N, OH, OW, OC, ICp, taps) if ldo == OC else 1
+    ws = torch.empty(ns * N * OH * OW * OC, dtype=F32, device=x.device) if ns > 1 else None
     _chk(_lib.d3d_conv(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
-                       IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), taps, _st()), "conv")
+                       IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), taps, _ptr(ws), ns,
+                       _st()), "conv")
 
 
 def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9, want_bias=False, dW=None, db=None, accumulate=False):

@@ -101,6 +101,7 @@ def test_gn_film_dropout(H):
 CONV_SHAPES = [
     # N, H, W, Cin, Cout, stride, residual, row_bias, scale
     (4, 16, 16, 128, 128, 1, True, False, 1 / math.sqrt(2)),
+    (12, 64, 64, 128, 128, 1, True, False, 1 / math.sqrt(2)),   # >= 384 tiles: no split-K
     (2, 8, 8, 256, 512, 1, False, False, 1.0),
     (2, 8, 8, 512, 256, 1, True, False, 1 / math.sqrt(2)),
     (2, 16, 16, 144, 256, 1, False, True, 1.0),
