@@ -40,6 +40,8 @@ SIGNATURES = {
     "d3d_pack_conv_weight": [P, P, I, I, I, I, I, P],
     "d3d_conv": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P],
     "d3d_conv_plan": [I, I, I, I, I, I],
+    "d3d_set_conv_korder": [I],
+    "d3d_set_wgrad_impl": [I],
     "d3d_conv_wgrad_plan2": [I, I, I, I, I, I, IP, IP],
     "d3d_conv_wgrad": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "d3d_pack_weight": [P, P, I, I, I, I, I, I, P],

@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(256, 2)
 conv_glds_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
             const bf16* __restrict__ zero16, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC,
-            int ldo, int stride, float scale, int res_nmod, float* __restrict__ part) {
+            int ldo, int stride, float scale, int res_nmod, float* __restrict__ part, int korder) {
   constexpr int BM = 128, BN = 128, BKk = 64;
   constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
   constexpr int STAGE = (BM + BN) * BKk;           // elements per stage
@@ -269,8 +269,18 @@ conv_glds_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   for (int i = 0; i < 4; ++i) wrow[i] = Wp + (long)(m0 + prow[i]) * Kp + lchunk * 8;
 
   auto issue = [&](int kstep, int stage) {
-    const int tap = TAPS == 9 ? kstep / (ICp / BKk) : 0;
-    const int c0 = (TAPS == 9 ? kstep % (ICp / BKk) : kstep) * BKk;
+    // korder 1 (channel-chunk major): the 9 taps of one 64-channel chunk are
+    // consecutive k-steps, so a block's shifted input rows are re-read while
+    // they are still in L2/L1 (tap-major order re-reads them ICp/64 steps
+    // apart and thrashes the XCD's 4 MB L2 at 64 resident blocks)
+    int tap, c0;
+    if (TAPS == 9 && korder) {
+      tap = kstep % 9;
+      c0 = (kstep / 9) * BKk;
+    } else {
+      tap = TAPS == 9 ? kstep / (ICp / BKk) : 0;
+      c0 = (TAPS == 9 ? kstep % (ICp / BKk) : kstep) * BKk;
+    }
     const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
     bf16* sA = smem + stage * STAGE;
     bf16* sB = sA + BM * BKk;
@@ -455,10 +465,25 @@ conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __r
   bf16* Bs = smem + 2 * WBK * AS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tap = blockIdx.x / ncb;                 // 0 when TAPS == 1
-  const int ci0 = (blockIdx.x % ncb) * BN;
-  const int m0 = blockIdx.y * BM;
-  const int split = blockIdx.z;
+  // XCD-aware remap of the linear block id: the hardware deals consecutive
+  // ids round-robin over the 8 XCDs; remapped, all (tap, ci-block) columns of
+  // one (co-tile, split) run on ONE XCD, so its dY slab and the shifted input
+  // rows are fetched into that XCD's L2 once instead of by every XCD.
+  int bx, by, bz;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const long T = (long)gx * gy * gridDim.z;
+    const long L = blockIdx.x + (long)gx * (blockIdx.y + (long)gy * blockIdx.z);
+    const long q = T / 8, r = T % 8, xcd = L % 8;
+    const long R = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    bx = (int)(R % gx);
+    by = (int)((R / gx) % gy);
+    bz = (int)(R / ((long)gx * gy));
+  }
+  const int tap = bx / ncb;                         // 0 when TAPS == 1
+  const int ci0 = (bx % ncb) * BN;
+  const int m0 = by * BM;
+  const int split = bz;
   const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
   const long P = (long)Nimg * OH * OW;
   const long p_begin = (long)split * pix_per_split;
@@ -535,7 +560,7 @@ conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __r
   __syncthreads();
   // fused bias gradient: the first (tap, ci) block column of every split also
   // sums its dY tile over pixels (thread -> column tid%BM, rows half tid/BM)
-  const bool do_bias = bws != nullptr && blockIdx.x == 0;
+  const bool do_bias = bws != nullptr && bx == 0;
   float bacc = 0.f;
   for (long s = 0; s < nsteps; ++s) {
     const int buf = (int)(s & 1);
@@ -577,6 +602,168 @@ conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __r
     if (m0 + col < OC) bws[((long)split * (256 / BM) + half) * OC + m0 + col] = bacc;
   }
   // partial slab: ws[split][co][tap*IC + ci]
+  const int fr = lane & 15, fq = lane >> 4;
+  const long KW = (long)TAPS * IC;
+  float* slab = ws + (long)split * OC * KW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int ci = ci0 + wn * WN + j * 16 + fr;
+    if (ci >= IC) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < OC) slab[(long)(co + e) * KW + tap * IC + ci] = acc[i][j][e];
+    }
+  }
+}
+
+// glds weight-gradient kernel: same GEMM and split-K as conv_wgrad_k, but
+// both operand tiles arrive global -> LDS by DMA (global_load_lds_dwordx4,
+// no VGPR staging, no ds_write pass), 64 pixels per stage, 2 stages behind a
+// counted vmcnt + raw s_barrier.  The LDS image is unpadded ([pixel][128 ch],
+// 256-B rows, lane-linear per 1-KiB DMA piece); bank conflicts of the
+// transpose reads are removed by an XOR swizzle instead of padding: logical
+// 16-B chunk c of row r lives at physical chunk c ^ 2*(r & 7) (the swizzle is
+// applied to the per-lane SOURCE address, rows 8 apart cover all 64 banks).
+template <int TAPS, int PK, int NS>
+__global__ void __launch_bounds__(256, 2)
+conv_wgrad_glds_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __restrict__ ws,
+                  const bf16* __restrict__ zero16, int Nimg, int IH, int IW, int IC, int OH, int OW, int OC,
+                  int stride, int pix_per_split, int ncb, float* __restrict__ bws, int lw, int lh) {
+  constexpr int BM = 128, BN = 128;
+  constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
+  constexpr int STAGE = PK * (BM + BN);
+  constexpr int PPW = PK / 16;                  // 1-KiB DMA pieces per wave per operand per stage
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
+  typedef __attribute__((address_space(3))) void lds_void;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int bx, by, bz;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const long T = (long)gx * gy * gridDim.z;
+    const long L = blockIdx.x + (long)gx * (blockIdx.y + (long)gy * blockIdx.z);
+    const long q = T / 8, r = T % 8, xcd = L % 8;
+    const long R = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    bx = (int)(R % gx);
+    by = (int)((R / gx) % gy);
+    bz = (int)(R / ((long)gx * gy));
+  }
+  const int tap = bx / ncb;
+  const int ci0 = (bx % ncb) * BN;
+  const int m0 = by * BM;
+  const int split = bz;
+  const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
+  const long P = (long)Nimg * OH * OW;
+  const long p_begin = (long)split * pix_per_split;
+  const long p_end = p_begin + pix_per_split < P ? p_begin + pix_per_split : P;
+  const int OHW = OH * OW;
+
+  // DMA lane mapping: wave w, piece i covers tile rows (w*PPW+i)*4 .. +3;
+  // lane L -> row +L/16, physical chunk L%16, logical chunk (L%16)^(2*(row&7))
+  const int lrow = lane >> 4, pch = lane & 15;
+  int trow[PPW], lch[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    trow[i] = (wave * PPW + i) * 4 + lrow;
+    lch[i] = pch ^ (2 * (trow[i] & 7));
+  }
+  auto issue = [&](long p0, int stage) {
+    bf16* sA = smem + stage * STAGE;
+    bf16* sB = sA + PK * BM;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const long p = p0 + trow[i];
+      const int co = m0 + lch[i] * 8;
+      const bf16* src = (p < p_end && co < OC) ? dY + p * OC + co : zero16;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sA + (wave * PPW + i) * 4 * BM), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const long p = p0 + trow[i];
+      const int ci = ci0 + lch[i] * 8;
+      bool ok = p < p_end && ci < IC;
+      int img = 0, oh = 0, ow = 0;
+      if (lw >= 0) {
+        ow = (int)(p & (OW - 1));
+        long t = p >> lw;
+        oh = (int)(t & (OH - 1));
+        img = (int)(t >> lh);
+      } else {
+        img = (int)(p / OHW);
+        int rem = (int)(p - (long)img * OHW);
+        oh = rem / OW;
+        ow = rem - oh * OW;
+      }
+      const int ih = oh * stride + kh - 1, iw = ow * stride + kw - 1;
+      ok = ok && ih >= 0 && ih < IH && iw >= 0 && iw < IW;
+      const bf16* src = ok ? I + (((long)img * IH + ih) * IW + iw) * IC + ci : zero16;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sB + (wave * PPW + i) * 4 * BN), 16, 0, 0);
+    }
+  };
+  auto sw = [](int row, int col) { return row * 128 + ((((col >> 3) ^ (2 * (row & 7)))) << 3) + (col & 7); };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
+  const long nsteps = (p_end - p_begin + PK - 1) / PK;
+  const bool do_bias = bws != nullptr && bx == 0;
+  float bacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (k < nsteps) issue(p_begin + k * PK, k);
+  for (long s = 0; s < nsteps; ++s) {
+    const int st = (int)(s % NS);
+    // retire stage s; the (up to NS-2) stages issued after it stay in flight
+    if (NS == 3 && s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();          // stage s visible; stage s-1 fully read by every wave
+    if (s + NS - 1 < nsteps) issue(p_begin + (s + NS - 1) * PK, (int)((s + NS - 1) % NS));
+    const bf16* a = smem + st * STAGE;
+    const bf16* b = a + PK * BM;
+    if (do_bias) {
+      const int col = tid & 127, r0 = (tid >> 7) * (PK / 2);
+#pragma unroll 8
+      for (int r = 0; r < PK / 2; ++r) bacc += (float)a[sw(r0 + r, col)];
+    }
+#pragma unroll
+    for (int kk = 0; kk < PK / 32; ++kk) {
+      const int r1 = kk * 32 + 4 * g + q, r2 = r1 + 16;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * WM + i * 16 + 4 * pc;
+        s16x4 lo = ds_tr(a + sw(r1, col));
+        s16x4 hi = ds_tr(a + sw(r2, col));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WN + j * 16 + 4 * pc;
+        s16x4 lo = ds_tr(b + sw(r1, col));
+        s16x4 hi = ds_tr(b + sw(r2, col));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads retired before the next top barrier
+  }
+  if (do_bias) {
+    const int col = tid & 127, half = tid >> 7;
+    if (m0 + col < OC) bws[((long)split * 2 + half) * OC + m0 + col] = bacc;
+  }
   const int fr = lane & 15, fq = lane >> 4;
   const long KW = (long)TAPS * IC;
   float* slab = ws + (long)split * OC * KW;
@@ -788,7 +975,19 @@ D3D_API int d3d_pack_all(const void* descs, int n, hipStream_t st) {
 // OCp % 128 == 0 and ICp % 64 == 0.  O: [N, OH, OW, ldo] bf16.  taps = 9 (3x3)
 // or 1 (1x1 / per-pixel linear).
 static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline
+static int g_conv_korder = 1;     // glds k-step order: 1 channel-chunk major, 0 tap major
+static int g_wgrad_impl = 0;      // 0: register-staged; 1-4: glds (PK,NS) = (64,2) (32,2) (32,3) (64,3)
 static const bf16* g_zero16 = nullptr;
+
+D3D_API int d3d_set_wgrad_impl(int impl) {
+  g_wgrad_impl = impl;
+  return 0;
+}
+
+D3D_API int d3d_set_conv_korder(int korder) {
+  g_conv_korder = korder;
+  return 0;
+}
 
 D3D_API int d3d_set_conv_impl(int impl, const void* zero16) {
   g_conv_impl = impl;
@@ -825,7 +1024,7 @@ D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const flo
 #define GLDS(TP, TR)                                                                                             \
   hipLaunchKernelGGL((conv_glds_k<TP, TR>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,        \
                      row_bias, (const bf16*)res, (bf16*)O, g_zero16, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, \
-                     scale, res_nmod, part)
+                     scale, res_nmod, part, g_conv_korder)
     if (taps == 9) {
       if (trans) GLDS(9, true); else GLDS(9, false);
     } else {
@@ -861,6 +1060,33 @@ D3D_API int d3d_conv3x3(const void* I, const void* Wp, const float* bias, const 
                   res_nmod, 9, nullptr, 1, st);
 }
 
+static void launch_wgrad(const void* dY, const void* I, float* ws, int N, int IH, int IW, int IC, int OH, int OW,
+                         int OC, int stride, int pps, int ncb, float* bws, int lw, int lh, int taps, dim3 grid,
+                         hipStream_t st) {
+  constexpr int BM = 128, BN = 128;
+  if (g_wgrad_impl >= 1 && g_zero16) {
+#define WG(TP, PKv, NSv)                                                                                         \
+  hipLaunchKernelGGL((conv_wgrad_glds_k<TP, PKv, NSv>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, \
+                     g_zero16, N, IH, IW, IC, OH, OW, OC, stride, pps, ncb, bws, lw, lh)
+#define WGT(PKv, NSv) do { if (taps == 9) WG(9, PKv, NSv); else WG(1, PKv, NSv); } while (0)
+    switch (g_wgrad_impl) {
+      case 2: WGT(32, 2); break;
+      case 3: WGT(32, 3); break;
+      case 4: WGT(64, 3); break;
+      default: WGT(64, 2); break;
+    }
+#undef WGT
+#undef WG
+    return;
+  }
+  if (taps == 9)
+    hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 9>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
+                       IW, IC, OH, OW, OC, stride, pps, ncb, bws, lw, lh);
+  else
+    hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 1>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
+                       IW, IC, OH, OW, OC, stride, pps, ncb, bws, lw, lh);
+}
+
 D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps, int* splits, int* pix_per_split) {
   constexpr int BM = 128, BN = 128;
   long P = (long)N * OH * OW;
@@ -872,7 +1098,7 @@ D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
   long pps = (P + want - 1) / want;
-  pps = (pps + WBK - 1) / WBK * WBK;
+  pps = (pps + 63) / 64 * 64;           // multiple of both kernels' pixel step
   *pix_per_split = (int)pps;
   *splits = (int)((P + pps - 1) / pps);
   return 0;
@@ -899,12 +1125,7 @@ D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW,
   auto lg2 = [](int v) { int l = 0; while ((1 << l) < v) ++l; return (1 << l) == v ? l : -1; };
   int lw = lg2(OW), lh = lg2(OH);
   if (lw < 0 || lh < 0) lw = lh = -1;
-  if (taps == 9)
-    hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 9>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
-                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh);
-  else
-    hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 1>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
-                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh);
+  launch_wgrad(dY, I, ws, N, IH, IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh, taps, grid, st);
   long g = (total + 255) / 256;
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL(wgrad_reduce_k, dim3((int)g), dim3(256), 0, st, ws, dW, OC, IC, splits, accumulate, taps, bws,
@@ -938,12 +1159,7 @@ D3D_API int d3d_conv_wgrad_seg(const void* dY, const void* I, float* ws, int N, 
   auto lg2 = [](int v) { int l = 0; while ((1 << l) < v) ++l; return (1 << l) == v ? l : -1; };
   int lw = lg2(OW), lh = lg2(OH);
   if (lw < 0 || lh < 0) lw = lh = -1;
-  if (taps == 9)
-    hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 9>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
-                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh);
-  else
-    hipLaunchKernelGGL((conv_wgrad_k<BM, BN, 1>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, N, IH,
-                       IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh);
+  launch_wgrad(dY, I, ws, N, IH, IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh, taps, grid, st);
   long g = (total + 255) / 256;
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL(wgrad_reduce_seg_k, dim3((int)g), dim3(256), 0, st, ws, OC, IC, splits, accumulate, taps, bws,

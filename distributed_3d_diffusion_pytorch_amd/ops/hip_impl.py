@@ -35,6 +35,20 @@ def set_conv_impl(impl: str) -> None:
     _chk(_lib.d3d_set_conv_impl(1 if impl == "glds" else 0, _ZERO_PAGE[dev].data_ptr()), "set_conv_impl")
 
 
+def set_conv_korder(korder: int) -> None:
+    """glds conv k-step order (1: channel-chunk major, default; 0: tap major)."""
+    _chk(_lib.d3d_set_conv_korder(int(korder)), "set_conv_korder")
+
+
+_WGRAD_IMPLS = {"reg": 0, "glds": 1, "glds64x2": 1, "glds32x2": 2, "glds32x3": 3, "glds64x3": 4}
+
+
+def set_wgrad_impl(impl: str) -> None:
+    """Weight-gradient kernel: 'reg' (register-staged, padded LDS rows) or a
+    DMA-staged variant 'glds<pixels per stage>x<stages>'."""
+    _chk(_lib.d3d_set_wgrad_impl(_WGRAD_IMPLS[impl]), "set_wgrad_impl")
+
+
 _IMPL_SET = [False]
 
 
@@ -306,6 +320,7 @@ def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo
 def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9, want_bias=False, dW=None, db=None, accumulate=False):
     """Split-K weight gradient (+ fused bias column sums).  Writes into the
     given dW/db (accumulating when asked) or into fresh fp32 tensors."""
+    _ensure_impl()
     s, pps = ctypes.c_int(), ctypes.c_int()
     _lib.d3d_conv_wgrad_plan2(N, OH, OW, OC, IC, taps, ctypes.byref(s), ctypes.byref(pps))
     extra = 2 * s.value * OC if (want_bias or db is not None) else 0
@@ -591,6 +606,7 @@ class _FiLMBatch(torch.autograd.Function):
             if not direct:
                 tw = [torch.zeros(w.shape, dtype=F32, device=x2.device) for w in Ws]
                 tb = [torch.zeros(b.shape, dtype=F32, device=x2.device) for b in Bs]
+            _ensure_impl()
             sp, pps = ctypes.c_int(), ctypes.c_int()
             _lib.d3d_conv_wgrad_plan2(rows, 1, 1, S, K, 1, ctypes.byref(sp), ctypes.byref(pps))
             ws = torch.empty(sp.value * S * K + 2 * sp.value * S, dtype=F32, device=x2.device)

@@ -77,8 +77,9 @@ def main():
         y = torch.empty(N, OH, OH, Co, dtype=BF, device=dev)
         g = torch.randn(N, OH, OH, Co, device=dev).to(BF)
         if "conv" in ops:
-            for impl in ("reg", "glds"):
-                H.set_conv_impl(impl)
+            for impl in ("glds-k0", "glds"):
+                H.set_conv_impl("glds")
+                H.set_conv_korder(0 if impl == "glds-k0" else 1)
                 rep("conv_fwd", shp, "hip-" + impl,
                     timeit(lambda: H._conv_fwd(x, wp, b, None, None, y, N, Hh, Hh, Ci, H._up(Ci, 64), OH, OH, Co, Co,
                                                s, False, 1.0), a.iters), fl)
@@ -91,14 +92,19 @@ def main():
         if "dgrad" in ops and s == 1:
             wt = H.packed_weight(w, True, 9)
             dx = torch.empty_like(x)
-            for impl in ("reg", "glds"):
-                H.set_conv_impl(impl)
+            for impl in ("glds-k0", "glds"):
+                H.set_conv_impl("glds")
+                H.set_conv_korder(0 if impl == "glds-k0" else 1)
                 rep("conv_dgrad", shp, "hip-" + impl,
                     timeit(lambda: H._conv_fwd(g, wt, None, None, None, dx, N, OH, OH, Co, H._up(Co, 64), Hh, Hh, Ci,
                                                Ci, s, True, 1.0), a.iters), fl)
             H.set_conv_impl("glds")
         if "wgrad" in ops:
-            rep("conv_wgrad", shp, "hip", timeit(lambda: H._wgrad(g, x, Co, Ci, N, Hh, Hh, OH, OH, s, 9), a.iters), fl)
+            for impl in ("reg", "glds64x2", "glds32x2", "glds32x3", "glds64x3"):
+                H.set_wgrad_impl(impl)
+                rep("conv_wgrad", shp, "hip-" + impl,
+                    timeit(lambda: H._wgrad(g, x, Co, Ci, N, Hh, Hh, OH, OH, s, 9), a.iters), fl)
+            H.set_wgrad_impl("reg")
     if "linear" in ops:
         for (P, Ci, Co) in [(N * 4096, 1024, 256), (N * 1024, 1024, 512), (N * 256, 1024, 512), (N * 64, 1024, 1024),
                             (N * 256, 256, 768), (N * 4096, 384, 128)]:
