@@ -869,6 +869,67 @@ __global__ void wgrad_reduce_seg_k(const float* __restrict__ ws, int OC, int IC,
   }
 }
 
+// Split-K slab reduction, parallel over splits as well as outputs: a block
+// owns 64 consecutive slab entries (16 float4 columns) and its 16 split lanes
+// each sum every 16th split with coalesced 16-B loads; an LDS tree finishes
+// the sum in a fixed order (deterministic).  Blocks past the dW range reduce
+// the bias partials the same way.  Destination: dW/db (OIHW) or, when
+// sg.n > 0, the per-parameter segments of a batched projection.
+__global__ void __launch_bounds__(256) wgrad_reduce2_k(const float* __restrict__ ws, int OC, int IC, int taps,
+                                                       int splits, int accumulate, const float* __restrict__ bws,
+                                                       int brows, float* __restrict__ dW, float* __restrict__ db,
+                                                       WSegs sg, int nblk_w) {
+  __shared__ f32x4 red[16][16];
+  const int col = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const bool is_bias = blockIdx.x >= nblk_w;
+  const long total = is_bias ? (long)OC : (long)OC * IC * taps;
+  const float* src = is_bias ? bws : ws;
+  const int nrows = is_bias ? brows : splits;
+  const long base = (long)(is_bias ? blockIdx.x - nblk_w : blockIdx.x) * 64 + col * 4;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (base < total) {
+    if (base + 3 < total) {
+      for (int k = sl; k < nrows; k += 16) a += *reinterpret_cast<const f32x4*>(src + (long)k * total + base);
+    } else {
+      for (int k = sl; k < nrows; k += 16)
+        for (int e = 0; e < 4 && base + e < total; ++e) a[e] += src[(long)k * total + base + e];
+    }
+  }
+  red[sl][col] = a;
+  __syncthreads();
+  if (sl == 0) {
+    f32x4 t = red[0][col];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][col];
+    for (int e = 0; e < 4; ++e) {
+      const long o = base + e;
+      if (o >= total) break;
+      float* d;
+      if (is_bias) {
+        const int c = (int)o;
+        if (sg.n > 0) {
+          const int g = seg_of(sg, c);
+          d = sg.b[g] ? sg.b[g] + (c - sg.row0[g]) : nullptr;
+        } else {
+          d = db ? db + c : nullptr;
+        }
+      } else {
+        const int ci = (int)(o % IC);
+        const long r = o / IC;
+        const int tap = (int)(r % taps);
+        const int co = (int)(r / taps);
+        if (sg.n > 0) {
+          const int g = seg_of(sg, co);
+          d = sg.w[g] + (((long)(co - sg.row0[g]) * IC + ci) * taps + tap);
+        } else {
+          d = dW + (((long)co * IC + ci) * taps + tap);
+        }
+      }
+      if (d) *d = accumulate ? *d + t[e] : t[e];
+    }
+  }
+}
+
 // per-image channel sums: block = 256 threads = 32 channel-vectors x 8 row lanes
 __global__ void chansum_k(const bf16* __restrict__ dy, float* __restrict__ part, int P, int C, int nchunks) {
   const int img = blockIdx.y, chunk = blockIdx.z;
@@ -1126,10 +1187,13 @@ D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW,
   int lw = lg2(OW), lh = lg2(OH);
   if (lw < 0 || lh < 0) lw = lh = -1;
   launch_wgrad(dY, I, ws, N, IH, IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh, taps, grid, st);
-  long g = (total + 255) / 256;
-  if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(wgrad_reduce_k, dim3((int)g), dim3(256), 0, st, ws, dW, OC, IC, splits, accumulate, taps, bws,
-                     db, splits * (256 / BM));
+  {
+    WSegs none{};
+    int nblk_w = (int)((total + 63) / 64);
+    int nblk_b = db ? (OC + 63) / 64 : 0;
+    hipLaunchKernelGGL(wgrad_reduce2_k, dim3(nblk_w + nblk_b), dim3(256), 0, st, ws, OC, IC, taps, splits, accumulate,
+                       bws, splits * (256 / BM), dW, db, none, nblk_w);
+  }
   return (int)hipGetLastError();
 }
 
@@ -1160,10 +1224,12 @@ D3D_API int d3d_conv_wgrad_seg(const void* dY, const void* I, float* ws, int N, 
   int lw = lg2(OW), lh = lg2(OH);
   if (lw < 0 || lh < 0) lw = lh = -1;
   launch_wgrad(dY, I, ws, N, IH, IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh, taps, grid, st);
-  long g = (total + 255) / 256;
-  if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(wgrad_reduce_seg_k, dim3((int)g), dim3(256), 0, st, ws, OC, IC, splits, accumulate, taps, bws,
-                     splits * (256 / BM), sg);
+  {
+    int nblk_w = (int)((total + 63) / 64);
+    int nblk_b = bws ? (OC + 63) / 64 : 0;
+    hipLaunchKernelGGL(wgrad_reduce2_k, dim3(nblk_w + nblk_b), dim3(256), 0, st, ws, OC, IC, taps, splits, accumulate,
+                       bws, splits * (256 / BM), (float*)nullptr, (float*)nullptr, sg, nblk_w);
+  }
   return (int)hipGetLastError();
 }
 
