@@ -46,7 +46,7 @@ SIGNATURES = {
     "d3d_conv_wgrad": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "d3d_pack_weight": [P, P, I, I, I, I, I, I, P],
     "d3d_set_conv_impl": [I, P],
-    "d3d_pack_all": [P, I, P],
+    "d3d_pack_all": [P, P, I, P],
     "d3d_conv_wgrad_seg": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "d3d_conv_wgrad2": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     # rays.hip

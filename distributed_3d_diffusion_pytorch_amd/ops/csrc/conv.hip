@@ -410,6 +410,195 @@ conv_glds_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   }
 }
 
+template <int TAPS, bool TRANS>
+__global__ void __launch_bounds__(256, 2)
+conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
+            const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
+            int in_bytes, int w_bytes, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC,
+            int ldo, int stride, float scale, int res_nmod, float* __restrict__ part, int korder) {
+  constexpr int BM = 128, BN = 128, BKk = 64;
+  constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
+  constexpr int STAGE = (BM + BN) * BKk;           // elements per stage
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
+  typedef __attribute__((address_space(3))) void lds_void;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const long Mpix = (long)Nimg * OH * OW;
+  const int nbx = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    int q = nbx / 8, r = nbx % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const long n0 = (long)bid * BN;
+  const int m0 = blockIdx.y * BM;
+  const int Kp = TAPS * ICp;
+
+  // LDS-DMA through buffer descriptors (buffer_load_dwordx4 ... lds): a
+  // 32-bit per-lane byte offset instead of a 64-bit address, and padding /
+  // out-of-range taps come back as zeros from the descriptor's range check
+  // (offset 0x80000000 is past every operand), so the per-k-step loader work
+  // is one add + one mask test per row -- the 64-bit im2col address math of
+  // conv_glds_k cost ~12 VALU per MFMA and made that kernel issue-bound.
+  // Same lane mapping / XOR swizzle as conv_glds_k.
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;
+  const __amdgpu_buffer_rsrc_t rI = __builtin_amdgcn_make_buffer_rsrc((void*)I, (short)0, in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, w_bytes, 0x00020000);
+  int boff[4], aoff[4];
+  unsigned vmask[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int prow = (wave * 4 + i) * 8 + lrow;
+    const long p = n0 + prow;
+    const bool pv = p < Mpix;
+    const long pp = pv ? p : 0;
+    const int pw = (int)(pp % OW);
+    const long t = pp / OW;
+    const int poh = (int)(t % OH);
+    const int pn = (int)(t / OH);
+    const int oh0 = TRANS ? poh : poh * stride, ow0 = TRANS ? pw : pw * stride;
+    boff[i] = (((pn * IH + oh0) * IW + ow0) * IC + lchunk * 8) * 2;
+    unsigned m = 0;
+#pragma unroll
+    for (int tp = 0; tp < TAPS; ++tp) {
+      const int kh = TAPS == 9 ? tp / 3 : 1, kw = TAPS == 9 ? tp % 3 : 1;
+      const int ih = TRANS ? oh0 + 1 - kh : oh0 + kh - 1, iw = TRANS ? ow0 + 1 - kw : ow0 + kw - 1;
+      if (pv && ih >= 0 && ih < IH && iw >= 0 && iw < IW) m |= 1u << tp;
+    }
+    vmask[i] = m;
+    aoff[i] = ((m0 + prow) * Kp + lchunk * 8) * 2;
+  }
+  const int lane_cmax = IC - lchunk * 8;          // chunk valid iff c0 < lane_cmax
+
+  auto issue = [&](int kstep, int stage) {
+    int tap, c0;
+    if (TAPS == 9 && korder) {
+      tap = kstep % 9;
+      c0 = (kstep / 9) * BKk;
+    } else {
+      tap = TAPS == 9 ? kstep / (ICp / BKk) : 0;
+      c0 = (TAPS == 9 ? kstep % (ICp / BKk) : kstep) * BKk;
+    }
+    const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
+    const int tapoff = (TRANS ? ((1 - kh) * IW + (1 - kw)) : ((kh - 1) * IW + (kw - 1))) * IC;
+    const int ubyte = (tapoff + c0) * 2;            // wave-uniform
+    const int soffA = (tap * ICp + c0) * 2;
+    bf16* sA = smem + stage * STAGE;
+    bf16* sB = sA + BM * BKk;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sA + (wave * 4 + i) * 8 * BKk), 16, aoff[i], soffA, 0,
+                                               0);
+    const bool cok = c0 < lane_cmax;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool ok = cok && ((vmask[i] >> tap) & 1u);
+      const unsigned vo = ok ? (unsigned)(boff[i] + ubyte) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rI, (lds_void*)(sB + (wave * 4 + i) * 8 * BKk), 16, vo, 0, 0, 0);
+    }
+  };
+  auto swz = [](int row, int chunk) { return row * BKk + ((chunk ^ (row & 7)) << 3); };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // split-K (small grids): blockIdx.z owns k-steps [k0, k1) and writes an
+  // fp32 partial slab; conv_splitk_epi_k sums the slabs and applies the epilogue
+  const int nk_all = Kp / BKk;
+  const int k0 = (int)((long)blockIdx.z * nk_all / gridDim.z);
+  const int k1 = (int)((long)(blockIdx.z + 1) * nk_all / gridDim.z);
+  const int nk = k1 - k0;
+  const int fr = lane & 15, fq = lane >> 4;
+  issue(k0, 0);
+  for (int ks = 0; ks < nk; ++ks) {
+    const int st = ks & 1;
+    if (ks + 1 < nk) {
+      issue(k0 + ks + 1, st ^ 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // retire stage st, keep st^1 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const bf16* a = smem + st * STAGE;
+    const bf16* b = a + BM * BKk;
+#pragma unroll
+    for (int kk = 0; kk < BKk / 32; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a + swz(wm * WM + i * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(b + swz(wn * WN + j * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                             // stage st free for reuse
+  }
+
+  const int OHW = OH * OW;
+  if (part) {
+    float* slab = part + (long)blockIdx.z * Mpix * OC;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      long pix = n0 + wn * WN + j * 16 + fr;
+      if (pix >= Mpix) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int co = m0 + wm * WM + i * 16 + fq * 4;
+        if (co >= OC) continue;
+        *reinterpret_cast<f32x4*>(slab + pix * OC + co) = acc[i][j];
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    long pix = n0 + wn * WN + j * 16 + fr;
+    if (pix >= Mpix) continue;
+    int img = (int)(pix / OHW);
+    const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int co = m0 + wm * WM + i * 16 + fq * 4;
+      if (co >= OC) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int cc = co + e < OC ? co + e : OC - 1;
+        float t = acc[i][j][e] + (bias ? bias[cc] : 0.f);
+        if (row_bias) t += row_bias[(long)img * OC + cc];
+        v[e] = t;
+      }
+      bf16* dst = O + pix * ldo + co;
+      if (co + 3 < OC && (ldo & 3) == 0) {
+        if (res) {
+          bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+        }
+        bf16x4 o4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o4[e] = (bf16)(v[e] * scale);
+        *reinterpret_cast<bf16x4*>(dst) = o4;
+      } else {
+        for (int e = 0; e < 4 && co + e < OC; ++e) {
+          float t = v[e];
+          if (res) t += (float)res[rpix * ldo + co + e];
+          dst[e] = (bf16)(t * scale);
+        }
+      }
+    }
+  }
+}
+
 // split-K epilogue: O[pix][co] = (sum_s part[s][pix][co] + bias + row_bias
 // (+ residual)) * scale, 4 channels per thread (OC % 4 == 0).
 __global__ void conv_splitk_epi_k(const float* __restrict__ part, int nsplit, long Mpix, int OC, int OHW,
@@ -996,38 +1185,58 @@ struct PackDesc {
   const float* src;
   bf16* dst;
   int OC, IC, OCp, ICp, taps, mode;     // mode 0: pack, 1: transposed pack, 2: cast (OC elements)
+  int blk0, pad;                        // first block of this descriptor in the flattened grid
 };
 
-__global__ void pack_all_k(const PackDesc* __restrict__ descs) {
-  const PackDesc d = descs[blockIdx.y];
-  long total = d.mode == 2 ? (long)d.OC : (long)d.OCp * d.taps * d.ICp;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    if (d.mode == 2) {
-      d.dst[t] = (bf16)d.src[t];
-      continue;
+// One launch repacks every cached bf16 operand.  The grid is flattened over
+// descriptors in proportion to their size (2048 destination elements per
+// block; a host-built block -> descriptor map), and each
+// thread writes 8 consecutive destination elements with one 16-B store.
+__global__ void __launch_bounds__(256) pack_all_k(const PackDesc* __restrict__ descs,
+                                                  const int* __restrict__ blk_desc) {
+  const PackDesc d = descs[blk_desc[blockIdx.x]];
+  const long total = d.mode == 2 ? (long)d.OC : (long)d.OCp * d.taps * d.ICp;
+  const long t0 = ((long)(blockIdx.x - d.blk0) * 256 + threadIdx.x) * 8;
+  if (t0 >= total) return;
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const long t = t0 + e;
+    float v = 0.f;
+    if (t < total) {
+      if (d.mode == 2) {
+        v = d.src[t];
+      } else {
+        int co, ci, tap;
+        if (d.mode == 0) {
+          ci = (int)(t % d.ICp);
+          long r = t / d.ICp;
+          tap = (int)(r % d.taps);
+          co = (int)(r / d.taps);
+        } else {
+          co = (int)(t % d.OCp);
+          long r = t / d.OCp;
+          tap = (int)(r % d.taps);
+          ci = (int)(r / d.taps);
+        }
+        v = (co < d.OC && ci < d.IC) ? d.src[((long)co * d.IC + ci) * d.taps + tap] : 0.f;
+      }
     }
-    int co, ci, tap;
-    if (d.mode == 0) {
-      ci = (int)(t % d.ICp);
-      long r = t / d.ICp;
-      tap = (int)(r % d.taps);
-      co = (int)(r / d.taps);
-    } else {
-      co = (int)(t % d.OCp);
-      long r = t / d.OCp;
-      tap = (int)(r % d.taps);
-      ci = (int)(r / d.taps);
-    }
-    float v = (co < d.OC && ci < d.IC) ? d.src[((long)co * d.IC + ci) * d.taps + tap] : 0.f;
-    d.dst[t] = (bf16)v;
+    o[e] = (bf16)v;
+  }
+  if (t0 + 7 < total && ((reinterpret_cast<uintptr_t>(d.dst + t0) & 15) == 0)) {
+    *reinterpret_cast<bf16x8*>(d.dst + t0) = o;
+  } else {
+    for (int e = 0; e < 8 && t0 + e < total; ++e) d.dst[t0 + e] = o[e];
   }
 }
 
 }  // namespace
 
-D3D_API int d3d_pack_all(const void* descs, int n, hipStream_t st) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(pack_all_k, dim3(512, n), dim3(256), 0, st, (const PackDesc*)descs);
+// descs: n PackDesc; blk_desc: [total_blocks] descriptor index of every block
+D3D_API int d3d_pack_all(const void* descs, const int* blk_desc, int total_blocks, hipStream_t st) {
+  if (total_blocks <= 0) return 0;
+  hipLaunchKernelGGL(pack_all_k, dim3(total_blocks), dim3(256), 0, st, (const PackDesc*)descs, blk_desc);
   return (int)hipGetLastError();
 }
 
@@ -1035,7 +1244,7 @@ D3D_API int d3d_pack_all(const void* descs, int n, hipStream_t st) {
 // I: [N, IH, IW, IC] bf16 (IC % 8 == 0), Wp: packed [OCp][taps][ICp] bf16 with
 // OCp % 128 == 0 and ICp % 64 == 0.  O: [N, OH, OW, ldo] bf16.  taps = 9 (3x3)
 // or 1 (1x1 / per-pixel linear).
-static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline
+static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline, 2: buffer-descriptor LDS-DMA
 static int g_conv_korder = 1;     // glds k-step order: 1 channel-chunk major, 0 tap major
 static int g_wgrad_impl = 0;      // 0: register-staged; 1-4: glds (PK,NS) = (64,2) (32,2) (32,3) (64,3)
 static const bf16* g_zero16 = nullptr;
@@ -1065,7 +1274,7 @@ D3D_API int d3d_conv_plan(int N, int OH, int OW, int OC, int ICp, int taps) {
   long Mpix = (long)N * OH * OW;
   long blocks = ((Mpix + BN - 1) / BN) * ((OC + BM - 1) / BM);
   int nk = taps * ICp / 64;
-  if (blocks >= 384 || (OC & 3) || g_conv_impl != 1) return 1;
+  if (blocks >= 384 || (OC & 3) || g_conv_impl < 1) return 1;
   long want = (512 + blocks - 1) / blocks;
   long maxs = nk / 6;
   if (want > maxs) want = maxs;
@@ -1078,9 +1287,31 @@ D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const flo
                      int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, hipStream_t st) {
   long Mpix = (long)N * OH * OW;
   constexpr int BM = 128, BN = 128;
-  if (nsplit < 1 || !ws || g_conv_impl != 1) nsplit = 1;
+  if (nsplit < 1 || !ws || g_conv_impl < 1) nsplit = 1;
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM), (unsigned)nsplit);
-  if (g_conv_impl == 1 && g_zero16) {
+  const long in_bytes = (long)N * IH * IW * IC * 2, w_bytes = (long)((OC + 127) / 128 * 128) * taps * ICp * 2;
+  if (g_conv_impl == 2 && (!trans || stride == 1) && in_bytes < (1L << 31) && w_bytes < (1L << 31)) {
+    float* part = nsplit > 1 ? ws : nullptr;
+#define BUFL(TP, TR)                                                                                             \
+  hipLaunchKernelGGL((conv_bufl_k<TP, TR>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,        \
+                     row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, \
+                     OC, ldo, stride, scale, res_nmod, part, g_conv_korder)
+    if (taps == 9) {
+      if (trans) BUFL(9, true); else BUFL(9, false);
+    } else {
+      if (trans) BUFL(1, true); else BUFL(1, false);
+    }
+#undef BUFL
+    if (part) {
+      long nv = Mpix * (OC / 4);
+      long g = (nv + 255) / 256;
+      if (g > 4096) g = 4096;
+      hipLaunchKernelGGL(conv_splitk_epi_k, dim3((unsigned)g), dim3(256), 0, st, part, nsplit, Mpix, OC, OH * OW,
+                         bias, row_bias, (const bf16*)res, res_nmod, (bf16*)O, ldo, scale);
+    }
+    return (int)hipGetLastError();
+  }
+  if (g_conv_impl >= 1 && g_zero16) {
     float* part = nsplit > 1 ? ws : nullptr;
 #define GLDS(TP, TR)                                                                                             \
   hipLaunchKernelGGL((conv_glds_k<TP, TR>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,        \

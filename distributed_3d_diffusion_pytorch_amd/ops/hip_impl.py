@@ -27,12 +27,13 @@ _ZERO_PAGE: Dict[int, torch.Tensor] = {}
 
 
 def set_conv_impl(impl: str) -> None:
-    """'glds' (default: direct-to-LDS pipelined MFMA kernel) or 'reg'
-    (register-staged variant, kept for A/B measurements)."""
+    """'bufl' (default: buffer-descriptor LDS-DMA pipelined MFMA kernel),
+    'glds' (flat-address LDS-DMA) or 'reg' (register-staged); the latter two
+    are kept for A/B measurements and for operands beyond 2 GiB."""
     dev = torch.cuda.current_device()
     if dev not in _ZERO_PAGE:
         _ZERO_PAGE[dev] = torch.zeros(64, dtype=BF16, device="cuda")
-    _chk(_lib.d3d_set_conv_impl(1 if impl == "glds" else 0, _ZERO_PAGE[dev].data_ptr()), "set_conv_impl")
+    _chk(_lib.d3d_set_conv_impl({"reg": 0, "glds": 1, "bufl": 2}[impl], _ZERO_PAGE[dev].data_ptr()), "set_conv_impl")
 
 
 def set_conv_korder(korder: int) -> None:
@@ -55,7 +56,7 @@ _IMPL_SET = [False]
 def _ensure_impl():
     if not _IMPL_SET[0]:
         import os
-        set_conv_impl(os.environ.get("D3D_CONV_IMPL", "glds"))
+        set_conv_impl(os.environ.get("D3D_CONV_IMPL", "bufl"))
         _IMPL_SET[0] = True
 
 
@@ -90,7 +91,7 @@ def _up(x: int, m: int) -> int:
 # entry alone.
 _EPOCH = [0]
 _WCACHE: Dict[Tuple, list] = {}          # key -> [tok, tensor, desc_tuple]
-_DESC_TABLE = [None, 0, -1]              # device tensor, count, revision
+_DESC_TABLE = [None, None, -1, 0]        # descriptors, block->descriptor map, revision, total blocks
 _REV = [0]
 
 
@@ -123,19 +124,25 @@ def refresh_weights() -> None:
     if _DESC_TABLE[2] != _REV[0]:
         import numpy as np
         rows = []
+        blk = 0
         for key, (tok, t, (p, desc)) in _WCACHE.items():
             if desc is None:
                 continue
             OC, IC, OCp, ICp, taps, mode = desc
-            rows.append((p.data_ptr(), t.data_ptr(), OC, IC, OCp, ICp, taps, mode))
+            total = OC if mode == 2 else OCp * taps * ICp
+            rows.append((p.data_ptr(), t.data_ptr(), OC, IC, OCp, ICp, taps, mode, blk, 0))
+            blk += (total + 2047) // 2048
         dt = np.dtype([("src", np.uint64), ("dst", np.uint64), ("OC", np.int32), ("IC", np.int32),
-                       ("OCp", np.int32), ("ICp", np.int32), ("taps", np.int32), ("mode", np.int32)])
+                       ("OCp", np.int32), ("ICp", np.int32), ("taps", np.int32), ("mode", np.int32),
+                       ("blk0", np.int32), ("pad", np.int32)])
         arr = np.array(rows, dtype=dt)
         host = torch.from_numpy(arr.view(np.uint8).copy())
         _DESC_TABLE[0] = host.to("cuda", non_blocking=False)
-        _DESC_TABLE[1] = len(rows)
+        counts = np.diff(np.append(arr["blk0"], blk))
+        _DESC_TABLE[1] = torch.from_numpy(np.repeat(np.arange(len(rows), dtype=np.int32), counts)).to("cuda")
         _DESC_TABLE[2] = _REV[0]
-    _chk(_lib.d3d_pack_all(_DESC_TABLE[0].data_ptr(), _DESC_TABLE[1], _st()), "pack_all")
+        _DESC_TABLE[3] = blk
+    _chk(_lib.d3d_pack_all(_DESC_TABLE[0].data_ptr(), _DESC_TABLE[1].data_ptr(), _DESC_TABLE[3], _st()), "pack_all")
     for ent in _WCACHE.values():
         p = ent[2][0]
         ent[0] = (p._version, _EPOCH[0])
@@ -215,7 +222,7 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0):
     dg = tg if direct else torch.empty(C, dtype=F32, device=dev)
     db = tb if direct else torch.empty(C, dtype=F32, device=dev)
     cp = torch.empty(N * nch * C * 2, dtype=F32, device=dev)
-    gp = torch.empty(N * nch * G * 2 + 64 * 2 * C, dtype=F32, device=dev)
+    gp = torch.empty(N * nch * G * 2 + N * 2 * C + 64 * 2 * C, dtype=F32, device=dev)
     coef = torch.empty(N * G * 2, dtype=F32, device=dev)
     _chk(_lib.d3d_gn_bwd2(mode, x.data_ptr(), dy.data_ptr(), _ptr(ss), stats.data_ptr(), w.data_ptr(),
                           b.data_ptr(), N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), dg.data_ptr(),

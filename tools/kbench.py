@@ -77,13 +77,12 @@ def main():
         y = torch.empty(N, OH, OH, Co, dtype=BF, device=dev)
         g = torch.randn(N, OH, OH, Co, device=dev).to(BF)
         if "conv" in ops:
-            for impl in ("glds-k0", "glds"):
-                H.set_conv_impl("glds")
-                H.set_conv_korder(0 if impl == "glds-k0" else 1)
+            for impl in ("glds", "bufl"):
+                H.set_conv_impl(impl)
                 rep("conv_fwd", shp, "hip-" + impl,
                     timeit(lambda: H._conv_fwd(x, wp, b, None, None, y, N, Hh, Hh, Ci, H._up(Ci, 64), OH, OH, Co, Co,
                                                s, False, 1.0), a.iters), fl)
-            H.set_conv_impl("glds")
+            H.set_conv_impl("bufl")
             if a.torch:
                 wb, bb = w.to(BF), b.to(BF)
                 xc = x.permute(0, 3, 1, 2)
@@ -92,13 +91,12 @@ def main():
         if "dgrad" in ops and s == 1:
             wt = H.packed_weight(w, True, 9)
             dx = torch.empty_like(x)
-            for impl in ("glds-k0", "glds"):
-                H.set_conv_impl("glds")
-                H.set_conv_korder(0 if impl == "glds-k0" else 1)
+            for impl in ("glds", "bufl"):
+                H.set_conv_impl(impl)
                 rep("conv_dgrad", shp, "hip-" + impl,
                     timeit(lambda: H._conv_fwd(g, wt, None, None, None, dx, N, OH, OH, Co, H._up(Co, 64), Hh, Hh, Ci,
                                                Ci, s, True, 1.0), a.iters), fl)
-            H.set_conv_impl("glds")
+            H.set_conv_impl("bufl")
         if "wgrad" in ops:
             for impl in ("reg", "glds64x2", "glds32x2", "glds32x3", "glds64x3"):
                 H.set_wgrad_impl(impl)
