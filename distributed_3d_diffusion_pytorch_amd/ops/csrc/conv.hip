@@ -970,6 +970,233 @@ conv_wgrad_glds_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float
   }
 }
 
+// Buffer descriptor whose inputs are forced wave-uniform (readfirstlane):
+// hipcc cannot always prove uniformity of values derived through loops and
+// would otherwise wrap every buffer op in a waterfall loop (guide T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, long bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)(bytes > 0 ? (bytes < 0x7fffffffL ? bytes : 0x7fffffffL) : 0));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, n, 0x00020000);
+}
+
+// LDS-DMA issue of one wgrad stage (a __device__ function rather than a
+// lambda: buffer-resource values must not appear in host-visible code).
+template <int PK, int PPW, bool FAST>
+__device__ __forceinline__ void wgrad_bufl_issue(bf16* sA, bf16* sB, const bf16* __restrict__ dY,
+                                                 const bf16* __restrict__ I, long in_elems, long p0, long p_end,
+                                                 int OC, int IC, int IH, int IW, int OH, int OW, int OHW, int stride,
+                                                 int kh, int kw, int dpix, int lw, int lh, int wave,
+                                                 const int* trow, const unsigned* aoff, const unsigned* boff,
+                                                 const bool* bok) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  constexpr int BM = 128, BN = 128;
+  const __amdgpu_buffer_rsrc_t rA = uniform_rsrc(dY + p0 * OC, (p_end - p0) * OC * 2);
+#pragma unroll
+  for (int i = 0; i < PPW; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sA + (wave * PPW + i) * 4 * BM), 16, aoff[i], 0, 0, 0);
+  if (FAST) {
+    // base may lie before the tensor (pb < 0: only masked top-padding rows
+    // see it) or, on the last stages, past its end: the record count is
+    // clamped at 0 so nothing beyond the tensor is ever read.  Base halves
+    // go through readfirstlane so the descriptor is provably wave-uniform
+    // (otherwise hipcc wraps every load in a waterfall loop).
+    const long pb = p0 + dpix;
+    const __amdgpu_buffer_rsrc_t rB = uniform_rsrc(I + pb * IC, (in_elems - pb * IC) * 2);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      bool ok = bok[i];
+      const int pp = (int)p0 + trow[i];            // kh / kw are wave-uniform: at most two tests
+      if (kw != 1) {
+        const int ow = pp & (OW - 1);
+        ok = ok && (kw == 0 ? ow != 0 : ow != OW - 1);
+      }
+      if (kh != 1) {
+        const int oh = (pp >> lw) & (OH - 1);
+        ok = ok && (kh == 0 ? oh != 0 : oh != OH - 1);
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * PPW + i) * 4 * BN), 16,
+                                               ok ? boff[i] : 0x80000000u, 0, 0, 0);
+    }
+  } else {
+    const __amdgpu_buffer_rsrc_t rB = uniform_rsrc(I, in_elems * 2);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const long p = p0 + trow[i];
+      int img, oh, ow;
+      if (lw >= 0) {
+        ow = (int)(p & (OW - 1));
+        const long t = p >> lw;
+        oh = (int)(t & (OH - 1));
+        img = (int)(t >> lh);
+      } else {
+        img = (int)(p / OHW);
+        const int rr = (int)(p - (long)img * OHW);
+        oh = rr / OW;
+        ow = rr - oh * OW;
+      }
+      const int ih = oh * stride + kh - 1, iw = ow * stride + kw - 1;
+      const bool ok = bok[i] && ih >= 0 && ih < IH && iw >= 0 && iw < IW;
+      const unsigned vo = (unsigned)((((img * IH + ih) * IW + iw) * IC) * 2) + (boff[i] - (unsigned)(trow[i] * IC * 2));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * PPW + i) * 4 * BN), 16,
+                                               ok ? vo : 0x80000000u, 0, 0, 0);
+    }
+  }
+}
+
+// Buffer-descriptor LDS-DMA weight-gradient kernel.  Same GEMM, split-K,
+// swizzled unpadded LDS image and transpose reads as conv_wgrad_glds_k, with
+// the VALU-issue bottleneck of the flat-address loaders removed:
+//  * operand descriptors are re-based per stage with scalar math (the pixel
+//    window advances by PK), so per-lane offsets are loop-invariant;
+//  * the dY descriptor's record count ends at this split's last pixel and
+//    the input descriptor's at the tensor end: rows past the range read as
+//    zero from the hardware range check (no compare / select);
+//  * FAST (stride 1, power-of-two H and W): the input row is the output row
+//    shifted by a wave-uniform pixel offset, so the only per-stage lane work
+//    is the padding test of the (uniform) tap: at most two mask compares;
+//  * transpose-read lane offsets are precomputed and the two LDS stages are
+//    unrolled so stage bases fold into instruction immediates.
+template <int TAPS, int PK, bool FAST>
+__global__ void __launch_bounds__(256, 2)
+conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __restrict__ ws, long in_elems,
+                  int Nimg, int IH, int IW, int IC, int OH, int OW, int OC, int stride, int pix_per_split, int ncb,
+                  float* __restrict__ bws, int lw, int lh) {
+  constexpr int BM = 128, BN = 128, NS = 2;
+  constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
+  constexpr int STAGE = PK * (BM + BN);
+  constexpr int PPW = PK / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
+  typedef __attribute__((address_space(3))) void lds_void;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int bx, by, bz;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const long T = (long)gx * gy * gridDim.z;
+    const long L = blockIdx.x + (long)gx * (blockIdx.y + (long)gy * blockIdx.z);
+    const long q = T / 8, r = T % 8, xcd = L % 8;
+    const long R = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    bx = (int)(R % gx);
+    by = (int)((R / gx) % gy);
+    bz = (int)(R / ((long)gx * gy));
+  }
+  const int tap = bx / ncb;
+  const int ci0 = (bx % ncb) * BN;
+  const int m0 = by * BM;
+  const int split = bz;
+  const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
+  const long P = (long)Nimg * OH * OW;
+  const long p_begin = (long)split * pix_per_split;
+  const long p_end = p_begin + pix_per_split < P ? p_begin + pix_per_split : P;
+  const int OHW = OH * OW;
+  const int dpix = (kh - 1) * IW + (kw - 1);       // FAST: input pixel = output pixel + dpix
+
+  const int lrow = lane >> 4, pch = lane & 15;
+  int trow[PPW];
+  unsigned aoff[PPW], boff[PPW];
+  bool bok[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    trow[i] = (wave * PPW + i) * 4 + lrow;
+    const int lc = pch ^ (2 * (trow[i] & 7));
+    const int co = m0 + lc * 8, ci = ci0 + lc * 8;
+    aoff[i] = co < OC ? (unsigned)((trow[i] * OC + co) * 2) : 0x80000000u;
+    boff[i] = (unsigned)((trow[i] * IC + ci) * 2);
+    bok[i] = ci < IC;
+  }
+  // transpose-read lane offsets (elements): row (4g+q) + swizzled column chunk
+  const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
+  const int x7 = 2 * ((4 * g + q) & 7);
+  int la[TM], lb[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) la[i] = (4 * g + q) * 128 + ((((wm * 8 + 2 * i + (pc >> 1)) ^ x7)) << 3) + (pc & 1) * 4;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) lb[j] = (4 * g + q) * 128 + ((((wn * 8 + 2 * j + (pc >> 1)) ^ x7)) << 3) + (pc & 1) * 4;
+
+  auto issue = [&](long p0, int stage) {
+    bf16* sA = smem + stage * STAGE;
+    wgrad_bufl_issue<PK, PPW, FAST>(sA, sA + PK * BM, dY, I, in_elems, p0, p_end, OC, IC, IH, IW, OH, OW, OHW, stride,
+                                    kh, kw, dpix, lw, lh, wave, trow, aoff, boff, bok);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const long nsteps = (p_end - p_begin + PK - 1) / PK;
+  const bool do_bias = bws != nullptr && bx == 0;
+  float bacc = 0.f;
+  // bias: thread -> column tid&127, rows half*(PK/2) .. +PK/2 (swizzled reads)
+  const int bcol = tid & 127, bhalf = tid >> 7;
+  auto compute = [&](const bf16* a) {
+    const bf16* b = a + PK * BM;
+    if (do_bias) {
+#pragma unroll
+      for (int r = 0; r < PK / 2; ++r) {
+        const int row = bhalf * (PK / 2) + r;
+        bacc += (float)a[row * 128 + ((((bcol >> 3) ^ (2 * (row & 7)))) << 3) + (bcol & 7)];
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < PK / 32; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        s16x4 lo = ds_tr(a + la[i] + kk * 32 * 128);
+        s16x4 hi = ds_tr(a + la[i] + kk * 32 * 128 + 16 * 128);
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        s16x4 lo = ds_tr(b + lb[j] + kk * 32 * 128);
+        s16x4 hi = ds_tr(b + lb[j] + kk * 32 * 128 + 16 * 128);
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  // one barrier per step: wait for this step's DMA, barrier (every wave's
+  // DMA landed AND every wave done reading the other slot), issue the next
+  // step into the other slot, compute.
+  if (nsteps > 0) issue(p_begin, 0);
+  for (long s = 0; s < nsteps; ++s) {
+    const int st = (int)(s & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nsteps) issue(p_begin + (s + 1) * PK, st ^ 1);
+    compute(smem + st * STAGE);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (do_bias) {
+    if (m0 + bcol < OC) bws[((long)split * 2 + bhalf) * OC + m0 + bcol] = bacc;
+  }
+  const int fr = lane & 15, fq = lane >> 4;
+  const long KW = (long)TAPS * IC;
+  float* slab = ws + (long)split * OC * KW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int ci = ci0 + wn * WN + j * 16 + fr;
+    if (ci >= IC) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < OC) slab[(long)(co + e) * KW + tap * IC + ci] = acc[i][j][e];
+    }
+  }
+}
+
 // sum the split slabs and write dW in OIHW fp32 layout (optionally accumulate)
 __global__ void wgrad_reduce_k(const float* __restrict__ ws, float* __restrict__ dW, int OC, int IC, int splits,
                                int accumulate, int taps, const float* __restrict__ bws, float* __restrict__ db,
@@ -1246,7 +1473,7 @@ D3D_API int d3d_pack_all(const void* descs, const int* blk_desc, int total_block
 // or 1 (1x1 / per-pixel linear).
 static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline, 2: buffer-descriptor LDS-DMA
 static int g_conv_korder = 1;     // glds k-step order: 1 channel-chunk major, 0 tap major
-static int g_wgrad_impl = 0;      // 0: register-staged; 1-4: glds (PK,NS) = (64,2) (32,2) (32,3) (64,3)
+static int g_wgrad_impl = 5;      // 0: register-staged; 1-4: glds (PK,NS) = (64,2) (32,2) (32,3) (64,3); 5: bufl
 static const bf16* g_zero16 = nullptr;
 
 D3D_API int d3d_set_wgrad_impl(int impl) {
@@ -1356,6 +1583,28 @@ static void launch_wgrad(const void* dY, const void* I, float* ws, int N, int IH
                          int OC, int stride, int pps, int ncb, float* bws, int lw, int lh, int taps, dim3 grid,
                          hipStream_t st) {
   constexpr int BM = 128, BN = 128;
+  const long in_elems = (long)N * IH * IW * IC;
+  const long dy_elems = (long)N * OH * OW * OC;
+  // measured exception (profiles/kbench_lin_wgrad.jsonl): very wide per-pixel
+  // GEMMs with very long per-split reductions (level-1 batched FiLM,
+  // 1024 -> 4608 over 65536-pixel splits) run 1.6x faster register-staged
+  const bool wide_long = taps == 1 && (long)OC * IC >= (4L << 20) && pps > 16384;
+  if (g_wgrad_impl >= 5 && !wide_long && in_elems * 2 < (1L << 30) && dy_elems * 2 < (1L << 30)) {
+    constexpr int PK = 32;
+    // (the FAST path measured slower on the 144-channel conditioning conv:
+    // keep it to full 128-channel tiles)
+    const bool fast = stride == 1 && lw >= 0 && IH == OH && IW == OW && IC % 128 == 0;
+#define WB(TP, F)                                                                                                \
+  hipLaunchKernelGGL((conv_wgrad_bufl_k<TP, PK, F>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws,   \
+                     in_elems, N, IH, IW, IC, OH, OW, OC, stride, pps, ncb, bws, lw, lh)
+    if (taps == 9) {
+      if (fast) WB(9, true); else WB(9, false);
+    } else {
+      if (fast) WB(1, true); else WB(1, false);
+    }
+#undef WB
+    return;
+  }
   if (g_wgrad_impl >= 1 && g_zero16) {
 #define WG(TP, PKv, NSv)                                                                                         \
   hipLaunchKernelGGL((conv_wgrad_glds_k<TP, PKv, NSv>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, \

@@ -41,7 +41,7 @@ def set_conv_korder(korder: int) -> None:
     _chk(_lib.d3d_set_conv_korder(int(korder)), "set_conv_korder")
 
 
-_WGRAD_IMPLS = {"reg": 0, "glds": 1, "glds64x2": 1, "glds32x2": 2, "glds32x3": 3, "glds64x3": 4}
+_WGRAD_IMPLS = {"reg": 0, "glds": 1, "glds64x2": 1, "glds32x2": 2, "glds32x3": 3, "glds64x3": 4, "bufl": 5}
 
 
 def set_wgrad_impl(impl: str) -> None:
@@ -57,6 +57,7 @@ def _ensure_impl():
     if not _IMPL_SET[0]:
         import os
         set_conv_impl(os.environ.get("D3D_CONV_IMPL", "bufl"))
+        set_wgrad_impl(os.environ.get("D3D_WGRAD_IMPL", "bufl"))
         _IMPL_SET[0] = True
 
 

@@ -19,3 +19,12 @@ def test_abi_symbols_exported():
     syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
     missing = [n for n in names if n not in syms]
     assert not missing, missing
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="native library not built")
+def test_no_unresolved_kernel_stubs():
+    """A kernel whose host stub was not emitted (e.g. device-only types in a
+    host-visible lambda) links fine but fails at dlopen on the GPU box."""
+    out = subprocess.check_output(["nm", "-u", LIB]).decode()
+    bad = [line for line in out.splitlines() if "__device_stub__" in line]
+    assert not bad, bad

@@ -98,14 +98,15 @@ def main():
                                                Ci, s, True, 1.0), a.iters), fl)
             H.set_conv_impl("bufl")
         if "wgrad" in ops:
-            for impl in ("reg", "glds64x2", "glds32x2", "glds32x3", "glds64x3"):
+            for impl in ("reg", "glds32x2", "bufl"):
                 H.set_wgrad_impl(impl)
                 rep("conv_wgrad", shp, "hip-" + impl,
                     timeit(lambda: H._wgrad(g, x, Co, Ci, N, Hh, Hh, OH, OH, s, 9), a.iters), fl)
-            H.set_wgrad_impl("reg")
+            H.set_wgrad_impl("bufl")
     if "linear" in ops:
-        for (P, Ci, Co) in [(N * 4096, 1024, 256), (N * 1024, 1024, 512), (N * 256, 1024, 512), (N * 64, 1024, 1024),
-                            (N * 256, 256, 768), (N * 4096, 384, 128)]:
+        for (P, Ci, Co) in [(N * 4096, 1024, 2048), (N * 1024, 1024, 4608), (N * 256, 1024, 4608),
+                            (N * 64, 1024, 3072), (N * 256, 256, 768), (N * 64, 512, 1536), (N * 4096, 384, 128),
+                            (N * 4096, 256, 128), (N * 1024, 512, 256)]:
             x = torch.randn(P, Ci, device=dev).to(BF)
             w = torch.randn(Co, Ci, device=dev) / math.sqrt(Ci)
             b = torch.randn(Co, device=dev)
@@ -117,7 +118,11 @@ def main():
             g = torch.randn(P, 1, 1, Co, device=dev).to(BF)
             rep("lin_fwd", shp, "hip", timeit(lambda: H._conv_fwd(x4, wp, b, None, None, y, P, 1, 1, Ci, H._up(Ci, 64),
                                                                    1, 1, Co, Co, 1, False, 1.0, 0, 1), a.iters), fl)
-            rep("lin_wgrad", shp, "hip", timeit(lambda: H._wgrad(g, x4, Co, Ci, P, 1, 1, 1, 1, 1, 1), a.iters), fl)
+            for impl in ("reg", "bufl"):
+                H.set_wgrad_impl(impl)
+                rep("lin_wgrad", shp, "hip-" + impl, timeit(lambda: H._wgrad(g, x4, Co, Ci, P, 1, 1, 1, 1, 1, 1),
+                                                             a.iters), fl)
+            H.set_wgrad_impl("bufl")
             if a.torch:
                 wb = w.to(BF)
                 rep("lin_fwd", shp, "hipblaslt", timeit(lambda: torch.addmm(b.to(BF), x, wb.t()), a.iters), fl)
