@@ -19,6 +19,7 @@ SIGNATURES = {
     "d3d_gn_apply": [P, P, P, P, P, I, I, I, I, I, P],
     "d3d_gn_film": [P, P, P, P, P, P, I, I, I, I, F, U64, I, P, P],
     "d3d_gn_bwd": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, P],
+    "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P],
     "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P],
     # elementwise.hip
     "d3d_silu": [P, P, L, P],

@@ -178,6 +178,78 @@ __global__ void gn_film_k(const bf16* __restrict__ x, const float* __restrict__ 
   }
 }
 
+// ----------------------------------------------- chunked apply (fused) ----
+// Same chunking as the statistics pass (grid = chunks x images): each block
+// merges its image's chunk partials into LDS (the separate finalize launch is
+// gone -- at small batch every GroupNorm paid ~10 us for it), block 0 of the
+// image also publishes mean / rstd for the backward pass.
+__device__ __forceinline__ void merge_image_stats(const float* __restrict__ part, int n, int nchunks, int G, int P,
+                                                  int rows, int Cg, float eps, float* s_st,
+                                                  float* __restrict__ stats_out, bool publish) {
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    Moments m = {0.f, 0.f, 0.f};
+    for (int c = 0; c < nchunks; ++c) {
+      const int q0 = c * rows, q1 = min(P, q0 + rows);
+      const float* pp = part + (((long)n * nchunks + c) * G + g) * 2;
+      Moments b = {(float)((q1 - q0) * Cg), pp[0], pp[1]};
+      m = merge_moments(m, b);
+    }
+    const float mean = m.mean, rstd = rsqrtf(fmaxf(m.m2 / m.n, 0.f) + eps);
+    s_st[g * 2 + 0] = mean;
+    s_st[g * 2 + 1] = rstd;
+    if (publish) {
+      stats_out[(n * G + g) * 2 + 0] = mean;
+      stats_out[(n * G + g) * 2 + 1] = rstd;
+    }
+  }
+  __syncthreads();
+}
+
+// MODE 0: GN, 1: GN+SiLU, 2: GN+FiLM(+dropout)
+template <int MODE>
+__global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, const float* __restrict__ part,
+                                                  float* __restrict__ stats_out, const float* __restrict__ gamma,
+                                                  const float* __restrict__ beta, const bf16* __restrict__ ss,
+                                                  bf16* __restrict__ y, int P, int C, int G, int rows, int nchunks,
+                                                  float eps, float p_drop, uint64_t seed, int ssld,
+                                                  const uint64_t* __restrict__ seed_dev) {
+  __shared__ float s_st[2 * 1024];
+  const int chunk = blockIdx.x, n = blockIdx.y;
+  const int Cg = C / G;
+  merge_image_stats(part, n, nchunks, G, P, rows, Cg, eps, s_st, stats_out, chunk == 0);
+  if (MODE == 2 && seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
+  const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const int r0 = chunk * rows, r1 = min(P, r0 + rows);
+  const int cv = C / 8;
+  const long nv = (long)(r1 - r0) * cv;
+  const long base = ((long)n * P + r0) * C;
+  for (long v = threadIdx.x; v < nv; v += NT) {
+    const long e = base + v * 8;
+    const int c0 = (int)(v % cv) * 8;
+    f32x8 a = ld8(x + e);
+    f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
+    f32x8 sc = {}, sf = {};
+    if (MODE == 2) {
+      const long pix = e / C;
+      sc = ld8(ss + pix * ssld + c0);
+      sf = ld8(ss + pix * ssld + C + c0);
+    }
+    f32x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int g = (c0 + j) / Cg;
+      float h = (a[j] - s_st[g * 2]) * s_st[g * 2 + 1] * gm[j] + bt[j];
+      if (MODE == 1) h = siluf_(h);
+      if (MODE == 2) {
+        h = h * (1.f + sc[j]) + sf[j];
+        if (p_drop > 0.f) h = (uniform01(seed, (uint64_t)(e + j)) < p_drop) ? 0.f : h * keep_scale;
+      }
+      o[j] = h;
+    }
+    st8(y + e, o);
+  }
+}
+
 // ------------------------------------------------------------- backward ----
 // MODE 0: plain GN, 1: GN+SiLU, 2: GN+FiLM(+dropout)
 template <int MODE>
@@ -337,6 +409,62 @@ __global__ void gn_bwd_apply_k(const bf16* __restrict__ x, const bf16* __restric
   }
 }
 
+// Chunked backward apply with the per-image group coefficients merged in
+// LDS from the reduce pass's partials (replaces gn_bwd_coef_k + gn_bwd_apply_k).
+template <int MODE>
+__global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                      const bf16* __restrict__ ss, const float* __restrict__ stats,
+                                                      const float* __restrict__ grp_part,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      bf16* __restrict__ dx, int P, int C, int G, int rows,
+                                                      int nchunks, float p_drop, uint64_t seed, int ssld,
+                                                      const uint64_t* __restrict__ seed_dev) {
+  __shared__ float s_c[4 * 1024];      // per group: mean, rstd, c1, c2
+  const int chunk = blockIdx.x, n = blockIdx.y;
+  const int Cg = C / G;
+  const float inv = 1.f / (float)((long)P * Cg);
+  for (int g = threadIdx.x; g < G; g += NT) {
+    float a = 0.f, b = 0.f;
+    for (int c = 0; c < nchunks; ++c) {
+      const float* pp = grp_part + (((long)n * nchunks + c) * G + g) * 2;
+      a += pp[0];
+      b += pp[1];
+    }
+    s_c[g * 4 + 0] = stats[(n * G + g) * 2];
+    s_c[g * 4 + 1] = stats[(n * G + g) * 2 + 1];
+    s_c[g * 4 + 2] = a * inv;
+    s_c[g * 4 + 3] = b * inv;
+  }
+  __syncthreads();
+  if (MODE == 2 && seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
+  const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const int r0 = chunk * rows, r1 = min(P, r0 + rows);
+  const int cv = C / 8;
+  const long nv = (long)(r1 - r0) * cv;
+  const long base = ((long)n * P + r0) * C;
+  for (long v = threadIdx.x; v < nv; v += NT) {
+    const long e = base + v * 8;
+    const int c0 = (int)(v % cv) * 8;
+    f32x8 xv = ld8(x + e), dv = ld8(dy + e);
+    f32x8 sc = {};
+    if (MODE == 2) sc = ld8(ss + (e / C) * ssld + c0);
+    f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
+    f32x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int g = (c0 + j) / Cg;
+      const float mean = s_c[g * 4], rstd = s_c[g * 4 + 1], c1 = s_c[g * 4 + 2], c2 = s_c[g * 4 + 3];
+      float keepmul = 1.f;
+      if (MODE == 2 && p_drop > 0.f) keepmul = (uniform01(seed, (uint64_t)(e + j)) < p_drop) ? 0.f : keep_scale;
+      float xhat, dA, dsc, dsh;
+      bwd_elem<MODE>(xv[j], dv[j], mean, rstd, gm[j], bt[j], sc[j], xhat, dA, dsc, dsh, keepmul);
+      const float dxh = dA * gm[j];
+      o[j] = rstd * (dxh - c1 - xhat * c2);
+    }
+    st8(dx + e, o);
+  }
+}
+
 inline int ew_grid(long nvec) {
   long g = (nvec + 255) / 256;
   if (g > 256L * 16) g = 256L * 16;
@@ -361,8 +489,29 @@ D3D_API int d3d_gn_stats(const void* x, int N, int P, int C, int G, float eps, f
   size_t lds = (size_t)p.rpi * C * 3 * sizeof(float);
   hipLaunchKernelGGL(gn_stats_partial_k, dim3(p.nchunks, N), dim3(NT), lds, st, (const bf16*)x, P, C, G, p.rows,
                      p.nchunks, part);
-  hipLaunchKernelGGL(gn_stats_final_k, dim3(cdiv((long)N * G, 256)), dim3(256), 0, st, part, N, P, G, C / G,
-                     p.rows, p.nchunks, eps, stats);
+  if (stats)     // legacy form: finalize separately (the fused apply path passes stats = nullptr)
+    hipLaunchKernelGGL(gn_stats_final_k, dim3(cdiv((long)N * G, 256)), dim3(256), 0, st, part, N, P, G, C / G,
+                       p.rows, p.nchunks, eps, stats);
+  return (int)hipGetLastError();
+}
+
+// Fused finalize + apply over the statistics pass's partials (part from
+// d3d_gn_stats with stats = nullptr).  mode 0 GN, 1 GN+SiLU, 2 GN+FiLM(+dropout;
+// ss [N,P,ssld]).  stats_out receives mean / rstd for the backward pass.
+D3D_API int d3d_gn_apply2(int mode, const void* x, const float* part, float* stats_out, const float* gamma,
+                          const float* beta, const void* ss, void* y, int N, int P, int C, int G, float eps,
+                          float p_drop, unsigned long long seed, int ssld, const void* seed_dev, hipStream_t st) {
+  if (G > 1024) return (int)hipErrorInvalidValue;
+  Plan p = make_plan(N, P, C);
+  if (ssld == 0) ssld = 2 * C;
+#define AP(M)                                                                                                   \
+  hipLaunchKernelGGL(gn_apply2_k<M>, dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, part, stats_out, gamma, \
+                     beta, (const bf16*)ss, (bf16*)y, P, C, G, p.rows, p.nchunks, eps, p_drop, (uint64_t)seed, ssld, \
+                     (const uint64_t*)seed_dev)
+  if (mode == 0) AP(0);
+  else if (mode == 1) AP(1);
+  else AP(2);
+#undef AP
   return (int)hipGetLastError();
 }
 
@@ -410,17 +559,14 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
   else if (mode == 1) RED(1);
   else RED(2);
 #undef RED
-  hipLaunchKernelGGL(gn_bwd_coef_k, dim3(cdiv((long)N * G, 256)), dim3(256), 0, st, grp_part, N, P, C, G,
-                     p.nchunks, coef);
   // dgamma/dbeta: chan_part is [N*nchunks][C][2] -> column sums over 2C
-  // interleaved columns (coef's workspace is reused after the apply kernel
-  // has been enqueued? no: use the tail of chan_part's allocation instead)
+  // interleaved columns (workspace: the tail of grp_part's allocation)
   d3d_colsum(chan_part, (long)N * p.nchunks, 2 * C, grp_part + (long)N * p.nchunks * G * 2, dgamma, dbeta,
              accumulate, st);
-  long nvec = (long)N * P * C / 8;
+  if (G > 1024) return (int)hipErrorInvalidValue;
 #define APP(M)                                                                                                  \
-  hipLaunchKernelGGL(gn_bwd_apply_k<M>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, (const bf16*)dy, \
-                     (const bf16*)ss, stats, coef, gamma, beta, (bf16*)dx, nvec, C, C / G, G, (long)P * C, p_drop, \
+  hipLaunchKernelGGL(gn_bwd_apply2_k<M>, dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, (const bf16*)dy,  \
+                     (const bf16*)ss, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows, p.nchunks, p_drop, \
                      (uint64_t)seed, ssld, (const uint64_t*)seed_dev)
   if (mode == 0) APP(0);
   else if (mode == 1) APP(1);

@@ -210,6 +210,22 @@ def _gn_stats(x, G, eps):
     return stats
 
 
+def _gn_fwd(mode, x, w, b, G, eps, ss=None, ssld=0, p=0.0, seed=0):
+    """Statistics pass + fused finalize/apply (mode 0 GN, 1 GN+SiLU, 2 GN+FiLM):
+    two launches; returns (y, stats) with stats = per-(image, group) mean/rstd."""
+    N, H, W, C = x.shape
+    P = H * W
+    nch, _ = _gn_plan(N, P, C)
+    part = torch.empty(N * nch * G * 2, dtype=F32, device=x.device)
+    stats = torch.empty(N * G * 2, dtype=F32, device=x.device)
+    _chk(_lib.d3d_gn_stats(x.data_ptr(), N, P, C, G, eps, part.data_ptr(), None, _st()), "gn_stats")
+    y = torch.empty_like(x)
+    _chk(_lib.d3d_gn_apply2(mode, x.data_ptr(), part.data_ptr(), stats.data_ptr(), w.data_ptr(), b.data_ptr(),
+                            _ptr(ss), y.data_ptr(), N, P, C, G, float(eps), float(p), int(seed), int(ssld),
+                            _ptr(_SEED_DEV[0]) if mode == 2 else None, _st()), "gn_apply2")
+    return y, stats
+
+
 def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0):
     N, H, W, C = x.shape
     P = H * W
@@ -241,10 +257,7 @@ class _GroupNorm(torch.autograd.Function):
     def forward(ctx, x, weight, bias, groups, eps, silu):
         x = x.contiguous()
         N, H, W, C = x.shape
-        stats = _gn_stats(x, groups, eps)
-        y = torch.empty_like(x)
-        _chk(_lib.d3d_gn_apply(x.data_ptr(), stats.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
-                               N, H * W, C, groups, int(silu), _st()), "gn_apply")
+        y, stats = _gn_fwd(1 if silu else 0, x, weight, bias, groups, eps)
         ctx.save_for_backward(x, weight, bias, stats)
         ctx.cfg = (groups, 1 if silu else 0)
         SINK.use(weight, ctx.needs_input_grad[1])
@@ -281,11 +294,7 @@ class _GNFiLM(torch.autograd.Function):
         N, H, W, C = x.shape
         slot = getattr(ss, "_d3d_slot", None)
         ss, ld = _ss_layout(ss, C)
-        stats = _gn_stats(x, groups, eps)
-        y = torch.empty_like(x)
-        _chk(_lib.d3d_gn_film(x.data_ptr(), stats.data_ptr(), weight.data_ptr(), bias.data_ptr(), ss.data_ptr(),
-                              y.data_ptr(), N, H * W, C, groups, float(p), int(seed), ld, _ptr(_SEED_DEV[0]), _st()),
-             "gn_film")
+        y, stats = _gn_fwd(2, x, weight, bias, groups, eps, ss, ld, p, seed)
         ctx.save_for_backward(x, weight, bias, ss, stats)
         ctx.cfg = (groups, p, seed, ld)
         ctx.slot = slot if ld != 2 * C or slot is not None else None
