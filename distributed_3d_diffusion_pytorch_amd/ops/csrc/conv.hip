@@ -1291,23 +1291,27 @@ __global__ void wgrad_reduce_seg_k(const float* __restrict__ ws, int OC, int IC,
 // the sum in a fixed order (deterministic).  Blocks past the dW range reduce
 // the bias partials the same way.  Destination: dW/db (OIHW) or, when
 // sg.n > 0, the per-parameter segments of a batched projection.
+template <int SL>
 __global__ void __launch_bounds__(256) wgrad_reduce2_k(const float* __restrict__ ws, int OC, int IC, int taps,
                                                        int splits, int accumulate, const float* __restrict__ bws,
                                                        int brows, float* __restrict__ dW, float* __restrict__ db,
                                                        WSegs sg, int nblk_w) {
-  __shared__ f32x4 red[16][16];
-  const int col = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  // 256 threads = COLS float4 columns x SL split lanes (SL = the split count
+  // rounded up to a power of two, <= 16: few splits -> wide blocks)
+  constexpr int COLS = 256 / SL;
+  __shared__ f32x4 red[SL][COLS];
+  const int col = threadIdx.x % COLS, sl = threadIdx.x / COLS;
   const bool is_bias = blockIdx.x >= nblk_w;
   const long total = is_bias ? (long)OC : (long)OC * IC * taps;
   const float* src = is_bias ? bws : ws;
   const int nrows = is_bias ? brows : splits;
-  const long base = (long)(is_bias ? blockIdx.x - nblk_w : blockIdx.x) * 64 + col * 4;
+  const long base = (long)(is_bias ? blockIdx.x - nblk_w : blockIdx.x) * (COLS * 4) + col * 4;
   f32x4 a = {0.f, 0.f, 0.f, 0.f};
   if (base < total) {
     if (base + 3 < total) {
-      for (int k = sl; k < nrows; k += 16) a += *reinterpret_cast<const f32x4*>(src + (long)k * total + base);
+      for (int k = sl; k < nrows; k += SL) a += *reinterpret_cast<const f32x4*>(src + (long)k * total + base);
     } else {
-      for (int k = sl; k < nrows; k += 16)
+      for (int k = sl; k < nrows; k += SL)
         for (int e = 0; e < 4 && base + e < total; ++e) a[e] += src[(long)k * total + base + e];
     }
   }
@@ -1316,7 +1320,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce2_k(const float* __restrict__
   if (sl == 0) {
     f32x4 t = red[0][col];
 #pragma unroll
-    for (int k = 1; k < 16; ++k) t += red[k][col];
+    for (int k = 1; k < SL; ++k) t += red[k][col];
     for (int e = 0; e < 4; ++e) {
       const long o = base + e;
       if (o >= total) break;
@@ -1579,6 +1583,29 @@ D3D_API int d3d_conv3x3(const void* I, const void* Wp, const float* bias, const 
                   res_nmod, 9, nullptr, 1, st);
 }
 
+// launches wgrad_reduce2_k<SL> with SL = splits rounded up to a power of two
+// (<= 16); bias rows (brows = 2 * splits) use the same lanes
+static void launch_reduce2(const float* ws, int OC, int IC, int taps, int splits, int accumulate, const float* bws,
+                           int brows, float* dW, float* db, WSegs sg, bool want_bias, hipStream_t st) {
+  int SL = 1;
+  while (SL < splits && SL < 16) SL <<= 1;
+  const long total = (long)OC * IC * taps;
+  const int per = 4 * (256 / SL);
+  const int nblk_w = (int)((total + per - 1) / per);
+  const int nblk_b = want_bias ? (OC + per - 1) / per : 0;
+  dim3 grid(nblk_w + nblk_b);
+#define RL(S) hipLaunchKernelGGL(wgrad_reduce2_k<S>, grid, dim3(256), 0, st, ws, OC, IC, taps, splits, accumulate, \
+                                 bws, brows, dW, db, sg, nblk_w)
+  switch (SL) {
+    case 1: RL(1); break;
+    case 2: RL(2); break;
+    case 4: RL(4); break;
+    case 8: RL(8); break;
+    default: RL(16); break;
+  }
+#undef RL
+}
+
 static void launch_wgrad(const void* dY, const void* I, float* ws, int N, int IH, int IW, int IC, int OH, int OW,
                          int OC, int stride, int pps, int ncb, float* bws, int lw, int lh, int taps, dim3 grid,
                          hipStream_t st) {
@@ -1669,10 +1696,7 @@ D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW,
   launch_wgrad(dY, I, ws, N, IH, IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh, taps, grid, st);
   {
     WSegs none{};
-    int nblk_w = (int)((total + 63) / 64);
-    int nblk_b = db ? (OC + 63) / 64 : 0;
-    hipLaunchKernelGGL(wgrad_reduce2_k, dim3(nblk_w + nblk_b), dim3(256), 0, st, ws, OC, IC, taps, splits, accumulate,
-                       bws, splits * (256 / BM), dW, db, none, nblk_w);
+    launch_reduce2(ws, OC, IC, taps, splits, accumulate, bws, splits * (256 / BM), dW, db, none, db != nullptr, st);
   }
   return (int)hipGetLastError();
 }
@@ -1704,12 +1728,8 @@ D3D_API int d3d_conv_wgrad_seg(const void* dY, const void* I, float* ws, int N, 
   int lw = lg2(OW), lh = lg2(OH);
   if (lw < 0 || lh < 0) lw = lh = -1;
   launch_wgrad(dY, I, ws, N, IH, IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh, taps, grid, st);
-  {
-    int nblk_w = (int)((total + 63) / 64);
-    int nblk_b = bws ? (OC + 63) / 64 : 0;
-    hipLaunchKernelGGL(wgrad_reduce2_k, dim3(nblk_w + nblk_b), dim3(256), 0, st, ws, OC, IC, taps, splits, accumulate,
-                       bws, splits * (256 / BM), (float*)nullptr, (float*)nullptr, sg, nblk_w);
-  }
+  launch_reduce2(ws, OC, IC, taps, splits, accumulate, bws, splits * (256 / BM), (float*)nullptr, (float*)nullptr, sg,
+                 bws != nullptr, st);
   return (int)hipGetLastError();
 }
 
