@@ -232,9 +232,14 @@ class ConditioningProcessor(nn.Module):
         assert cond_mask.shape == (B,), (cond_mask.shape, B)
         logsnr_emb = self.logsnr_embedding(batch["logsnr"])
         # Data-dependent part: NeRF-encoded camera rays (masked), no gradient.
-        rays = ops.ray_posenc(batch["R"], batch["t"], batch["K"], self.H, self.W,
-                              cond_mask.to(batch["R"].device).bool(), None, None, None,
-                              rescale_from=128 if self.rescale_intrinsics else 0, out_dtype=dtype)
+        # A pinhole ray's origin is the camera centre, identical for every
+        # pixel, so the 93 origin channels form a constant image per frame:
+        # only the 51 direction channels go through the spatial conv, the
+        # origin half enters as per-image tap biases (ops.cond_conv).
+        mask = cond_mask.to(batch["R"].device).bool()
+        rays_dir = ops.ray_posenc_dir(batch["R"], batch["t"], batch["K"], self.H, self.W, mask,
+                                      rescale_from=128 if self.rescale_intrinsics else 0, out_dtype=dtype)
+        orig_pe = ops.ray_origin_pe(batch["t"], mask)
         # Convolution is linear, so conv(rays + emb) = conv(rays) + conv(emb):
         # the learned term is convolved once per FRAME (2 images) and added as
         # a batch-broadcast residual.  Its input gradient (for pos_emb /
@@ -245,8 +250,8 @@ class ConditioningProcessor(nn.Module):
         for i, conv in enumerate(self.convs):
             s = 2 ** i
             e_emb = ops.conv3x3(emb_img, conv.weight, None, stride=s) if emb_img is not None else None
-            e = ops.conv3x3(rays, conv.weight, conv.bias, stride=s, row_bias=logsnr_emb, residual=e_emb,
-                            res_period=2 if e_emb is not None else 0)
+            e = ops.cond_conv(rays_dir, orig_pe, conv.weight, conv.bias, s, row_bias=logsnr_emb, residual=e_emb,
+                              res_period=2 if e_emb is not None else 0)
             sembs.append(ops.silu(e))
         return sembs
 

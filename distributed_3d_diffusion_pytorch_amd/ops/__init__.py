@@ -50,6 +50,23 @@ def linear(x, weight, bias, residual: Optional[torch.Tensor] = None, out_scale: 
     return _t.linear(x, weight, bias, residual, out_scale)
 
 
+def cond_conv(rays_dir, orig_pe, weight, bias, stride: int, row_bias=None, residual=None, res_period: int = 0):
+    if use_hip(rays_dir):
+        return _h().cond_conv(rays_dir, orig_pe, weight, bias, stride, row_bias, residual, res_period)
+    return _t.cond_conv(rays_dir, orig_pe, weight, bias, stride, row_bias, residual, res_period)
+
+
+def ray_posenc_dir(R, t, K, H: int, W: int, cond_mask, rescale_from: int = 0, out_dtype=None):
+    if out_dtype == torch.bfloat16 and R.is_cuda and use_hip(R, any_dtype=True):
+        return _h().ray_posenc_dir(R, t, K, H, W, cond_mask, rescale_from)
+    y = _t.ray_posenc_dir(R, t, K, H, W, cond_mask, rescale_from)
+    return y.to(out_dtype) if out_dtype is not None else y
+
+
+def ray_origin_pe(t, cond_mask):
+    return _t.ray_origin_pe(t, cond_mask)
+
+
 def film_batch(semb, weights, biases):
     if use_hip(semb):
         return _h().film_batch(semb, weights, biases)
@@ -93,6 +110,7 @@ posenc_ddpm = _t.posenc_ddpm
 camera_rays = _t.camera_rays
 posenc_nerf = _t.posenc_nerf
 
-__all__ = ["group_norm", "gn_film", "conv3x3", "linear", "film_batch", "attention", "avgpool2", "upsample2",
+__all__ = ["group_norm", "gn_film", "conv3x3", "linear", "film_batch", "cond_conv", "ray_posenc_dir",
+           "ray_origin_pe", "attention", "avgpool2", "upsample2",
            "silu", "ray_posenc", "posenc_ddpm", "camera_rays", "posenc_nerf", "set_backend",
            "use_hip", "load_library", "library_error", "lib_path"]

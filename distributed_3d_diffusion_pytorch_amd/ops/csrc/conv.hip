@@ -1416,7 +1416,8 @@ struct PackDesc {
   const float* src;
   bf16* dst;
   int OC, IC, OCp, ICp, taps, mode;     // mode 0: pack, 1: transposed pack, 2: cast (OC elements)
-  int blk0, pad;                        // first block of this descriptor in the flattened grid
+  int blk0;                             // first block of this descriptor in the flattened grid
+  int ICs;                              // source IC stride (0: IC) -- channel slices of a weight
 };
 
 // One launch repacks every cached bf16 operand.  The grid is flattened over
@@ -1450,7 +1451,8 @@ __global__ void __launch_bounds__(256) pack_all_k(const PackDesc* __restrict__ d
           tap = (int)(r % d.taps);
           ci = (int)(r / d.taps);
         }
-        v = (co < d.OC && ci < d.IC) ? d.src[((long)co * d.IC + ci) * d.taps + tap] : 0.f;
+        const int ics = d.ICs ? d.ICs : d.IC;
+        v = (co < d.OC && ci < d.IC) ? d.src[((long)co * ics + ci) * d.taps + tap] : 0.f;
       }
     }
     o[e] = (bf16)v;

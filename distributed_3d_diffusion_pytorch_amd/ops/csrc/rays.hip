@@ -73,7 +73,71 @@ __global__ void ray_posenc_k(const float* __restrict__ Rm, const float* __restri
     out[i] = (bf16)val;
   }
 }
+// Direction half only (channels 93..143 -> 0..50), masked, zero-padded to
+// ld channels: the conditioning convs take the spatially constant origin half
+// as per-image biases instead (see cond.hip), so only these 51 channels are
+// convolved.  16-byte stores of 8 channels per thread.
+__global__ void ray_dir_k(const float* __restrict__ Rm, const float* __restrict__ Kinv,
+                          const uint8_t* __restrict__ mask, bf16* __restrict__ out, int B, int H, int W, int ld) {
+  const int cv = ld / 8;
+  const long total = (long)B * 2 * H * W * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cv) * 8;
+    const long pix = i / cv;
+    const int w = (int)(pix % W);
+    const long t1 = pix / W;
+    const int h = (int)(t1 % H);
+    const int nf = (int)(t1 / H);
+    const int b = nf >> 1;
+    bf16x8 o;
+    const bool on = mask == nullptr || mask[b];
+    float src[3] = {0.f, 0.f, 0.f};
+    if (on) {
+      const float* R = Rm + (long)nf * 9;
+      const float* Ki = Kinv + (long)b * 9;
+      const float px = w + 0.5f, py = h + 0.5f;
+      float d0 = Ki[0] * px + Ki[1] * py + Ki[2];
+      float d1 = Ki[3] * px + Ki[4] * py + Ki[5];
+      float d2 = Ki[6] * px + Ki[7] * py + Ki[8];
+      const float inv = rsqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+      d0 *= inv; d1 *= inv; d2 *= inv;
+      src[0] = R[0] * d0 + R[1] * d1 + R[2] * d2;
+      src[1] = R[3] * d0 + R[4] * d1 + R[5] * d2;
+      src[2] = R[6] * d0 + R[7] * d1 + R[8] * d2;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int local = c8 + j;
+      float val = 0.f;
+      if (on && local < 51) {
+        if (local < 3) {
+          val = src[local];
+        } else {
+          int e = local - 3;
+          const bool shifted = e >= 24;
+          if (shifted) e -= 24;
+          const int k = e / 3, comp = e % 3;
+          float a = src[comp] * (float)(1 << k);
+          if (shifted) a = a + 1.5707963267948966f;
+          val = sinf(a);
+        }
+      }
+      o[j] = (bf16)val;
+    }
+    *reinterpret_cast<bf16x8*>(out + pix * ld + c8) = o;
+  }
+}
 }  // namespace
+
+D3D_API int d3d_ray_dir(const float* Rm, const float* Kinv, const unsigned char* mask, void* out, int B, int H,
+                        int W, int ld, hipStream_t st) {
+  if (ld % 8 || ld < 51) return (int)hipErrorInvalidValue;
+  const long total = (long)B * 2 * H * W * (ld / 8);
+  long g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(ray_dir_k, dim3((int)g), dim3(256), 0, st, Rm, Kinv, mask, (bf16*)out, B, H, W, ld);
+  return (int)hipGetLastError();
+}
 
 // Rm: [2B,3,3] fp32 rotations, tv: [2B,3], Kinv: [B,3,3], mask: [B] uint8 or
 // null, pos_emb [144,H,W] / first_emb, other_emb [144] fp32 or null.

@@ -129,13 +129,15 @@ def refresh_weights() -> None:
         for key, (tok, t, (p, desc)) in _WCACHE.items():
             if desc is None:
                 continue
-            OC, IC, OCp, ICp, taps, mode = desc
+            OC, IC, OCp, ICp, taps, mode = desc[:6]
+            src_off = desc[6] if len(desc) > 6 else 0        # byte offset (channel slice)
+            ics = desc[7] if len(desc) > 7 else 0            # source IC stride
             total = OC if mode == 2 else OCp * taps * ICp
-            rows.append((p.data_ptr(), t.data_ptr(), OC, IC, OCp, ICp, taps, mode, blk, 0))
+            rows.append((p.data_ptr() + src_off, t.data_ptr(), OC, IC, OCp, ICp, taps, mode, blk, ics))
             blk += (total + 2047) // 2048
         dt = np.dtype([("src", np.uint64), ("dst", np.uint64), ("OC", np.int32), ("IC", np.int32),
                        ("OCp", np.int32), ("ICp", np.int32), ("taps", np.int32), ("mode", np.int32),
-                       ("blk0", np.int32), ("pad", np.int32)])
+                       ("blk0", np.int32), ("ICs", np.int32)])
         arr = np.array(rows, dtype=dt)
         host = torch.from_numpy(arr.view(np.uint8).copy())
         _DESC_TABLE[0] = host.to("cuda", non_blocking=False)
@@ -169,6 +171,22 @@ def packed_weight(w: torch.Tensor, trans: bool, taps: int = 9) -> torch.Tensor:
     else:   # kernel-side names: rows = IC (padded 128), K = OC (padded 64)
         desc = (OC, IC, _up(OC, 64), _up(IC, 128), taps, 1)
     return _cached(w, f"pack{taps}{'T' if trans else ''}", build, desc)
+
+
+def packed_weight_slice(w: torch.Tensor, ic0: int, nic: int, ICp: int) -> torch.Tensor:
+    """Forward-packed [OCp][9][ICp] bf16 operand of the input-channel slice
+    w[:, ic0:ic0+nic] of a 3x3 weight (the ray-direction half of a
+    conditioning conv), refreshed with every other cached operand."""
+    OC, IC = w.shape[0], w.shape[1]
+    OCp = _up(OC, 128)
+
+    def build():
+        v = w.detach()[:, ic0:ic0 + nic].reshape(OC, nic, 9).permute(0, 2, 1)
+        out = torch.zeros(OCp, 9, ICp, dtype=BF16, device=w.device)
+        out[:OC, :, :nic] = v.to(BF16)
+        return out.reshape(-1)
+    desc = (OC, nic, OCp, ICp, 9, 0, ic0 * 9 * 4, IC)
+    return _cached(w, f"slice{ic0}_{nic}_{ICp}", build, desc)
 
 
 def packed_conv_weight(w: torch.Tensor, trans: bool) -> torch.Tensor:
@@ -465,6 +483,126 @@ def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=No
     rbe = F.pad(row_bias, (0, OCe - OC)) if row_bias is not None else None
     y = _Conv.apply(xe, we, be, stride, re, out_scale, rbe, res_period, 9)
     return y[..., :OC].contiguous() if OCe != OC else y
+
+
+# ------------------------------------------------- conditioning conv ------
+_TAPCOEF: Dict[Tuple, torch.Tensor] = {}
+
+
+def _tap_coef(IH, IW, OH, OW, stride, device):
+    """[9, 9] matrix M with dU[n, t] = sum_k M[t, k] * stats[n, k] over
+    stats = [image total, first row, last row, first col, last col, corners
+    (0,0) (0,W-1) (H-1,0) (H-1,W-1)]: the sum of dy over the pixels where tap t
+    reads inside the image, by inclusion-exclusion (built once per geometry,
+    eagerly, so graph capture never sees the host copy)."""
+    key = (IH, IW, OH, OW, stride, str(device))
+    m = _TAPCOEF.get(key)
+    if m is None:
+        rows = []
+        for t in range(9):
+            kh, kw = t // 3, t % 3
+            top = kh - 1 < 0
+            bot = (OH - 1) * stride + kh - 1 >= IH
+            left = kw - 1 < 0
+            right = (OW - 1) * stride + kw - 1 >= IW
+            rows.append([1.0, -top, -bot, -left, -right, top and left, top and right, bot and left, bot and right])
+        m = torch.tensor(rows, dtype=F32).to(device)
+        _TAPCOEF[key] = m
+    return m
+
+
+class _CondConv(torch.autograd.Function):
+    """Conditioning conv (`xunet.py:292-299,340-350`) on the split ray input:
+    MFMA conv over the 51 direction channels (padded to 64) + the constant
+    origin half as per-image tap biases (cond.hip).  Same result as the
+    144-channel conv; 3x fewer conv FLOPs and half the weight-gradient tiles."""
+
+    @staticmethod
+    def forward(ctx, rays_dir, orig_pe, weight, bias, row_bias, residual, stride, res_period):
+        N, H, W, ICd = rays_dir.shape
+        OC, IC = weight.shape[0], weight.shape[1]
+        no = orig_pe.shape[1]
+        nd = IC - no
+        OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+        wp = packed_weight_slice(weight, no, nd, ICd)
+        W_o = weight.detach()[:, :no].reshape(OC, no, 9)
+        U = torch.einsum("nk,okt->nto", orig_pe, W_o).contiguous()          # [N, 9, OC] fp32
+        rb = U.sum(1)
+        if row_bias is not None:
+            rb = rb + row_bias.float()
+        out = torch.empty(N, OH, OW, OC, dtype=BF16, device=rays_dir.device)
+        res = residual.contiguous() if residual is not None else None
+        _conv_fwd(rays_dir, wp, bias, rb.contiguous(), res, out, N, H, W, ICd, ICd, OH, OW, OC, OC, stride, False,
+                  1.0, res_period, 9)
+        _chk(_lib.d3d_border_fix(out.data_ptr(), U.data_ptr(), N, H, W, OH, OW, OC, stride, _st()), "border_fix")
+        ctx.save_for_backward(rays_dir, orig_pe, weight)
+        ctx.cfg = (stride, residual is not None, row_bias is not None, bias is not None, res_period)
+        ctx.bias_param = bias
+        SINK.use(weight, ctx.needs_input_grad[2])
+        SINK.use(bias, ctx.needs_input_grad[3])
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        rays_dir, orig_pe, weight = ctx.saved_tensors
+        stride, has_res, has_rb, has_b, res_period = ctx.cfg
+        g = dy.contiguous()
+        N, OH, OW, OC = g.shape
+        _, H, W, ICd = rays_dir.shape
+        IC, no = weight.shape[1], orig_pe.shape[1]
+        nd = IC - no
+        bias = ctx.bias_param
+        need_w, need_b = ctx.needs_input_grad[2], has_b and ctx.needs_input_grad[3]
+        per, tot = _chansum(g, True)                                        # [N, OC], [OC]
+        dW = db = None
+        if need_w:
+            dWd, _ = _wgrad(g, rays_dir, OC, ICd, N, H, W, OH, OW, stride, 9)   # [OC, ICd, 9]
+            S = torch.empty(N, 8, OC, dtype=F32, device=g.device)
+            _chk(_lib.d3d_border_sums(g.data_ptr(), S.data_ptr(), N, OH, OW, OC, _st()), "border_sums")
+            stats = torch.cat([per[:, None], S], 1)                         # [N, 9, OC]
+            dU = torch.einsum("tk,nko->nto", _tap_coef(H, W, OH, OW, stride, g.device), stats)
+            dWo = torch.einsum("nto,nk->okt", dU, orig_pe)                  # [OC, no, 9]
+            tw = SINK.target(weight)
+            if tw is not None:
+                tv = tw.view(OC, IC, 9)
+                tv[:, :no].add_(dWo)
+                tv[:, no:].add_(dWd[:, :nd])
+                SINK.done(weight)
+            else:
+                dW = torch.cat([dWo, dWd[:, :nd]], 1).reshape(weight.shape)
+        if need_b:
+            tb = SINK.target(bias)
+            if tb is not None:
+                tb.add_(tot)
+                SINK.done(bias)
+            else:
+                db = tot
+        drb = per if has_rb else None
+        dres = None
+        if has_res:
+            dres = g if not res_period else \
+                g.reshape(N // res_period, res_period, *g.shape[1:]).float().sum(0).to(g.dtype)
+        return None, None, dW, db, drb, dres, None, None
+
+
+def cond_conv(rays_dir, orig_pe, weight, bias, stride, row_bias=None, residual=None, res_period=0):
+    _need_bf16(rays_dir, residual)
+    return _CondConv.apply(rays_dir, orig_pe.float().contiguous(), weight, bias, row_bias, residual, stride,
+                           res_period)
+
+
+def ray_posenc_dir(R, t, K, H, W, cond_mask, rescale_from=0, ld=64):
+    B = R.shape[0]
+    Kd = K.to(torch.float64)
+    if rescale_from:
+        Kd = torch.cat([Kd[:, 0:1] * (W / rescale_from), Kd[:, 1:2] * (H / rescale_from), Kd[:, 2:3]], 1)
+    Kinv = _inv3x3(Kd).float().contiguous()
+    Rf = R.float().reshape(B * 2, 9).contiguous()
+    mask = cond_mask.to(torch.uint8).contiguous()
+    out = torch.empty(B * 2, H, W, ld, dtype=BF16, device=R.device)
+    _chk(_lib.d3d_ray_dir(Rf.data_ptr(), Kinv.data_ptr(), mask.data_ptr(), out.data_ptr(), B, H, W, ld, _st()),
+         "ray_dir")
+    return out
 
 
 # --------------------------------------------------------------- linear ----

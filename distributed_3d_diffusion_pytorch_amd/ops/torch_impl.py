@@ -160,7 +160,8 @@ def posenc_nerf(x: torch.Tensor, min_deg: int, max_deg: int) -> torch.Tensor:
     (`xunet.py:49-59`)."""
     if min_deg == max_deg:
         return x
-    scales = torch.tensor([2.0 ** i for i in range(min_deg, max_deg)], dtype=x.dtype, device=x.device)
+    # exact powers of two built on the device (no host->device copy: graph-capturable)
+    scales = torch.pow(2.0, torch.arange(min_deg, max_deg, device=x.device, dtype=torch.float32)).to(x.dtype)
     xb = (x[..., None, :] * scales[:, None]).flatten(-2)
     emb = torch.sin(torch.cat([xb, xb + math.pi / 2.0], dim=-1))
     return torch.cat([x, emb], dim=-1)
@@ -203,3 +204,34 @@ def film_batch(semb, weights, biases):
     y = F.linear(semb, torch.cat([w.to(semb.dtype) for w in weights], 0),
                  torch.cat([b.to(semb.dtype) for b in biases], 0))
     return tuple(torch.split(y, [w.shape[0] for w in weights], dim=-1))
+
+
+def ray_posenc_dir(R, t, K, H, W, cond_mask, rescale_from: int = 0, ld: int = 64):
+    """Direction half of the ray conditioning (channels 93..143 of
+    :func:`ray_posenc`, masked, no learned embeddings), zero-padded to ``ld``
+    channels: [2B, H, W, ld] fp32."""
+    _, dirs = camera_rays(R, t, K, H, W, rescale_from)
+    emb = posenc_nerf(dirs, 0, 8)
+    emb = torch.where(cond_mask.view(-1, 1, 1, 1, 1), emb, torch.zeros_like(emb))
+    B = emb.shape[0]
+    emb = emb.reshape(B * 2, H, W, emb.shape[-1])
+    return F.pad(emb, (0, ld - emb.shape[-1]))
+
+
+def ray_origin_pe(t, cond_mask):
+    """Origin half (channels 0..92): NeRF posenc of the camera position, which
+    is the same for every pixel of an image: [2B, 93] fp32."""
+    B = t.shape[0]
+    pe = posenc_nerf(t.float().reshape(B * 2, 3), 0, 15)
+    m = cond_mask.to(pe.dtype).repeat_interleave(2)
+    return pe * m[:, None]
+
+
+def cond_conv(rays_dir, orig_pe, weight, bias, stride, row_bias=None, residual=None, res_period=0):
+    """Conditioning conv on the split ray input (oracle): rebuild the 144
+    channels (origin broadcast over pixels + direction) and convolve."""
+    N, H, W, _ = rays_dir.shape
+    nd = weight.shape[1] - orig_pe.shape[1]
+    full = torch.cat([orig_pe[:, None, None, :].to(rays_dir.dtype).expand(N, H, W, orig_pe.shape[1]),
+                      rays_dir[..., :nd]], dim=-1)
+    return conv3x3(full, weight, bias, stride, residual, 1.0, row_bias, res_period)
