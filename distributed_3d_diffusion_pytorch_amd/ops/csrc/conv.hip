@@ -1613,12 +1613,13 @@ static void launch_wgrad(const void* dY, const void* I, float* ws, int N, int IH
                          hipStream_t st) {
   constexpr int BM = 128, BN = 128;
   const long in_elems = (long)N * IH * IW * IC;
-  const long dy_elems = (long)N * OH * OW * OC;
   // measured exception (profiles/kbench_lin_wgrad.jsonl): very wide per-pixel
   // GEMMs with very long per-split reductions (level-1 batched FiLM,
   // 1024 -> 4608 over 65536-pixel splits) run 1.6x faster register-staged
   const bool wide_long = taps == 1 && (long)OC * IC >= (4L << 20) && pps > 16384;
-  if (g_wgrad_impl >= 5 && !wide_long && in_elems * 2 < (1L << 30) && dy_elems * 2 < (1L << 30)) {
+  // the dY descriptor is re-based per stage (its records span one split), so
+  // only the input tensor's size is limited by the 32-bit offsets
+  if (g_wgrad_impl >= 5 && !wide_long && in_elems * 2 < (1L << 30) && (long)pps * OC * 2 < (1L << 31)) {
     constexpr int PK = 32;
     // (the FAST path measured slower on the 144-channel conditioning conv:
     // keep it to full 128-channel tiles)
@@ -1634,7 +1635,7 @@ static void launch_wgrad(const void* dY, const void* I, float* ws, int N, int IH
 #undef WB
     return;
   }
-  if (g_wgrad_impl >= 1 && g_zero16) {
+  if (g_wgrad_impl >= 1 && g_wgrad_impl <= 4 && g_zero16) {
 #define WG(TP, PKv, NSv)                                                                                         \
   hipLaunchKernelGGL((conv_wgrad_glds_k<TP, PKv, NSv>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws, \
                      g_zero16, N, IH, IW, IC, OH, OW, OC, stride, pps, ncb, bws, lw, lh)
