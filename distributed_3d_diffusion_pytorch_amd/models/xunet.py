@@ -87,10 +87,20 @@ class ResnetBlock(nn.Module):
         nn.init.zeros_(self.conv2.weight)
         self._seed_slot = 0
 
-    def forward(self, x: torch.Tensor, semb: torch.Tensor) -> torch.Tensor:
-        N, H, W, C = x.shape
-        assert C == self.in_features, (C, self.in_features)
-        h = self.groupnorm0(x, silu=True)
+    def forward(self, x, semb: torch.Tensor) -> torch.Tensor:
+        skip = None
+        if isinstance(x, tuple):
+            # decoder: x is the skip concatenation [h | hs] (xunet.py:521-531),
+            # never materialised -- GN0 and the 1x1 skip read both halves
+            a, b = x
+            assert a.shape[-1] + b.shape[-1] == self.in_features and self.in_features != self.features
+            h, skip = ops.cat_gn_silu_dense(a, b, self.groupnorm0.gn.weight, self.groupnorm0.gn.bias,
+                                            self.dense.weight, self.dense.bias, self.groupnorm0.gn.num_groups,
+                                            self.groupnorm0.gn.eps)
+        else:
+            N, H, W, C = x.shape
+            assert C == self.in_features, (C, self.in_features)
+            h = self.groupnorm0(x, silu=True)
         h = ops.conv3x3(h, self.conv1.weight, self.conv1.bias)
         ss = self.__dict__.pop("_ss", None)     # precomputed by the level-batched FiLM
         if ss is None:
@@ -98,10 +108,8 @@ class ResnetBlock(nn.Module):
         h = ops.gn_film(h, self.groupnorm1.gn.weight, self.groupnorm1.gn.bias, ss,
                         self.groupnorm1.gn.num_groups, self.groupnorm1.gn.eps,
                         self.dropout_p, self.training, _next_seed(self))
-        if self.in_features != self.features:
-            skip = ops.linear(x, self.dense.weight, self.dense.bias)
-        else:
-            skip = x
+        if skip is None:
+            skip = ops.linear(x, self.dense.weight, self.dense.bias) if self.in_features != self.features else x
         h = ops.conv3x3(h, self.conv2.weight, self.conv2.bias, residual=skip, out_scale=INV_SQRT2)
         if self.resample == "down":
             h = ops.avgpool2(h)
@@ -167,8 +175,9 @@ class XUNetBlock(nn.Module):
             self.attnblock_self = AttnBlock("self", attn_heads, features)
             self.attnblock_cross = AttnBlock("cross", attn_heads, features)
 
-    def forward(self, x: torch.Tensor, semb: torch.Tensor) -> torch.Tensor:
-        assert x.shape[-1] == self.in_channels, (x.shape, self.in_channels)
+    def forward(self, x, semb: torch.Tensor) -> torch.Tensor:
+        c = sum(t.shape[-1] for t in x) if isinstance(x, tuple) else x.shape[-1]
+        assert c == self.in_channels, (c, self.in_channels)
         h = self.resnetblock(x, semb)
         if self.use_attn:
             h = self.attnblock_self(h)
@@ -386,8 +395,7 @@ class XUNet(nn.Module):
         for i in reversed(range(L)):
             level = self.upsample[str(i)]
             for j in range(self.num_res_blocks + 1):
-                h = torch.cat([h, hs.pop()], dim=-1)
-                h = level[j](h, sembs[i])
+                h = level[j]((h, hs.pop()), sembs[i])       # skip concat, fused into the block entry
             if i != 0:
                 h = level[-1](h, sembs[i])
         assert not hs

@@ -67,6 +67,12 @@ def ray_origin_pe(t, cond_mask):
     return _t.ray_origin_pe(t, cond_mask)
 
 
+def cat_gn_silu_dense(a, b, gw, gb, dw, db, groups: int = 32, eps: float = 1e-5):
+    if use_hip(a):
+        return _h().cat_gn_silu_dense(a, b, gw, gb, dw, db, groups, eps)
+    return _t.cat_gn_silu_dense(a, b, gw, gb, dw, db, groups, eps)
+
+
 def film_batch(semb, weights, biases):
     if use_hip(semb):
         return _h().film_batch(semb, weights, biases)
@@ -110,7 +116,7 @@ posenc_ddpm = _t.posenc_ddpm
 camera_rays = _t.camera_rays
 posenc_nerf = _t.posenc_nerf
 
-__all__ = ["group_norm", "gn_film", "conv3x3", "linear", "film_batch", "cond_conv", "ray_posenc_dir",
+__all__ = ["group_norm", "gn_film", "conv3x3", "linear", "film_batch", "cat_gn_silu_dense", "cond_conv", "ray_posenc_dir",
            "ray_origin_pe", "attention", "avgpool2", "upsample2",
            "silu", "ray_posenc", "posenc_ddpm", "camera_rays", "posenc_nerf", "set_backend",
            "use_hip", "load_library", "library_error", "lib_path"]

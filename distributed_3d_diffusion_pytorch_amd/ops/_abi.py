@@ -15,15 +15,15 @@ IP = C.POINTER(C.c_int)
 SIGNATURES = {
     # norm.hip
     "d3d_gn_plan": [I, I, I, IP, IP],
-    "d3d_gn_stats": [P, I, I, I, I, F, P, P, P],
+    "d3d_gn_stats": [P, I, I, I, I, F, P, P, P, I, P],
     "d3d_gn_apply": [P, P, P, P, P, I, I, I, I, I, P],
     "d3d_gn_film": [P, P, P, P, P, P, I, I, I, I, F, U64, I, P, P],
     "d3d_gn_bwd": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, P],
     "d3d_ray_dir": [P, P, P, P, I, I, I, I, P],
     "d3d_border_fix": [P, P, I, I, I, I, I, I, I, P],
     "d3d_border_sums": [P, P, I, I, I, I, P],
-    "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P],
-    "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P],
+    "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, P],
+    "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P],
     # elementwise.hip
     "d3d_silu": [P, P, L, P],
     "d3d_dsilu": [P, P, P, L, P],
@@ -51,6 +51,7 @@ SIGNATURES = {
     "d3d_pack_weight": [P, P, I, I, I, I, I, I, P],
     "d3d_set_conv_impl": [I, P],
     "d3d_pack_all": [P, P, I, P],
+    "d3d_conv_wgrad_cat": [P, P, P, I, P, P, P, I, I, I, I, I, I, P],
     "d3d_conv_wgrad_seg": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "d3d_conv_wgrad2": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     # rays.hip

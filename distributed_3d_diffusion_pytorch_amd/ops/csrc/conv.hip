@@ -1060,9 +1060,9 @@ __device__ __forceinline__ void wgrad_bufl_issue(bf16* sA, bf16* sB, const bf16*
 //    unrolled so stage bases fold into instruction immediates.
 template <int TAPS, int PK, bool FAST>
 __global__ void __launch_bounds__(256, 2)
-conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __restrict__ ws, long in_elems,
-                  int Nimg, int IH, int IW, int IC, int OH, int OW, int OC, int stride, int pix_per_split, int ncb,
-                  float* __restrict__ bws, int lw, int lh) {
+conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I0, float* __restrict__ ws, long in_pix,
+                  int Nimg, int IH, int IW, int ICt, int OH, int OW, int OC, int stride, int pix_per_split, int ncb,
+                  float* __restrict__ bws, int lw, int lh, const bf16* __restrict__ I2, int C1) {
   constexpr int BM = 128, BN = 128, NS = 2;
   constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
   constexpr int STAGE = PK * (BM + BN);
@@ -1083,7 +1083,7 @@ conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float
     bz = (int)(R / ((long)gx * gy));
   }
   const int tap = bx / ncb;
-  const int ci0 = (bx % ncb) * BN;
+  const int ci0g = (bx % ncb) * BN;                // channel tile in the (possibly concatenated) input
   const int m0 = by * BM;
   const int split = bz;
   const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
@@ -1092,6 +1092,13 @@ conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float
   const long p_end = p_begin + pix_per_split < P ? p_begin + pix_per_split : P;
   const int OHW = OH * OW;
   const int dpix = (kh - 1) * IW + (kw - 1);       // FAST: input pixel = output pixel + dpix
+  // virtual channel concat [I0 | I2] (decoder skip concat): a 128-channel
+  // tile lies in one source (C1 % 128 == 0), chosen per block
+  const bool second = I2 != nullptr && ci0g >= C1;
+  const bf16* I = second ? I2 : I0;
+  const int IC = I2 == nullptr ? ICt : (second ? ICt - C1 : C1);
+  const int ci0 = second ? ci0g - C1 : ci0g;
+  const long in_elems = in_pix * IC;
 
   const int lrow = lane >> 4, pch = lane & 15;
   int trow[PPW];
@@ -1181,18 +1188,19 @@ conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float
     if (m0 + bcol < OC) bws[((long)split * 2 + bhalf) * OC + m0 + bcol] = bacc;
   }
   const int fr = lane & 15, fq = lane >> 4;
-  const long KW = (long)TAPS * IC;
+  const long KW = (long)TAPS * ICt;
   float* slab = ws + (long)split * OC * KW;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    int ci = ci0 + wn * WN + j * 16 + fr;
-    if (ci >= IC) continue;
+    const int cl = ci0 + wn * WN + j * 16 + fr;   // channel within the source
+    if (cl >= IC) continue;
+    const int ci = ci0g - ci0 + cl;                 // channel within the concatenation
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       int co = m0 + wm * WM + i * 16 + fq * 4;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (co + e < OC) slab[(long)(co + e) * KW + tap * IC + ci] = acc[i][j][e];
+        if (co + e < OC) slab[(long)(co + e) * KW + tap * ICt + ci] = acc[i][j][e];
     }
   }
 }
@@ -1610,7 +1618,7 @@ static void launch_reduce2(const float* ws, int OC, int IC, int taps, int splits
 
 static void launch_wgrad(const void* dY, const void* I, float* ws, int N, int IH, int IW, int IC, int OH, int OW,
                          int OC, int stride, int pps, int ncb, float* bws, int lw, int lh, int taps, dim3 grid,
-                         hipStream_t st) {
+                         hipStream_t st, const void* I2 = nullptr, int C1 = 0) {
   constexpr int BM = 128, BN = 128;
   const long in_elems = (long)N * IH * IW * IC;
   // measured exception (profiles/kbench_lin_wgrad.jsonl): very wide per-pixel
@@ -1626,7 +1634,7 @@ static void launch_wgrad(const void* dY, const void* I, float* ws, int N, int IH
     const bool fast = stride == 1 && lw >= 0 && IH == OH && IW == OW && IC % 128 == 0;
 #define WB(TP, F)                                                                                                \
   hipLaunchKernelGGL((conv_wgrad_bufl_k<TP, PK, F>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws,   \
-                     in_elems, N, IH, IW, IC, OH, OW, OC, stride, pps, ncb, bws, lw, lh)
+                     (long)N * IH * IW, N, IH, IW, IC, OH, OW, OC, stride, pps, ncb, bws, lw, lh, (const bf16*)I2, C1)
     if (taps == 9) {
       if (fast) WB(9, true); else WB(9, false);
     } else {
@@ -1701,6 +1709,29 @@ D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW,
     WSegs none{};
     launch_reduce2(ws, OC, IC, taps, splits, accumulate, bws, splits * (256 / BM), dW, db, none, db != nullptr, st);
   }
+  return (int)hipGetLastError();
+}
+
+// Per-pixel dense weight gradient over a virtual channel concat [I | I2]
+// (I: [rows, C1], I2: [rows, IC - C1], C1 % 128 == 0): dW [OC][IC].  Returns
+// -1 (nothing launched) when the buffer kernel cannot take the shape; the
+// caller then runs one GEMM per source.
+D3D_API int d3d_conv_wgrad_cat(const void* dY, const void* I, const void* I2, int C1, float* ws, float* dW, float* db,
+                               int rows, int IC, int OC, int splits, int pix_per_split, int accumulate,
+                               hipStream_t st) {
+  constexpr int BM = 128, BN = 128;
+  if (g_wgrad_impl < 5 || C1 % BN || (long)rows * IC * 2 >= (1L << 30) ||
+      (long)pix_per_split * OC * 2 >= (1L << 31))
+    return -1;
+  const bool wide_long = (long)OC * IC >= (4L << 20) && pix_per_split > 16384;
+  if (wide_long) return -1;
+  int ncb = (IC + BN - 1) / BN;
+  dim3 grid(ncb, (OC + BM - 1) / BM, splits);
+  long total = (long)OC * IC;
+  float* bws = db ? ws + (long)splits * total : nullptr;
+  launch_wgrad(dY, I, ws, rows, 1, 1, IC, 1, 1, OC, 1, pix_per_split, ncb, bws, 0, 0, 1, grid, st, I2, C1);
+  WSegs none{};
+  launch_reduce2(ws, OC, IC, 1, splits, accumulate, bws, splits * (256 / BM), dW, db, none, db != nullptr, st);
   return (int)hipGetLastError();
 }
 

@@ -48,9 +48,28 @@ Plan make_plan(int N, int P, int C) {
   return p;
 }
 
+// Virtual channel concat [x | x2] (decoder skip concatenation, xunet.py:521-531):
+// channels [0, C1) live in x ([.., C1]), [C1, C) in x2 ([.., C - C1]); the
+// concatenated tensor is never materialised.  x2 == nullptr: plain x [.., C].
+struct Cat {
+  const bf16* x2;
+  bf16* dx2;
+  int C1;
+};
+
+__device__ __forceinline__ const bf16* xsrc(const bf16* x, const Cat& k, long pix, int c0, int C) {
+  if (k.x2 == nullptr) return x + pix * C + c0;
+  return c0 < k.C1 ? x + pix * k.C1 + c0 : k.x2 + pix * (C - k.C1) + (c0 - k.C1);
+}
+
+__device__ __forceinline__ bf16* dxdst(bf16* dx, const Cat& k, long pix, int c0, int C) {
+  if (k.x2 == nullptr) return dx + pix * C + c0;
+  return c0 < k.C1 ? dx + pix * k.C1 + c0 : k.dx2 + pix * (C - k.C1) + (c0 - k.C1);
+}
+
 // ---------------------------------------------------------------- stats ----
 __global__ void __launch_bounds__(NT) gn_stats_partial_k(const bf16* __restrict__ x, int P, int C, int G,
-                                                         int rows, int nchunks, float* __restrict__ part) {
+                                                         int rows, int nchunks, float* __restrict__ part, Cat cat) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][C][3]
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int tpr = C / 8, rpi = NT / tpr;
@@ -63,17 +82,17 @@ __global__ void __launch_bounds__(NT) gn_stats_partial_k(const bf16* __restrict_
 #pragma unroll
   for (int j = 0; j < 8; ++j) { sh[j] = 0.f; s[j] = 0.f; q[j] = 0.f; }
   if (active) {
-    const bf16* base = x + ((long)n * P) * C + c0;
+    const long pix0 = (long)n * P;
     int r = r0 + roff;
     if (r < r1) {
-      f32x8 a = ld8(base + (long)r * C);
+      f32x8 a = ld8(xsrc(x, cat, pix0 + r, c0, C));
 #pragma unroll
       for (int j = 0; j < 8; ++j) sh[j] = a[j];
       cnt = 1.f;
       r += rpi;
     }
     for (; r < r1; r += rpi) {
-      f32x8 a = ld8(base + (long)r * C);
+      f32x8 a = ld8(xsrc(x, cat, pix0 + r, c0, C));
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float d = a[j] - sh[j];
@@ -212,7 +231,7 @@ __global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, co
                                                   const float* __restrict__ beta, const bf16* __restrict__ ss,
                                                   bf16* __restrict__ y, int P, int C, int G, int rows, int nchunks,
                                                   float eps, float p_drop, uint64_t seed, int ssld,
-                                                  const uint64_t* __restrict__ seed_dev) {
+                                                  const uint64_t* __restrict__ seed_dev, Cat cat) {
   __shared__ float s_st[2 * 1024];
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int Cg = C / G;
@@ -226,7 +245,7 @@ __global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, co
   for (long v = threadIdx.x; v < nv; v += NT) {
     const long e = base + v * 8;
     const int c0 = (int)(v % cv) * 8;
-    f32x8 a = ld8(x + e);
+    f32x8 a = ld8(xsrc(x, cat, (long)n * P + r0 + v / cv, c0, C));
     f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
     f32x8 sc = {}, sf = {};
     if (MODE == 2) {
@@ -276,7 +295,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
                                                       int P, int C, int G, int rows, int nchunks, float p_drop,
                                                       uint64_t seed, bf16* __restrict__ dss,
                                                       float* __restrict__ chan_part, float* __restrict__ grp_part,
-                                                      int ssld, const uint64_t* __restrict__ seed_dev) {
+                                                      int ssld, const uint64_t* __restrict__ seed_dev, Cat cat) {
   if (seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][C][4]
   const int chunk = blockIdx.x, n = blockIdx.y;
@@ -303,7 +322,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
     for (int r = r0 + roff; r < r1; r += rpi) {
       long pix = (long)n * P + r;
       long e = pix * C + c0;
-      f32x8 xv = ld8(x + e), dv = ld8(dy + e);
+      f32x8 xv = ld8(xsrc(x, cat, pix, c0, C)), dv = ld8(dy + e);
       f32x8 sc = {}, o_s, o_t;
       if (MODE == 2) sc = ld8(ss + pix * ssld + c0);
 #pragma unroll
@@ -418,7 +437,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       bf16* __restrict__ dx, int P, int C, int G, int rows,
                                                       int nchunks, float p_drop, uint64_t seed, int ssld,
-                                                      const uint64_t* __restrict__ seed_dev) {
+                                                      const uint64_t* __restrict__ seed_dev, Cat cat) {
   __shared__ float s_c[4 * 1024];      // per group: mean, rstd, c1, c2
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int Cg = C / G;
@@ -445,7 +464,8 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
   for (long v = threadIdx.x; v < nv; v += NT) {
     const long e = base + v * 8;
     const int c0 = (int)(v % cv) * 8;
-    f32x8 xv = ld8(x + e), dv = ld8(dy + e);
+    const long pixv = (long)n * P + r0 + v / cv;
+    f32x8 xv = ld8(xsrc(x, cat, pixv, c0, C)), dv = ld8(dy + e);
     f32x8 sc = {};
     if (MODE == 2) sc = ld8(ss + (e / C) * ssld + c0);
     f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
@@ -461,7 +481,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
       const float dxh = dA * gm[j];
       o[j] = rstd * (dxh - c1 - xhat * c2);
     }
-    st8(dx + e, o);
+    st8(dxdst(dx, cat, pixv, c0, C), o);
   }
 }
 
@@ -484,11 +504,12 @@ D3D_API int d3d_gn_plan(int N, int P, int C, int* nchunks, int* rows) {
 
 // stats: [N*G*2] fp32 (mean, rstd); part: workspace [N*nchunks*G*2]
 D3D_API int d3d_gn_stats(const void* x, int N, int P, int C, int G, float eps, float* part, float* stats,
-                         hipStream_t st) {
+                         const void* x2, int C1, hipStream_t st) {
   Plan p = make_plan(N, P, C);
   size_t lds = (size_t)p.rpi * C * 3 * sizeof(float);
+  Cat cat{(const bf16*)x2, nullptr, C1};
   hipLaunchKernelGGL(gn_stats_partial_k, dim3(p.nchunks, N), dim3(NT), lds, st, (const bf16*)x, P, C, G, p.rows,
-                     p.nchunks, part);
+                     p.nchunks, part, cat);
   if (stats)     // legacy form: finalize separately (the fused apply path passes stats = nullptr)
     hipLaunchKernelGGL(gn_stats_final_k, dim3(cdiv((long)N * G, 256)), dim3(256), 0, st, part, N, P, G, C / G,
                        p.rows, p.nchunks, eps, stats);
@@ -500,14 +521,16 @@ D3D_API int d3d_gn_stats(const void* x, int N, int P, int C, int G, float eps, f
 // ss [N,P,ssld]).  stats_out receives mean / rstd for the backward pass.
 D3D_API int d3d_gn_apply2(int mode, const void* x, const float* part, float* stats_out, const float* gamma,
                           const float* beta, const void* ss, void* y, int N, int P, int C, int G, float eps,
-                          float p_drop, unsigned long long seed, int ssld, const void* seed_dev, hipStream_t st) {
+                          float p_drop, unsigned long long seed, int ssld, const void* seed_dev, const void* x2,
+                          int C1, hipStream_t st) {
   if (G > 1024) return (int)hipErrorInvalidValue;
+  Cat cat{(const bf16*)x2, nullptr, C1};
   Plan p = make_plan(N, P, C);
   if (ssld == 0) ssld = 2 * C;
 #define AP(M)                                                                                                   \
   hipLaunchKernelGGL(gn_apply2_k<M>, dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, part, stats_out, gamma, \
                      beta, (const bf16*)ss, (bf16*)y, P, C, G, p.rows, p.nchunks, eps, p_drop, (uint64_t)seed, ssld, \
-                     (const uint64_t*)seed_dev)
+                     (const uint64_t*)seed_dev, cat)
   if (mode == 0) AP(0);
   else if (mode == 1) AP(1);
   else AP(2);
@@ -546,15 +569,16 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
                         const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
                         unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
                         float* grp_part, float* coef, int accumulate, int ssld, const void* seed_dev,
-                        hipStream_t st) {
+                        const void* x2, void* dx2, int C1, hipStream_t st) {
   Plan p = make_plan(N, P, C);
+  Cat cat{(const bf16*)x2, (bf16*)dx2, C1};
   if (ssld == 0) ssld = 2 * C;
   size_t lds = (size_t)p.rpi * C * 4 * sizeof(float);
   dim3 g(p.nchunks, N);
 #define RED(M)                                                                                                    \
   hipLaunchKernelGGL(gn_bwd_reduce_k<M>, g, dim3(NT), lds, st, (const bf16*)x, (const bf16*)dy, (const bf16*)ss, \
                      stats, gamma, beta, P, C, G, p.rows, p.nchunks, p_drop, (uint64_t)seed, (bf16*)dss,          \
-                     chan_part, grp_part, ssld, (const uint64_t*)seed_dev)
+                     chan_part, grp_part, ssld, (const uint64_t*)seed_dev, cat)
   if (mode == 0) RED(0);
   else if (mode == 1) RED(1);
   else RED(2);
@@ -567,7 +591,7 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
 #define APP(M)                                                                                                  \
   hipLaunchKernelGGL(gn_bwd_apply2_k<M>, dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, (const bf16*)dy,  \
                      (const bf16*)ss, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows, p.nchunks, p_drop, \
-                     (uint64_t)seed, ssld, (const uint64_t*)seed_dev)
+                     (uint64_t)seed, ssld, (const uint64_t*)seed_dev, cat)
   if (mode == 0) APP(0);
   else if (mode == 1) APP(1);
   else APP(2);
@@ -580,5 +604,5 @@ D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, 
                        unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
                        float* grp_part, float* coef, hipStream_t st) {
   return d3d_gn_bwd2(mode, x, dy, ss, stats, gamma, beta, N, P, C, G, p_drop, seed, dx, dss, dgamma, dbeta,
-                     chan_part, grp_part, coef, 0, 0, nullptr, st);
+                     chan_part, grp_part, coef, 0, 0, nullptr, nullptr, nullptr, 0, st);
 }

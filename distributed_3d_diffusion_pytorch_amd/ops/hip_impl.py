@@ -224,32 +224,37 @@ def _gn_stats(x, G, eps):
     nch, _ = _gn_plan(N, P, C)
     part = torch.empty(N * nch * G * 2, dtype=F32, device=x.device)
     stats = torch.empty(N * G * 2, dtype=F32, device=x.device)
-    _chk(_lib.d3d_gn_stats(x.data_ptr(), N, P, C, G, eps, part.data_ptr(), stats.data_ptr(), _st()), "gn_stats")
+    _chk(_lib.d3d_gn_stats(x.data_ptr(), N, P, C, G, eps, part.data_ptr(), stats.data_ptr(), None, 0, _st()),
+         "gn_stats")
     return stats
 
 
-def _gn_fwd(mode, x, w, b, G, eps, ss=None, ssld=0, p=0.0, seed=0):
+def _gn_fwd(mode, x, w, b, G, eps, ss=None, ssld=0, p=0.0, seed=0, x2=None):
     """Statistics pass + fused finalize/apply (mode 0 GN, 1 GN+SiLU, 2 GN+FiLM):
-    two launches; returns (y, stats) with stats = per-(image, group) mean/rstd."""
-    N, H, W, C = x.shape
+    two launches; returns (y, stats) with stats = per-(image, group) mean/rstd.
+    With x2, the input is the virtual channel concat [x | x2]."""
+    N, H, W, C1 = x.shape
+    C = C1 + (x2.shape[-1] if x2 is not None else 0)
     P = H * W
     nch, _ = _gn_plan(N, P, C)
     part = torch.empty(N * nch * G * 2, dtype=F32, device=x.device)
     stats = torch.empty(N * G * 2, dtype=F32, device=x.device)
-    _chk(_lib.d3d_gn_stats(x.data_ptr(), N, P, C, G, eps, part.data_ptr(), None, _st()), "gn_stats")
-    y = torch.empty_like(x)
+    _chk(_lib.d3d_gn_stats(x.data_ptr(), N, P, C, G, eps, part.data_ptr(), None, _ptr(x2), C1, _st()), "gn_stats")
+    y = torch.empty(N, H, W, C, dtype=x.dtype, device=x.device)
     _chk(_lib.d3d_gn_apply2(mode, x.data_ptr(), part.data_ptr(), stats.data_ptr(), w.data_ptr(), b.data_ptr(),
                             _ptr(ss), y.data_ptr(), N, P, C, G, float(eps), float(p), int(seed), int(ssld),
-                            _ptr(_SEED_DEV[0]) if mode == 2 else None, _st()), "gn_apply2")
+                            _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), C1, _st()), "gn_apply2")
     return y, stats
 
 
-def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0):
-    N, H, W, C = x.shape
+def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None):
+    N, H, W, C1 = x.shape
+    C = C1 + (x2.shape[-1] if x2 is not None else 0)
     P = H * W
     nch, _ = _gn_plan(N, P, C)
     dev = x.device
     dx = torch.empty_like(x)
+    dx2 = torch.empty_like(x2) if x2 is not None else None
     if dss is None and ss is not None:
         dss = torch.empty_like(ss)
     tg, tb = SINK.target(w), SINK.target(b)
@@ -262,7 +267,9 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0):
     _chk(_lib.d3d_gn_bwd2(mode, x.data_ptr(), dy.data_ptr(), _ptr(ss), stats.data_ptr(), w.data_ptr(),
                           b.data_ptr(), N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), dg.data_ptr(),
                           db.data_ptr(), cp.data_ptr(), gp.data_ptr(), coef.data_ptr(), int(direct), int(ssld),
-                          _ptr(_SEED_DEV[0]) if mode == 2 else None, _st()), "gn_bwd")
+                          _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), _ptr(dx2), C1, _st()), "gn_bwd")
+    if x2 is not None:
+        dx = (dx, dx2)
     if direct:
         SINK.done(w)
         SINK.done(b)
@@ -288,6 +295,97 @@ class _GroupNorm(torch.autograd.Function):
         G, mode = ctx.cfg
         dx, _, dg, db = _gn_bwd(mode, x, dy.contiguous(), None, stats, w, b, G, 0.0, 0)
         return dx, dg, db, None, None, None
+
+
+import os as _os
+_CAT_FUSE = _os.environ.get("D3D_CAT_FUSE", "1")
+
+
+class _CatGNDense(torch.autograd.Function):
+    """Decoder ResnetBlock entry on the virtual concat x = [h | skip]
+    (`xunet.py:521-531` + `xunet.py:139-150`): returns silu(GN0(x)) and the
+    1x1 NIN skip dense(x) without materialising x: the GroupNorm kernels read
+    both halves in place, the dense is two accumulating GEMMs, and the backward
+    writes the two input gradients directly (no concat / split copies, no
+    accumulation of the two branches' gradients)."""
+
+    @staticmethod
+    def forward(ctx, a, b, gw, gb, dw, db, groups, eps):
+        a, b = a.contiguous(), b.contiguous()
+        N, H, W, C1 = a.shape
+        C2 = b.shape[-1]
+        y, stats = _gn_fwd(1, a, gw, gb, groups, eps, x2=b)
+        wb = bf16_weight(dw)                                    # [OC, C1 + C2]
+        OC = wb.shape[0]
+        a2, b2 = a.reshape(-1, C1), b.reshape(-1, C2)
+        skip = torch.addmm(bf16_weight(db), a2, wb[:, :C1].t()) if db is not None else torch.mm(a2, wb[:, :C1].t())
+        skip.addmm_(b2, wb[:, C1:].t())
+        ctx.save_for_backward(a, b, gw, gb, stats, dw)
+        ctx.cfg = (groups, db is not None)
+        ctx.params = (dw, db)
+        SINK.use(gw, ctx.needs_input_grad[2])
+        SINK.use(gb, ctx.needs_input_grad[3])
+        SINK.use(dw, ctx.needs_input_grad[4])
+        SINK.use(db, ctx.needs_input_grad[5])
+        return y, skip.view(N, H, W, OC)
+
+    @staticmethod
+    def backward(ctx, dy, dskip):
+        a, b, gw, gb, stats, dw = ctx.saved_tensors
+        G, has_db = ctx.cfg
+        N, H, W, C1 = a.shape
+        C2 = b.shape[-1]
+        (da, db_in), _, dgw, dgb = _gn_bwd(1, a, dy.contiguous(), None, stats, gw, gb, G, 0.0, 0, x2=b)
+        g = dskip.contiguous()
+        OC = g.shape[-1]
+        g2 = g.reshape(-1, OC)
+        wb = bf16_weight(dw)
+        da.view(-1, C1).addmm_(g2, wb[:, :C1])
+        db_in.view(-1, C2).addmm_(g2, wb[:, C1:])
+        rows = g2.shape[0]
+        C = C1 + C2
+        dwp, dbp = ctx.params
+        gW = gB = None
+        tw = SINK.target(dwp)
+        tb = SINK.target(dbp) if has_db else None
+        direct = tw is not None and (not has_db or tb is not None)
+        dWt = tw.view(OC, C) if direct else torch.zeros(OC, C, dtype=F32, device=g.device)
+        dbt = (tb if direct else torch.zeros(OC, dtype=F32, device=g.device)) if has_db else None
+        # one weight-gradient GEMM over the virtual concat (the kernel picks
+        # the source per 128-channel tile); two GEMMs when it cannot
+        _ensure_impl()
+        sp, pps = ctypes.c_int(), ctypes.c_int()
+        _lib.d3d_conv_wgrad_plan2(rows, 1, 1, OC, C, 1, ctypes.byref(sp), ctypes.byref(pps))
+        ws = torch.empty(sp.value * OC * C + 2 * sp.value * OC, dtype=F32, device=g.device)
+        rc = _lib.d3d_conv_wgrad_cat(g2.data_ptr(), a.data_ptr(), b.data_ptr(), C1, ws.data_ptr(), dWt.data_ptr(),
+                                     _ptr(dbt), rows, C, OC, sp.value, pps.value, 1, _st())
+        if rc < 0:
+            g4 = g2.reshape(rows, 1, 1, OC)
+            dW1, dbias = _wgrad(g4, a.reshape(rows, 1, 1, C1), OC, C1, rows, 1, 1, 1, 1, 1, 1, want_bias=has_db)
+            dW2, _ = _wgrad(g4, b.reshape(rows, 1, 1, C2), OC, C2, rows, 1, 1, 1, 1, 1, 1)
+            dWt[:, :C1].add_(dW1.view(OC, C1))
+            dWt[:, C1:].add_(dW2.view(OC, C2))
+            if has_db:
+                dbt.add_(dbias)
+        else:
+            _chk(rc, "wgrad_cat")
+        if direct:
+            SINK.done(dwp)
+            if has_db:
+                SINK.done(dbp)
+        else:
+            gW = dWt.view(dwp.shape)
+            gB = dbt
+        return da, db_in, dgw, dgb, gW, gB, None, None
+
+
+def cat_gn_silu_dense(a, b, gw, gb, dw, db, groups=32, eps=1e-5):
+    _need_bf16(a, b)
+    C1, C2 = a.shape[-1], b.shape[-1]
+    if C1 % 8 or C2 % 8 or (C1 + C2) // groups > 1024 or _CAT_FUSE == "0":
+        x = torch.cat([a, b], -1)
+        return group_norm(x, gw, gb, groups, eps, True), linear(x, dw, db)
+    return _CatGNDense.apply(a, b, gw, gb, dw, db, groups, eps)
 
 
 def group_norm(x, weight, bias, groups=32, eps=1e-5, silu=False):
@@ -464,7 +562,7 @@ class _Conv(torch.autograd.Function):
         dres = None
         if has_res:
             dres = g if not res_period else \
-                g.reshape(N // res_period, res_period, *g.shape[1:]).float().sum(0).to(g.dtype)
+                g.reshape(N // res_period, res_period, *g.shape[1:]).sum(0, dtype=F32).to(g.dtype)
         return dx, dW, db, None, dres, None, drb, None, None
 
 
@@ -581,7 +679,7 @@ class _CondConv(torch.autograd.Function):
         dres = None
         if has_res:
             dres = g if not res_period else \
-                g.reshape(N // res_period, res_period, *g.shape[1:]).float().sum(0).to(g.dtype)
+                g.reshape(N // res_period, res_period, *g.shape[1:]).sum(0, dtype=F32).to(g.dtype)
         return None, None, dW, db, drb, dres, None, None
 
 

@@ -235,3 +235,9 @@ def cond_conv(rays_dir, orig_pe, weight, bias, stride, row_bias=None, residual=N
     full = torch.cat([orig_pe[:, None, None, :].to(rays_dir.dtype).expand(N, H, W, orig_pe.shape[1]),
                       rays_dir[..., :nd]], dim=-1)
     return conv3x3(full, weight, bias, stride, residual, 1.0, row_bias, res_period)
+
+
+def cat_gn_silu_dense(a, b, gw, gb, dw, db, groups: int = 32, eps: float = 1e-5):
+    """silu(GN(cat[a, b])) and dense(cat[a, b]) (decoder block entry, oracle)."""
+    x = torch.cat([a, b], -1)
+    return group_norm(x, gw, gb, groups, eps, True), linear(x, dw, db)

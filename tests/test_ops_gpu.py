@@ -406,3 +406,31 @@ def test_ray_dir_matches_torch(H):
     assert (a - b).abs().max().item() < 2e-2
     full = T.ray_posenc(R, t, K, Hh, Hh, mask, None, None, None)
     assert torch.allclose(T.ray_origin_pe(t, mask)[:, None, None, :].expand(-1, Hh, Hh, -1), full[..., :93])
+
+
+@pytest.mark.parametrize("C1,C2,OC", [(256, 128, 128), (128, 128, 128), (512, 512, 512), (512, 256, 256)])
+def test_cat_gn_silu_dense(H, C1, C2, OC):
+    """Decoder block entry on the virtual concat == GN+SiLU and dense on the
+    materialised concat (forward and every gradient)."""
+    torch.manual_seed(11)
+    N, Hh = 4, 8
+    a = (torch.randn(N, Hh, Hh, C1, device=DEV) + 0.3).to(BF)
+    b = (torch.randn(N, Hh, Hh, C2, device=DEV) * 2).to(BF)
+    gw = torch.rand(C1 + C2, device=DEV) + 0.5
+    gb = torch.randn(C1 + C2, device=DEV) * 0.1
+    dw = torch.randn(OC, C1 + C2, 1, 1, device=DEV) / 20
+    db = torch.randn(OC, device=DEV) * 0.1
+    gy = torch.randn(N, Hh, Hh, C1 + C2, device=DEV)
+    gs = torch.randn(N, Hh, Hh, OC, device=DEV)
+
+    def run(hip):
+        ins = [leaf(a) if hip else leaf(a, torch.float32), leaf(b) if hip else leaf(b, torch.float32),
+               leaf(gw), leaf(gb), leaf(dw), leaf(db)]
+        y, s = (H if hip else T).cat_gn_silu_dense(*ins, 32, 1e-5)
+        ((y.float() * gy).sum() + (s.float() * gs).sum()).backward()
+        return [y, s] + [t.grad for t in ins]
+
+    hr, rr = run(True), run(False)
+    names = ["y", "skip", "da", "db", "dgw", "dgb", "ddw", "ddb"]
+    for n, x, r in zip(names, hr, rr):
+        assert rel(x, r) < 3e-2, (n, rel(x, r))
