@@ -410,7 +410,7 @@ conv_glds_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   }
 }
 
-template <int TAPS, bool TRANS>
+template <int TAPS, bool TRANS, bool ONEBAR>
 __global__ void __launch_bounds__(256, 2)
 conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
@@ -515,17 +515,29 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   const int nk = k1 - k0;
   const int fr = lane & 15, fq = lane >> 4;
   issue(k0, 0);
+  if (ONEBAR) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
   for (int ks = 0; ks < nk; ++ks) {
     const int st = ks & 1;
-    if (ks + 1 < nk) {
-      issue(k0 + ks + 1, st ^ 1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // retire stage st, keep st^1 in flight
+    if (ONEBAR) {
+      // one barrier per k-step (cdna guide T3/T4 "minimum 2-phase"): stage
+      // the next tile first (its buffer was last read before the previous
+      // barrier), compute this one at raised priority, then wait + barrier
+      if (ks + 1 < nk) issue(k0 + ks + 1, st ^ 1);
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (ks + 1 < nk) {
+        issue(k0 + ks + 1, st ^ 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // retire stage st, keep st^1 in flight
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
     }
-    __builtin_amdgcn_s_barrier();
     const bf16* a = smem + st * STAGE;
     const bf16* b = a + BM * BKk;
+    if (ONEBAR) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < BKk / 32; ++kk) {
       bf16x8 af[TM], bfr[TN];
@@ -538,6 +550,12 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (ONEBAR) {
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();                           // next stage landed everywhere; this one free
+      continue;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                             // stage st free for reuse
@@ -1531,16 +1549,24 @@ D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const flo
   if (nsplit < 1 || !ws || g_conv_impl < 1) nsplit = 1;
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM), (unsigned)nsplit);
   const long in_bytes = (long)N * IH * IW * IC * 2, w_bytes = (long)((OC + 127) / 128 * 128) * taps * ICp * 2;
-  if (g_conv_impl == 2 && (!trans || stride == 1) && in_bytes < (1L << 31) && w_bytes < (1L << 31)) {
+  if (g_conv_impl >= 2 && (!trans || stride == 1) && in_bytes < (1L << 31) && w_bytes < (1L << 31)) {
     float* part = nsplit > 1 ? ws : nullptr;
-#define BUFL(TP, TR)                                                                                             \
-  hipLaunchKernelGGL((conv_bufl_k<TP, TR>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,        \
+#define BUFL(TP, TR, OB)                                                                                         \
+  hipLaunchKernelGGL((conv_bufl_k<TP, TR, OB>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,    \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, \
                      OC, ldo, stride, scale, res_nmod, part, g_conv_korder)
-    if (taps == 9) {
-      if (trans) BUFL(9, true); else BUFL(9, false);
+    if (g_conv_impl == 3) {
+      if (taps == 9) {
+        if (trans) BUFL(9, true, true); else BUFL(9, false, true);
+      } else {
+        if (trans) BUFL(1, true, true); else BUFL(1, false, true);
+      }
     } else {
-      if (trans) BUFL(1, true); else BUFL(1, false);
+      if (taps == 9) {
+        if (trans) BUFL(9, true, false); else BUFL(9, false, false);
+      } else {
+        if (trans) BUFL(1, true, false); else BUFL(1, false, false);
+      }
     }
 #undef BUFL
     if (part) {
