@@ -64,7 +64,9 @@ class OptimConfig:
     eps: float = 1e-8
     weight_decay: float = 0.0
     # D6: the paper warms up over 10M examples; the reference's DDP loop
-    # effectively uses none (last_step = num_epochs / batch_size).
+    # effectively uses none (last_step = num_epochs / batch_size).  -1 = one
+    # pass over the training set (the Lightning module's n_samples/batch_size
+    # warmup steps, lightning/diff3d.py:118-127).
     warmup_examples: int = 0
     use_cosine: bool = False         # lightning/diff3d.py:111-113
     cosine_tmax: int = 300
@@ -97,6 +99,8 @@ class TrainConfig:
     ckpt_every: int = 50
     out_dir: str = ""
     transfer: str = ""               # resume dir (reads <dir>/latest.pt)
+    pretrained: str = ""             # init model (+optim) from a checkpoint file, step restarts at 0
+                                     # (Lightning `pretrained_model`, lightning/diff3d.py:40-45)
     dtype: str = "bf16"              # compute dtype on GPU: bf16 | fp32
     backend: str = "auto"            # ops backend: auto | hip | torch
     seed: int = 0

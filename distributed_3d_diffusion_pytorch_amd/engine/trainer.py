@@ -91,6 +91,11 @@ class Trainer:
         self.logger = MetricsLogger(os.path.join(self.out_dir, "metrics.jsonl") if self.ctx.is_main else None)
         self.fault_step = int(os.environ.get("D3D_FAULT_AT_STEP", "-1"))
         self.fault_rank = int(os.environ.get("D3D_FAULT_RANK", "-1"))
+        if cfg.pretrained and not cfg.transfer:
+            ck = load_checkpoint(cfg.pretrained, map_location="cpu")
+            load_model_weights(self.model, ck["model"])
+            if "optim" in ck:
+                self.optim.load_state_dict(ck["optim"])
         if cfg.transfer:
             self.resume(cfg.transfer)
         if self.reducer is not None:
@@ -232,6 +237,10 @@ class Trainer:
     def fit(self, steps_per_epoch: int = 0) -> Dict[str, float]:
         cfg = self.cfg
         data, ds, sampler = self.make_data()
+        if cfg.optim.warmup_examples < 0:
+            # one pass over the training set (Lightning: n_samples / batch_size steps)
+            n = len(ds) if ds is not None else cfg.global_batch
+            self.warmup_steps = n / cfg.global_batch
         timer = StepTimer(cfg.global_batch, train_flops_per_example(cfg.model.H), self.device)
         timer.start()
         last = {}

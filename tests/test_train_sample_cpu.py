@@ -122,3 +122,33 @@ def test_sampler_quirk_and_shards():
         assert out.shape == (2, 3, 16, 16) and torch.isfinite(out).all()
     spans = [shard_range(8, r, 3) for r in range(3)]
     assert spans == [(0, 3), (3, 6), (6, 8)]
+
+
+def test_lightning_cli_layout(srn_root, tmp_path):
+    """`lightning/train.py` (reference T3): cars.pickle index inside --train_data,
+    --transfer initialises from a checkpoint FILE and restarts at step 0,
+    warmup spans one pass over the training set."""
+    import shutil
+    import lightning.train as ltrain
+    from lightning.xunet import XUNet as LX
+    from lightning.diff3d import Diff3D  # noqa: F401
+    from lightning.SRNdataset import dataset  # noqa: F401
+    from distributed_3d_diffusion_pytorch_amd.models import XUNet
+    assert LX is XUNet
+    shutil.copy(os.path.join(srn_root, "index.pkl"), os.path.join(srn_root, "cars.pickle"))
+    tiny = [f"{k}={v}" for k, v in TINY_OV.items() if k not in ("global_batch",)]
+    out = str(tmp_path / "lt")
+    ltrain.main(["--train_data", srn_root, "--out_dir", out, "max_steps=2", "num_epochs=100"] + tiny)
+    ck = torch.load(os.path.join(out, "latest.pt"), weights_only=True)
+    assert ck["step"] == 2
+    # the Lightning defaults reach the trainer config
+    _, rargs = ltrain.to_root_args(ltrain.parse(["--train_data", srn_root, "--transfer", "x.pt"]))
+    ov = dict(o.split("=", 1) for o in rargs.overrides)
+    assert ov["global_batch"] == "4" and ov["optim.warmup_examples"] == "-1" and ov["pretrained"] == "x.pt"
+    assert rargs.index.endswith("cars.pickle")
+    # --transfer FILE: weights come from the file, the step counter restarts
+    out2 = str(tmp_path / "lt2")
+    ltrain.main(["--train_data", srn_root, "--out_dir", out2, "--transfer", os.path.join(out, "latest.pt"),
+                 "max_steps=1", "num_epochs=100"] + tiny)
+    ck2 = torch.load(os.path.join(out2, "latest.pt"), weights_only=True)
+    assert ck2["step"] == 1
