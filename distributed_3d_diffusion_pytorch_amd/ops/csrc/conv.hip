@@ -494,8 +494,9 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     const bool cok = c0 < lane_cmax;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const bool ok = cok && ((vmask[i] >> tap) & 1u);
-      const unsigned vo = ok ? (unsigned)(boff[i] + ubyte) : 0x80000000u;
+      // branch-free: a failed test sets bit 31 (past every operand's range)
+      const unsigned okb = (unsigned)cok & (vmask[i] >> tap) & 1u;
+      const unsigned vo = (unsigned)(boff[i] + ubyte) | ((okb - 1u) & 0x80000000u);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rI, (lds_void*)(sB + (wave * 4 + i) * 8 * BKk), 16, vo, 0, 0, 0);
     }
   };
@@ -591,6 +592,195 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         int cc = co + e < OC ? co + e : OC - 1;
+        float t = acc[i][j][e] + (bias ? bias[cc] : 0.f);
+        if (row_bias) t += row_bias[(long)img * OC + cc];
+        v[e] = t;
+      }
+      bf16* dst = O + pix * ldo + co;
+      if (co + 3 < OC && (ldo & 3) == 0) {
+        if (res) {
+          bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+        }
+        bf16x4 o4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o4[e] = (bf16)(v[e] * scale);
+        *reinterpret_cast<bf16x4*>(dst) = o4;
+      } else {
+        for (int e = 0; e < 4 && co + e < OC; ++e) {
+          float t = v[e];
+          if (res) t += (float)res[rpix * ldo + co + e];
+          dst[e] = (bf16)(t * scale);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------ 8-wave large tile ------
+// conv_bufl_k's loader and LDS image at one 512-thread block per CU with a
+// BM x 256 tile (BM = 256 or 128 output channels x 256 pixels).  Why: at two
+// 128x128 blocks per CU a BK=64 k-step moves 64 KiB through L2 for 4.2 MFLOP,
+// i.e. ~64 B/clk/CU at the MFMA rate -- above the ~56 B/clk/CU the L2 can
+// deliver per CU (34.5 TB/s / 256 CUs / 2.4 GHz).  A 256x256 tile halves the
+// bytes per FLOP (32 B/clk at the MFMA rate), and its k-step (64 MFMA per wave,
+// 2 waves per SIMD, ~2k cycles) is several times the ~250-400 cycle LDS-DMA
+// landing latency, so two LDS stages with one barrier per k-step keep the
+// next tile in flight behind the whole MFMA phase.  Waves are 2 (channels) x
+// 4 (pixels); each owns a (BM/2) x 64 output tile = TM x 4 16x16 MFMA tiles.
+// One k-step's LDS-DMA issue for conv_w8_k (a __device__ function: a buffer
+// resource captured by a kernel lambda can suppress the kernel's host stub).
+template <int TAPS, bool TRANS, int BM, int APW, int BPW>
+__device__ __forceinline__ void w8_issue(bf16* sA, const bf16* I, const bf16* Wp, int in_bytes, int w_bytes, int kstep,
+                                         int korder, int ICp, int IC, int IW, int wave, const int* aoff,
+                                         const int* boff, const unsigned* vmask, int lane_cmax) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  constexpr int BKk = 64;
+  const __amdgpu_buffer_rsrc_t rI = __builtin_amdgcn_make_buffer_rsrc((void*)I, (short)0, in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, w_bytes, 0x00020000);
+  int tap, c0;
+  if (TAPS == 9 && korder) {
+    tap = kstep % 9;
+    c0 = (kstep / 9) * BKk;
+  } else {
+    tap = TAPS == 9 ? kstep / (ICp / BKk) : 0;
+    c0 = (TAPS == 9 ? kstep % (ICp / BKk) : kstep) * BKk;
+  }
+  const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
+  const int tapoff = (TRANS ? ((1 - kh) * IW + (1 - kw)) : ((kh - 1) * IW + (kw - 1))) * IC;
+  const int ubyte = (tapoff + c0) * 2;
+  const int soffA = (tap * ICp + c0) * 2;
+  bf16* sB = sA + BM * BKk;
+#pragma unroll
+  for (int i = 0; i < APW; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sA + (wave * APW + i) * 8 * BKk), 16, aoff[i] + soffA, 0,
+                                             0, 0);
+  const bool cok = c0 < lane_cmax;
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) {
+    const unsigned okb = (unsigned)cok & (vmask[i] >> tap) & 1u;     // branch-free select
+    const unsigned vo = (unsigned)(boff[i] + ubyte) | ((okb - 1u) & 0x80000000u);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rI, (lds_void*)(sB + (wave * BPW + i) * 8 * BKk), 16, vo, 0, 0, 0);
+  }
+}
+
+template <int TAPS, bool TRANS, int BM, int BN>
+__global__ void __launch_bounds__(512, 1)
+conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
+          const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
+          int in_bytes, int w_bytes, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC,
+          int ldo, int stride, float scale, int res_nmod, int korder) {
+  constexpr int BKk = 64;
+  constexpr int WM = BM / 2, WN = BN / 4, TM = WM / 16, TN = WN / 16;
+  constexpr int APW = BM / 64, BPW = BN / 64;      // 1-KiB DMA pieces per wave per operand
+  constexpr int STAGE = (BM + BN) * BKk;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
+  typedef __attribute__((address_space(3))) void lds_void;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // SGPR: LDS-DMA bases stay scalar
+  const int wm = wave >> 2, wn = wave & 3;
+  const long Mpix = (long)Nimg * OH * OW;
+  const int nbx = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    int q = nbx / 8, r = nbx % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const long n0 = (long)bid * BN;
+  const int m0 = blockIdx.y * BM;
+  const int Kp = TAPS * ICp;
+
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;
+  int boff[BPW], aoff[APW];
+  unsigned vmask[BPW];
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) {
+    const int prow = (wave * BPW + i) * 8 + lrow;
+    const long p = n0 + prow;
+    const bool pv = p < Mpix;
+    const unsigned pp = pv ? (unsigned)p : 0u;       // 32-bit: Mpix < 2^31 (host checks operand sizes)
+    const int pw = (int)(pp % (unsigned)OW);
+    const unsigned t = pp / (unsigned)OW;
+    const int poh = (int)(t % (unsigned)OH);
+    const int pn = (int)(t / (unsigned)OH);
+    const int oh0 = TRANS ? poh : poh * stride, ow0 = TRANS ? pw : pw * stride;
+    boff[i] = (((pn * IH + oh0) * IW + ow0) * IC + lchunk * 8) * 2;
+    unsigned m = 0;
+#pragma unroll
+    for (int tp = 0; tp < TAPS; ++tp) {
+      const int kh = TAPS == 9 ? tp / 3 : 1, kw = TAPS == 9 ? tp % 3 : 1;
+      const int ih = TRANS ? oh0 + 1 - kh : oh0 + kh - 1, iw = TRANS ? ow0 + 1 - kw : ow0 + kw - 1;
+      if (pv && ih >= 0 && ih < IH && iw >= 0 && iw < IW) m |= 1u << tp;
+    }
+    vmask[i] = m;
+  }
+  // weight rows past the packed tensor (OC tile overhang) fall outside the
+  // descriptor's range and read as zeros
+#pragma unroll
+  for (int i = 0; i < APW; ++i) aoff[i] = ((m0 + (wave * APW + i) * 8 + lrow) * Kp + lchunk * 8) * 2;
+  const int lane_cmax = IC - lchunk * 8;
+
+  auto issue = [&](int kstep, int stage) {
+    w8_issue<TAPS, TRANS, BM, APW, BPW>(smem + stage * STAGE, I, Wp, in_bytes, w_bytes, kstep, korder, ICp, IC, IW,
+                                        wave, aoff, boff, vmask, lane_cmax);
+  };
+  auto swz = [](int row, int chunk) { return row * BKk + ((chunk ^ (row & 7)) << 3); };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = Kp / BKk;
+  const int fr = lane & 15, fq = lane >> 4;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int st = ks & 1;
+    // buffer st^1 was last read before the previous barrier: restage it now,
+    // it lands while this k-step's MFMAs run
+    if (ks + 1 < nk) issue(ks + 1, st ^ 1);
+    const bf16* a = smem + st * STAGE;
+    const bf16* b = a + BM * BKk;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < BKk / 32; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(b + swz(wn * WN + j * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a + swz(wm * WM + i * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  const int OHW = OH * OW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const long pix = n0 + wn * WN + j * 16 + fr;
+    if (pix >= Mpix) continue;
+    const int img = (int)(pix / OHW);
+    const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int co = m0 + wm * WM + i * 16 + fq * 4;
+      if (co >= OC) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int cc = co + e < OC ? co + e : OC - 1;
         float t = acc[i][j][e] + (bias ? bias[cc] : 0.f);
         if (row_bias) t += row_bias[(long)img * OC + cc];
         v[e] = t;
@@ -1549,13 +1739,45 @@ D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const flo
   if (nsplit < 1 || !ws || g_conv_impl < 1) nsplit = 1;
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM), (unsigned)nsplit);
   const long in_bytes = (long)N * IH * IW * IC * 2, w_bytes = (long)((OC + 127) / 128 * 128) * taps * ICp * 2;
+  if (g_conv_impl >= 4 && (!trans || stride == 1) && in_bytes < (1L << 31) && w_bytes < (1L << 31) && OC >= 64) {
+    // large-tile 8-wave kernel when its grid still covers every CU
+    const int bm = (OC % 256 == 0 || OC > 384) ? 256 : 128;
+    // 128 / 384-channel layers only as 128x512 tiles on request (impl 6):
+    // 128x256 tiles measured slower than two 128x128 blocks per CU (bufl1)
+    const bool wide = bm == 128 && g_conv_impl == 6;
+    const int bn = wide ? 512 : 256;
+    const long ptiles = (Mpix + bn - 1) / bn;
+    const long blocks = ptiles * ((OC + bm - 1) / bm);
+    if ((bm == 256 || wide) && blocks >= 256) {
+      dim3 g8((unsigned)ptiles, (unsigned)((OC + bm - 1) / bm), 1);
+#define W8(TP, TR, BMv, BNv)                                                                                     \
+  hipLaunchKernelGGL((conv_w8_k<TP, TR, BMv, BNv>), g8, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias, \
+                     row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, \
+                     OC, ldo, stride, scale, res_nmod, g_conv_korder)
+      if (bm == 256) {
+        if (taps == 9) {
+          if (trans) W8(9, true, 256, 256); else W8(9, false, 256, 256);
+        } else {
+          if (trans) W8(1, true, 256, 256); else W8(1, false, 256, 256);
+        }
+      } else {
+        if (taps == 9) {
+          if (trans) W8(9, true, 128, 512); else W8(9, false, 128, 512);
+        } else {
+          if (trans) W8(1, true, 128, 512); else W8(1, false, 128, 512);
+        }
+      }
+#undef W8
+      return (int)hipGetLastError();
+    }
+  }
   if (g_conv_impl >= 2 && (!trans || stride == 1) && in_bytes < (1L << 31) && w_bytes < (1L << 31)) {
     float* part = nsplit > 1 ? ws : nullptr;
 #define BUFL(TP, TR, OB)                                                                                         \
   hipLaunchKernelGGL((conv_bufl_k<TP, TR, OB>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,    \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, \
                      OC, ldo, stride, scale, res_nmod, part, g_conv_korder)
-    if (g_conv_impl == 3) {
+    if (g_conv_impl >= 3) {
       if (taps == 9) {
         if (trans) BUFL(9, true, true); else BUFL(9, false, true);
       } else {

@@ -1,6 +1,7 @@
 """Numerics of every HIP kernel against the fp32 PyTorch composition of the
 same op (ops.torch_impl) on identical bf16-rounded inputs.  GPU only."""
 import math
+import os
 
 import pytest
 import torch
@@ -143,6 +144,25 @@ def test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale):
     for i, (a, c) in enumerate(zip(gh, gr)):
         assert a is not None and c is not None
         assert rel(a, c) < 3e-2, (names[i], rel(a, c))
+
+
+W8_SHAPES = [
+    # large grids (>= 256 blocks of 256 pixels): the 8-wave conv_w8_k path
+    (32, 64, 64, 128, 128, 1, True, False, 1 / math.sqrt(2)),     # BM=128 (w8w: 128x512 tiles)
+    (64, 32, 32, 256, 256, 1, False, True, 1.0),                  # BM=256
+    (300, 12, 20, 128, 384, 1, False, False, 1.0),                # partial pixel tile, OC 384 -> 3 x BM=128
+    (16, 64, 64, 64, 640, 1, True, False, 0.5),                   # OC 640: BM=256 tile overhangs the weights
+]
+
+
+@pytest.mark.parametrize("impl", ["w8", "w8w"])
+@pytest.mark.parametrize("N,Hh,W,Ci,Co,s,res,rb,scale", W8_SHAPES)
+def test_conv3x3_w8(H, impl, N, Hh, W, Ci, Co, s, res, rb, scale):
+    H.set_conv_impl(impl)
+    try:
+        test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale)
+    finally:
+        H.set_conv_impl(os.environ.get("D3D_CONV_IMPL", "w8w"))
 
 
 def test_linear(H):

@@ -25,6 +25,7 @@ def main(path, match=""):
         bc = c.get("SQ_LDS_BANK_CONFLICT", 0)
         print(f"{key[0]:<40} wg={key[1]:<7} vgpr={key[2]}/{key[3]} n={len(n[key])} "
               f"mfma/busy={mf:.2f} ldsconf={bc:.3g} " + " ".join(parts))
+        print("    " + " ".join(f"{k}={v:.4g}" for k, v in sorted(c.items())))
 
 
 if __name__ == "__main__":
