@@ -53,6 +53,7 @@ SIGNATURES = {
     "d3d_pack_all": [P, P, I, P],
     "d3d_conv_wgrad_cat": [P, P, P, I, P, P, P, I, I, I, I, I, I, P],
     "d3d_conv_wgrad_seg": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
+    "d3d_wgrad_scatter": [P, I, I, I, I, P, I, I, P, P, P, P],
     "d3d_conv_wgrad2": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     # rays.hip
     "d3d_ray_posenc": [P, P, P, P, P, P, P, P, I, I, I, P],

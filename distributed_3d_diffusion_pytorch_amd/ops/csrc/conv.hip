@@ -2015,6 +2015,27 @@ D3D_API int d3d_conv_wgrad_seg(const void* dY, const void* I, float* ws, int N, 
   return (int)hipGetLastError();
 }
 
+// Scatter (accumulate) an already reduced [OC][IC] fp32 weight gradient --
+// e.g. a hipBLASLt dY^T X product -- and optional [brows][OC] bias partials
+// into the per-parameter segments of a batched projection (same segment
+// description as d3d_conv_wgrad_seg).
+D3D_API int d3d_wgrad_scatter(const float* ws, int OC, int IC, int splits, int accumulate, const float* bws,
+                              int brows, int nseg, const int* row0, float* const* wdst, float* const* bdst,
+                              hipStream_t st) {
+  if (nseg < 1 || nseg > kMaxSegs) return (int)hipErrorInvalidValue;
+  WSegs sg{};
+  sg.n = nseg;
+  for (int i = 0; i < nseg; ++i) {
+    sg.row0[i] = row0[i];
+    sg.w[i] = wdst[i];
+    sg.b[i] = bdst ? bdst[i] : nullptr;
+  }
+  sg.row0[nseg] = OC;
+  launch_reduce2(ws, OC, IC, 1, splits, accumulate, bws, brows, (float*)nullptr, (float*)nullptr, sg,
+                 bws != nullptr, st);
+  return (int)hipGetLastError();
+}
+
 D3D_API int d3d_conv_wgrad(const void* dY, const void* I, float* ws, float* dW, int N, int IH, int IW, int IC, int OH,
                            int OW, int OC, int stride, int splits, int pix_per_split, int accumulate, int taps,
                            hipStream_t st) {

@@ -9,6 +9,7 @@ graph.
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from typing import Dict, Optional, Tuple
 
@@ -24,6 +25,9 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 
 _ZERO_PAGE: Dict[int, torch.Tensor] = {}
+# FiLM weight gradients: "blas" (hipBLASLt product + segment scatter, default)
+# or "mfma" (split-K MFMA kernel with fused bias sums)
+_FILM_WGRAD_BLAS = os.environ.get("D3D_FILM_WGRAD", "blas") == "blas"
 
 
 def set_conv_impl(impl: str) -> None:
@@ -860,14 +864,26 @@ class _FiLMBatch(torch.autograd.Function):
                 tw = [torch.zeros(w.shape, dtype=F32, device=x2.device) for w in Ws]
                 tb = [torch.zeros(b.shape, dtype=F32, device=x2.device) for b in Bs]
             _ensure_impl()
-            sp, pps = ctypes.c_int(), ctypes.c_int()
-            _lib.d3d_conv_wgrad_plan2(rows, 1, 1, S, K, 1, ctypes.byref(sp), ctypes.byref(pps))
-            ws = torch.empty(sp.value * S * K + 2 * sp.value * S, dtype=F32, device=x2.device)
             row0 = (ctypes.c_int * n)(*offs[:n])
             wd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tw])
             bd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tb])
-            _chk(_lib.d3d_conv_wgrad_seg(dy.data_ptr(), x2.data_ptr(), ws.data_ptr(), rows, 1, 1, K, 1, 1, S, 1,
-                                         sp.value, pps.value, 1, 1, n, row0, wd, bd, _st()), "film_wgrad")
+            if _FILM_WGRAD_BLAS:
+                # wide FiLM weight gradients ([S, 1024] over every pixel of the
+                # level) run 1.4-1.6x faster on hipBLASLt (850-880 TF/s,
+                # profiles/kbench_lin_v2.jsonl) than on the split-K MFMA
+                # kernel; its fp32 [S, K] product and the bias column sums are
+                # then scattered into the parameters' gradients in one launch
+                prod = _mm_f32(dy.t(), x2)
+                nimg = 64 if rows % 64 == 0 else 1
+                _, bsum = _chansum(dy.view(nimg, rows // nimg, 1, S), False)
+                _chk(_lib.d3d_wgrad_scatter(prod.data_ptr(), S, K, 1, 1, bsum.data_ptr(), 1, n, row0, wd, bd,
+                                            _st()), "film_wgrad_scatter")
+            else:
+                sp, pps = ctypes.c_int(), ctypes.c_int()
+                _lib.d3d_conv_wgrad_plan2(rows, 1, 1, S, K, 1, ctypes.byref(sp), ctypes.byref(pps))
+                ws = torch.empty(sp.value * S * K + 2 * sp.value * S, dtype=F32, device=x2.device)
+                _chk(_lib.d3d_conv_wgrad_seg(dy.data_ptr(), x2.data_ptr(), ws.data_ptr(), rows, 1, 1, K, 1, 1, S,
+                                             1, sp.value, pps.value, 1, 1, n, row0, wd, bd, _st()), "film_wgrad")
             if direct:
                 for w, b in zip(Ws, Bs):
                     SINK.done(w)

@@ -324,8 +324,9 @@ def test_sampler_step_matches_posterior(H):
     assert abs(nz.mean().item()) < 0.05 and abs(nz.std().item() - 1) < 0.05
 
 
+@pytest.mark.parametrize("blas", [True, False])
 @pytest.mark.parametrize("chans", [[128, 128, 256], [512, 512]])
-def test_film_batch_with_gn_film(H, chans):
+def test_film_batch_with_gn_film(H, chans, blas):
     """Level-batched FiLM projection feeding strided GN-FiLM: forward, the
     shared d(scale|shift) buffer and the segmented weight-gradient scatter
     against per-block fp32 linears."""
@@ -355,7 +356,12 @@ def test_film_batch_with_gn_film(H, chans):
         loss.backward()
         return [s.grad] + [w.grad for w in ws] + [b.grad for b in bs]
 
-    gh, gr = run(True), run(False)
+    prev = H._FILM_WGRAD_BLAS
+    H._FILM_WGRAD_BLAS = blas          # hipBLASLt product + scatter, or the split-K MFMA kernel
+    try:
+        gh, gr = run(True), run(False)
+    finally:
+        H._FILM_WGRAD_BLAS = prev
     for a, b in zip(gh, gr):
         assert rel(a, b) < 3e-2, rel(a, b)
 

@@ -116,8 +116,23 @@ def main():
             wp = H.packed_weight(w, False, 1)
             y = torch.empty(P, 1, 1, Co, dtype=BF, device=dev)
             g = torch.randn(P, 1, 1, Co, device=dev).to(BF)
-            rep("lin_fwd", shp, "hip", timeit(lambda: H._conv_fwd(x4, wp, b, None, None, y, P, 1, 1, Ci, H._up(Ci, 64),
-                                                                   1, 1, Co, Co, 1, False, 1.0, 0, 1), a.iters), fl)
+            for impl in ("bufl1", "w8w"):
+                H.set_conv_impl(impl)
+                rep("lin_fwd", shp, "hip-" + impl,
+                    timeit(lambda: H._conv_fwd(x4, wp, b, None, None, y, P, 1, 1, Ci, H._up(Ci, 64), 1, 1, Co, Co, 1,
+                                               False, 1.0, 0, 1), a.iters), fl)
+            H.set_conv_impl("w8w")
+            wt = H.packed_weight(w, True, 1)
+            g4 = torch.randn(P, 1, 1, Co, device=dev).to(BF)
+            dx = torch.empty(P, 1, 1, Ci, dtype=BF, device=dev)
+            if P * Co * 2 < (1 << 31):
+                rep("lin_dgrad", shp, "hip-w8w", timeit(lambda: H._conv_fwd(g4, wt, None, None, None, dx, P, 1, 1, Co,
+                                                                              H._up(Co, 64), 1, 1, Ci, Ci, 1, False,
+                                                                              1.0, 0, 1), a.iters), fl)
+            if a.torch:
+                wb = w.to(BF)
+                g2 = g4.reshape(P, Co)
+                rep("lin_dgrad", shp, "hipblaslt", timeit(lambda: torch.mm(g2, wb), a.iters), fl)
             for impl in ("reg", "bufl"):
                 H.set_wgrad_impl(impl)
                 rep("lin_wgrad", shp, "hip-" + impl, timeit(lambda: H._wgrad(g, x4, Co, Ci, P, 1, 1, 1, 1, 1, 1),
