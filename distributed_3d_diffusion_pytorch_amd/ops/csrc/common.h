@@ -60,6 +60,26 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
   return (hash_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);
 }
 
+// Dropout mask: a 32-bit counter hash ("lowbias32": two multiplies) of the
+// element index xor a per-call key, compared with p * 2^32.  A quarter of the
+// VALU cost of splitmix64 -- the GN-FiLM-dropout passes are VALU-bound on the
+// 64-bit mixer.  Forward and backward regenerate the same mask.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
+  return lowbias32((uint32_t)seed ^ lowbias32((uint32_t)(seed >> 32) + 0x9e3779b9U));
+}
+__device__ __forceinline__ uint32_t drop_threshold(float p) { return (uint32_t)((double)p * 4294967296.0); }
+__device__ __forceinline__ bool drop_elem(uint32_t key, uint64_t idx, uint32_t thr) {
+  return lowbias32((uint32_t)idx ^ key) < thr;
+}
+
 // Box-Muller normal from two counter-based uniforms.
 __device__ __forceinline__ float normal01(uint64_t seed, uint64_t idx) {
   float u1 = ((hash_u32(seed, 2 * idx) >> 8) + 1) * (1.0f / 16777217.0f);

@@ -67,9 +67,28 @@ __device__ __forceinline__ bf16* dxdst(bf16* dx, const Cat& k, long pix, int c0,
   return c0 < k.C1 ? dx + pix * k.C1 + c0 : k.dx2 + pix * (C - k.C1) + (c0 - k.C1);
 }
 
+// Channel-fixed row walk of the chunked kernels: thread t owns the 8
+// channels c0 = (t % cv) * 8 of rows t / cv, t / cv + rpi, ... (rpi = NT / cv
+// rows per pass; the NT % cv leftover threads idle), so every per-channel
+// constant (affine, group statistics) is loaded once into registers and the
+// loop carries no index division.  Rows are processed UNR at a time with all
+// loads issued first (memory-level parallelism for a bandwidth-bound pass).
+constexpr int UNR = 4;
+
+struct RowSrc {          // one thread's source row pointer / stride (virtual concat aware)
+  const bf16* p;
+  long ld;
+};
+__device__ __forceinline__ RowSrc row_src(const bf16* x, const Cat& k, int c0, int C) {
+  if (k.x2 == nullptr) return {x + c0, (long)C};
+  if (c0 < k.C1) return {x + c0, (long)k.C1};
+  return {k.x2 + (c0 - k.C1), (long)(C - k.C1)};
+}
+
 // ---------------------------------------------------------------- stats ----
 __global__ void __launch_bounds__(NT) gn_stats_partial_k(const bf16* __restrict__ x, int P, int C, int G,
                                                          int rows, int nchunks, float* __restrict__ part, Cat cat) {
+  constexpr int U = 2;      // rows in flight per thread
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][C][3]
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int tpr = C / 8, rpi = NT / tpr;
@@ -91,15 +110,23 @@ __global__ void __launch_bounds__(NT) gn_stats_partial_k(const bf16* __restrict_
       cnt = 1.f;
       r += rpi;
     }
-    for (; r < r1; r += rpi) {
-      f32x8 a = ld8(xsrc(x, cat, pix0 + r, c0, C));
+    const RowSrc src = row_src(x, cat, c0, C);
+    for (; r < r1; r += U * rpi) {
+      f32x8 a[U];                         // U rows in flight
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float d = a[j] - sh[j];
-        s[j] += d;
-        q[j] += d * d;
+      for (int u = 0; u < U; ++u)
+        if (r + u * rpi < r1) a[u] = ld8(src.p + (pix0 + r + u * rpi) * src.ld);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (r + u * rpi >= r1) break;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float d = a[u][j] - sh[j];
+          s[j] += d;
+          q[j] += d * d;
+        }
+        cnt += 1.f;
       }
-      cnt += 1.f;
     }
   }
   if (active) {
@@ -174,6 +201,7 @@ __global__ void gn_film_k(const bf16* __restrict__ x, const float* __restrict__ 
                           long PC, float p_drop, uint64_t seed, int ssld, const uint64_t* __restrict__ seed_dev) {
   if (seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;   // graph replays: per-step seed lives on the device
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const uint32_t dkey = drop_key(seed), dthr = drop_threshold(p_drop);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
     long e = i * 8;
     int c0 = (int)(e % C);
@@ -190,7 +218,7 @@ __global__ void gn_film_k(const bf16* __restrict__ x, const float* __restrict__ 
       float mean = stats[(n * G + g) * 2], rstd = stats[(n * G + g) * 2 + 1];
       float h = (a[j] - mean) * rstd * gm[j] + bt[j];
       float z = h * (1.f + sc[j]) + sf[j];
-      if (p_drop > 0.f) z = (uniform01(seed, (uint64_t)(e + j)) < p_drop) ? 0.f : z * keep_scale;
+      if (p_drop > 0.f) z = drop_elem(dkey, (uint64_t)(e + j), dthr) ? 0.f : z * keep_scale;
       o[j] = z;
     }
     st8(y + e, o);
@@ -232,40 +260,65 @@ __global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, co
                                                   bf16* __restrict__ y, int P, int C, int G, int rows, int nchunks,
                                                   float eps, float p_drop, uint64_t seed, int ssld,
                                                   const uint64_t* __restrict__ seed_dev, Cat cat) {
+  constexpr int U = MODE == 2 ? 2 : UNR;      // rows in flight per thread
   __shared__ float s_st[2 * 1024];
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int Cg = C / G;
   merge_image_stats(part, n, nchunks, G, P, rows, Cg, eps, s_st, stats_out, chunk == 0);
   if (MODE == 2 && seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-  const int r0 = chunk * rows, r1 = min(P, r0 + rows);
-  const int cv = C / 8;
-  const long nv = (long)(r1 - r0) * cv;
-  const long base = ((long)n * P + r0) * C;
-  for (long v = threadIdx.x; v < nv; v += NT) {
-    const long e = base + v * 8;
-    const int c0 = (int)(v % cv) * 8;
-    f32x8 a = ld8(xsrc(x, cat, (long)n * P + r0 + v / cv, c0, C));
-    f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
-    f32x8 sc = {}, sf = {};
-    if (MODE == 2) {
-      const long pix = e / C;
-      sc = ld8(ss + pix * ssld + c0);
-      sf = ld8(ss + pix * ssld + C + c0);
-    }
-    f32x8 o;
+  const uint32_t dkey = drop_key(seed), dthr = drop_threshold(p_drop);
+  const int cv = C / 8, rpi = NT / cv;
+  const int tid = threadIdx.x, roff = tid / cv;
+  if (roff >= rpi) return;
+  const int c0 = (tid % cv) * 8;
+  // y = x * A + B with A = rstd * gamma, B = beta - mean * rstd * gamma
+  float A[8], Bc[8];
+  {
+    const f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int g = (c0 + j) / Cg;
-      float h = (a[j] - s_st[g * 2]) * s_st[g * 2 + 1] * gm[j] + bt[j];
-      if (MODE == 1) h = siluf_(h);
-      if (MODE == 2) {
-        h = h * (1.f + sc[j]) + sf[j];
-        if (p_drop > 0.f) h = (uniform01(seed, (uint64_t)(e + j)) < p_drop) ? 0.f : h * keep_scale;
-      }
-      o[j] = h;
+      A[j] = s_st[g * 2 + 1] * gm[j];
+      Bc[j] = bt[j] - s_st[g * 2] * A[j];
     }
-    st8(y + e, o);
+  }
+  const RowSrc src = row_src(x, cat, c0, C);
+  const long pix0 = (long)n * P;
+  const int r1 = min(P, chunk * rows + rows);
+  for (int r = chunk * rows + roff; r < r1; r += U * rpi) {
+    f32x8 a[U], sc[U], sf[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rr = r + u * rpi;
+      if (rr < r1) {
+        const long pix = pix0 + rr;
+        a[u] = ld8(src.p + pix * src.ld);
+        if (MODE == 2) {
+          sc[u] = ld8(ss + pix * ssld + c0);
+          sf[u] = ld8(ss + pix * ssld + C + c0);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rr = r + u * rpi;
+      if (rr >= r1) break;
+      const long pix = pix0 + rr;
+      const uint64_t e = (uint64_t)pix * C + c0;
+      f32x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float h = a[u][j] * A[j] + Bc[j];
+        if (MODE == 1) h = siluf_(h);
+        if (MODE == 2) {
+          h = h * (1.f + sc[u][j]) + sf[u][j];
+          if (p_drop > 0.f) h = drop_elem(dkey, e + j, dthr) ? 0.f : h * keep_scale;
+        }
+        o[j] = h;
+      }
+      st8(y + pix * C + c0, o);
+    }
   }
 }
 
@@ -296,6 +349,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
                                                       uint64_t seed, bf16* __restrict__ dss,
                                                       float* __restrict__ chan_part, float* __restrict__ grp_part,
                                                       int ssld, const uint64_t* __restrict__ seed_dev, Cat cat) {
+  constexpr int U = 1;      // rows in flight per thread (more: VGPR-bound occupancy, measured slower)
   if (seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][C][4]
   const int chunk = blockIdx.x, n = blockIdx.y;
@@ -306,6 +360,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
   const int r0 = chunk * rows, r1 = min(P, r0 + rows);
   const int Cg = C / G;
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const uint32_t dkey = drop_key(seed), dthr = drop_threshold(p_drop);
   float dg[8], db[8], gs[8], gs2[8], mean[8], rstd[8];
   f32x8 gm = {}, bt = {};
 #pragma unroll
@@ -319,29 +374,45 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
       mean[j] = stats[(n * G + g) * 2];
       rstd[j] = stats[(n * G + g) * 2 + 1];
     }
-    for (int r = r0 + roff; r < r1; r += rpi) {
-      long pix = (long)n * P + r;
-      long e = pix * C + c0;
-      f32x8 xv = ld8(xsrc(x, cat, pix, c0, C)), dv = ld8(dy + e);
-      f32x8 sc = {}, o_s, o_t;
-      if (MODE == 2) sc = ld8(ss + pix * ssld + c0);
+    const RowSrc src = row_src(x, cat, c0, C);
+    for (int r = r0 + roff; r < r1; r += U * rpi) {
+      f32x8 xv[U], dv[U], sc[U];     // loads of U rows first (memory-level parallelism)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float keepmul = 1.f;
-        if (MODE == 2 && p_drop > 0.f) keepmul = (uniform01(seed, (uint64_t)(e + j)) < p_drop) ? 0.f : keep_scale;
-        float xhat, dA, dsc = 0.f, dsh = 0.f;
-        bwd_elem<MODE>(xv[j], dv[j], mean[j], rstd[j], gm[j], bt[j], sc[j], xhat, dA, dsc, dsh, keepmul);
-        o_s[j] = dsc;
-        o_t[j] = dsh;
-        dg[j] += dA * xhat;
-        db[j] += dA;
-        float dxh = dA * gm[j];
-        gs[j] += dxh;
-        gs2[j] += dxh * xhat;
+      for (int u = 0; u < U; ++u) {
+        const int rr = r + u * rpi;
+        if (rr < r1) {
+          const long pix = (long)n * P + rr;
+          xv[u] = ld8(src.p + pix * src.ld);
+          dv[u] = ld8(dy + pix * C + c0);
+          if (MODE == 2) sc[u] = ld8(ss + pix * ssld + c0);
+        }
       }
-      if (MODE == 2) {
-        st8(dss + pix * ssld + c0, o_s);
-        st8(dss + pix * ssld + C + c0, o_t);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rr = r + u * rpi;
+        if (rr >= r1) break;
+        const long pix = (long)n * P + rr;
+        const uint64_t e = (uint64_t)pix * C + c0;
+        f32x8 o_s, o_t;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float keepmul = 1.f;
+          if (MODE == 2 && p_drop > 0.f) keepmul = drop_elem(dkey, e + j, dthr) ? 0.f : keep_scale;
+          float xhat, dA, dsc = 0.f, dsh = 0.f;
+          bwd_elem<MODE>(xv[u][j], dv[u][j], mean[j], rstd[j], gm[j], bt[j], MODE == 2 ? sc[u][j] : 0.f, xhat, dA,
+                         dsc, dsh, keepmul);
+          o_s[j] = dsc;
+          o_t[j] = dsh;
+          dg[j] += dA * xhat;
+          db[j] += dA;
+          const float dxh = dA * gm[j];
+          gs[j] += dxh;
+          gs2[j] += dxh * xhat;
+        }
+        if (MODE == 2) {
+          st8(dss + pix * ssld + c0, o_s);
+          st8(dss + pix * ssld + C + c0, o_t);
+        }
       }
     }
 #pragma unroll
@@ -402,6 +473,7 @@ __global__ void gn_bwd_apply_k(const bf16* __restrict__ x, const bf16* __restric
                                uint64_t seed, int ssld, const uint64_t* __restrict__ seed_dev) {
   if (seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const uint32_t dkey = drop_key(seed), dthr = drop_threshold(p_drop);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
     long e = i * 8;
     int c0 = (int)(e % C);
@@ -418,7 +490,7 @@ __global__ void gn_bwd_apply_k(const bf16* __restrict__ x, const bf16* __restric
       float mean = stats[(n * G + g) * 2], rstd = stats[(n * G + g) * 2 + 1];
       float c1 = coef[(n * G + g) * 2], c2 = coef[(n * G + g) * 2 + 1];
       float keepmul = 1.f;
-      if (MODE == 2 && p_drop > 0.f) keepmul = (uniform01(seed, (uint64_t)(e + j)) < p_drop) ? 0.f : keep_scale;
+      if (MODE == 2 && p_drop > 0.f) keepmul = drop_elem(dkey, (uint64_t)(e + j), dthr) ? 0.f : keep_scale;
       float xhat, dA, dsc, dsh;
       bwd_elem<MODE>(xv[j], dv[j], mean, rstd, gm[j], bt[j], sc[j], xhat, dA, dsc, dsh, keepmul);
       float dxh = dA * gm[j];
@@ -438,6 +510,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
                                                       bf16* __restrict__ dx, int P, int C, int G, int rows,
                                                       int nchunks, float p_drop, uint64_t seed, int ssld,
                                                       const uint64_t* __restrict__ seed_dev, Cat cat) {
+  constexpr int U = 2;      // rows in flight per thread
   __shared__ float s_c[4 * 1024];      // per group: mean, rstd, c1, c2
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int Cg = C / G;
@@ -457,31 +530,64 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
   __syncthreads();
   if (MODE == 2 && seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-  const int r0 = chunk * rows, r1 = min(P, r0 + rows);
-  const int cv = C / 8;
-  const long nv = (long)(r1 - r0) * cv;
-  const long base = ((long)n * P + r0) * C;
-  for (long v = threadIdx.x; v < nv; v += NT) {
-    const long e = base + v * 8;
-    const int c0 = (int)(v % cv) * 8;
-    const long pixv = (long)n * P + r0 + v / cv;
-    f32x8 xv = ld8(xsrc(x, cat, pixv, c0, C)), dv = ld8(dy + e);
-    f32x8 sc = {};
-    if (MODE == 2) sc = ld8(ss + (e / C) * ssld + c0);
-    f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
-    f32x8 o;
+  const uint32_t dkey = drop_key(seed), dthr = drop_threshold(p_drop);
+  const int cv = C / 8, rpi = NT / cv;
+  const int tid = threadIdx.x, roff = tid / cv;
+  if (roff >= rpi) return;
+  const int c0 = (tid % cv) * 8;
+  float mean[8], rstd[8], c1[8], c2[8], gm[8], bt[8];
+  {
+    const f32x8 g8 = ld8f(gamma + c0), b8 = ld8f(beta + c0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int g = (c0 + j) / Cg;
-      const float mean = s_c[g * 4], rstd = s_c[g * 4 + 1], c1 = s_c[g * 4 + 2], c2 = s_c[g * 4 + 3];
-      float keepmul = 1.f;
-      if (MODE == 2 && p_drop > 0.f) keepmul = (uniform01(seed, (uint64_t)(e + j)) < p_drop) ? 0.f : keep_scale;
-      float xhat, dA, dsc, dsh;
-      bwd_elem<MODE>(xv[j], dv[j], mean, rstd, gm[j], bt[j], sc[j], xhat, dA, dsc, dsh, keepmul);
-      const float dxh = dA * gm[j];
-      o[j] = rstd * (dxh - c1 - xhat * c2);
+      mean[j] = s_c[g * 4];
+      rstd[j] = s_c[g * 4 + 1];
+      c1[j] = s_c[g * 4 + 2];
+      c2[j] = s_c[g * 4 + 3];
+      gm[j] = g8[j];
+      bt[j] = b8[j];
     }
-    st8(dxdst(dx, cat, pixv, c0, C), o);
+  }
+  const RowSrc src = row_src(x, cat, c0, C);
+  bf16* dst;
+  long dld;
+  if (cat.x2 == nullptr) { dst = dx + c0; dld = C; }
+  else if (c0 < cat.C1) { dst = dx + c0; dld = cat.C1; }
+  else { dst = cat.dx2 + (c0 - cat.C1); dld = C - cat.C1; }
+  const long pix0 = (long)n * P;
+  const int r1 = min(P, chunk * rows + rows);
+  for (int r = chunk * rows + roff; r < r1; r += U * rpi) {
+    f32x8 xv[U], dv[U], sc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rr = r + u * rpi;
+      if (rr < r1) {
+        const long pix = pix0 + rr;
+        xv[u] = ld8(src.p + pix * src.ld);
+        dv[u] = ld8(dy + pix * C + c0);
+        if (MODE == 2) sc[u] = ld8(ss + pix * ssld + c0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rr = r + u * rpi;
+      if (rr >= r1) break;
+      const long pix = pix0 + rr;
+      const uint64_t e = (uint64_t)pix * C + c0;
+      f32x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float keepmul = 1.f;
+        if (MODE == 2 && p_drop > 0.f) keepmul = drop_elem(dkey, e + j, dthr) ? 0.f : keep_scale;
+        float xhat, dA, dsc, dsh;
+        bwd_elem<MODE>(xv[u][j], dv[u][j], mean[j], rstd[j], gm[j], bt[j], MODE == 2 ? sc[u][j] : 0.f, xhat, dA,
+                       dsc, dsh, keepmul);
+        const float dxh = dA * gm[j];
+        o[j] = rstd[j] * (dxh - c1[j] - xhat * c2[j]);
+      }
+      st8(dst + pix * dld, o);
+    }
   }
 }
 
