@@ -46,6 +46,7 @@ def main() -> None:
     ap.add_argument("--grad_dtype", default="fp32")
     ap.add_argument("--graph", type=int, default=0, help="1: replay the step from captured HIP graphs")
     ap.add_argument("--profile", default="", help="write a torch.profiler kernel table (text) here")
+    ap.add_argument("--profile_stack", type=int, default=0, help="with --profile: also group by N stack frames")
     ap.add_argument("--mode", default="train", choices=["train", "sample"],
                     help="sample: 256-step stochastic-conditioning CFG sampling wall-clock (BASELINE config 5)")
     ap.add_argument("--sample_batch", type=int, default=64)
@@ -94,7 +95,8 @@ def main() -> None:
     prof = None
     if args.profile:
         prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
-                                                  torch.profiler.ProfilerActivity.CUDA])
+                                                  torch.profiler.ProfilerActivity.CUDA],
+                                      with_stack=bool(args.profile_stack))
         prof.__enter__()
     t0 = time.perf_counter()
     loss = None
@@ -109,6 +111,9 @@ def main() -> None:
         if ctx.rank == 0:
             with open(args.profile, "w") as f:
                 f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+                if args.profile_stack:     # which Python lines issue the glue ops
+                    f.write("\n\n" + prof.key_averages(group_by_stack_n=args.profile_stack).table(
+                        sort_by="self_cuda_time_total", row_limit=80))
     from distributed_3d_diffusion_pytorch_amd.parallel import all_reduce_max
     dt = all_reduce_max(dt, ctx.device)
     lv = float(loss) if loss is not None else float("nan")

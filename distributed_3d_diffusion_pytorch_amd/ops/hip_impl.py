@@ -120,6 +120,17 @@ def _cached(p: torch.Tensor, kind: str, build, desc=None):
     return v
 
 
+def _pack_blocks(OC: int, OCp: int, ICp: int, mode: int) -> int:
+    """Blocks of pack_all_k for one operand (must match its tiling): fwd pack
+    = one output row x 256 input channels, transposed pack = 32 x 16 channel
+    tiles, plain cast = 2048 elements."""
+    if mode == 0:
+        return OCp * ((ICp + 255) // 256)
+    if mode == 1:
+        return ((OCp + 31) // 32) * ((ICp + 15) // 16)
+    return (OC + 2047) // 2048
+
+
 def refresh_weights() -> None:
     """After an optimizer update of the master weights: one launch repacks
     every cached operand; cache tokens advance to the new epoch."""
@@ -136,9 +147,8 @@ def refresh_weights() -> None:
             OC, IC, OCp, ICp, taps, mode = desc[:6]
             src_off = desc[6] if len(desc) > 6 else 0        # byte offset (channel slice)
             ics = desc[7] if len(desc) > 7 else 0            # source IC stride
-            total = OC if mode == 2 else OCp * taps * ICp
             rows.append((p.data_ptr() + src_off, t.data_ptr(), OC, IC, OCp, ICp, taps, mode, blk, ics))
-            blk += (total + 2047) // 2048
+            blk += _pack_blocks(OC, OCp, ICp, mode)
         dt = np.dtype([("src", np.uint64), ("dst", np.uint64), ("OC", np.int32), ("IC", np.int32),
                        ("OCp", np.int32), ("ICp", np.int32), ("taps", np.int32), ("mode", np.int32),
                        ("blk0", np.int32), ("ICs", np.int32)])

@@ -460,3 +460,26 @@ def test_cat_gn_silu_dense(H, C1, C2, OC):
     names = ["y", "skip", "da", "db", "dgw", "dgb", "ddw", "ddb"]
     for n, x, r in zip(names, hr, rr):
         assert rel(x, r) < 3e-2, (n, rel(x, r))
+
+
+@pytest.mark.parametrize("OC,IC,taps", [(128, 128, 9), (256, 384, 9), (1024, 144, 9), (3, 128, 9),
+                                        (2048, 1024, 1), (768, 256, 1), (128, 3, 9)])
+def test_batched_weight_refresh_matches_pack(H, OC, IC, taps):
+    """pack_all_k (one launch re-derives every cached operand after the
+    optimizer step) == the per-weight pack kernel, for forward and transposed
+    packs and the plain bf16 cast."""
+    torch.manual_seed(11)
+    shape = (OC, IC, 3, 3) if taps == 9 else (OC, IC)
+    w = torch.nn.Parameter(torch.randn(*shape, device=DEV))
+    fwd = H.packed_weight(w, False, taps)
+    trn = H.packed_weight(w, True, taps)
+    cast = H.bf16_weight(w) if taps == 1 else None
+    with torch.no_grad():
+        w.mul_(-0.5).add_(0.25)           # an "optimizer step" on the fp32 master
+    H.refresh_weights()
+    ref_f = H.packed_weight(torch.nn.Parameter(w.detach().clone()), False, taps)
+    ref_t = H.packed_weight(torch.nn.Parameter(w.detach().clone()), True, taps)
+    assert torch.equal(fwd, ref_f)
+    assert torch.equal(trn, ref_t)
+    if cast is not None:
+        assert torch.equal(cast.reshape(-1), w.detach().to(BF).reshape(-1))
