@@ -47,6 +47,7 @@ SIGNATURES = {
     "d3d_set_conv_korder": [I],
     "d3d_set_wgrad_impl": [I],
     "d3d_conv_wgrad_plan2": [I, I, I, I, I, I, IP, IP],
+    "d3d_conv_wgrad_plan3": [I, I, I, I, I, I, I, I, I, IP, IP],
     "d3d_conv_wgrad": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "d3d_pack_weight": [P, P, I, I, I, I, I, I, P],
     "d3d_set_conv_impl": [I, P],

@@ -1413,6 +1413,252 @@ conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I0, floa
   }
 }
 
+// ------------------------------------------------ 8-wave weight gradient --
+// conv_wgrad_bufl_k at one 512-thread block per CU with a BM (output
+// channels) x BN (input channels of one tap) tile and 64-pixel stages.  The
+// 128x128 / 32-pixel kernel measured 52-59 % of wave cycles parked on
+// vmcnt / barrier (profiles/pmc_wgrad): a stage is only 16 MFMA per wave, far
+// shorter than an LDS-DMA round trip.  Here a stage is 64 (BM=256: 128x64
+// wave tiles) or 32 MFMA per wave at 2 waves per SIMD, so one stage in flight
+// behind the barrier covers the landing latency.  FAST addressing only
+// (stride 1, power-of-two H = W, same in/out size): the input rows of a tap
+// are the output rows shifted by a wave-uniform pixel offset.
+//
+// LDS image per stage: [64 pixels][BM] dY and [64 pixels][BN] input, rows of
+// W bf16 (W = BM or BN, 256 or 128).  16-B chunk c of row r lives at
+// physical chunk (c & ~15) | ((c & 15) ^ 2 * (r & 7)): the 128-wide kernel's
+// conflict-free swizzle applied inside each 256-B half of a row (banks repeat
+// every 256 B).  The swizzle is in the per-lane DMA source address.
+template <int W>
+__device__ __forceinline__ int w8w_phys(int c, int r) { return (c & ~15) | ((c & 15) ^ (2 * (r & 7))); }
+
+template <int BM, int BN>
+__device__ __forceinline__ void wgrad_w8_issue(bf16* sA, bf16* sB, const bf16* __restrict__ dY,
+                                               const bf16* __restrict__ I, long in_elems, long p0, long p_end,
+                                               int OC, int IC, int IH, int OH, int OW, int kh, int kw, int dpix,
+                                               int lw, int wave, const int* arow, const unsigned* aoff,
+                                               const int* brow, const unsigned* boff) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  constexpr int PK = 64;
+  constexpr int APW = PK * BM * 2 / 1024 / 8, BPW = PK * BN * 2 / 1024 / 8;   // 1-KiB pieces per wave
+  const __amdgpu_buffer_rsrc_t rA = uniform_rsrc(dY + p0 * OC, (p_end - p0) * OC * 2);
+#pragma unroll
+  for (int i = 0; i < APW; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sA + (wave * APW + i) * 512), 16, aoff[i], 0, 0, 0);
+  const long pb = p0 + dpix;
+  const __amdgpu_buffer_rsrc_t rB = uniform_rsrc(I + pb * IC, (in_elems - pb * IC) * 2);
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) {
+    const int pp = (int)p0 + brow[i];
+    unsigned bad = 0u;                               // tap padding: at most two wave-uniform tests
+    if (kw != 1) {
+      const int ow = pp & (OW - 1);
+      bad |= (unsigned)(kw == 0 ? ow == 0 : ow == OW - 1);
+    }
+    if (kh != 1) {
+      const int oh = (pp >> lw) & (OH - 1);
+      bad |= (unsigned)(kh == 0 ? oh == 0 : oh == OH - 1);
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * BPW + i) * 512), 16,
+                                             boff[i] | (bad << 31), 0, 0, 0);
+  }
+}
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(512, 1)
+conv_wgrad_w8_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __restrict__ ws, long in_pix,
+                int Nimg, int IH, int IW, int IC, int OH, int OW, int OC, int pix_per_split, int ncb,
+                float* __restrict__ bws, int lw, int lh) {
+  constexpr int PK = 64, NS = 2;
+  constexpr int WM = BM / 2, WN = BN / 4, TM = WM / 16, TN = WN / 16;
+  constexpr int STAGE = PK * (BM + BN);
+  constexpr int APW = PK * BM * 2 / 1024 / 8, BPW = PK * BN * 2 / 1024 / 8;
+  constexpr int ARP = 1024 / (BM * 2), BRP = 1024 / (BN * 2);          // rows per 1-KiB piece
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int bx, by, bz;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const long T = (long)gx * gy * gridDim.z;
+    const long L = blockIdx.x + (long)gx * (blockIdx.y + (long)gy * blockIdx.z);
+    const long q = T / 8, r = T % 8, xcd = L % 8;
+    const long R = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    bx = (int)(R % gx);
+    by = (int)((R / gx) % gy);
+    bz = (int)(R / ((long)gx * gy));
+  }
+  const int tap = bx / ncb;
+  const int ci0 = (bx % ncb) * BN;
+  const int m0 = by * BM;
+  const int split = bz;
+  const int kh = tap / 3, kw = tap % 3;
+  const long P = (long)Nimg * OH * OW;
+  const long p_begin = (long)split * pix_per_split;
+  const long p_end = p_begin + pix_per_split < P ? p_begin + pix_per_split : P;
+  const int dpix = (kh - 1) * IW + (kw - 1);
+  const long in_elems = in_pix * IC;
+
+  // DMA lane mapping: lane L -> row L / (W/8) of its piece, physical chunk
+  // L % (W/8), logical chunk w8w_phys(physical, row) (the XOR is an involution)
+  int arow[APW], brow[BPW];
+  unsigned aoff[APW], boff[BPW];
+#pragma unroll
+  for (int i = 0; i < APW; ++i) {
+    arow[i] = (wave * APW + i) * ARP + lane / (BM / 8);
+    const int lc = w8w_phys<BM>(lane % (BM / 8), arow[i]);
+    const int co = m0 + lc * 8;
+    aoff[i] = co < OC ? (unsigned)((arow[i] * OC + co) * 2) : 0x80000000u;
+  }
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) {
+    brow[i] = (wave * BPW + i) * BRP + lane / (BN / 8);
+    const int lc = w8w_phys<BN>(lane % (BN / 8), brow[i]);
+    const int ci = ci0 + lc * 8;
+    boff[i] = ci < IC ? (unsigned)((brow[i] * IC + ci) * 2) : 0x80000000u;
+  }
+  // transpose-read lane offsets (elements) for rows 4g+q (+16, +32, +48)
+  const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
+  const int rr = 4 * g + q;
+  int la[TM], lb[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) la[i] = rr * BM + (w8w_phys<BM>((wm * WM + i * 16) / 8 + (pc >> 1), rr) << 3) + (pc & 1) * 4;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) lb[j] = rr * BN + (w8w_phys<BN>((wn * WN + j * 16) / 8 + (pc >> 1), rr) << 3) + (pc & 1) * 4;
+
+  auto issue = [&](long p0, int stage) {
+    bf16* sA = smem + stage * STAGE;
+    wgrad_w8_issue<BM, BN>(sA, sA + PK * BM, dY, I, in_elems, p0, p_end, OC, IC, IH, OH, OW, kh, kw, dpix, lw, wave,
+                           arow, aoff, brow, boff);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const long nsteps = (p_end - p_begin + PK - 1) / PK;
+  // fused bias: the first (tap, ci) column block of every split sums its dY
+  // tile; thread -> column tid % BM, half (tid / BM) & 1 of the stage's rows
+  const bool do_bias = bws != nullptr && bx == 0 && tid < 2 * BM;
+  float bacc = 0.f;
+  const int bcol = tid % BM, bhalf = (tid / BM) & 1;
+  auto compute = [&](const bf16* a) {
+    const bf16* b = a + PK * BM;
+    if (do_bias) {
+#pragma unroll 8
+      for (int r = 0; r < PK / 2; ++r) {
+        const int row = bhalf * (PK / 2) + r;
+        bacc += (float)a[row * BM + (w8w_phys<BM>(bcol >> 3, row) << 3) + (bcol & 7)];
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < PK / 32; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        s16x4 lo = ds_tr(b + lb[j] + kk * 32 * BN);
+        s16x4 hi = ds_tr(b + lb[j] + kk * 32 * BN + 16 * BN);
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        s16x4 lo = ds_tr(a + la[i] + kk * 32 * BM);
+        s16x4 hi = ds_tr(a + la[i] + kk * 32 * BM + 16 * BM);
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  // one barrier per stage: wait for this stage's DMA, barrier (landed
+  // everywhere AND every wave done reading the other buffer), issue the next
+  // stage into it, compute at raised MFMA priority
+  if (nsteps > 0) issue(p_begin, 0);
+  for (long s = 0; s < nsteps; ++s) {
+    const int st = (int)(s & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nsteps) issue(p_begin + (s + 1) * PK, st ^ 1);
+    __builtin_amdgcn_s_setprio(1);
+    compute(smem + st * STAGE);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (do_bias && m0 + bcol < OC) bws[((long)split * 2 + bhalf) * OC + m0 + bcol] = bacc;
+  const int fr = lane & 15, fq = lane >> 4;
+  const long KW = 9L * IC;
+  float* slab = ws + (long)split * OC * KW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int ci = ci0 + wn * WN + j * 16 + fr;
+    if (ci >= IC) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < OC) slab[(long)(co + e) * KW + tap * IC + ci] = acc[i][j][e];
+    }
+  }
+}
+
+// 3x3 split-K reduce with the [co][tap][ci] -> OIHW ([co][ci][tap])
+// transposition staged in LDS: a block owns (co, 64 input channels), reads
+// the 9 tap rows of every split coalesced (64 consecutive ci each) and writes
+// (or accumulates into) 576 CONTIGUOUS floats of dW.  The element-wise
+// reduce wrote OIHW 36 B apart (one read-modify-write per 4-B element): ~86
+// us for a 2-split 512x512 weight, now bandwidth-bound.  Blocks past
+// nblk_w sum the bias partials (brows rows) into db.
+__global__ void __launch_bounds__(256) wgrad_reduce9_k(const float* __restrict__ ws, int OC, int IC, int splits,
+                                                       int accumulate, const float* __restrict__ bws, int brows,
+                                                       float* __restrict__ dW, float* __restrict__ db, int nblk_w) {
+  __shared__ float tile[64 * 9];
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= nblk_w) {
+    const int c = ((int)blockIdx.x - nblk_w) * 256 + tid;
+    if (c < OC && db) {
+      float s = 0.f;
+      for (int k = 0; k < brows; ++k) s += bws[(long)k * OC + c];
+      db[c] = accumulate ? db[c] + s : s;
+    }
+    return;
+  }
+  const int ncg = (IC + 63) / 64;
+  const int co = blockIdx.x / ncg, ci0 = (blockIdx.x % ncg) * 64;
+  const int nci = min(64, IC - ci0);
+  const long total = (long)OC * 9 * IC;
+  const long rowbase = (long)co * 9 * IC;
+  for (int k = tid; k < 9 * 64; k += 256) {
+    const int tap = k >> 6, ci = k & 63;
+    float sum = 0.f;
+    if (ci < nci) {
+      const float* src = ws + rowbase + (long)tap * IC + ci0 + ci;
+      int s = 0;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      for (; s + 4 <= splits; s += 4) {           // independent loads in flight
+        a0 += src[(long)s * total];
+        a1 += src[(long)(s + 1) * total];
+        a2 += src[(long)(s + 2) * total];
+        a3 += src[(long)(s + 3) * total];
+      }
+      for (; s < splits; ++s) a0 += src[(long)s * total];
+      sum = (a0 + a1) + (a2 + a3);
+    }
+    tile[ci * 9 + tap] = sum;
+  }
+  __syncthreads();
+  float* dst = dW + ((long)co * IC + ci0) * 9;
+  for (int m = tid; m < nci * 9; m += 256) dst[m] = accumulate ? dst[m] + tile[m] : tile[m];
+}
+
 // sum the split slabs and write dW in OIHW fp32 layout (optionally accumulate)
 __global__ void wgrad_reduce_k(const float* __restrict__ ws, float* __restrict__ dW, int OC, int IC, int splits,
                                int accumulate, int taps, const float* __restrict__ bws, float* __restrict__ db,
@@ -1748,7 +1994,7 @@ D3D_API int d3d_conv_plan(int N, int OH, int OW, int OC, int ICp, int taps) {
   long blocks = ((Mpix + BN - 1) / BN) * ((OC + BM - 1) / BM);
   int nk = taps * ICp / 64;
   if (blocks >= 384 || (OC & 3) || g_conv_impl < 1) return 1;
-  long want = (512 + blocks - 1) / blocks;
+  long want = 512 / blocks;         // rounded down: no nearly empty extra round of blocks
   long maxs = nk / 6;
   if (want > maxs) want = maxs;
   if (want > 16) want = 16;
@@ -1869,6 +2115,13 @@ D3D_API int d3d_conv3x3(const void* I, const void* Wp, const float* bias, const 
 // (<= 16); bias rows (brows = 2 * splits) use the same lanes
 static void launch_reduce2(const float* ws, int OC, int IC, int taps, int splits, int accumulate, const float* bws,
                            int brows, float* dW, float* db, WSegs sg, bool want_bias, hipStream_t st) {
+  if (taps == 9 && sg.n == 0) {
+    const int nblk_w = OC * ((IC + 63) / 64);
+    const int nblk_b = want_bias ? (OC + 255) / 256 : 0;
+    hipLaunchKernelGGL(wgrad_reduce9_k, dim3(nblk_w + nblk_b), dim3(256), 0, st, ws, OC, IC, splits, accumulate, bws,
+                       brows, dW, db, nblk_w);
+    return;
+  }
   int SL = 1;
   while (SL < splits && SL < 16) SL <<= 1;
   const long total = (long)OC * IC * taps;
@@ -1943,13 +2196,51 @@ D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps
   long P = (long)N * OH * OW;
   int tiles = taps * ((IC + BN - 1) / BN) * ((OC + BM - 1) / BM);
   // ~2 blocks per CU (the kernel's occupancy) and >= 1024 pixels per split:
-  // every extra split costs a full fp32 OCxK slab of write + reduce traffic
-  long want = (512 + tiles - 1) / tiles;
+  // every extra split costs a full fp32 OCxK slab of write + reduce traffic.
+  // Rounded DOWN: 513 blocks (9 tiles x 57 splits) ran a whole extra round
+  // for one block
+  long want = 512 / tiles;
   long maxs = (P + 255) / 256;       // small reductions (8x8 level at small batch): fill the chip first
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
   long pps = (P + want - 1) / want;
   pps = (pps + 63) / 64 * 64;           // multiple of both kernels' pixel step
+  *pix_per_split = (int)pps;
+  *splits = (int)((P + pps - 1) / pps);
+  return 0;
+}
+
+// conv_wgrad_w8_k takes a 3x3 stride-1 same-size power-of-two shape when
+// at least one of its channel counts fills a 256-wide tile side (the 128x128
+// level-0 convs stay on the 4-wave kernel); impl 6 enables it.
+static bool wgrad_w8_ok(int taps, int IH, int IW, int OH, int OW, int IC, int OC, int stride, long in_elems, int* bm,
+                        int* bn) {
+  auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
+  if (g_wgrad_impl != 6 || taps != 9 || stride != 1 || IH != OH || IW != OW || !pow2(OH) || !pow2(OW) ||
+      IC % 128 || OC % 8 || in_elems * 2 >= (1L << 30))
+    return false;
+  *bm = OC >= 256 ? 256 : 128;
+  *bn = IC >= 256 ? 256 : 128;
+  return *bm == 256 || *bn == 256;
+}
+
+// Split plan that knows the input geometry (and therefore which kernel runs):
+// the 8-wave kernel wants ~one block per CU (256), the 4-wave one ~two.
+D3D_API int d3d_conv_wgrad_plan3(int N, int IH, int IW, int OH, int OW, int OC, int IC, int taps, int stride,
+                                 int* splits, int* pix_per_split) {
+  int bm, bn;
+  if (!wgrad_w8_ok(taps, IH, IW, OH, OW, IC, OC, stride, (long)N * IH * IW * IC, &bm, &bn))
+    return d3d_conv_wgrad_plan2(N, OH, OW, OC, IC, taps, splits, pix_per_split);
+  const long P = (long)N * OH * OW;
+  const int tiles = 9 * ((IC + bn - 1) / bn) * ((OC + bm - 1) / bm);
+  // at one block per CU a grid just past 256 blocks runs a second, nearly
+  // empty round: round the split count DOWN to fit one wave of blocks
+  long want = 256 / tiles;
+  long maxs = (P + 1023) / 1024;        // >= 16 stages of 64 pixels per split
+  if (want > maxs) want = maxs;
+  if (want < 1) want = 1;
+  long pps = (P + want - 1) / want;
+  pps = (pps + 63) / 64 * 64;
   *pix_per_split = (int)pps;
   *splits = (int)((P + pps - 1) / pps);
   return 0;
@@ -1969,14 +2260,27 @@ D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW,
                             int IC, int OH, int OW, int OC, int stride, int splits, int pix_per_split, int accumulate,
                             int taps, hipStream_t st) {
   constexpr int BM = 128, BN = 128;
-  int ncb = (IC + BN - 1) / BN;
-  dim3 grid(taps * ncb, (OC + BM - 1) / BM, splits);
   long total = (long)OC * IC * taps;
   float* bws = db ? ws + (long)splits * total : nullptr;
   auto lg2 = [](int v) { int l = 0; while ((1 << l) < v) ++l; return (1 << l) == v ? l : -1; };
   int lw = lg2(OW), lh = lg2(OH);
   if (lw < 0 || lh < 0) lw = lh = -1;
-  launch_wgrad(dY, I, ws, N, IH, IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh, taps, grid, st);
+  int bm, bn;
+  if (wgrad_w8_ok(taps, IH, IW, OH, OW, IC, OC, stride, (long)N * IH * IW * IC, &bm, &bn)) {
+    const int ncb = (IC + bn - 1) / bn;
+    dim3 g8(9 * ncb, (OC + bm - 1) / bm, splits);
+#define WW(BMv, BNv)                                                                                             \
+  hipLaunchKernelGGL((conv_wgrad_w8_k<BMv, BNv>), g8, dim3(512), 0, st, (const bf16*)dY, (const bf16*)I, ws,       \
+                     (long)N * IH * IW, N, IH, IW, IC, OH, OW, OC, pix_per_split, ncb, bws, lw, lh)
+    if (bm == 256 && bn == 256) WW(256, 256);
+    else if (bm == 256) WW(256, 128);
+    else WW(128, 256);
+#undef WW
+  } else {
+    int ncb = (IC + BN - 1) / BN;
+    dim3 grid(taps * ncb, (OC + BM - 1) / BM, splits);
+    launch_wgrad(dY, I, ws, N, IH, IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh, taps, grid, st);
+  }
   {
     WSegs none{};
     launch_reduce2(ws, OC, IC, taps, splits, accumulate, bws, splits * (256 / BM), dW, db, none, db != nullptr, st);

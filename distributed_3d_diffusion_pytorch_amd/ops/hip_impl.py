@@ -45,7 +45,8 @@ def set_conv_korder(korder: int) -> None:
     _chk(_lib.d3d_set_conv_korder(int(korder)), "set_conv_korder")
 
 
-_WGRAD_IMPLS = {"reg": 0, "glds": 1, "glds64x2": 1, "glds32x2": 2, "glds32x3": 3, "glds64x3": 4, "bufl": 5}
+_WGRAD_IMPLS = {"reg": 0, "glds": 1, "glds64x2": 1, "glds32x2": 2, "glds32x3": 3, "glds64x3": 4, "bufl": 5,
+                "w8": 6}
 
 
 def set_wgrad_impl(impl: str) -> None:
@@ -61,7 +62,7 @@ def _ensure_impl():
     if not _IMPL_SET[0]:
         import os
         set_conv_impl(os.environ.get("D3D_CONV_IMPL", "w8w"))
-        set_wgrad_impl(os.environ.get("D3D_WGRAD_IMPL", "bufl"))
+        set_wgrad_impl(os.environ.get("D3D_WGRAD_IMPL", "w8"))
         _IMPL_SET[0] = True
 
 
@@ -469,7 +470,7 @@ def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9, want_bias=False, dW=No
     given dW/db (accumulating when asked) or into fresh fp32 tensors."""
     _ensure_impl()
     s, pps = ctypes.c_int(), ctypes.c_int()
-    _lib.d3d_conv_wgrad_plan2(N, OH, OW, OC, IC, taps, ctypes.byref(s), ctypes.byref(pps))
+    _lib.d3d_conv_wgrad_plan3(N, H, W, OH, OW, OC, IC, taps, stride, ctypes.byref(s), ctypes.byref(pps))
     extra = 2 * s.value * OC if (want_bias or db is not None) else 0
     ws = torch.empty(s.value * OC * taps * IC + extra, dtype=F32, device=x.device)
     if dW is None:

@@ -165,6 +165,24 @@ def test_conv3x3_w8(H, impl, N, Hh, W, Ci, Co, s, res, rb, scale):
         H.set_conv_impl(os.environ.get("D3D_CONV_IMPL", "w8w"))
 
 
+WGRAD_W8_SHAPES = [
+    # 3x3 stride-1 weight gradients on the 8-wave kernel (impl "w8")
+    (8, 32, 32, 256, 256, 1, False, False, 1.0),                  # 256 x 256 tiles
+    (3, 16, 16, 128, 256, 1, True, False, 1.0),                   # 256 x 128, partial last split
+    (4, 16, 16, 384, 128, 1, False, False, 1.0),                  # 128 x 256, IC tile overhang
+    (2, 8, 8, 512, 512, 1, True, False, 1 / math.sqrt(2)),
+]
+
+
+@pytest.mark.parametrize("N,Hh,W,Ci,Co,s,res,rb,scale", WGRAD_W8_SHAPES)
+def test_conv3x3_wgrad_w8(H, N, Hh, W, Ci, Co, s, res, rb, scale):
+    H.set_wgrad_impl("w8")
+    try:
+        test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale)
+    finally:
+        H.set_wgrad_impl(os.environ.get("D3D_WGRAD_IMPL", "w8"))
+
+
 def test_linear(H):
     torch.manual_seed(4)
     x = torch.randn(2, 64, 256, device=DEV).to(BF)

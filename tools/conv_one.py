@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--ci", type=int, default=128)
     ap.add_argument("--co", type=int, default=128)
     ap.add_argument("--dgrad", action="store_true")
+    ap.add_argument("--wgrad", default="", help="weight-gradient kernel impl (reg|bufl|...) instead of fwd")
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     from distributed_3d_diffusion_pytorch_amd.ops import hip_impl as H
@@ -27,7 +28,11 @@ def main():
     x = torch.randn(N, Hh, Hh, Ci, device="cuda").to(BF)
     w = torch.randn(Co, Ci, 3, 3, device="cuda") / math.sqrt(9 * Ci)
     b = torch.randn(Co, device="cuda")
-    if a.dgrad:
+    if a.wgrad:
+        H.set_wgrad_impl(a.wgrad)
+        g = torch.randn(N, Hh, Hh, Co, device="cuda").to(BF)
+        fn = lambda: H._wgrad(g, x, Co, Ci, N, Hh, Hh, Hh, Hh, 1, 9)
+    elif a.dgrad:
         g = torch.randn(N, Hh, Hh, Co, device="cuda").to(BF)
         wt = H.packed_weight(w, True, 9)
         dx = torch.empty_like(x)
@@ -47,7 +52,8 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / a.iters
     fl = 2.0 * N * Hh * Hh * Ci * Co * 9
-    print(f"{a.impl} N{N} H{Hh} {Ci}->{Co} {'dgrad' if a.dgrad else 'fwd'}: {us:.1f} us {fl / us / 1e6:.1f} TF/s")
+    kind = 'wgrad-' + a.wgrad if a.wgrad else ('dgrad' if a.dgrad else 'fwd')
+    print(f"{a.impl} N{N} H{Hh} {Ci}->{Co} {kind}: {us:.1f} us {fl / us / 1e6:.1f} TF/s")
 
 
 if __name__ == "__main__":

@@ -98,7 +98,7 @@ def main():
                                                Ci, s, True, 1.0), a.iters), fl)
             H.set_conv_impl("bufl")
         if "wgrad" in ops:
-            for impl in ("reg", "glds32x2", "bufl"):
+            for impl in ("bufl", "w8"):
                 H.set_wgrad_impl(impl)
                 rep("conv_wgrad", shp, "hip-" + impl,
                     timeit(lambda: H._wgrad(g, x, Co, Ci, N, Hh, Hh, OH, OH, s, 9), a.iters), fl)
