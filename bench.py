@@ -44,7 +44,10 @@ def main() -> None:
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--bucket_mb", type=float, default=64.0)
     ap.add_argument("--grad_dtype", default="fp32")
-    ap.add_argument("--graph", type=int, default=0, help="1: replay the step from captured HIP graphs")
+    ap.add_argument("--graph", default="auto",
+                    help="1: replay the step from captured HIP graphs; auto: when the per-GPU micro-batch is "
+                         "<= 32 (there the eager step is host-launch-bound, so any host jitter shows up in the "
+                         "step time; the replayed step is not)")
     ap.add_argument("--profile", default="", help="write a torch.profiler kernel table (text) here")
     ap.add_argument("--profile_stack", type=int, default=0, help="with --profile: also group by N stack frames")
     ap.add_argument("--mode", default="train", choices=["train", "sample"],
@@ -74,11 +77,15 @@ def main() -> None:
     mb = args.micro_batch
     if mb < 0:
         mb = 0 if local <= 64 else 64
+    if args.graph == "auto":
+        graph = ctx.device.type == "cuda" and (mb or local) <= 32
+    else:
+        graph = bool(int(args.graph))
     cfg = make_config(None, {"model.H": args.imgsize, "model.W": args.imgsize, "data.imgsize": args.imgsize,
                              "global_batch": global_batch, "micro_batch": mb, "data.synthetic": True,
                              "backend": args.backend, "dtype": args.dtype, "log_every": 0, "ckpt_every": 0,
                              "dist.bucket_mb": args.bucket_mb, "dist.grad_dtype": args.grad_dtype,
-                             "graph": bool(args.graph)})
+                             "graph": graph})
     trainer = Trainer(cfg, ctx)
     data = SyntheticBatches(local, args.imgsize, ctx.device, seed=1234 + ctx.rank)
     pool = [next(data) for _ in range(4)]
@@ -132,7 +139,7 @@ def main() -> None:
             "config": {"model": "XUNet ch128 ch_mult(1,2,2,4) 136.7M params (3DiM, reference xunet.py)",
                        "global_batch": global_batch, "seq_len": args.imgsize * args.imgsize,
                        "image_size": args.imgsize, "per_gpu_batch": local, "micro_batch": mb or local,
-                       "hip_graph": bool(args.graph),
+                       "hip_graph": graph,
                        "parallelism": f"dp{N}",
                        "backend": "hip" if (ctx.device.type == "cuda" and use_hip(probe)) else "torch"},
             "final_loss": lv,

@@ -121,3 +121,39 @@ def gpu_sink_reducer(out_dir):
     with open(os.path.join(out_dir, f"g{ctx.rank}.txt"), "w") as f:
         f.write(f"{cos} {rel}")
     cleanup()
+
+
+def gpu_graph_vs_eager(out_dir):
+    """Two ranks sharing one GPU over gloo: the HIP-graph step (one flat
+    all-reduce between the replayed graphs) must track the eager step
+    (bucketed all-reduce from backward hooks) and keep the replicas equal."""
+    import torch
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    ctx = init_distributed("gloo", 180, use_gpu=True)
+
+    def make(graph):
+        cfg = make_config(None, {"model.H": 32, "model.W": 32, "model.dropout": 0.0, "data.imgsize": 32,
+                                 "global_batch": 8, "micro_batch": 2, "data.synthetic": True, "log_every": 0,
+                                 "ckpt_every": 0, "graph": graph, "optim.warmup_examples": 16})
+        return Trainer(cfg, ctx)
+
+    data = SyntheticBatches(4, 32, "cuda", seed=11 + ctx.rank)
+    batches = [next(data) for _ in range(3)]
+    out = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        tr = make(graph)
+        losses = [float(tr.train_step(*b)) for b in batches]
+        p = tr.flat.data.clone()
+        other = p.clone()
+        torch.distributed.broadcast(other, 0)
+        out.append((losses, p, (p - other).abs().max().item()))
+        del tr
+    (le, pe, de), (lg, pg, dg) = out
+    d = (pe - pg).abs().max().item()
+    with open(os.path.join(out_dir, f"gr{ctx.rank}.txt"), "w") as f:
+        f.write(f"{d} {de} {dg} {max(abs(a - b) for a, b in zip(le, lg))}")
+    cleanup()

@@ -323,6 +323,20 @@ def test_grad_sink_and_reducer_two_ranks_one_gpu(tmp_path):
         assert cos > 0.9999 and rel < 1e-2, (r, cos, rel)
 
 
+def test_graph_step_two_ranks_one_gpu(tmp_path):
+    """world=2 HIP-graph step (flat all-reduce between the graphs) == eager
+    step (bucketed hooks); replicas identical after every step."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import dist_workers as W
+    from distributed_3d_diffusion_pytorch_amd.parallel import spawn
+    spawn(W.gpu_graph_vs_eager, 2, (str(tmp_path),))
+    for r in range(2):
+        d, de, dg, dl = map(float, open(tmp_path / f"gr{r}.txt").read().split())
+        assert de == 0.0 and dg == 0.0, (r, de, dg)
+        assert d < 5e-4 and dl < 2e-3, (r, d, dl)
+
+
 def test_sampler_step_matches_posterior(H):
     from distributed_3d_diffusion_pytorch_amd.diffusion import cfg_posterior
     torch.manual_seed(11)
