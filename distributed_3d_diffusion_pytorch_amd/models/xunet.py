@@ -101,7 +101,9 @@ class ResnetBlock(nn.Module):
             N, H, W, C = x.shape
             assert C == self.in_features, (C, self.in_features)
             h = self.groupnorm0(x, silu=True)
-        h = ops.conv3x3(h, self.conv1.weight, self.conv1.bias)
+        # the conv epilogues also emit the partial statistics of the GroupNorm
+        # that reads their output (GN1 here; the next block's GN0 below)
+        h = ops.conv3x3(h, self.conv1.weight, self.conv1.bias, gn_groups=self.groupnorm1.gn.num_groups)
         ss = self.__dict__.pop("_ss", None)     # precomputed by the level-batched FiLM
         if ss is None:
             ss = self.film(semb)
@@ -110,7 +112,8 @@ class ResnetBlock(nn.Module):
                         self.dropout_p, self.training, _next_seed(self))
         if skip is None:
             skip = ops.linear(x, self.dense.weight, self.dense.bias) if self.in_features != self.features else x
-        h = ops.conv3x3(h, self.conv2.weight, self.conv2.bias, residual=skip, out_scale=INV_SQRT2)
+        h = ops.conv3x3(h, self.conv2.weight, self.conv2.bias, residual=skip, out_scale=INV_SQRT2,
+                        gn_groups=self.groupnorm1.gn.num_groups if self.resample is None else 0)
         if self.resample == "down":
             h = ops.avgpool2(h)
         elif self.resample == "up":

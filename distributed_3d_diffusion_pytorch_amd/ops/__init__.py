@@ -38,9 +38,12 @@ def gn_film(x, weight, bias, ss, groups: int = 32, eps: float = 1e-5, dropout_p:
 
 
 def conv3x3(x, weight, bias, stride: int = 1, residual: Optional[torch.Tensor] = None,
-            out_scale: float = 1.0, row_bias: Optional[torch.Tensor] = None, res_period: int = 0):
+            out_scale: float = 1.0, row_bias: Optional[torch.Tensor] = None, res_period: int = 0,
+            gn_groups: int = 0):
+    """gn_groups: the output feeds a GroupNorm with that many groups (the HIP
+    path then fuses that GroupNorm's statistics into the conv epilogue)."""
     if use_hip(x):
-        return _h().conv3x3(x, weight, bias, stride, residual, out_scale, row_bias, res_period)
+        return _h().conv3x3(x, weight, bias, stride, residual, out_scale, row_bias, res_period, gn_groups)
     return _t.conv3x3(x, weight, bias, stride, residual, out_scale, row_bias, res_period)
 
 

@@ -410,12 +410,78 @@ conv_glds_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   }
 }
 
+// ----------------------------------------- fused GroupNorm statistics -----
+// GroupNorm partial statistics of a conv output, produced by the conv's
+// epilogue so the GroupNorm that consumes the output skips its statistics
+// pass (one full read of the activation).  Granularity: one group x 64
+// pixels of one image (HW % 64 == 0): gnp[((n * G + g) * nparts + t) * 2] =
+// (sum, sum of squares) of the bf16-rounded outputs, t = (pixel % HW) / 64,
+// nparts = HW / 64.  Every slot is written by exactly one wave: no atomics,
+// deterministic.  s/q: per (16-channel MFMA row tile i, 64-pixel half h)
+// lane sums over its 4 channels and its pixels.
+template <int TM, int NH>
+__device__ __forceinline__ void gn_part_store(float (&s)[TM][NH], float (&q)[TM][NH], int lane, int co_base,
+                                              long pix0, int OC, int G, int HW, long Mpix, float* __restrict__ gnp) {
+  const int fr = lane & 15, fq = lane >> 4;
+  const int Cg = OC / G;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      float a = s[i][h], b = q[i][h];
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {         // the 16 pixels of a fragment column
+        a += __shfl_xor(a, m, 64);
+        b += __shfl_xor(b, m, 64);
+      }
+      if (Cg >= 8) {                              // 4-channel lane groups -> 8 / 16 / 32-channel groups
+        a += __shfl_xor(a, 16, 64);
+        b += __shfl_xor(b, 16, 64);
+      }
+      if (Cg >= 16) {
+        a += __shfl_xor(a, 32, 64);
+        b += __shfl_xor(b, 32, 64);
+      }
+      s[i][h] = a;
+      q[i][h] = b;
+    }
+  if (fr != 0) return;
+  const int nparts = HW / 64;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int co = co_base + i * 16 + fq * 4;
+    if (Cg >= 32) {                               // 32-channel groups span two row tiles
+      if ((i & 1) || fq != 0) continue;
+    } else if (fq % (Cg / 4) != 0) {
+      continue;
+    }
+    if (co >= OC) continue;
+    const int g = co / Cg;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const long p = pix0 + h * 64;
+      if (p >= Mpix) continue;
+      float a = s[i][h], b = q[i][h];
+      if (Cg >= 32 && i + 1 < TM) {
+        a += s[i + 1][h];
+        b += q[i + 1][h];
+      }
+      const long n = p / HW;
+      const int t = (int)(p - n * HW) / 64;
+      float* d = gnp + ((n * G + g) * nparts + t) * 2;
+      d[0] = a;
+      d[1] = b;
+    }
+  }
+}
+
 template <int TAPS, bool TRANS, bool ONEBAR>
 __global__ void __launch_bounds__(256, 2)
 conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
             int in_bytes, int w_bytes, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC,
-            int ldo, int stride, float scale, int res_nmod, float* __restrict__ part, int korder) {
+            int ldo, int stride, float scale, int res_nmod, float* __restrict__ part, int korder,
+            float* __restrict__ gnp, int gn_groups) {
   constexpr int BM = 128, BN = 128, BKk = 64;
   constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
   constexpr int STAGE = (BM + BN) * BKk;           // elements per stage
@@ -578,6 +644,9 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     }
     return;
   }
+  float gs[TM][1], gq[TM][1];                     // fused GroupNorm partials (gn_part_store)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) gs[i][0] = gq[i][0] = 0.f;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     long pix = n0 + wn * WN + j * 16 + fr;
@@ -605,17 +674,26 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
         }
         bf16x4 o4;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o4[e] = (bf16)(v[e] * scale);
+        for (int e = 0; e < 4; ++e) {
+          o4[e] = (bf16)(v[e] * scale);
+          const float y = (float)o4[e];
+          gs[i][0] += y;
+          gq[i][0] += y * y;
+        }
         *reinterpret_cast<bf16x4*>(dst) = o4;
       } else {
         for (int e = 0; e < 4 && co + e < OC; ++e) {
           float t = v[e];
           if (res) t += (float)res[rpix * ldo + co + e];
           dst[e] = (bf16)(t * scale);
+          const float y = (float)dst[e];
+          gs[i][0] += y;
+          gq[i][0] += y * y;
         }
       }
     }
   }
+  if (gnp) gn_part_store<TM, 1>(gs, gq, lane, m0 + wm * WM, n0 + wn * WN, OC, gn_groups, OHW, Mpix, gnp);
 }
 
 // ------------------------------------------------ 8-wave large tile ------
@@ -670,7 +748,7 @@ __global__ void __launch_bounds__(512, 1)
 conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
           const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
           int in_bytes, int w_bytes, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC,
-          int ldo, int stride, float scale, int res_nmod, int korder) {
+          int ldo, int stride, float scale, int res_nmod, int korder, float* __restrict__ gnp, int gn_groups) {
   constexpr int BKk = 64;
   constexpr int WM = BM / 2, WN = BN / 4, TM = WM / 16, TN = WN / 16;
   constexpr int APW = BM / 64, BPW = BN / 64;      // 1-KiB DMA pieces per wave per operand
@@ -767,6 +845,12 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
   }
 
   const int OHW = OH * OW;
+  constexpr int NH = WN / 64;                     // 64-pixel GroupNorm partial slots per wave slice
+  float gs[TM][NH], gq[TM][NH];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) gs[i][h] = gq[i][h] = 0.f;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const long pix = n0 + wn * WN + j * 16 + fr;
@@ -794,17 +878,26 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
         }
         bf16x4 o4;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o4[e] = (bf16)(v[e] * scale);
+        for (int e = 0; e < 4; ++e) {
+          o4[e] = (bf16)(v[e] * scale);
+          const float y = (float)o4[e];
+          gs[i][j / 4] += y;
+          gq[i][j / 4] += y * y;
+        }
         *reinterpret_cast<bf16x4*>(dst) = o4;
       } else {
         for (int e = 0; e < 4 && co + e < OC; ++e) {
           float t = v[e];
           if (res) t += (float)res[rpix * ldo + co + e];
           dst[e] = (bf16)(t * scale);
+          const float y = (float)dst[e];
+          gs[i][j / 4] += y;
+          gq[i][j / 4] += y * y;
         }
       }
     }
   }
+  if (gnp) gn_part_store<TM, NH>(gs, gq, lane, m0 + wm * WM, n0 + wn * WN, OC, gn_groups, OHW, Mpix, gnp);
 }
 
 // split-K epilogue: O[pix][co] = (sum_s part[s][pix][co] + bias + row_bias
@@ -2001,10 +2094,22 @@ D3D_API int d3d_conv_plan(int N, int OH, int OW, int OC, int ICp, int taps) {
   return want < 2 ? 1 : (int)want;
 }
 
-D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
-                     void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
-                     int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, hipStream_t st) {
+// gnp != nullptr: also produce the GroupNorm partial statistics of the
+// output (gn_part_store layout, gn_groups groups) when the chosen kernel can;
+// *gn_done reports whether it did (the caller runs the statistics pass
+// otherwise).
+D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
+                      void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
+                      int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, float* gnp,
+                      int gn_groups, int* gn_done, hipStream_t st) {
   long Mpix = (long)N * OH * OW;
+  if (gn_done) *gn_done = 0;
+  if (gnp) {
+    const int Cg = gn_groups > 0 && OC % gn_groups == 0 ? OC / gn_groups : 0;
+    const bool ok = (Cg == 4 || Cg == 8 || Cg == 16 || Cg == 32) && (OH * OW) % 64 == 0 && Mpix % 64 == 0 &&
+                    ldo == OC;
+    if (!ok) gnp = nullptr;
+  }
   constexpr int BM = 128, BN = 128;
   if (nsplit < 1 || !ws || g_conv_impl < 1) nsplit = 1;
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM), (unsigned)nsplit);
@@ -2023,7 +2128,7 @@ D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const flo
 #define W8(TP, TR, BMv, BNv)                                                                                     \
   hipLaunchKernelGGL((conv_w8_k<TP, TR, BMv, BNv>), g8, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias, \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, \
-                     OC, ldo, stride, scale, res_nmod, g_conv_korder)
+                     OC, ldo, stride, scale, res_nmod, g_conv_korder, gnp, gn_groups)
       if (bm == 256) {
         if (taps == 9) {
           if (trans) W8(9, true, 256, 256); else W8(9, false, 256, 256);
@@ -2038,6 +2143,7 @@ D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const flo
         }
       }
 #undef W8
+      if (gn_done && gnp) *gn_done = 1;
       return (int)hipGetLastError();
     }
   }
@@ -2046,7 +2152,7 @@ D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const flo
 #define BUFL(TP, TR, OB)                                                                                         \
   hipLaunchKernelGGL((conv_bufl_k<TP, TR, OB>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,    \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, \
-                     OC, ldo, stride, scale, res_nmod, part, g_conv_korder)
+                     OC, ldo, stride, scale, res_nmod, part, g_conv_korder, part ? nullptr : gnp, gn_groups)
     if (g_conv_impl >= 3) {
       if (taps == 9) {
         if (trans) BUFL(9, true, true); else BUFL(9, false, true);
@@ -2067,6 +2173,8 @@ D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const flo
       if (g > 4096) g = 4096;
       hipLaunchKernelGGL(conv_splitk_epi_k, dim3((unsigned)g), dim3(256), 0, st, part, nsplit, Mpix, OC, OH * OW,
                          bias, row_bias, (const bf16*)res, res_nmod, (bf16*)O, ldo, scale);
+    } else if (gn_done && gnp) {
+      *gn_done = 1;
     }
     return (int)hipGetLastError();
   }
@@ -2102,6 +2210,13 @@ D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const flo
   }
 #undef LAUNCH
   return (int)hipGetLastError();
+}
+
+D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
+                     void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
+                     int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, hipStream_t st) {
+  return d3d_conv2(I, Wp, bias, row_bias, res, O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans, scale,
+                   res_nmod, taps, ws, nsplit, nullptr, 0, nullptr, st);
 }
 
 D3D_API int d3d_conv3x3(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,

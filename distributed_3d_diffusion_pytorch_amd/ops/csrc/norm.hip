@@ -230,12 +230,64 @@ __global__ void gn_film_k(const bf16* __restrict__ x, const float* __restrict__ 
 // merges its image's chunk partials into LDS (the separate finalize launch is
 // gone -- at small batch every GroupNorm paid ~10 us for it), block 0 of the
 // image also publishes mean / rstd for the backward pass.
+// conv_parts > 0: part holds the producing conv's fused epilogue partials
+// ([N][G][conv_parts] x (sum, sum of squares) over 64 pixels x Cg channels,
+// conv.hip gn_part_store) instead of the statistics pass's chunk moments.
 __device__ __forceinline__ void merge_image_stats(const float* __restrict__ part, int n, int nchunks, int G, int P,
                                                   int rows, int Cg, float eps, float* s_st,
-                                                  float* __restrict__ stats_out, bool publish) {
+                                                  float* __restrict__ stats_out, bool publish, int conv_parts) {
+  if (conv_parts > 0 && G <= NT) {
+    // NT / G threads per group each fold a strided subset of the parts, then
+    // the group's thread merges the subsets in fixed order (deterministic)
+    __shared__ float s_sub[3 * NT];
+    const int subs = NT / G;
+    const int g = threadIdx.x % G, sub = threadIdx.x / G;
+    const float cnt = 64.f * Cg;
+    Moments m = {0.f, 0.f, 0.f};
+    if (sub < subs) {
+      const float* pp = part + ((long)n * G + g) * conv_parts * 2;
+      for (int t = sub; t < conv_parts; t += subs) {
+        const float sm = pp[2 * t], q = pp[2 * t + 1];
+        const float mean = sm / cnt;
+        Moments b = {cnt, mean, fmaxf(q - sm * mean, 0.f)};
+        m = merge_moments(m, b);
+      }
+    }
+    s_sub[threadIdx.x * 3 + 0] = m.n;
+    s_sub[threadIdx.x * 3 + 1] = m.mean;
+    s_sub[threadIdx.x * 3 + 2] = m.m2;
+    __syncthreads();
+    if (threadIdx.x < G) {
+      Moments a = {0.f, 0.f, 0.f};
+      for (int k = 0; k < subs; ++k) {
+        const int i = (k * G + g) * 3;
+        Moments b = {s_sub[i], s_sub[i + 1], s_sub[i + 2]};
+        if (b.n > 0.f) a = merge_moments(a, b);
+      }
+      const float mean = a.mean, rstd = rsqrtf(fmaxf(a.m2 / a.n, 0.f) + eps);
+      s_st[g * 2 + 0] = mean;
+      s_st[g * 2 + 1] = rstd;
+      if (publish) {
+        stats_out[(n * G + g) * 2 + 0] = mean;
+        stats_out[(n * G + g) * 2 + 1] = rstd;
+      }
+    }
+    __syncthreads();
+    return;
+  }
   for (int g = threadIdx.x; g < G; g += blockDim.x) {
     Moments m = {0.f, 0.f, 0.f};
-    for (int c = 0; c < nchunks; ++c) {
+    if (conv_parts > 0) {            // (G > NT)
+      const float cnt = 64.f * Cg;
+      const float* pp = part + ((long)n * G + g) * conv_parts * 2;
+      for (int t = 0; t < conv_parts; ++t) {
+        const float sm = pp[2 * t], q = pp[2 * t + 1];
+        const float mean = sm / cnt;
+        Moments b = {cnt, mean, fmaxf(q - sm * mean, 0.f)};
+        m = merge_moments(m, b);
+      }
+    }
+    for (int c = 0; c < (conv_parts > 0 ? 0 : nchunks); ++c) {
       const int q0 = c * rows, q1 = min(P, q0 + rows);
       const float* pp = part + (((long)n * nchunks + c) * G + g) * 2;
       Moments b = {(float)((q1 - q0) * Cg), pp[0], pp[1]};
@@ -259,12 +311,12 @@ __global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, co
                                                   const float* __restrict__ beta, const bf16* __restrict__ ss,
                                                   bf16* __restrict__ y, int P, int C, int G, int rows, int nchunks,
                                                   float eps, float p_drop, uint64_t seed, int ssld,
-                                                  const uint64_t* __restrict__ seed_dev, Cat cat) {
+                                                  const uint64_t* __restrict__ seed_dev, Cat cat, int conv_parts) {
   constexpr int U = MODE == 2 ? 2 : UNR;      // rows in flight per thread
   __shared__ float s_st[2 * 1024];
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int Cg = C / G;
-  merge_image_stats(part, n, nchunks, G, P, rows, Cg, eps, s_st, stats_out, chunk == 0);
+  merge_image_stats(part, n, nchunks, G, P, rows, Cg, eps, s_st, stats_out, chunk == 0, conv_parts);
   if (MODE == 2 && seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   const uint32_t dkey = drop_key(seed), dthr = drop_threshold(p_drop);
@@ -628,7 +680,7 @@ D3D_API int d3d_gn_stats(const void* x, int N, int P, int C, int G, float eps, f
 D3D_API int d3d_gn_apply2(int mode, const void* x, const float* part, float* stats_out, const float* gamma,
                           const float* beta, const void* ss, void* y, int N, int P, int C, int G, float eps,
                           float p_drop, unsigned long long seed, int ssld, const void* seed_dev, const void* x2,
-                          int C1, hipStream_t st) {
+                          int C1, int conv_parts, hipStream_t st) {
   if (G > 1024) return (int)hipErrorInvalidValue;
   Cat cat{(const bf16*)x2, nullptr, C1};
   Plan p = make_plan(N, P, C);
@@ -636,7 +688,7 @@ D3D_API int d3d_gn_apply2(int mode, const void* x, const float* part, float* sta
 #define AP(M)                                                                                                   \
   hipLaunchKernelGGL(gn_apply2_k<M>, dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, part, stats_out, gamma, \
                      beta, (const bf16*)ss, (bf16*)y, P, C, G, p.rows, p.nchunks, eps, p_drop, (uint64_t)seed, ssld, \
-                     (const uint64_t*)seed_dev, cat)
+                     (const uint64_t*)seed_dev, cat, conv_parts)
   if (mode == 0) AP(0);
   else if (mode == 1) AP(1);
   else AP(2);

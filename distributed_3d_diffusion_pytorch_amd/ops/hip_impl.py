@@ -251,14 +251,21 @@ def _gn_fwd(mode, x, w, b, G, eps, ss=None, ssld=0, p=0.0, seed=0, x2=None):
     N, H, W, C1 = x.shape
     C = C1 + (x2.shape[-1] if x2 is not None else 0)
     P = H * W
-    nch, _ = _gn_plan(N, P, C)
-    part = torch.empty(N * nch * G * 2, dtype=F32, device=x.device)
     stats = torch.empty(N * G * 2, dtype=F32, device=x.device)
-    _chk(_lib.d3d_gn_stats(x.data_ptr(), N, P, C, G, eps, part.data_ptr(), None, _ptr(x2), C1, _st()), "gn_stats")
+    fused = getattr(x, "_d3d_gnpart", None) if x2 is None else None
+    if fused is not None and fused[1] == G:
+        part, conv_parts = fused[0], fused[2]       # statistics came out of the producing conv's epilogue
+    else:
+        nch, _ = _gn_plan(N, P, C)
+        part = torch.empty(N * nch * G * 2, dtype=F32, device=x.device)
+        conv_parts = 0
+        _chk(_lib.d3d_gn_stats(x.data_ptr(), N, P, C, G, eps, part.data_ptr(), None, _ptr(x2), C1, _st()),
+             "gn_stats")
     y = torch.empty(N, H, W, C, dtype=x.dtype, device=x.device)
     _chk(_lib.d3d_gn_apply2(mode, x.data_ptr(), part.data_ptr(), stats.data_ptr(), w.data_ptr(), b.data_ptr(),
                             _ptr(ss), y.data_ptr(), N, P, C, G, float(eps), float(p), int(seed), int(ssld),
-                            _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), C1, _st()), "gn_apply2")
+                            _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), C1, int(conv_parts), _st()),
+         "gn_apply2")
     return y, stats
 
 
@@ -456,13 +463,21 @@ def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=Fa
 
 # ----------------------------------------------------------------- conv ----
 def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale, res_nmod=0,
-              taps=9):
+              taps=9, gn_groups=0):
+    """Launch the conv; with gn_groups > 0 the epilogue may also emit the
+    GroupNorm partial statistics of ``out``: returns (part, nparts) when it
+    did (the consuming GroupNorm then skips its statistics pass), else None."""
     _ensure_impl()
     ns = _lib.d3d_conv_plan(N, OH, OW, OC, ICp, taps) if ldo == OC else 1
     ws = torch.empty(ns * N * OH * OW * OC, dtype=F32, device=x.device) if ns > 1 else None
-    _chk(_lib.d3d_conv(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
-                       IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), taps, _ptr(ws), ns,
-                       _st()), "conv")
+    gnp = None
+    if gn_groups and (OH * OW) % 64 == 0:
+        gnp = torch.empty(N * gn_groups * (OH * OW // 64) * 2, dtype=F32, device=x.device)
+    done = ctypes.c_int(0)
+    _chk(_lib.d3d_conv2(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
+                        IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), taps, _ptr(ws), ns,
+                        _ptr(gnp), int(gn_groups), ctypes.byref(done), _st()), "conv")
+    return (gnp, OH * OW // 64) if done.value else None
 
 
 def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9, want_bias=False, dW=None, db=None, accumulate=False):
@@ -500,7 +515,7 @@ class _Conv(torch.autograd.Function):
     via the split-K transpose-read kernel, bias grads via channel sums."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias, res_period, taps):
+    def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias, res_period, taps, gn=None):
         x = x.contiguous()
         N, H, W, IC = x.shape
         OC = weight.shape[0]
@@ -514,8 +529,10 @@ class _Conv(torch.autograd.Function):
         out = torch.empty(N, OH, OW, OC, dtype=BF16, device=x.device)
         res = residual.contiguous() if residual is not None else None
         rb = row_bias.contiguous().float() if row_bias is not None else None
-        _conv_fwd(x, wp, bias, rb, res, out, N, H, W, IC, _up(IC, 64), OH, OW, OC, OC, stride, False, out_scale,
-                  res_period, taps)
+        parts = _conv_fwd(x, wp, bias, rb, res, out, N, H, W, IC, _up(IC, 64), OH, OW, OC, OC, stride, False,
+                          out_scale, res_period, taps, gn["groups"] if gn is not None else 0)
+        if gn is not None and parts is not None:
+            gn["part"] = parts
         ctx.save_for_backward(x, weight)
         ctx.cfg = (stride, out_scale, residual is not None, row_bias is not None, bias is not None, res_period, taps)
         ctx.bias_param = bias
@@ -578,14 +595,22 @@ class _Conv(torch.autograd.Function):
         if has_res:
             dres = g if not res_period else \
                 g.reshape(N // res_period, res_period, *g.shape[1:]).sum(0, dtype=F32).to(g.dtype)
-        return dx, dW, db, None, dres, None, drb, None, None
+        return dx, dW, db, None, dres, None, drb, None, None, None
 
 
-def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=None, res_period=0):
+def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=None, res_period=0, gn_groups=0):
+    """3x3 conv.  gn_groups > 0: the output feeds a GroupNorm with that many
+    groups -- the conv epilogue then also emits the GroupNorm's partial
+    statistics when its kernel can (attached to the output as ``_d3d_gnpart``
+    and consumed by :func:`group_norm` / :func:`gn_film`)."""
     _need_bf16(x, residual)
     OC, IC = weight.shape[0], weight.shape[1]
     if IC % 8 == 0 and OC % 8 == 0:
-        return _Conv.apply(x, weight, bias, stride, residual, out_scale, row_bias, res_period, 9)
+        gn = {"groups": int(gn_groups)} if gn_groups else None
+        y = _Conv.apply(x, weight, bias, stride, residual, out_scale, row_bias, res_period, 9, gn)
+        if gn is not None and "part" in gn:
+            y._d3d_gnpart = (gn["part"][0], int(gn_groups), gn["part"][1])
+        return y
     # stem (IC=3) / head (OC=3): zero-pad channels to a multiple of 8 so every
     # access stays 16-byte vectorised; the padding costs < 0.1 % of FLOPs.
     ICe, OCe = _up(IC, 8), _up(OC, 8)

@@ -515,3 +515,32 @@ def test_batched_weight_refresh_matches_pack(H, OC, IC, taps):
     assert torch.equal(trn, ref_t)
     if cast is not None:
         assert torch.equal(cast.reshape(-1), w.detach().to(BF).reshape(-1))
+
+
+@pytest.mark.parametrize("N,Hh,Ci,Co,fused", [
+    (16, 64, 128, 128, True),      # w8 128x512 tiles, 4-channel groups
+    (32, 32, 256, 256, True),      # 8-channel groups
+    (128, 16, 256, 256, True),     # 4-wave 128x128 kernel
+    (32, 32, 512, 512, True),      # w8 256x256, 16-channel groups
+    (16, 32, 1024, 1024, True),    # 32-channel groups span two MFMA row tiles
+    (64, 8, 512, 512, False),      # split-K grid: separate statistics pass
+    (2, 16, 128, 256, False)])
+def test_conv_fused_gn_stats(H, N, Hh, Ci, Co, fused):
+    """GroupNorm statistics emitted by the conv epilogue (w8 / bufl paths)
+    == the separate statistics pass: GN+SiLU and GN-FiLM outputs and grads."""
+    torch.manual_seed(12)
+    x = torch.randn(N, Hh, Hh, Ci, device=DEV).to(BF)
+    w = torch.randn(Co, Ci, 3, 3, device=DEV) / math.sqrt(9 * Ci)
+    b = torch.randn(Co, device=DEV) * 0.3 + 0.2
+    gam = torch.rand(Co, device=DEV) + 0.5
+    bet = torch.randn(Co, device=DEV) * 0.1
+    y = H.conv3x3(x, w, b, gn_groups=32)
+    assert hasattr(y, "_d3d_gnpart") == fused, "fused GroupNorm partials not produced as planned"
+    plain = y.detach().clone()            # no partials attached: statistics pass
+    a = H.group_norm(y, gam, bet, 32, 1e-5, True)
+    r = H.group_norm(plain, gam, bet, 32, 1e-5, True)
+    assert rel(a, r) < 1e-2, rel(a, r)
+    ss = (torch.randn(N, Hh, Hh, 2 * Co, device=DEV) * 0.5).to(BF)
+    a2 = H.gn_film(y, gam, bet, ss, 32, 1e-5, 0.0, False, 0)
+    r2 = H.gn_film(plain, gam, bet, ss, 32, 1e-5, 0.0, False, 0)
+    assert rel(a2, r2) < 1e-2, rel(a2, r2)
