@@ -31,6 +31,7 @@
 //   pixels with fp32 partial slabs + a deterministic reduce kernel that also
 //   writes the OIHW layout of the parameter gradient.
 #include "common.h"
+#include <stdlib.h>
 
 D3D_API int d3d_colsum(const float* in, long R, int Cc, float* part, float* out, float* out_odd, int accumulate,
                        hipStream_t st);
@@ -1284,13 +1285,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, lo
 
 // LDS-DMA issue of one wgrad stage (a __device__ function rather than a
 // lambda: buffer-resource values must not appear in host-visible code).
-template <int PK, int PPW, bool FAST>
+template <int PK, int PPW, bool FAST, bool PAIR>
 __device__ __forceinline__ void wgrad_bufl_issue(bf16* sA, bf16* sB, const bf16* __restrict__ dY,
                                                  const bf16* __restrict__ I, long in_elems, long p0, long p_end,
                                                  int OC, int IC, int IH, int IW, int OH, int OW, int OHW, int stride,
                                                  int kh, int kw, int dpix, int lw, int lh, int wave,
                                                  const int* trow, const unsigned* aoff, const unsigned* boff,
-                                                 const bool* bok) {
+                                                 const bool* bok, const int* khl, const int* kwl) {
   typedef __attribute__((address_space(3))) void lds_void;
   constexpr int BM = 128, BN = 128;
   const __amdgpu_buffer_rsrc_t rA = uniform_rsrc(dY + p0 * OC, (p_end - p0) * OC * 2);
@@ -1337,7 +1338,7 @@ __device__ __forceinline__ void wgrad_bufl_issue(bf16* sA, bf16* sB, const bf16*
         oh = rr / OW;
         ow = rr - oh * OW;
       }
-      const int ih = oh * stride + kh - 1, iw = ow * stride + kw - 1;
+      const int ih = oh * stride + (PAIR ? khl[i] : kh) - 1, iw = ow * stride + (PAIR ? kwl[i] : kw) - 1;
       const bool ok = bok[i] && ih >= 0 && ih < IH && iw >= 0 && iw < IW;
       const unsigned vo = (unsigned)((((img * IH + ih) * IW + iw) * IC) * 2) + (boff[i] - (unsigned)(trow[i] * IC * 2));
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * PPW + i) * 4 * BN), 16,
@@ -1359,7 +1360,11 @@ __device__ __forceinline__ void wgrad_bufl_issue(bf16* sA, bf16* sB, const bf16*
 //    is the padding test of the (uniform) tap: at most two mask compares;
 //  * transpose-read lane offsets are precomputed and the two LDS stages are
 //    unrolled so stage bases fold into instruction immediates.
-template <int TAPS, int PK, bool FAST>
+// PAIR (64-channel inputs, the 51 -> 64 ray-direction half of the
+// conditioning convs): the 128-channel B tile holds TWO taps x 64 channels
+// instead of one tap with half the tile zero; slab columns tap * 64 + c of
+// consecutive taps are contiguous, so the pair writes columns tap0 * 64 + [0,128).
+template <int TAPS, int PK, bool FAST, bool PAIR = false>
 __global__ void __launch_bounds__(256, 2)
 conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I0, float* __restrict__ ws, long in_pix,
                   int Nimg, int IH, int IW, int ICt, int OH, int OW, int OC, int stride, int pix_per_split, int ncb,
@@ -1383,8 +1388,8 @@ conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I0, floa
     by = (int)((R / gx) % gy);
     bz = (int)(R / ((long)gx * gy));
   }
-  const int tap = bx / ncb;
-  const int ci0g = (bx % ncb) * BN;                // channel tile in the (possibly concatenated) input
+  const int tap = PAIR ? 2 * bx : bx / ncb;        // PAIR: first tap of the pair
+  const int ci0g = PAIR ? 0 : (bx % ncb) * BN;     // channel tile in the (possibly concatenated) input
   const int m0 = by * BM;
   const int split = bz;
   const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
@@ -1402,17 +1407,27 @@ conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I0, floa
   const long in_elems = in_pix * IC;
 
   const int lrow = lane >> 4, pch = lane & 15;
-  int trow[PPW];
+  int trow[PPW], khl[PPW], kwl[PPW];
   unsigned aoff[PPW], boff[PPW];
   bool bok[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
     trow[i] = (wave * PPW + i) * 4 + lrow;
     const int lc = pch ^ (2 * (trow[i] & 7));
-    const int co = m0 + lc * 8, ci = ci0 + lc * 8;
+    const int co = m0 + lc * 8;
     aoff[i] = co < OC ? (unsigned)((trow[i] * OC + co) * 2) : 0x80000000u;
-    boff[i] = (unsigned)((trow[i] * IC + ci) * 2);
-    bok[i] = ci < IC;
+    if (PAIR) {                                    // chunks 0-7: tap, 8-15: tap + 1
+      const int tl = tap + (lc >> 3), ci = (lc & 7) * 8;
+      boff[i] = (unsigned)((trow[i] * IC + ci) * 2);
+      bok[i] = tl < TAPS;
+      khl[i] = tl / 3;
+      kwl[i] = tl % 3;
+    } else {
+      const int ci = ci0 + lc * 8;
+      boff[i] = (unsigned)((trow[i] * IC + ci) * 2);
+      bok[i] = ci < IC;
+      khl[i] = kwl[i] = 0;
+    }
   }
   // transpose-read lane offsets (elements): row (4g+q) + swizzled column chunk
   const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
@@ -1425,8 +1440,8 @@ conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I0, floa
 
   auto issue = [&](long p0, int stage) {
     bf16* sA = smem + stage * STAGE;
-    wgrad_bufl_issue<PK, PPW, FAST>(sA, sA + PK * BM, dY, I, in_elems, p0, p_end, OC, IC, IH, IW, OH, OW, OHW, stride,
-                                    kh, kw, dpix, lw, lh, wave, trow, aoff, boff, bok);
+    wgrad_bufl_issue<PK, PPW, FAST, PAIR>(sA, sA + PK * BM, dY, I, in_elems, p0, p_end, OC, IC, IH, IW, OH, OW, OHW,
+                                          stride, kh, kw, dpix, lw, lh, wave, trow, aoff, boff, bok, khl, kwl);
   };
 
   f32x4 acc[TM][TN];
@@ -1493,8 +1508,8 @@ conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I0, floa
   float* slab = ws + (long)split * OC * KW;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int cl = ci0 + wn * WN + j * 16 + fr;   // channel within the source
-    if (cl >= IC) continue;
+    const int cl = ci0 + wn * WN + j * 16 + fr;   // channel within the source (PAIR: within the tap pair)
+    if (PAIR ? tap * IC + cl >= TAPS * IC : cl >= IC) continue;
     const int ci = ci0g - ci0 + cl;                 // channel within the concatenation
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -2275,7 +2290,13 @@ static void launch_wgrad(const void* dY, const void* I, float* ws, int N, int IH
 #define WB(TP, F)                                                                                                \
   hipLaunchKernelGGL((conv_wgrad_bufl_k<TP, PK, F>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws,   \
                      (long)N * IH * IW, N, IH, IW, IC, OH, OW, OC, stride, pps, ncb, bws, lw, lh, (const bf16*)I2, C1)
-    if (taps == 9) {
+    if (taps == 9 && IC == 64 && !fast && I2 == nullptr) {
+      // tap pairs: the grid's x dimension covers ceil(9 / 2) pairs
+      dim3 gp(5, grid.y, grid.z);
+      hipLaunchKernelGGL((conv_wgrad_bufl_k<9, PK, false, true>), gp, dim3(256), 0, st, (const bf16*)dY,
+                         (const bf16*)I, ws, (long)N * IH * IW, N, IH, IW, IC, OH, OW, OC, stride, pps, 1, bws, lw, lh,
+                         (const bf16*)nullptr, 0);
+    } else if (taps == 9) {
       if (fast) WB(9, true); else WB(9, false);
     } else {
       if (fast) WB(1, true); else WB(1, false);
@@ -2309,12 +2330,15 @@ static void launch_wgrad(const void* dY, const void* I, float* ws, int N, int IH
 D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps, int* splits, int* pix_per_split) {
   constexpr int BM = 128, BN = 128;
   long P = (long)N * OH * OW;
-  int tiles = taps * ((IC + BN - 1) / BN) * ((OC + BM - 1) / BM);
-  // ~2 blocks per CU (the kernel's occupancy) and >= 1024 pixels per split:
-  // every extra split costs a full fp32 OCxK slab of write + reduce traffic.
-  // Rounded DOWN: 513 blocks (9 tiles x 57 splits) ran a whole extra round
-  // for one block
-  long want = 512 / tiles;
+  int tiles = (taps == 9 && IC == 64 ? 5 : taps * ((IC + BN - 1) / BN)) * ((OC + BM - 1) / BM);
+  // block target: the kernel runs ~4 blocks per CU (32 KiB LDS, 64 VGPRs),
+  // so ~1024 blocks fill the chip in one round; rounded down (no straggler
+  // round).  Sweep on the X-UNet shapes (profiles/kbench_wgrad_plan.txt):
+  // 1024 beats 512 by 10-35 %.  Every extra split costs a full fp32 OCxK slab
+  // of write + reduce traffic.  D3D_WGRAD_TARGET / D3D_WGRAD_CEIL: tuning knobs
+  static const long target = getenv("D3D_WGRAD_TARGET") ? atol(getenv("D3D_WGRAD_TARGET")) : 1024;
+  static const bool ceil_ = getenv("D3D_WGRAD_CEIL") && atoi(getenv("D3D_WGRAD_CEIL"));
+  long want = ceil_ ? (target + tiles - 1) / tiles : target / tiles;
   long maxs = (P + 255) / 256;       // small reductions (8x8 level at small batch): fill the chip first
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
@@ -2334,9 +2358,20 @@ static bool wgrad_w8_ok(int taps, int IH, int IW, int OH, int OW, int IC, int OC
   if (g_wgrad_impl != 6 || taps != 9 || stride != 1 || IH != OH || IW != OW || !pow2(OH) || !pow2(OW) ||
       IC % 128 || OC % 8 || in_elems * 2 >= (1L << 30))
     return false;
-  *bm = OC >= 256 ? 256 : 128;
+  // 256 output channels per tile: the 128-row form (384 -> 128) measured
+  // 1.5x slower than the 4-wave kernel at its 1024-block plan
+  *bm = 256;
   *bn = IC >= 256 ? 256 : 128;
-  return *bm == 256 || *bn == 256;
+  if (OC < 256) return false;
+  // short reductions (16x16 / 8x8 levels at small per-GPU batch) cannot give
+  // ~one block per CU >= 16 stages each: the 4-wave kernel is faster there
+  // (kbench batch 16: 268 vs 196 TF/s at 16x16, 256 channels)
+  const long P = in_elems / IC;
+  const int tiles = 9 * ((IC + *bn - 1) / *bn) * ((OC + *bm - 1) / *bm);
+  long splits = 256 / tiles;
+  if (splits > P / 1024) splits = P / 1024;
+  if (splits < 1) splits = 1;
+  return tiles * splits >= 128;
 }
 
 // Split plan that knows the input geometry (and therefore which kernel runs):
@@ -2387,9 +2422,8 @@ D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW,
 #define WW(BMv, BNv)                                                                                             \
   hipLaunchKernelGGL((conv_wgrad_w8_k<BMv, BNv>), g8, dim3(512), 0, st, (const bf16*)dY, (const bf16*)I, ws,       \
                      (long)N * IH * IW, N, IH, IW, IC, OH, OW, OC, pix_per_split, ncb, bws, lw, lh)
-    if (bm == 256 && bn == 256) WW(256, 256);
-    else if (bm == 256) WW(256, 128);
-    else WW(128, 256);
+    if (bn == 256) WW(256, 256);
+    else WW(256, 128);
 #undef WW
   } else {
     int ncb = (IC + BN - 1) / BN;
