@@ -22,7 +22,8 @@
 // Backward (flash v2 recompute, one workgroup per 64-key block):
 // S = Q K^T and dP = dO V^T with KEYS on the lane, so P and dS are already the
 // A operands of dV = P^T dO and dK = dS^T Q; dQ = dS K goes through LDS once
-// and is accumulated across key blocks with fp32 atomics.
+// into a per-key-block fp32 slab, and the slabs are summed in fixed order
+// (deterministic, no atomics).
 #include "common.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -300,11 +301,15 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
         bf16x8 b = tr8(Kt, TS, 32 * kc + 4 * g + qq, 32 * kc + 16 + 4 * g + qq, 16 * t + 4 * pc);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
       }
-      // acc rows: q = 16qt + 4g + i, col d = 16t + fr ... (A rows = q)
+      // acc rows: q = 16qt + 4g + i, col d = 16t + fr ... (A rows = q).
+      // This key block's dQ contribution goes to its own slab (plain stores,
+      // every element written once); dq_convert_k sums the slabs in key-block
+      // order, so dQ is bitwise reproducible (fp32 atomics were not)
+      float* slab = dq_acc + (long)kblk * gridDim.z * L * C;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         long row = (long)n * L + q0 + 16 * qt + 4 * g + i;
-        atomicAdd(dq_acc + row * C + h * D + 16 * t + fr, acc[i] * scale);
+        slab[row * C + h * D + 16 * t + fr] = acc[i] * scale;
       }
     }
   }
@@ -319,12 +324,15 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
     }
 }
 
-__global__ void dq_convert_k(const float* __restrict__ dq, bf16* __restrict__ dqkv, long rows, int C) {
-  long total = rows * C / 8;
+// dQ = sum over the kb key-block slabs (fixed order) -> bf16 q-columns of dqkv
+__global__ void dq_convert_k(const float* __restrict__ dq, bf16* __restrict__ dqkv, long rows, int C, int kb) {
+  const long total = rows * C / 8, slab = rows * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     long r = (i * 8) / C;
     int c = (int)((i * 8) % C);
-    st8(dqkv + r * 3L * C + c, ld8f(dq + i * 8));
+    f32x8 s = ld8f(dq + i * 8);
+    for (int k = 1; k < kb; ++k) s += ld8f(dq + k * slab + i * 8);
+    st8(dqkv + r * 3L * C + c, s);
   }
 }
 
@@ -347,8 +355,9 @@ D3D_API int d3d_attn_fwd(const void* qkv, void* out, float* lse, int N, int L, i
   return (int)hipGetLastError();
 }
 
-// dq_acc: [N, L, C] fp32 zero-initialised workspace; Dv: [N, heads, L] fp32
-// workspace; dqkv: [N, L, 3C] bf16 output (every element written).
+// dq_acc: [L/64, N, L, C] fp32 workspace (one slab per key block, fully
+// written); Dv: [N, heads, L] fp32 workspace; dqkv: [N, L, 3C] bf16 output
+// (every element written).
 D3D_API int d3d_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* Dv,
                          float* dq_acc, void* dqkv, int N, int L, int C, int heads, int cross, float scale,
                          hipStream_t st) {
@@ -368,6 +377,6 @@ D3D_API int d3d_attn_bwd(const void* qkv, const void* out, const void* dout, con
   long rows = (long)N * L;
   long g = (rows * C / 8 + 255) / 256;
   if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(dq_convert_k, dim3((int)g), dim3(256), 0, st, dq_acc, (bf16*)dqkv, rows, C);
+  hipLaunchKernelGGL(dq_convert_k, dim3((int)g), dim3(256), 0, st, dq_acc, (bf16*)dqkv, rows, C, L / 64);
   return (int)hipGetLastError();
 }

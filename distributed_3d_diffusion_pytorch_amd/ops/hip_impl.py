@@ -981,7 +981,8 @@ class _Attention(torch.autograd.Function):
         C = C3 // 3
         dout = dout.contiguous()
         Dv = torch.empty(N, heads, L, dtype=F32, device=qkv.device)
-        dq = torch.zeros(N, L, C, dtype=F32, device=qkv.device)
+        # one fp32 dQ slab per 64-key block, summed in fixed order (deterministic)
+        dq = torch.empty(L // 64, N, L, C, dtype=F32, device=qkv.device)
         dqkv = torch.empty_like(qkv)
         _chk(_lib.d3d_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), Dv.data_ptr(),
                                dq.data_ptr(), dqkv.data_ptr(), N, L, C, heads, int(cross), scale, _st()), "attn_bwd")
