@@ -9,9 +9,33 @@ those gradients, the sink tracks how many uses of each parameter the current
 forward made and tells the data-parallel reducer when the last one has been
 deposited (a parameter can be used more than once, e.g. the conditioning
 convs run on the rays and on the learned-embedding image).
+
+Weight-gradient stream.  A deposited weight gradient has no consumer until the
+all-reduce / optimizer, so :meth:`GradSink.producer` runs it on a second HIP
+stream: the compute stream goes straight on to the next layer's input
+gradient (the critical path of backward) while the weight-gradient GEMMs and
+their split-K reductions fill the CUs it leaves idle -- at 16 examples per GPU
+most backward launches cover well under the 256 CUs.  The side stream first
+waits for the compute stream (its operands are ready), the operands are
+``record_stream``-ed so the caching allocator cannot hand their memory to the
+compute stream early (during graph capture such frees are deferred to the end
+of the capture), and an end-of-backward autograd callback joins the side
+stream back into the caller's stream, so optimizers, graph capture and tests
+see the same ordering as a single stream.  Collectives over the deposited
+gradients are issued from behind the side stream (:meth:`collective`).
+Per-parameter accumulation order is unchanged (one side stream, launch
+order), so results stay bitwise reproducible.  ``D3D_WGRAD_STREAM=0`` runs
+everything on the compute stream.  Not used inside HIP-graph capture: there
+the replayed step is already back-to-back on the GPU (99 % kernel-busy at 16
+examples per GPU, profiles/busy_bs16_side_stream.txt) and each cross-stream
+edge of the graph costs ~7 us of dependency latency, which ate the overlap
+(eager bs128: 761 -> 786 examples/s with the side stream; graph bs16: 444 ->
+440).
 """
 from __future__ import annotations
 
+import contextlib
+import os
 from typing import Callable, Dict, Optional
 
 import torch
@@ -25,6 +49,10 @@ class GradSink:
         self.uses: Dict[int, int] = {}
         self.seen = set()
         self.notify: Optional[Callable[[int], None]] = None
+        self.stream_enabled = os.environ.get("D3D_WGRAD_STREAM", "1") != "0"
+        self._streams: Dict[int, "torch.cuda.Stream"] = {}
+        self._forked = set()
+        self._cb_queued = False
 
     def attach(self, params, views, notify: Optional[Callable[[int], None]] = None) -> None:
         self.views = {id(p): v for p, v in zip(params, views)}
@@ -66,6 +94,61 @@ class GradSink:
         self.uses[k] = n
         if n == 0 and self.notify is not None:
             self.notify(self.index[k])
+
+    # ------------------------------------------------ weight-gradient stream
+    def _side(self, idx: int):
+        st = self._streams.get(idx)
+        if st is None:
+            st = self._streams[idx] = torch.cuda.Stream(device=idx)
+        return st
+
+    @contextlib.contextmanager
+    def producer(self, dev: torch.device, *keep):
+        """Run the enclosed sink-depositing work on the side stream (see the
+        module doc).  ``keep``: tensors the work reads that autograd may free
+        right after the enclosing backward returns."""
+        if not (self.stream_enabled and dev.type == "cuda") or torch.cuda.is_current_stream_capturing():
+            yield
+            return
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        side = self._side(idx)
+        side.wait_stream(torch.cuda.current_stream(idx))
+        with torch.cuda.stream(side):
+            yield
+        for t in keep:
+            if t is not None:
+                t.record_stream(side)
+        self._forked.add(idx)
+        if not self._cb_queued:
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+                self._cb_queued = True
+            except RuntimeError:        # not inside a backward pass: join now
+                self.join()
+
+    def _end_of_backward(self) -> None:
+        self._cb_queued = False
+        self.join()
+
+    def join(self) -> None:
+        """Make the current stream wait for every deposited gradient."""
+        for idx in list(self._forked):
+            torch.cuda.current_stream(idx).wait_stream(self._streams[idx])
+        self._forked.clear()
+
+    @contextlib.contextmanager
+    def collective(self):
+        """Issue a collective over deposited gradients: from behind the side
+        stream (which first catches up with the compute stream), so it reads
+        both streams' gradients without stalling the compute stream."""
+        if not self._forked:
+            yield
+            return
+        idx = torch.cuda.current_device()
+        side = self._side(idx)
+        side.wait_stream(torch.cuda.current_stream(idx))
+        with torch.cuda.stream(side):
+            yield
 
     def reset(self) -> None:
         self.uses = {}

@@ -8,6 +8,7 @@ graph.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import math
@@ -376,21 +377,23 @@ class _CatGNDense(torch.autograd.Function):
         # one weight-gradient GEMM over the virtual concat (the kernel picks
         # the source per 128-channel tile); two GEMMs when it cannot
         _ensure_impl()
-        sp, pps = ctypes.c_int(), ctypes.c_int()
-        _lib.d3d_conv_wgrad_plan2(rows, 1, 1, OC, C, 1, ctypes.byref(sp), ctypes.byref(pps))
-        ws = torch.empty(sp.value * OC * C + 2 * sp.value * OC, dtype=F32, device=g.device)
-        rc = _lib.d3d_conv_wgrad_cat(g2.data_ptr(), a.data_ptr(), b.data_ptr(), C1, ws.data_ptr(), dWt.data_ptr(),
-                                     _ptr(dbt), rows, C, OC, sp.value, pps.value, 1, _st())
-        if rc < 0:
-            g4 = g2.reshape(rows, 1, 1, OC)
-            dW1, dbias = _wgrad(g4, a.reshape(rows, 1, 1, C1), OC, C1, rows, 1, 1, 1, 1, 1, 1, want_bias=has_db)
-            dW2, _ = _wgrad(g4, b.reshape(rows, 1, 1, C2), OC, C2, rows, 1, 1, 1, 1, 1, 1)
-            dWt[:, :C1].add_(dW1.view(OC, C1))
-            dWt[:, C1:].add_(dW2.view(OC, C2))
-            if has_db:
-                dbt.add_(dbias)
-        else:
-            _chk(rc, "wgrad_cat")
+        side = SINK.producer(g.device, g2, a, b) if direct else contextlib.nullcontext()
+        with side:
+            sp, pps = ctypes.c_int(), ctypes.c_int()
+            _lib.d3d_conv_wgrad_plan2(rows, 1, 1, OC, C, 1, ctypes.byref(sp), ctypes.byref(pps))
+            ws = torch.empty(sp.value * OC * C + 2 * sp.value * OC, dtype=F32, device=g.device)
+            rc = _lib.d3d_conv_wgrad_cat(g2.data_ptr(), a.data_ptr(), b.data_ptr(), C1, ws.data_ptr(), dWt.data_ptr(),
+                                         _ptr(dbt), rows, C, OC, sp.value, pps.value, 1, _st())
+            if rc < 0:
+                g4 = g2.reshape(rows, 1, 1, OC)
+                dW1, dbias = _wgrad(g4, a.reshape(rows, 1, 1, C1), OC, C1, rows, 1, 1, 1, 1, 1, 1, want_bias=has_db)
+                dW2, _ = _wgrad(g4, b.reshape(rows, 1, 1, C2), OC, C2, rows, 1, 1, 1, 1, 1, 1)
+                dWt[:, :C1].add_(dW1.view(OC, C1))
+                dWt[:, C1:].add_(dW2.view(OC, C2))
+                if has_db:
+                    dbt.add_(dbias)
+            else:
+                _chk(rc, "wgrad_cat")
         if direct:
             SINK.done(dwp)
             if has_db:
@@ -578,8 +581,9 @@ class _Conv(torch.autograd.Function):
         if need_w:
             direct = tw is not None and (not need_b or tb is not None)
             if direct:
-                _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, dW=tw.view(OC, IC, taps),
-                       db=tb if need_b else None, accumulate=True)
+                with SINK.producer(g.device, g, x):
+                    _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, dW=tw.view(OC, IC, taps),
+                           db=tb if need_b else None, accumulate=True)
                 SINK.done(weight)
                 if need_b:
                     SINK.done(bias)
@@ -799,7 +803,8 @@ class _Linear(torch.autograd.Function):
             tw = SINK.target(weight)
             tb = SINK.target(bias) if need_b else None
             if tw is not None and (not need_b or tb is not None):
-                _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, dW=tw.view(OC, IC, 1), db=tb, accumulate=True)
+                with SINK.producer(g.device, g4, x4):
+                    _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, dW=tw.view(OC, IC, 1), db=tb, accumulate=True)
                 SINK.done(weight)
                 if need_b:
                     SINK.done(bias)
@@ -900,26 +905,28 @@ class _FiLMBatch(torch.autograd.Function):
                 tw = [torch.zeros(w.shape, dtype=F32, device=x2.device) for w in Ws]
                 tb = [torch.zeros(b.shape, dtype=F32, device=x2.device) for b in Bs]
             _ensure_impl()
-            row0 = (ctypes.c_int * n)(*offs[:n])
-            wd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tw])
-            bd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tb])
-            if _FILM_WGRAD_BLAS:
-                # wide FiLM weight gradients ([S, 1024] over every pixel of the
-                # level) run 1.4-1.6x faster on hipBLASLt (850-880 TF/s,
-                # profiles/kbench_lin_v2.jsonl) than on the split-K MFMA
-                # kernel; its fp32 [S, K] product and the bias column sums are
-                # then scattered into the parameters' gradients in one launch
-                prod = _mm_f32(dy.t(), x2)
-                nimg = 64 if rows % 64 == 0 else 1
-                _, bsum = _chansum(dy.view(nimg, rows // nimg, 1, S), False)
-                _chk(_lib.d3d_wgrad_scatter(prod.data_ptr(), S, K, 1, 1, bsum.data_ptr(), 1, n, row0, wd, bd,
-                                            _st()), "film_wgrad_scatter")
-            else:
-                sp, pps = ctypes.c_int(), ctypes.c_int()
-                _lib.d3d_conv_wgrad_plan2(rows, 1, 1, S, K, 1, ctypes.byref(sp), ctypes.byref(pps))
-                ws = torch.empty(sp.value * S * K + 2 * sp.value * S, dtype=F32, device=x2.device)
-                _chk(_lib.d3d_conv_wgrad_seg(dy.data_ptr(), x2.data_ptr(), ws.data_ptr(), rows, 1, 1, K, 1, 1, S,
-                                             1, sp.value, pps.value, 1, 1, n, row0, wd, bd, _st()), "film_wgrad")
+            side = SINK.producer(x2.device, dy, x2) if direct else contextlib.nullcontext()
+            with side:
+                row0 = (ctypes.c_int * n)(*offs[:n])
+                wd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tw])
+                bd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tb])
+                if _FILM_WGRAD_BLAS:
+                    # wide FiLM weight gradients ([S, 1024] over every pixel of the
+                    # level) run 1.4-1.6x faster on hipBLASLt (850-880 TF/s,
+                    # profiles/kbench_lin_v2.jsonl) than on the split-K MFMA
+                    # kernel; its fp32 [S, K] product and the bias column sums are
+                    # then scattered into the parameters' gradients in one launch
+                    prod = _mm_f32(dy.t(), x2)
+                    nimg = 64 if rows % 64 == 0 else 1
+                    _, bsum = _chansum(dy.view(nimg, rows // nimg, 1, S), False)
+                    _chk(_lib.d3d_wgrad_scatter(prod.data_ptr(), S, K, 1, 1, bsum.data_ptr(), 1, n, row0, wd, bd,
+                                                _st()), "film_wgrad_scatter")
+                else:
+                    sp, pps = ctypes.c_int(), ctypes.c_int()
+                    _lib.d3d_conv_wgrad_plan2(rows, 1, 1, S, K, 1, ctypes.byref(sp), ctypes.byref(pps))
+                    ws = torch.empty(sp.value * S * K + 2 * sp.value * S, dtype=F32, device=x2.device)
+                    _chk(_lib.d3d_conv_wgrad_seg(dy.data_ptr(), x2.data_ptr(), ws.data_ptr(), rows, 1, 1, K, 1, 1, S,
+                                                 1, sp.value, pps.value, 1, 1, n, row0, wd, bd, _st()), "film_wgrad")
             if direct:
                 for w, b in zip(Ws, Bs):
                     SINK.done(w)

@@ -102,15 +102,19 @@ class GradReducer:
         self._launched[b] = True
         bk = self.buckets[b]
         view = self.flat.grad[bk["start"]: bk["end"]]
-        if self.grad_dtype == torch.float32:
-            self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
-        else:
-            tmp = view.to(self.grad_dtype)
-            self._works.append((dist.all_reduce(tmp, group=self.group, async_op=True), tmp, view))
+        ctx = self.sink.collective() if self.sink is not None else contextlib.nullcontext()
+        with ctx:       # behind the sink's weight-gradient stream (ops/gradsink.py)
+            if self.grad_dtype == torch.float32:
+                self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+            else:
+                tmp = view.to(self.grad_dtype)
+                self._works.append((dist.all_reduce(tmp, group=self.group, async_op=True), tmp, view))
 
     def finish(self) -> None:
         """Launch any bucket whose gradients never arrived (unused params) and
         make the current stream wait for every reduction."""
+        if self.sink is not None:
+            self.sink.join()
         if self.world == 1 or not self.enabled:
             self.reset()
             return

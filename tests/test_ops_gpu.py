@@ -549,7 +549,8 @@ def test_conv_fused_gn_stats(H, N, Hh, Ci, Co, fused):
 def test_training_step_bitwise_deterministic():
     """Race screen: two identical 2-step training runs through
     every HIP kernel (split-K slabs, fused GroupNorm partials, attention,
-    dropout masks) produce bitwise-identical parameters and losses."""
+    dropout masks) produce bitwise-identical parameters and losses, with the
+    weight gradients on the side stream (ops/gradsink.py) or not."""
     from distributed_3d_diffusion_pytorch_amd.config import make_config
     from distributed_3d_diffusion_pytorch_amd.engine import Trainer
     from distributed_3d_diffusion_pytorch_amd.parallel import DistContext
@@ -557,8 +558,13 @@ def test_training_step_bitwise_deterministic():
     ctx = DistContext(device=torch.device("cuda", 0))
     data = SyntheticBatches(8, 64, "cuda", seed=21)
     batches = [next(data) for _ in range(2)]
+    from distributed_3d_diffusion_pytorch_amd.ops.gradsink import SINK
     runs = []
-    for _ in range(2):
+    prev = SINK.stream_enabled
+    # the third run puts the weight gradients back on the compute stream: the
+    # side stream must not change a single bit either
+    for side in (True, True, False):
+        SINK.stream_enabled = side
         torch.manual_seed(0)
         cfg = make_config(None, {"model.H": 64, "model.W": 64, "data.imgsize": 64, "global_batch": 8,
                                  "micro_batch": 4, "data.synthetic": True, "log_every": 0, "ckpt_every": 0,
@@ -567,5 +573,7 @@ def test_training_step_bitwise_deterministic():
         losses = [tr.train_step(*b).item() for b in batches]
         runs.append((losses, tr.flat.data.clone()))
         del tr
-    assert runs[0][0] == runs[1][0], runs
-    assert torch.equal(runs[0][1], runs[1][1]), (runs[0][1] - runs[1][1]).abs().max().item()
+    SINK.stream_enabled = prev
+    for r in runs[1:]:
+        assert runs[0][0] == r[0], runs
+        assert torch.equal(runs[0][1], r[1]), (runs[0][1] - r[1]).abs().max().item()

@@ -12,12 +12,38 @@ def main():
     ap.add_argument("--steps", type=int, default=0, help="divide totals by K (per-step ms)")
     ap.add_argument("--top", type=int, default=45)
     ap.add_argument("--grid", action="store_true", help="split rows by grid size")
+    ap.add_argument("--busy", type=float, default=0.0,
+                    help="occupancy of the last BUSY ms of the trace: union of kernel intervals vs span vs the sum "
+                         "of kernel times (>1 overlap factor = concurrent kernels)")
     a = ap.parse_args()
     db = sqlite3.connect(a.db)
     cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
     name_col = "kernel_name" if "kernel_name" in cols else "name"
     gx = "grid_x" if "grid_x" in cols else None
     q = f"select {name_col}, start, end" + (f", {gx}, grid_y, grid_z, workgroup_x" if gx else "") + " from kernels"
+    if a.busy:
+        iv = sorted((r[1], r[2]) for r in db.execute(f"select {name_col}, start, end from kernels"))
+        end = max(e for _, e in iv)
+        lo = end - a.busy * 1e6
+        iv = [(max(s0, lo), e) for s0, e in iv if e > lo]
+        tot = sum(e - s0 for s0, e in iv)
+        busy, cur_s, cur_e, gaps = 0, None, None, []
+        for s0, e in iv:
+            if cur_e is None or s0 > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                    gaps.append(s0 - cur_e)
+                cur_s, cur_e = s0, e
+            else:
+                cur_e = max(cur_e, e)
+        busy += cur_e - cur_s
+        span = end - lo
+        gaps.sort()
+        print(f"window {span * 1e-6:.2f} ms: busy (union) {busy * 1e-6:.2f} ms = {100 * busy / span:.1f}%, "
+              f"kernel sum {tot * 1e-6:.2f} ms (overlap x{tot / max(busy, 1):.2f}), {len(iv)} kernels, "
+              f"{len(gaps)} gaps, median gap {gaps[len(gaps) // 2] * 1e-3 if gaps else 0:.2f} us, "
+              f"gap sum {sum(gaps) * 1e-6:.2f} ms")
+        return
     agg = defaultdict(lambda: [0.0, 0])
     t0, t1 = None, None
     for r in db.execute(q):
