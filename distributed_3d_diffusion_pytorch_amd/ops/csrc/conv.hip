@@ -751,7 +751,11 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
           int in_bytes, int w_bytes, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC,
           int ldo, int stride, float scale, int res_nmod, int korder, float* __restrict__ gnp, int gn_groups) {
   constexpr int BKk = 64;
-  constexpr int WM = BM / 2, WN = BN / 4, TM = WM / 16, TN = WN / 16;
+  // 8 waves as 2 x 4 (M x N) over >= 256-pixel tiles; 4 x 2 over the
+  // 128-pixel tile (256 x 128: the 32x32 level at 16 examples per GPU, one
+  // block per CU) so every wave still owns a whole 64-pixel GN slot
+  constexpr int WGN = BN >= 256 ? 4 : 2, WGM = 8 / WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
   constexpr int APW = BM / 64, BPW = BN / 64;      // 1-KiB DMA pieces per wave per operand
   constexpr int STAGE = (BM + BN) * BKk;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
@@ -759,7 +763,7 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // SGPR: LDS-DMA bases stay scalar
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WGN, wn = wave % WGN;
   const long Mpix = (long)Nimg * OH * OW;
   const int nbx = gridDim.x;
   int bid = blockIdx.x;
@@ -931,6 +935,73 @@ __global__ void conv_splitk_epi_k(const float* __restrict__ part, int nsplit, lo
 #pragma unroll
     for (int e = 0; e < 4; ++e) o4[e] = (bf16)(a[e] * scale);
     *reinterpret_cast<bf16x4*>(O + pix * ldo + co) = o4;
+  }
+}
+
+// split-K epilogue that also emits the GroupNorm partial statistics of its
+// output (gn_part_store layout): one block per (64-pixel part, 64-channel
+// slab) -- whole groups (Cg <= 32) of one image, so every (image, group,
+// part) slot is written by exactly one block, no atomics.  Statistics are
+// taken on the stored bf16 values, like the statistics pass.
+__global__ void __launch_bounds__(256) conv_splitk_epi_gn_k(const float* __restrict__ part, int nsplit, long Mpix,
+                                                            int OC, int OHW, const float* __restrict__ bias,
+                                                            const float* __restrict__ row_bias,
+                                                            const bf16* __restrict__ res, int res_nmod,
+                                                            bf16* __restrict__ O, float scale,
+                                                            float* __restrict__ gnp, int G) {
+  constexpr int CB = 64, TPC = CB / 4, PPI = 256 / TPC;   // 16 threads per pixel, 16 pixels per pass
+  __shared__ float s_s[PPI][CB / 4], s_q[PPI][CB / 4];
+  const int tid = threadIdx.x, r = tid / TPC, cq = tid % TPC;
+  const long pix0 = (long)blockIdx.x * 64;
+  const int co = blockIdx.y * CB + cq * 4;
+  const long slab = Mpix * OC;
+  const int Cg = OC / G;
+  float sum = 0.f, sq = 0.f;
+  for (int k = 0; k < 64 / PPI; ++k) {
+    const long pix = pix0 + k * PPI + r;
+    f32x4 a = *reinterpret_cast<const f32x4*>(part + pix * OC + co);
+    for (int sp = 1; sp < nsplit; ++sp) a += *reinterpret_cast<const f32x4*>(part + sp * slab + pix * OC + co);
+    const int img = (int)(pix / OHW);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = a[e] + (bias ? bias[co + e] : 0.f);
+      if (row_bias) t += row_bias[(long)img * OC + co + e];
+      a[e] = t;
+    }
+    if (res) {
+      const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
+      bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * OC + co);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] += (float)r4[e];
+    }
+    bf16x4 o4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o4[e] = (bf16)(a[e] * scale);
+      const float y = (float)o4[e];
+      sum += y;
+      sq += y * y;
+    }
+    *reinterpret_cast<bf16x4*>(O + pix * OC + co) = o4;
+  }
+  s_s[r][cq] = sum;
+  s_q[r][cq] = sq;
+  __syncthreads();
+  const int ng = CB / Cg;                          // groups in this slab
+  if (tid < ng) {
+    const int q4 = Cg / 4;
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < PPI; ++rr)
+      for (int j = 0; j < q4; ++j) {
+        a += s_s[rr][tid * q4 + j];
+        b += s_q[rr][tid * q4 + j];
+      }
+    const long n = pix0 / OHW;
+    const int t = (int)(pix0 - n * OHW) / 64;
+    const int g = (blockIdx.y * CB) / Cg + tid;
+    float* d = gnp + ((n * G + g) * (OHW / 64) + t) * 2;
+    d[0] = a;
+    d[1] = b;
   }
 }
 
@@ -2134,17 +2205,30 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
     const int bm = (OC % 256 == 0 || OC > 384) ? 256 : 128;
     // 128 / 384-channel layers only as 128x512 tiles on request (impl 6):
     // 128x256 tiles measured slower than two 128x128 blocks per CU (bufl1)
-    const bool wide = bm == 128 && g_conv_impl == 6;
-    const int bn = wide ? 512 : 256;
-    const long ptiles = (Mpix + bn - 1) / bn;
-    const long blocks = ptiles * ((OC + bm - 1) / bm);
+    const bool wide = bm == 128 && g_conv_impl >= 6;
+    int bn = wide ? 512 : 256;
+    long ptiles = (Mpix + bn - 1) / bn;
+    long blocks = ptiles * ((OC + bm - 1) / bm);
+    // impl 7: 256 x 128 tiles when 256 x 256 ones would leave CUs idle but
+    // the narrower tile still gives every CU a block
+    if (g_conv_impl == 7 && bm == 256 && blocks < 256 && ((Mpix + 127) / 128) * ((OC + 255) / 256) >= 256) {
+      bn = 128;
+      ptiles = (Mpix + bn - 1) / bn;
+      blocks = ptiles * ((OC + bm - 1) / bm);
+    }
     if ((bm == 256 || wide) && blocks >= 256) {
       dim3 g8((unsigned)ptiles, (unsigned)((OC + bm - 1) / bm), 1);
 #define W8(TP, TR, BMv, BNv)                                                                                     \
   hipLaunchKernelGGL((conv_w8_k<TP, TR, BMv, BNv>), g8, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias, \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, \
                      OC, ldo, stride, scale, res_nmod, g_conv_korder, gnp, gn_groups)
-      if (bm == 256) {
+      if (bn == 128) {
+        if (taps == 9) {
+          if (trans) W8(9, true, 256, 128); else W8(9, false, 256, 128);
+        } else {
+          if (trans) W8(1, true, 256, 128); else W8(1, false, 256, 128);
+        }
+      } else if (bm == 256) {
         if (taps == 9) {
           if (trans) W8(9, true, 256, 256); else W8(9, false, 256, 256);
         } else {
@@ -2182,7 +2266,13 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
       }
     }
 #undef BUFL
-    if (part) {
+    if (part && gnp && OC % 64 == 0) {
+      // gnp non-null implies ldo == OC, 64 | H*W and Cg <= 32
+      hipLaunchKernelGGL(conv_splitk_epi_gn_k, dim3((unsigned)(Mpix / 64), (unsigned)(OC / 64)), dim3(256), 0, st,
+                         part, nsplit, Mpix, OC, OH * OW, bias, row_bias, (const bf16*)res, res_nmod, (bf16*)O,
+                         scale, gnp, gn_groups);
+      if (gn_done) *gn_done = 1;
+    } else if (part) {
       long nv = Mpix * (OC / 4);
       long g = (nv + 255) / 256;
       if (g > 4096) g = 4096;

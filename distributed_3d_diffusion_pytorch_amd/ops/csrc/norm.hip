@@ -477,7 +477,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
     }
   }
   __syncthreads();
-  const long prow = (long)n * nchunks + chunk;
+  const long prow = (long)n * nchunks + chunk, R = (long)gridDim.y * nchunks;
   for (int c = tid; c < C; c += NT) {
     float a = 0.f, b = 0.f;
     for (int rr = 0; rr < rpi; ++rr) {
@@ -485,8 +485,8 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
       a += o[0];
       b += o[1];
     }
-    chan_part[(prow * C + c) * 2 + 0] = a;
-    chan_part[(prow * C + c) * 2 + 1] = b;
+    chan_part[(2L * c) * R + prow] = a;         // [2C][R]: one contiguous row per dgamma / dbeta entry
+    chan_part[(2L * c + 1) * R + prow] = b;
   }
   for (int g = tid; g < G; g += NT) {
     float a = 0.f, b = 0.f;
@@ -554,6 +554,33 @@ __global__ void gn_bwd_apply_k(const bf16* __restrict__ x, const bf16* __restric
 
 // Chunked backward apply with the per-image group coefficients merged in
 // LDS from the reduce pass's partials (replaces gn_bwd_coef_k + gn_bwd_apply_k).
+// dgamma / dbeta of the backward: chan_part is [2C][R] (R = images x
+// chunks; row 2c -> dgamma[c], row 2c+1 -> dbeta[c]); one wave sums one
+// contiguous row in a fixed order (8 accumulators per lane, butterfly).  Run
+// by the leading rows of gn_bwd_apply2_k's grid (dispatched first, they
+// overlap the apply work): replaces two colsum launches per backward.
+__device__ __forceinline__ void dgb_rowsum(const float* __restrict__ part, long R, int nrows, int row,
+                                           float* __restrict__ dgamma, float* __restrict__ dbeta, int acc) {
+  if (row >= nrows) return;
+  const int lane = threadIdx.x & 63;
+  const float* src = part + (long)row * R;
+  float a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = 0.f;
+  long i = lane;
+  for (; i + 7 * 64 < R; i += 8 * 64)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += src[i + k * 64];
+  for (int k = 0; i < R; i += 64, ++k) a[k & 7] += src[i];
+  float t = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m, 64);
+  if (lane == 0) {
+    float* o = (row & 1) ? dbeta + (row >> 1) : dgamma + (row >> 1);
+    *o = acc ? *o + t : t;
+  }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                       const bf16* __restrict__ ss, const float* __restrict__ stats,
@@ -561,10 +588,19 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       bf16* __restrict__ dx, int P, int C, int G, int rows,
                                                       int nchunks, float p_drop, uint64_t seed, int ssld,
-                                                      const uint64_t* __restrict__ seed_dev, Cat cat) {
+                                                      const uint64_t* __restrict__ seed_dev, Cat cat,
+                                                      const float* __restrict__ chan_part,
+                                                      float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                      int accumulate, int trows) {
+  if ((int)blockIdx.y < trows) {        // leading grid rows: dgamma / dbeta, 4 rows (waves) per block
+    const int blk = blockIdx.y * nchunks + blockIdx.x;
+    dgb_rowsum(chan_part, (long)(gridDim.y - trows) * nchunks, 2 * C, blk * (NT / 64) + (threadIdx.x >> 6), dgamma,
+               dbeta, accumulate);
+    return;
+  }
   constexpr int U = 2;      // rows in flight per thread
   __shared__ float s_c[4 * 1024];      // per group: mean, rstd, c1, c2
-  const int chunk = blockIdx.x, n = blockIdx.y;
+  const int chunk = blockIdx.x, n = blockIdx.y - trows;
   const int Cg = C / G;
   const float inv = 1.f / (float)((long)P * Cg);
   for (int g = threadIdx.x; g < G; g += NT) {
@@ -720,7 +756,7 @@ D3D_API int d3d_gn_film(const void* x, const float* stats, const float* gamma, c
   return (int)hipGetLastError();
 }
 
-// mode: 0 plain, 1 silu, 2 film.  Workspaces: chan_part [N*nchunks*C*2],
+// mode: 0 plain, 1 silu, 2 film.  Workspaces: chan_part [2C][N*nchunks],
 // grp_part [N*nchunks*G*2 + 64*2*C] (tail = column-sum partials), coef [N*G*2].  Outputs dx (bf16), dgamma/dbeta
 // (fp32 [C]) and, for mode 2, dss (bf16 [N,P,2C]).
 D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss, const float* stats,
@@ -741,15 +777,16 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
   else if (mode == 1) RED(1);
   else RED(2);
 #undef RED
-  // dgamma/dbeta: chan_part is [N*nchunks][C][2] -> column sums over 2C
-  // interleaved columns (workspace: the tail of grp_part's allocation)
-  d3d_colsum(chan_part, (long)N * p.nchunks, 2 * C, grp_part + (long)N * p.nchunks * G * 2, dgamma, dbeta,
-             accumulate, st);
+  // dgamma/dbeta: chan_part is [2C][N*nchunks] -> 2C row sums, 4 per block,
+  // by `trows` leading rows of the apply grid
   if (G > 1024) return (int)hipErrorInvalidValue;
-#define APP(M)                                                                                                  \
-  hipLaunchKernelGGL(gn_bwd_apply2_k<M>, dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, (const bf16*)dy,  \
-                     (const bf16*)ss, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows, p.nchunks, p_drop, \
-                     (uint64_t)seed, ssld, (const uint64_t*)seed_dev, cat)
+  const int tblocks = (2 * C + NT / 64 - 1) / (NT / 64);
+  const int trows = (tblocks + p.nchunks - 1) / p.nchunks;
+#define APP(M)                                                                                                    \
+  hipLaunchKernelGGL(gn_bwd_apply2_k<M>, dim3(p.nchunks, N + trows), dim3(NT), 0, st, (const bf16*)x,             \
+                     (const bf16*)dy, (const bf16*)ss, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows,    \
+                     p.nchunks, p_drop, (uint64_t)seed, ssld, (const uint64_t*)seed_dev, cat, chan_part, dgamma,    \
+                     dbeta, accumulate, trows)
   if (mode == 0) APP(0);
   else if (mode == 1) APP(1);
   else APP(2);

@@ -38,7 +38,7 @@ def set_conv_impl(impl: str) -> None:
     dev = torch.cuda.current_device()
     if dev not in _ZERO_PAGE:
         _ZERO_PAGE[dev] = torch.zeros(64, dtype=BF16, device="cuda")
-    _chk(_lib.d3d_set_conv_impl({"reg": 0, "glds": 1, "bufl": 2, "bufl1": 3, "w8": 4, "w8w": 6}[impl], _ZERO_PAGE[dev].data_ptr()), "set_conv_impl")
+    _chk(_lib.d3d_set_conv_impl({"reg": 0, "glds": 1, "bufl": 2, "bufl1": 3, "w8": 4, "w8w": 6, "w8n": 7}[impl], _ZERO_PAGE[dev].data_ptr()), "set_conv_impl")
 
 
 def set_conv_korder(korder: int) -> None:

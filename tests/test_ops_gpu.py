@@ -5,6 +5,7 @@ import os
 
 import pytest
 import torch
+import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
@@ -152,10 +153,12 @@ W8_SHAPES = [
     (64, 32, 32, 256, 256, 1, False, True, 1.0),                  # BM=256
     (300, 12, 20, 128, 384, 1, False, False, 1.0),                # partial pixel tile, OC 384 -> 3 x BM=128
     (16, 64, 64, 64, 640, 1, True, False, 0.5),                   # OC 640: BM=256 tile overhangs the weights
+    (32, 32, 32, 256, 256, 1, True, False, 1.0),                  # w8n: 256 x 128 tiles (128 of 256x256 < 256 CUs)
+    (16, 32, 32, 512, 512, 1, False, True, 0.5),                  # w8n: 2 x 128 tiles of 256 x 128
 ]
 
 
-@pytest.mark.parametrize("impl", ["w8", "w8w"])
+@pytest.mark.parametrize("impl", ["w8", "w8w", "w8n"])
 @pytest.mark.parametrize("N,Hh,W,Ci,Co,s,res,rb,scale", W8_SHAPES)
 def test_conv3x3_w8(H, impl, N, Hh, W, Ci, Co, s, res, rb, scale):
     H.set_conv_impl(impl)
@@ -517,24 +520,30 @@ def test_batched_weight_refresh_matches_pack(H, OC, IC, taps):
         assert torch.equal(cast.reshape(-1), w.detach().to(BF).reshape(-1))
 
 
-@pytest.mark.parametrize("N,Hh,Ci,Co,fused", [
-    (16, 64, 128, 128, True),      # w8 128x512 tiles, 4-channel groups
-    (32, 32, 256, 256, True),      # 8-channel groups
-    (128, 16, 256, 256, True),     # 4-wave 128x128 kernel
-    (32, 32, 512, 512, True),      # w8 256x256, 16-channel groups
-    (16, 32, 1024, 1024, True),    # 32-channel groups span two MFMA row tiles
-    (64, 8, 512, 512, False),      # split-K grid: separate statistics pass
-    (2, 16, 128, 256, False)])
-def test_conv_fused_gn_stats(H, N, Hh, Ci, Co, fused):
-    """GroupNorm statistics emitted by the conv epilogue (w8 / bufl paths)
-    == the separate statistics pass: GN+SiLU and GN-FiLM outputs and grads."""
+@pytest.mark.parametrize("N,Hh,Ci,Co,fused,res", [
+    (16, 64, 128, 128, True, False),      # w8 128x512 tiles, 4-channel groups
+    (32, 32, 256, 256, True, False),      # 8-channel groups
+    (128, 16, 256, 256, True, True),      # 4-wave 128x128 kernel
+    (32, 32, 512, 512, True, False),      # w8 256x256, 16-channel groups
+    (16, 32, 1024, 1024, True, False),    # 32-channel groups span two MFMA row tiles
+    (64, 8, 512, 512, True, True),        # split-K grid: statistics from the split-K epilogue
+    (2, 16, 128, 256, True, False),       # split-K, 8-channel groups
+    (2, 16, 64, 96, False, False)])       # OC % 64 != 0 under split-K: separate statistics pass
+def test_conv_fused_gn_stats(H, N, Hh, Ci, Co, fused, res):
+    """GroupNorm statistics emitted by the conv epilogue (w8 / bufl / split-K
+    epilogue paths) == the separate statistics pass: GN+SiLU and GN-FiLM."""
     torch.manual_seed(12)
     x = torch.randn(N, Hh, Hh, Ci, device=DEV).to(BF)
     w = torch.randn(Co, Ci, 3, 3, device=DEV) / math.sqrt(9 * Ci)
     b = torch.randn(Co, device=DEV) * 0.3 + 0.2
     gam = torch.rand(Co, device=DEV) + 0.5
     bet = torch.randn(Co, device=DEV) * 0.1
-    y = H.conv3x3(x, w, b, gn_groups=32)
+    r = torch.randn(N, Hh, Hh, Co, device=DEV).to(BF) if res else None
+    y = H.conv3x3(x, w, b, residual=r, out_scale=1 / math.sqrt(2) if res else 1.0, gn_groups=32)
+    if res:
+        ref = F.conv2d(x.float().permute(0, 3, 1, 2), w, b, 1, 1).permute(0, 2, 3, 1)
+        ref = (ref + r.float()) / math.sqrt(2)
+        assert rel(y, ref) < 2e-2, rel(y, ref)
     assert hasattr(y, "_d3d_gnpart") == fused, "fused GroupNorm partials not produced as planned"
     plain = y.detach().clone()            # no partials attached: statistics pass
     a = H.group_norm(y, gam, bet, 32, 1e-5, True)
