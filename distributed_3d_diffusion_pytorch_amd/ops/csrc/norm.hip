@@ -12,6 +12,7 @@
 // reductions never re-read the input in a second pass (partials in LDS,
 // tiny cross-chunk merge kernels).
 #include "common.h"
+#include <stdlib.h>
 
 D3D_API int d3d_colsum(const float* in, long R, int Cc, float* part, float* out, float* out_odd, int accumulate,
                        hipStream_t st);
@@ -27,12 +28,25 @@ struct Plan {
   int rows;     // rows per chunk (multiple of rpi)
 };
 
+// blocks per GroupNorm launch (D3D_GN_TARGET overrides; read once).  1024
+// beat 2048 and 512 by 0.5-1 % on both headline configs (the per-block
+// merge / LDS epilogue amortises over more rows; profiles/ab_gn_target.txt)
+static int gn_target_blocks() {
+  static int t = -1;
+  if (t < 0) {
+    const char* e = getenv("D3D_GN_TARGET");
+    t = e ? atoi(e) : 1024;
+    if (t < 64) t = 1024;
+  }
+  return t;
+}
+
 Plan make_plan(int N, int P, int C) {
   Plan p;
   p.tpr = C / 8;
   p.rpi = NT / p.tpr;
   if (p.rpi < 1) p.rpi = 1;
-  int target_blocks = 2048;
+  int target_blocks = gn_target_blocks();
   int nch = (target_blocks + N - 1) / N;
   int maxch = (P + p.rpi - 1) / p.rpi;
   if (nch > maxch) nch = maxch;
@@ -236,21 +250,42 @@ __global__ void gn_film_k(const bf16* __restrict__ x, const float* __restrict__ 
 __device__ __forceinline__ void merge_image_stats(const float* __restrict__ part, int n, int nchunks, int G, int P,
                                                   int rows, int Cg, float eps, float* s_st,
                                                   float* __restrict__ stats_out, bool publish, int conv_parts) {
-  if (conv_parts > 0 && G <= NT) {
-    // NT / G threads per group each fold a strided subset of the parts, then
-    // the group's thread merges the subsets in fixed order (deterministic)
+  // NT / G threads per group each fold a strided subset of the parts -- 8
+  // loads issued back to back per round, so a 64-part image costs one L2
+  // round trip instead of a chain of dependent ones -- then the group's
+  // thread merges the subsets in fixed order (deterministic).
+  constexpr int B = 8;
+  if (G <= NT) {
     __shared__ float s_sub[3 * NT];
     const int subs = NT / G;
     const int g = threadIdx.x % G, sub = threadIdx.x / G;
-    const float cnt = 64.f * Cg;
+    const int nparts = conv_parts > 0 ? conv_parts : nchunks;
     Moments m = {0.f, 0.f, 0.f};
     if (sub < subs) {
-      const float* pp = part + ((long)n * G + g) * conv_parts * 2;
-      for (int t = sub; t < conv_parts; t += subs) {
-        const float sm = pp[2 * t], q = pp[2 * t + 1];
-        const float mean = sm / cnt;
-        Moments b = {cnt, mean, fmaxf(q - sm * mean, 0.f)};
-        m = merge_moments(m, b);
+      for (int t0 = sub; t0 < nparts; t0 += B * subs) {
+        float u[B], v[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+          const int t = t0 + k * subs;
+          const float* pp = conv_parts > 0 ? part + (((long)n * G + g) * conv_parts + t) * 2
+                                           : part + (((long)n * nchunks + t) * G + g) * 2;
+          u[k] = t < nparts ? pp[0] : 0.f;
+          v[k] = t < nparts ? pp[1] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+          const int t = t0 + k * subs;
+          if (t >= nparts) break;
+          Moments bm;
+          if (conv_parts > 0) {          // (sum, sum of squares) over 64 pixels x Cg channels
+            const float cnt = 64.f * Cg, mean = u[k] / cnt;
+            bm = {cnt, mean, fmaxf(v[k] - u[k] * mean, 0.f)};
+          } else {                        // statistics pass: (mean, M2) over the chunk's rows
+            const int q0 = t * rows, q1 = min(P, q0 + rows);
+            bm = {(float)((q1 - q0) * Cg), u[k], v[k]};
+          }
+          m = merge_moments(m, bm);
+        }
       }
     }
     s_sub[threadIdx.x * 3 + 0] = m.n;
@@ -258,13 +293,13 @@ __device__ __forceinline__ void merge_image_stats(const float* __restrict__ part
     s_sub[threadIdx.x * 3 + 2] = m.m2;
     __syncthreads();
     if (threadIdx.x < G) {
-      Moments a = {0.f, 0.f, 0.f};
+      Moments acc = {0.f, 0.f, 0.f};
       for (int k = 0; k < subs; ++k) {
         const int i = (k * G + g) * 3;
-        Moments b = {s_sub[i], s_sub[i + 1], s_sub[i + 2]};
-        if (b.n > 0.f) a = merge_moments(a, b);
+        Moments bm = {s_sub[i], s_sub[i + 1], s_sub[i + 2]};
+        if (bm.n > 0.f) acc = merge_moments(acc, bm);
       }
-      const float mean = a.mean, rstd = rsqrtf(fmaxf(a.m2 / a.n, 0.f) + eps);
+      const float mean = acc.mean, rstd = rsqrtf(fmaxf(acc.m2 / acc.n, 0.f) + eps);
       s_st[g * 2 + 0] = mean;
       s_st[g * 2 + 1] = rstd;
       if (publish) {
@@ -283,15 +318,15 @@ __device__ __forceinline__ void merge_image_stats(const float* __restrict__ part
       for (int t = 0; t < conv_parts; ++t) {
         const float sm = pp[2 * t], q = pp[2 * t + 1];
         const float mean = sm / cnt;
-        Moments b = {cnt, mean, fmaxf(q - sm * mean, 0.f)};
-        m = merge_moments(m, b);
+        Moments bm = {cnt, mean, fmaxf(q - sm * mean, 0.f)};
+        m = merge_moments(m, bm);
       }
     }
     for (int c = 0; c < (conv_parts > 0 ? 0 : nchunks); ++c) {
       const int q0 = c * rows, q1 = min(P, q0 + rows);
       const float* pp = part + (((long)n * nchunks + c) * G + g) * 2;
-      Moments b = {(float)((q1 - q0) * Cg), pp[0], pp[1]};
-      m = merge_moments(m, b);
+      Moments bm = {(float)((q1 - q0) * Cg), pp[0], pp[1]};
+      m = merge_moments(m, bm);
     }
     const float mean = m.mean, rstd = rsqrtf(fmaxf(m.m2 / m.n, 0.f) + eps);
     s_st[g * 2 + 0] = mean;
@@ -300,6 +335,62 @@ __device__ __forceinline__ void merge_image_stats(const float* __restrict__ part
       stats_out[(n * G + g) * 2 + 0] = mean;
       stats_out[(n * G + g) * 2 + 1] = rstd;
     }
+  }
+  __syncthreads();
+}
+
+// Sum the backward's per-chunk group partials of image n (grp_part
+// [N][nchunks][G] x 2) with every thread of the block (batched loads, fixed
+// merge order): out[g] = (sum a, sum b).
+__device__ __forceinline__ void sum_group_parts(const float* __restrict__ grp_part, int n, int nchunks, int G,
+                                                float* s_out) {
+  constexpr int B = 8;
+  if (G <= NT) {
+    __shared__ float s_sub[2 * NT];
+    const int subs = NT / G;
+    const int g = threadIdx.x % G, sub = threadIdx.x / G;
+    float a = 0.f, b = 0.f;
+    if (sub < subs) {
+      for (int c0 = sub; c0 < nchunks; c0 += B * subs) {
+        float u[B], v[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+          const int c = c0 + k * subs;
+          const float* pp = grp_part + (((long)n * nchunks + c) * G + g) * 2;
+          u[k] = c < nchunks ? pp[0] : 0.f;
+          v[k] = c < nchunks ? pp[1] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+          a += u[k];
+          b += v[k];
+        }
+      }
+    }
+    s_sub[threadIdx.x * 2 + 0] = a;
+    s_sub[threadIdx.x * 2 + 1] = b;
+    __syncthreads();
+    if (threadIdx.x < G) {
+      float x = 0.f, y = 0.f;
+      for (int k = 0; k < subs; ++k) {
+        x += s_sub[(k * G + g) * 2];
+        y += s_sub[(k * G + g) * 2 + 1];
+      }
+      s_out[g * 2 + 0] = x;
+      s_out[g * 2 + 1] = y;
+    }
+    __syncthreads();
+    return;
+  }
+  for (int g = threadIdx.x; g < G; g += NT) {
+    float a = 0.f, b = 0.f;
+    for (int c = 0; c < nchunks; ++c) {
+      const float* pp = grp_part + (((long)n * nchunks + c) * G + g) * 2;
+      a += pp[0];
+      b += pp[1];
+    }
+    s_out[g * 2 + 0] = a;
+    s_out[g * 2 + 1] = b;
   }
   __syncthreads();
 }
@@ -603,17 +694,13 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
   const int chunk = blockIdx.x, n = blockIdx.y - trows;
   const int Cg = C / G;
   const float inv = 1.f / (float)((long)P * Cg);
+  __shared__ float s_ab[2 * 1024];
+  sum_group_parts(grp_part, n, nchunks, G, s_ab);
   for (int g = threadIdx.x; g < G; g += NT) {
-    float a = 0.f, b = 0.f;
-    for (int c = 0; c < nchunks; ++c) {
-      const float* pp = grp_part + (((long)n * nchunks + c) * G + g) * 2;
-      a += pp[0];
-      b += pp[1];
-    }
     s_c[g * 4 + 0] = stats[(n * G + g) * 2];
     s_c[g * 4 + 1] = stats[(n * G + g) * 2 + 1];
-    s_c[g * 4 + 2] = a * inv;
-    s_c[g * 4 + 3] = b * inv;
+    s_c[g * 4 + 2] = s_ab[g * 2] * inv;
+    s_c[g * 4 + 3] = s_ab[g * 2 + 1] * inv;
   }
   __syncthreads();
   if (MODE == 2 && seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
