@@ -26,9 +26,12 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 
 _ZERO_PAGE: Dict[int, torch.Tensor] = {}
-# FiLM weight gradients: "blas" (hipBLASLt product + segment scatter, default)
-# or "mfma" (split-K MFMA kernel with fused bias sums)
-_FILM_WGRAD_BLAS = os.environ.get("D3D_FILM_WGRAD", "blas") == "blas"
+# FiLM weight gradients: "blas" (hipBLASLt product + segment scatter), "mfma"
+# (split-K MFMA kernel with fused bias sums) or "auto": mfma up to 32 frames
+# per micro-batch (16 examples: the 8-GPU headline's per-GPU share, 33.7 ->
+# 33.2 ms/step), hipBLASLt above (bs128 on one GPU: 792 -> 804 examples/s);
+# profiles/ab_film_wgrad.txt
+_FILM_WGRAD = os.environ.get("D3D_FILM_WGRAD", "auto")
 
 
 def set_conv_impl(impl: str) -> None:
@@ -910,7 +913,7 @@ class _FiLMBatch(torch.autograd.Function):
                 row0 = (ctypes.c_int * n)(*offs[:n])
                 wd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tw])
                 bd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tb])
-                if _FILM_WGRAD_BLAS:
+                if _FILM_WGRAD == "blas" or (_FILM_WGRAD == "auto" and shp[0] > 32):
                     # wide FiLM weight gradients ([S, 1024] over every pixel of the
                     # level) run 1.4-1.6x faster on hipBLASLt (850-880 TF/s,
                     # profiles/kbench_lin_v2.jsonl) than on the split-K MFMA

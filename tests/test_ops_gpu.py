@@ -391,12 +391,12 @@ def test_film_batch_with_gn_film(H, chans, blas):
         loss.backward()
         return [s.grad] + [w.grad for w in ws] + [b.grad for b in bs]
 
-    prev = H._FILM_WGRAD_BLAS
-    H._FILM_WGRAD_BLAS = blas          # hipBLASLt product + scatter, or the split-K MFMA kernel
+    prev = H._FILM_WGRAD
+    H._FILM_WGRAD = "blas" if blas else "mfma"   # hipBLASLt product + scatter, or the split-K MFMA kernel
     try:
         gh, gr = run(True), run(False)
     finally:
-        H._FILM_WGRAD_BLAS = prev
+        H._FILM_WGRAD = prev
     for a, b in zip(gh, gr):
         assert rel(a, b) < 3e-2, rel(a, b)
 
