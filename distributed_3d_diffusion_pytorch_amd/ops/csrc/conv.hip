@@ -905,6 +905,216 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
   if (gnp) gn_part_store<TM, NH>(gs, gq, lane, m0 + wm * WM, n0 + wn * WN, OC, gn_groups, OHW, Mpix, gnp);
 }
 
+// ------------------------------------------------- halo (direct) 3x3 conv ----
+// Stride-1 3x3 conv (and its input gradient, TRANS) that stages each input
+// pixel in LDS ONCE per 32-channel chunk and feeds all nine taps from it.
+// The implicit-GEMM kernels above re-fetch the im2col row of every tap from
+// L2: at 128 output channels the 128 x 512 tile moves 80 KiB per 64-deep
+// k-step (~39 B/clk/CU at the MFMA rate, against ~56 B/clk of L2->CU
+// bandwidth), so the 64x64-level convs ran L2-bound at ~600 TF/s.  Here a
+// block owns TR full image rows x OW (= 512 pixels) x 128 output channels:
+//   * the (TR+2) x (OW+2) halo of a 32-channel chunk (64-byte pixel rows, 42
+//     KiB at OW=64) is LDS-DMA'd once and read by the nine taps by pure
+//     address shift -- the MFMA B fragment of tap (kh, kw) is the halo row
+//     (r+kh) * (OW+2) + c + kw -- so the input crosses L2 ~1.3x instead of 9x;
+//   * the weights of one (tap, chunk) step (128 x 32, 8 KiB, one 1-KiB DMA
+//     piece per wave) stream through a 4-deep LDS ring, the halo through two
+//     buffers filled one whole chunk (nine steps) ahead; total L2 traffic is
+//     ~12 B/clk/CU at the MFMA rate;
+//   * XOR swizzle of the 16-byte channel quarter by ((row >> 2) & 3) keeps
+//     every 16-row fragment read conflict-free for any tap shift;
+//   * one barrier per step; the counted vmcnt waits only for the step's own
+//     weights (issue order: weights then halo, so in-order completion lets the
+//     halo land up to four steps later).
+// Waves are 2 (channels) x 4 (pixels), 64 x 128 each (TM=4, TN=8), as in
+// conv_w8_k, and the epilogue (bias / per-image bias / residual / scale,
+// fused GroupNorm partials) is the same.
+constexpr int HALO_CH = 32;
+
+template <int OWT>
+struct HaloGeom {
+  static constexpr int TR = 512 / OWT;                        // image rows per tile
+  static constexpr int HW2 = OWT + 2;                          // halo row length
+  static constexpr int HP = (TR + 2) * HW2;                    // halo pixels
+  static constexpr int HPW = (HP + 127) / 128;                 // 1-KiB pieces per wave (16 pixels each)
+  static constexpr int HBUF = HPW * 8 * 16 * HALO_CH;          // bf16 elements per halo buffer
+  static constexpr int ABUF = 128 * HALO_CH;                   // bf16 elements per weight ring slot
+};
+
+__device__ __forceinline__ void halo_issue_a(bf16* sA, const bf16* Wp, int w_bytes, int aoff, int soff, int wave) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, w_bytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sA + wave * 16 * HALO_CH), 16, aoff, soff, 0, 0);
+}
+
+template <int HPW>
+__device__ __forceinline__ void halo_issue_b(bf16* sH, const bf16* I, int in_bytes, const unsigned* hoff, int cbyte,
+                                             int wave) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  const __amdgpu_buffer_rsrc_t rI = __builtin_amdgcn_make_buffer_rsrc((void*)I, (short)0, in_bytes, 0x00020000);
+#pragma unroll
+  for (int k = 0; k < HPW; ++k)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rI, (lds_void*)(sH + (wave + 8 * k) * 16 * HALO_CH), 16,
+                                             hoff[k] + (unsigned)cbyte, 0, 0, 0);
+}
+
+template <int OWT, bool TRANS>
+__global__ void __launch_bounds__(512, 1)
+conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
+            const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
+            int w_bytes, int Nimg, int OH, int IC, int ICp, int OC, float scale, int res_nmod,
+            float* __restrict__ gnp, int gn_groups) {
+  typedef HaloGeom<OWT> Gm;
+  constexpr int BM = 128, BN = 512, WM = 64, WN = 128, TM = 4, TN = 8;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * Gm::HBUF + 4 * Gm::ABUF];
+  bf16* const sH = smem;                       // [2][HBUF]
+  bf16* const sAr = smem + 2 * Gm::HBUF;       // [4][ABUF]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int OW = OWT, IH = OH, IW = OW;
+  const int tiles = Nimg * (OH / Gm::TR);
+  int bid = blockIdx.x;
+  {
+    // XCD-aware: consecutive row tiles (which share halo rows) on one XCD
+    int q = tiles / 8, r = tiles % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int img = bid / (OH / Gm::TR);
+  const int r0 = (bid - img * (OH / Gm::TR)) * Gm::TR;
+  const long n0 = ((long)img * OH + r0) * OW;    // first output pixel of the tile
+  const long Mpix = (long)Nimg * OH * OW;
+  const int m0 = blockIdx.y * BM;
+  const int Kp = 9 * ICp;
+
+  // weights: row = wave*16 + (lane>>2), source quarter = slot ^ ((row>>2)&3)
+  const int arow = wave * 16 + (lane >> 2);
+  const int aoff = ((m0 + arow) * Kp + (((lane & 3) ^ ((arow >> 2) & 3)) << 3)) * 2;
+  // halo pieces: flat halo pixel fi = (wave + 8k)*16 + (lane>>2)
+  unsigned hoff[Gm::HPW];
+#pragma unroll
+  for (int k = 0; k < Gm::HPW; ++k) {
+    const int fi = (wave + 8 * k) * 16 + (lane >> 2);
+    const int hr = fi / Gm::HW2, hc = fi - hr * Gm::HW2;
+    const int ih = r0 - 1 + hr, iw = hc - 1;
+    const bool ok = fi < Gm::HP && ih >= 0 && ih < IH && iw >= 0 && iw < IW;
+    const int q = (lane & 3) ^ ((fi >> 2) & 3);
+    const unsigned o = (unsigned)((((img * IH + (ok ? ih : 0)) * IW + (ok ? iw : 0)) * IC + q * 8) * 2);
+    hoff[k] = ok ? o : 0x80000000u;            // past every operand: the range check returns zeros
+  }
+
+  const int NCH = IC / HALO_CH, S = 9 * NCH;
+  auto a_soff = [&](int s) {
+    const int ss = s < S ? s : S - 1;          // tail re-loads keep the wait counts uniform
+    const int c = ss / 9, t = ss - c * 9;
+    return (t * ICp + c * HALO_CH) * 2;
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // halo row of each B fragment's pixel at tap (0, 0)
+  int hp0[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int p = wn * WN + j * 16 + fr;
+    hp0[j] = (p / OWT) * Gm::HW2 + (p % OWT);
+  }
+
+  halo_issue_b<Gm::HPW>(sH, I, in_bytes, hoff, 0, wave);
+  halo_issue_a(sAr, Wp, w_bytes, aoff, a_soff(0), wave);
+  halo_issue_a(sAr + Gm::ABUF, Wp, w_bytes, aoff, a_soff(1), wave);
+  halo_issue_a(sAr + 2 * Gm::ABUF, Wp, w_bytes, aoff, a_soff(2), wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  for (int c = 0; c < NCH; ++c) {
+    const bf16* hb = sH + (c & 1) * Gm::HBUF;
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t) {
+      const int s = c * 9 + t;
+      // this step's weights landed; newer loads may stay in flight
+      if (t >= 1 && t <= 3) {                     // (wave-uniform branch)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + Gm::HPW) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      halo_issue_a(sAr + ((s + 3) & 3) * Gm::ABUF, Wp, w_bytes, aoff, a_soff(s + 3), wave);
+      if (t == 0) {
+        const int cn = c + 1 < NCH ? c + 1 : NCH - 1;
+        halo_issue_b<Gm::HPW>(sH + ((c + 1) & 1) * Gm::HBUF, I, in_bytes, hoff, cn * HALO_CH * 2, wave);
+      }
+      const bf16* a = sAr + (s & 3) * Gm::ABUF;
+      const int kh = TRANS ? 2 - t / 3 : t / 3, kw = TRANS ? 2 - t % 3 : t % 3;
+      const int dsh = kh * Gm::HW2 + kw;
+      __builtin_amdgcn_s_setprio(1);
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int hp = hp0[j] + dsh;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(hb + hp * HALO_CH + ((fq ^ ((hp >> 2) & 3)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(a + row * HALO_CH + ((fq ^ ((row >> 2) & 3)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tail re-loads drained before exit
+
+  const int OHW = OH * OW;
+  constexpr int NH = WN / 64;
+  float gs[TM][NH], gq[TM][NH];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) gs[i][h] = gq[i][h] = 0.f;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const long pix = n0 + wn * WN + j * 16 + fr;
+    const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int co = m0 + wm * WM + i * 16 + fq * 4;
+      if (co >= OC) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float tv = acc[i][j][e] + (bias ? bias[co + e] : 0.f);
+        if (row_bias) tv += row_bias[(long)img * OC + co + e];
+        v[e] = tv;
+      }
+      if (res) {
+        bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * OC + co);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+      }
+      bf16x4 o4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o4[e] = (bf16)(v[e] * scale);
+        const float y = (float)o4[e];
+        gs[i][j / 4] += y;
+        gq[i][j / 4] += y * y;
+      }
+      *reinterpret_cast<bf16x4*>(O + pix * OC + co) = o4;
+    }
+  }
+  if (gnp) gn_part_store<TM, NH>(gs, gq, lane, m0 + wm * WM, n0 + wn * WN, OC, gn_groups, OHW, Mpix, gnp);
+}
+
 // split-K epilogue: O[pix][co] = (sum_s part[s][pix][co] + bias + row_bias
 // (+ residual)) * scale, 4 channels per thread (OC % 4 == 0).
 __global__ void conv_splitk_epi_k(const float* __restrict__ part, int nsplit, long Mpix, int OC, int OHW,
@@ -2142,6 +2352,9 @@ D3D_API int d3d_pack_all(const void* descs, const int* blk_desc, int total_block
 // I: [N, IH, IW, IC] bf16 (IC % 8 == 0), Wp: packed [OCp][taps][ICp] bf16 with
 // OCp % 128 == 0 and ICp % 64 == 0.  O: [N, OH, OW, ldo] bf16.  taps = 9 (3x3)
 // or 1 (1x1 / per-pixel linear).
+// 32-wide images on the halo kernel too (measured 2-7 % slower than conv_w8_k
+// there, profiles/kbench_conv_halo.jsonl; kept selectable for the sweep)
+static int g_halo32 = getenv("D3D_HALO32") ? atoi(getenv("D3D_HALO32")) : 0;
 static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline, 2: buffer-descriptor LDS-DMA
 static int g_conv_korder = 1;     // glds k-step order: 1 channel-chunk major, 0 tap major
 static int g_wgrad_impl = 5;      // 0: register-staged; 1-4: glds (PK,NS) = (64,2) (32,2) (32,3) (64,3); 5: bufl
@@ -2200,12 +2413,32 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
   if (nsplit < 1 || !ws || g_conv_impl < 1) nsplit = 1;
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM), (unsigned)nsplit);
   const long in_bytes = (long)N * IH * IW * IC * 2, w_bytes = (long)((OC + 127) / 128 * 128) * taps * ICp * 2;
+  if (g_conv_impl == 8 && taps == 9 && stride == 1 && IW == OW && IH == OH && ldo == OC && IC % HALO_CH == 0 &&
+      OC % 128 == 0 && (OW == 64 || OW == 128 || (OW == 32 && g_halo32)) && OH % (512 / OW) == 0 &&
+      in_bytes < (1L << 31) &&
+      w_bytes < (1L << 31) && (long)N * (OH / (512 / OW)) * (OC / 128) >= 256) {
+    dim3 gh((unsigned)(N * (OH / (512 / OW))), (unsigned)(OC / 128), 1);
+#define HALO(OWv, TR)                                                                                              \
+  hipLaunchKernelGGL((conv_halo_k<OWv, TR>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias, row_bias, \
+                     (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale, res_nmod,  \
+                     gnp, gn_groups)
+    if (OW == 32) {
+      if (trans) HALO(32, true); else HALO(32, false);
+    } else if (OW == 64) {
+      if (trans) HALO(64, true); else HALO(64, false);
+    } else {
+      if (trans) HALO(128, true); else HALO(128, false);
+    }
+#undef HALO
+    if (gn_done && gnp) *gn_done = 1;
+    return (int)hipGetLastError();
+  }
   if (g_conv_impl >= 4 && (!trans || stride == 1) && in_bytes < (1L << 31) && w_bytes < (1L << 31) && OC >= 64) {
     // large-tile 8-wave kernel when its grid still covers every CU
     const int bm = (OC % 256 == 0 || OC > 384) ? 256 : 128;
     // 128 / 384-channel layers only as 128x512 tiles on request (impl 6):
     // 128x256 tiles measured slower than two 128x128 blocks per CU (bufl1)
-    const bool wide = bm == 128 && g_conv_impl >= 6;
+    const bool wide = bm == 128 && g_conv_impl >= 6;         // w8w, w8n, halo
     int bn = wide ? 512 : 256;
     long ptiles = (Mpix + bn - 1) / bn;
     long blocks = ptiles * ((OC + bm - 1) / bm);

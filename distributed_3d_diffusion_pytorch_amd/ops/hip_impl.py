@@ -41,7 +41,7 @@ def set_conv_impl(impl: str) -> None:
     dev = torch.cuda.current_device()
     if dev not in _ZERO_PAGE:
         _ZERO_PAGE[dev] = torch.zeros(64, dtype=BF16, device="cuda")
-    _chk(_lib.d3d_set_conv_impl({"reg": 0, "glds": 1, "bufl": 2, "bufl1": 3, "w8": 4, "w8w": 6, "w8n": 7}[impl], _ZERO_PAGE[dev].data_ptr()), "set_conv_impl")
+    _chk(_lib.d3d_set_conv_impl({"reg": 0, "glds": 1, "bufl": 2, "bufl1": 3, "w8": 4, "w8w": 6, "w8n": 7, "halo": 8}[impl], _ZERO_PAGE[dev].data_ptr()), "set_conv_impl")
 
 
 def set_conv_korder(korder: int) -> None:
@@ -65,7 +65,7 @@ _IMPL_SET = [False]
 def _ensure_impl():
     if not _IMPL_SET[0]:
         import os
-        set_conv_impl(os.environ.get("D3D_CONV_IMPL", "w8w"))
+        set_conv_impl(os.environ.get("D3D_CONV_IMPL", "halo"))
         set_wgrad_impl(os.environ.get("D3D_WGRAD_IMPL", "w8"))
         _IMPL_SET[0] = True
 

@@ -155,17 +155,20 @@ W8_SHAPES = [
     (16, 64, 64, 64, 640, 1, True, False, 0.5),                   # OC 640: BM=256 tile overhangs the weights
     (32, 32, 32, 256, 256, 1, True, False, 1.0),                  # w8n: 256 x 128 tiles (128 of 256x256 < 256 CUs)
     (16, 32, 32, 512, 512, 1, False, True, 0.5),                  # w8n: 2 x 128 tiles of 256 x 128
+    (32, 64, 64, 384, 128, 1, True, True, 1 / math.sqrt(2)),      # halo: 8-row tiles, 12 channel chunks
+    (8, 128, 128, 128, 256, 1, False, False, 1.0),                # halo: 4-row tiles of 128-wide images
+    (64, 32, 32, 128, 256, 1, False, False, 1.0),                 # 32-wide: halo only with D3D_HALO32=1
 ]
 
 
-@pytest.mark.parametrize("impl", ["w8", "w8w", "w8n"])
+@pytest.mark.parametrize("impl", ["w8", "w8w", "w8n", "halo"])
 @pytest.mark.parametrize("N,Hh,W,Ci,Co,s,res,rb,scale", W8_SHAPES)
 def test_conv3x3_w8(H, impl, N, Hh, W, Ci, Co, s, res, rb, scale):
     H.set_conv_impl(impl)
     try:
         test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale)
     finally:
-        H.set_conv_impl(os.environ.get("D3D_CONV_IMPL", "w8w"))
+        H.set_conv_impl(os.environ.get("D3D_CONV_IMPL", "halo"))
 
 
 WGRAD_W8_SHAPES = [

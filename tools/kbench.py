@@ -77,7 +77,7 @@ def main():
         y = torch.empty(N, OH, OH, Co, dtype=BF, device=dev)
         g = torch.randn(N, OH, OH, Co, device=dev).to(BF)
         if "conv" in ops:
-            for impl in ("bufl1", "w8w", "w8n"):
+            for impl in ("w8w", "halo"):
                 H.set_conv_impl(impl)
                 rep("conv_fwd", shp, "hip-" + impl,
                     timeit(lambda: H._conv_fwd(x, wp, b, None, None, y, N, Hh, Hh, Ci, H._up(Ci, 64), OH, OH, Co, Co,
@@ -91,7 +91,7 @@ def main():
         if "dgrad" in ops and s == 1:
             wt = H.packed_weight(w, True, 9)
             dx = torch.empty_like(x)
-            for impl in ("bufl1", "w8w", "w8n"):
+            for impl in ("w8w", "halo"):
                 H.set_conv_impl(impl)
                 rep("conv_dgrad", shp, "hip-" + impl,
                     timeit(lambda: H._conv_fwd(g, wt, None, None, None, dx, N, OH, OH, Co, H._up(Co, 64), Hh, Hh, Ci,
