@@ -41,8 +41,8 @@ class GroupNorm(nn.Module):
         super().__init__()
         self.gn = nn.GroupNorm(num_groups=num_groups, num_channels=num_channels)
 
-    def forward(self, h: torch.Tensor, silu: bool = False) -> torch.Tensor:
-        return ops.group_norm(h, self.gn.weight, self.gn.bias, self.gn.num_groups, self.gn.eps, silu)
+    def forward(self, h: torch.Tensor, silu: bool = False, res_slot=None) -> torch.Tensor:
+        return ops.group_norm(h, self.gn.weight, self.gn.bias, self.gn.num_groups, self.gn.eps, silu, res_slot)
 
 
 class FiLM(nn.Module):
@@ -88,7 +88,7 @@ class ResnetBlock(nn.Module):
         self._seed_slot = 0
 
     def forward(self, x, semb: torch.Tensor) -> torch.Tensor:
-        skip = None
+        skip = slot = None
         if isinstance(x, tuple):
             # decoder: x is the skip concatenation [h | hs] (xunet.py:521-531),
             # never materialised -- GN0 and the 1x1 skip read both halves
@@ -100,7 +100,10 @@ class ResnetBlock(nn.Module):
         else:
             N, H, W, C = x.shape
             assert C == self.in_features, (C, self.in_features)
-            h = self.groupnorm0(x, silu=True)
+            # x's two consumers here (GN0 and the residual / NIN branch) hand
+            # their gradients over inside the GN0 backward kernel
+            slot = ops.res_slot(x) if torch.is_grad_enabled() and x.requires_grad else None
+            h = self.groupnorm0(x, silu=True, res_slot=slot)
         # the conv epilogues also emit the partial statistics of the GroupNorm
         # that reads their output (GN1 here; the next block's GN0 below)
         h = ops.conv3x3(h, self.conv1.weight, self.conv1.bias, gn_groups=self.groupnorm1.gn.num_groups)
@@ -110,10 +113,14 @@ class ResnetBlock(nn.Module):
         h = ops.gn_film(h, self.groupnorm1.gn.weight, self.groupnorm1.gn.bias, ss,
                         self.groupnorm1.gn.num_groups, self.groupnorm1.gn.eps,
                         self.dropout_p, self.training, _next_seed(self))
+        rslot = None
         if skip is None:
-            skip = ops.linear(x, self.dense.weight, self.dense.bias) if self.in_features != self.features else x
+            if self.in_features != self.features:
+                skip = ops.linear(x, self.dense.weight, self.dense.bias, in_slot=slot)
+            else:
+                skip, rslot = x, slot
         h = ops.conv3x3(h, self.conv2.weight, self.conv2.bias, residual=skip, out_scale=INV_SQRT2,
-                        gn_groups=self.groupnorm1.gn.num_groups if self.resample is None else 0)
+                        gn_groups=self.groupnorm1.gn.num_groups if self.resample is None else 0, res_slot=rslot)
         if self.resample == "down":
             h = ops.avgpool2(h)
         elif self.resample == "up":
@@ -157,10 +164,11 @@ class AttnBlock(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         N, H, W, C = x.shape
         assert C == self.in_channels
-        hn = self.groupnorm(x).reshape(N, H * W, C)
+        slot = ops.res_slot(x) if torch.is_grad_enabled() and x.requires_grad else None
+        hn = self.groupnorm(x, res_slot=slot).reshape(N, H * W, C)
         o = self.attn_layer(hn, cross=(self.attn_type == "cross"))
         y = ops.linear(o, self.linear.weight, self.linear.bias, residual=x.reshape(N, H * W, C),
-                       out_scale=INV_SQRT2)
+                       out_scale=INV_SQRT2, res_slot=slot)
         return y.reshape(N, H, W, C)
 
 

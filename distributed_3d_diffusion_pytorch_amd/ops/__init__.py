@@ -24,9 +24,9 @@ def _h():
     return _hip
 
 
-def group_norm(x, weight, bias, groups: int = 32, eps: float = 1e-5, silu: bool = False):
+def group_norm(x, weight, bias, groups: int = 32, eps: float = 1e-5, silu: bool = False, res_slot=None):
     if use_hip(x):
-        return _h().group_norm(x, weight, bias, groups, eps, silu)
+        return _h().group_norm(x, weight, bias, groups, eps, silu, res_slot)
     return _t.group_norm(x, weight, bias, groups, eps, silu)
 
 
@@ -39,17 +39,20 @@ def gn_film(x, weight, bias, ss, groups: int = 32, eps: float = 1e-5, dropout_p:
 
 def conv3x3(x, weight, bias, stride: int = 1, residual: Optional[torch.Tensor] = None,
             out_scale: float = 1.0, row_bias: Optional[torch.Tensor] = None, res_period: int = 0,
-            gn_groups: int = 0):
+            gn_groups: int = 0, res_slot=None):
     """gn_groups: the output feeds a GroupNorm with that many groups (the HIP
-    path then fuses that GroupNorm's statistics into the conv epilogue)."""
+    path then fuses that GroupNorm's statistics into the conv epilogue).
+    res_slot / in_slot (HIP path; :class:`ResGradSlot`): hand the residual's /
+    the input's gradient to the GroupNorm that reads the same tensor."""
     if use_hip(x):
-        return _h().conv3x3(x, weight, bias, stride, residual, out_scale, row_bias, res_period, gn_groups)
+        return _h().conv3x3(x, weight, bias, stride, residual, out_scale, row_bias, res_period, gn_groups, res_slot)
     return _t.conv3x3(x, weight, bias, stride, residual, out_scale, row_bias, res_period)
 
 
-def linear(x, weight, bias, residual: Optional[torch.Tensor] = None, out_scale: float = 1.0):
+def linear(x, weight, bias, residual: Optional[torch.Tensor] = None, out_scale: float = 1.0, res_slot=None,
+           in_slot=None):
     if use_hip(x):
-        return _h().linear(x, weight, bias, residual, out_scale)
+        return _h().linear(x, weight, bias, residual, out_scale, res_slot, in_slot)
     return _t.linear(x, weight, bias, residual, out_scale)
 
 
@@ -123,3 +126,10 @@ __all__ = ["group_norm", "gn_film", "conv3x3", "linear", "film_batch", "cat_gn_s
            "ray_origin_pe", "attention", "avgpool2", "upsample2",
            "silu", "ray_posenc", "posenc_ddpm", "camera_rays", "posenc_nerf", "set_backend",
            "use_hip", "load_library", "library_error", "lib_path"]
+
+
+def res_slot(x: torch.Tensor):
+    """A residual-gradient hand-off slot for x (HIP path), else None."""
+    if use_hip(x):
+        return _h().ResGradSlot()
+    return None

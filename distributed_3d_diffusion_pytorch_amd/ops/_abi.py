@@ -23,7 +23,7 @@ SIGNATURES = {
     "d3d_border_fix": [P, P, I, I, I, I, I, I, I, P],
     "d3d_border_sums": [P, P, I, I, I, I, P],
     "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, I, P],
-    "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P],
+    "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P, F, P],
     # elementwise.hip
     "d3d_silu": [P, P, L, P],
     "d3d_dsilu": [P, P, P, L, P],
@@ -57,6 +57,7 @@ SIGNATURES = {
     "d3d_conv_wgrad_seg": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "d3d_wgrad_scatter": [P, I, I, I, I, P, I, I, P, P, P, P],
     "d3d_conv_wgrad2": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    "d3d_conv_wgrad3": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, P],
     # rays.hip
     "d3d_ray_posenc": [P, P, P, P, P, P, P, P, I, I, I, P],
     # attention.hip

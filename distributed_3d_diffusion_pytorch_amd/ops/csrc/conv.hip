@@ -2008,7 +2008,8 @@ conv_wgrad_w8_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* 
 // nblk_w sum the bias partials (brows rows) into db.
 __global__ void __launch_bounds__(256) wgrad_reduce9_k(const float* __restrict__ ws, int OC, int IC, int splits,
                                                        int accumulate, const float* __restrict__ bws, int brows,
-                                                       float* __restrict__ dW, float* __restrict__ db, int nblk_w) {
+                                                       float* __restrict__ dW, float* __restrict__ db, int nblk_w,
+                                                       float scale) {
   __shared__ float tile[64 * 9];
   const int tid = threadIdx.x;
   if ((int)blockIdx.x >= nblk_w) {
@@ -2016,6 +2017,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce9_k(const float* __restrict__
     if (c < OC && db) {
       float s = 0.f;
       for (int k = 0; k < brows; ++k) s += bws[(long)k * OC + c];
+      s *= scale;
       db[c] = accumulate ? db[c] + s : s;
     }
     return;
@@ -2039,7 +2041,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce9_k(const float* __restrict__
         a3 += src[(long)(s + 3) * total];
       }
       for (; s < splits; ++s) a0 += src[(long)s * total];
-      sum = (a0 + a1) + (a2 + a3);
+      sum = ((a0 + a1) + (a2 + a3)) * scale;
     }
     tile[ci * 9 + tap] = sum;
   }
@@ -2146,7 +2148,7 @@ template <int SL>
 __global__ void __launch_bounds__(256) wgrad_reduce2_k(const float* __restrict__ ws, int OC, int IC, int taps,
                                                        int splits, int accumulate, const float* __restrict__ bws,
                                                        int brows, float* __restrict__ dW, float* __restrict__ db,
-                                                       WSegs sg, int nblk_w) {
+                                                       WSegs sg, int nblk_w, float scale) {
   // 256 threads = COLS float4 columns x SL split lanes (SL = the split count
   // rounded up to a power of two, <= 16: few splits -> wide blocks)
   constexpr int COLS = 256 / SL;
@@ -2172,6 +2174,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce2_k(const float* __restrict__
     f32x4 t = red[0][col];
 #pragma unroll
     for (int k = 1; k < SL; ++k) t += red[k][col];
+    t *= scale;                                   // d(scale * dY) = scale * d(dY): no scaled dY copy
     for (int e = 0; e < 4; ++e) {
       const long o = base + e;
       if (o >= total) break;
@@ -2567,12 +2570,13 @@ D3D_API int d3d_conv3x3(const void* I, const void* Wp, const float* bias, const 
 // launches wgrad_reduce2_k<SL> with SL = splits rounded up to a power of two
 // (<= 16); bias rows (brows = 2 * splits) use the same lanes
 static void launch_reduce2(const float* ws, int OC, int IC, int taps, int splits, int accumulate, const float* bws,
-                           int brows, float* dW, float* db, WSegs sg, bool want_bias, hipStream_t st) {
+                           int brows, float* dW, float* db, WSegs sg, bool want_bias, hipStream_t st,
+                           float scale = 1.f) {
   if (taps == 9 && sg.n == 0) {
     const int nblk_w = OC * ((IC + 63) / 64);
     const int nblk_b = want_bias ? (OC + 255) / 256 : 0;
     hipLaunchKernelGGL(wgrad_reduce9_k, dim3(nblk_w + nblk_b), dim3(256), 0, st, ws, OC, IC, splits, accumulate, bws,
-                       brows, dW, db, nblk_w);
+                       brows, dW, db, nblk_w, scale);
     return;
   }
   int SL = 1;
@@ -2583,7 +2587,7 @@ static void launch_reduce2(const float* ws, int OC, int IC, int taps, int splits
   const int nblk_b = want_bias ? (OC + per - 1) / per : 0;
   dim3 grid(nblk_w + nblk_b);
 #define RL(S) hipLaunchKernelGGL(wgrad_reduce2_k<S>, grid, dim3(256), 0, st, ws, OC, IC, taps, splits, accumulate, \
-                                 bws, brows, dW, db, sg, nblk_w)
+                                 bws, brows, dW, db, sg, nblk_w, scale)
   switch (SL) {
     case 1: RL(1); break;
     case 2: RL(2); break;
@@ -2729,9 +2733,9 @@ D3D_API int d3d_conv_wgrad_plan(int N, int OH, int OW, int OC, int IC, int* spli
 // dW (and db when non-null) are written (accumulate=0) or added to
 // (accumulate=1) -- the latter lets kernels deposit straight into the flat
 // gradient buffer across micro-batches.
-D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW, float* db, int N, int IH, int IW,
+D3D_API int d3d_conv_wgrad3(const void* dY, const void* I, float* ws, float* dW, float* db, int N, int IH, int IW,
                             int IC, int OH, int OW, int OC, int stride, int splits, int pix_per_split, int accumulate,
-                            int taps, hipStream_t st) {
+                            int taps, float scale, hipStream_t st) {
   constexpr int BM = 128, BN = 128;
   long total = (long)OC * IC * taps;
   float* bws = db ? ws + (long)splits * total : nullptr;
@@ -2755,9 +2759,19 @@ D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW,
   }
   {
     WSegs none{};
-    launch_reduce2(ws, OC, IC, taps, splits, accumulate, bws, splits * (256 / BM), dW, db, none, db != nullptr, st);
+    launch_reduce2(ws, OC, IC, taps, splits, accumulate, bws, splits * (256 / BM), dW, db, none, db != nullptr, st,
+                   scale);
   }
   return (int)hipGetLastError();
+}
+
+// dW (+ db) of the conv whose output gradient is scale * dY (scale folded
+// into the split reduction)
+D3D_API int d3d_conv_wgrad2(const void* dY, const void* I, float* ws, float* dW, float* db, int N, int IH, int IW,
+                            int IC, int OH, int OW, int OC, int stride, int splits, int pix_per_split, int accumulate,
+                            int taps, hipStream_t st) {
+  return d3d_conv_wgrad3(dY, I, ws, dW, db, N, IH, IW, IC, OH, OW, OC, stride, splits, pix_per_split, accumulate,
+                         taps, 1.f, st);
 }
 
 // Per-pixel dense weight gradient over a virtual channel concat [I | I2]

@@ -682,7 +682,8 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
                                                       const uint64_t* __restrict__ seed_dev, Cat cat,
                                                       const float* __restrict__ chan_part,
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                      int accumulate, int trows) {
+                                                      int accumulate, int trows, const bf16* __restrict__ dres,
+                                                      float dres_scale) {
   if ((int)blockIdx.y < trows) {        // leading grid rows: dgamma / dbeta, 4 rows (waves) per block
     const int blk = blockIdx.y * nchunks + blockIdx.x;
     dgb_rowsum(chan_part, (long)(gridDim.y - trows) * nchunks, 2 * C, blk * (NT / 64) + (threadIdx.x >> 6), dgamma,
@@ -733,7 +734,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
   const long pix0 = (long)n * P;
   const int r1 = min(P, chunk * rows + rows);
   for (int r = chunk * rows + roff; r < r1; r += U * rpi) {
-    f32x8 xv[U], dv[U], sc[U];
+    f32x8 xv[U], dv[U], sc[U], rv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int rr = r + u * rpi;
@@ -742,6 +743,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
         xv[u] = ld8(src.p + pix * src.ld);
         dv[u] = ld8(dy + pix * C + c0);
         if (MODE == 2) sc[u] = ld8(ss + pix * ssld + c0);
+        if (dres) rv[u] = ld8(dres + pix * C + c0);
       }
     }
 #pragma unroll
@@ -761,6 +763,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
         const float dxh = dA * gm[j];
         o[j] = rstd[j] * (dxh - c1[j] - xhat * c2[j]);
       }
+      if (dres) o += rv[u] * dres_scale;    // the residual branch's gradient of the same input
       st8(dst + pix * dld, o);
     }
   }
@@ -850,10 +853,11 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
                         const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
                         unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
                         float* grp_part, float* coef, int accumulate, int ssld, const void* seed_dev,
-                        const void* x2, void* dx2, int C1, hipStream_t st) {
+                        const void* x2, void* dx2, int C1, const void* dres, float dres_scale, hipStream_t st) {
   Plan p = make_plan(N, P, C);
   Cat cat{(const bf16*)x2, (bf16*)dx2, C1};
   if (ssld == 0) ssld = 2 * C;
+  if (x2) dres = nullptr;                  // (the caller never combines the two)
   size_t lds = (size_t)p.rpi * C * 4 * sizeof(float);
   dim3 g(p.nchunks, N);
 #define RED(M)                                                                                                    \
@@ -873,7 +877,7 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
   hipLaunchKernelGGL(gn_bwd_apply2_k<M>, dim3(p.nchunks, N + trows), dim3(NT), 0, st, (const bf16*)x,             \
                      (const bf16*)dy, (const bf16*)ss, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows,    \
                      p.nchunks, p_drop, (uint64_t)seed, ssld, (const uint64_t*)seed_dev, cat, chan_part, dgamma,    \
-                     dbeta, accumulate, trows)
+                     dbeta, accumulate, trows, (const bf16*)dres, dres_scale)
   if (mode == 0) APP(0);
   else if (mode == 1) APP(1);
   else APP(2);
@@ -886,5 +890,5 @@ D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, 
                        unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
                        float* grp_part, float* coef, hipStream_t st) {
   return d3d_gn_bwd2(mode, x, dy, ss, stats, gamma, beta, N, P, C, G, p_drop, seed, dx, dss, dgamma, dbeta,
-                     chan_part, grp_part, coef, 0, 0, nullptr, nullptr, nullptr, 0, st);
+                     chan_part, grp_part, coef, 0, 0, nullptr, nullptr, nullptr, 0, nullptr, 1.f, st);
 }

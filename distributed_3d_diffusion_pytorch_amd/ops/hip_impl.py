@@ -273,7 +273,41 @@ def _gn_fwd(mode, x, w, b, G, eps, ss=None, ssld=0, p=0.0, seed=0, x2=None):
     return y, stats
 
 
-def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None):
+class ResGradSlot:
+    """Hand-off of the gradient of a tensor x between its two consumers in a
+    block: a GroupNorm (GN0 / the attention GN) and the block's residual
+    branch (the conv2 / out-projection residual, or the 1x1 NIN skip's input).
+    The residual branch's backward -- which autograd runs before the
+    GroupNorm's, since the GroupNorm output feeds it -- deposits its gradient
+    here instead of returning it, and the GroupNorm backward adds it inside
+    its apply kernel: no bf16 autograd add over x's gradient.  If the
+    GroupNorm backward ran first after all, the branch returns its gradient
+    normally (``consumed``), so any order stays correct.  The deposit is
+    ``scale * g`` kept unscaled (the kernel applies the scale), so the
+    branch's own backward never materialises its scaled output gradient."""
+    __slots__ = ("g", "scale", "consumed")
+
+    def __init__(self):
+        self.g = None
+        self.scale = 1.0
+        self.consumed = False
+
+    def deposit(self, g: torch.Tensor, scale: float = 1.0) -> bool:
+        if self.consumed:
+            return False
+        if self.g is None:
+            self.g, self.scale = g, float(scale)
+        else:
+            self.g, self.scale = (self.g.float() * self.scale + g.float() * scale).to(g.dtype), 1.0
+        return True
+
+    def take(self):
+        g, sc = self.g, self.scale
+        self.g, self.scale, self.consumed = None, 1.0, True
+        return g, sc
+
+
+def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None, dres=None, dres_scale=1.0):
     N, H, W, C1 = x.shape
     C = C1 + (x2.shape[-1] if x2 is not None else 0)
     P = H * W
@@ -293,7 +327,9 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None)
     _chk(_lib.d3d_gn_bwd2(mode, x.data_ptr(), dy.data_ptr(), _ptr(ss), stats.data_ptr(), w.data_ptr(),
                           b.data_ptr(), N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), dg.data_ptr(),
                           db.data_ptr(), cp.data_ptr(), gp.data_ptr(), coef.data_ptr(), int(direct), int(ssld),
-                          _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), _ptr(dx2), C1, _st()), "gn_bwd")
+                          _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), _ptr(dx2), C1, _ptr(dres),
+                          float(dres_scale), _st()),
+         "gn_bwd")
     if x2 is not None:
         dx = (dx, dx2)
     if direct:
@@ -305,12 +341,13 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None)
 
 class _GroupNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, groups, eps, silu):
+    def forward(ctx, x, weight, bias, groups, eps, silu, slot=None):
         x = x.contiguous()
         N, H, W, C = x.shape
         y, stats = _gn_fwd(1 if silu else 0, x, weight, bias, groups, eps)
         ctx.save_for_backward(x, weight, bias, stats)
         ctx.cfg = (groups, 1 if silu else 0)
+        ctx.slot = slot
         SINK.use(weight, ctx.needs_input_grad[1])
         SINK.use(bias, ctx.needs_input_grad[2])
         return y
@@ -319,8 +356,11 @@ class _GroupNorm(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, b, stats = ctx.saved_tensors
         G, mode = ctx.cfg
-        dx, _, dg, db = _gn_bwd(mode, x, dy.contiguous(), None, stats, w, b, G, 0.0, 0)
-        return dx, dg, db, None, None, None
+        dres, rsc = ctx.slot.take() if ctx.slot is not None else (None, 1.0)
+        if dres is not None:
+            dres = dres.reshape(x.shape).contiguous()
+        dx, _, dg, db = _gn_bwd(mode, x, dy.contiguous(), None, stats, w, b, G, 0.0, 0, dres=dres, dres_scale=rsc)
+        return dx, dg, db, None, None, None, None
 
 
 import os as _os
@@ -416,9 +456,9 @@ def cat_gn_silu_dense(a, b, gw, gb, dw, db, groups=32, eps=1e-5):
     return _CatGNDense.apply(a, b, gw, gb, dw, db, groups, eps)
 
 
-def group_norm(x, weight, bias, groups=32, eps=1e-5, silu=False):
+def group_norm(x, weight, bias, groups=32, eps=1e-5, silu=False, res_slot=None):
     _need_bf16(x)
-    return _GroupNorm.apply(x, weight, bias, groups, eps, silu)
+    return _GroupNorm.apply(x, weight, bias, groups, eps, silu, res_slot)
 
 
 def _ss_layout(ss: torch.Tensor, C: int):
@@ -486,7 +526,8 @@ def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo
     return (gnp, OH * OW // 64) if done.value else None
 
 
-def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9, want_bias=False, dW=None, db=None, accumulate=False):
+def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9, want_bias=False, dW=None, db=None, accumulate=False,
+           scale=1.0):
     """Split-K weight gradient (+ fused bias column sums).  Writes into the
     given dW/db (accumulating when asked) or into fresh fp32 tensors."""
     _ensure_impl()
@@ -498,8 +539,9 @@ def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9, want_bias=False, dW=No
         dW = torch.empty(OC, IC, taps, dtype=F32, device=x.device)
     if want_bias and db is None:
         db = torch.empty(OC, dtype=F32, device=x.device)
-    _chk(_lib.d3d_conv_wgrad2(g.data_ptr(), x.data_ptr(), ws.data_ptr(), dW.data_ptr(), _ptr(db), N, H, W, IC, OH,
-                              OW, OC, stride, s.value, pps.value, int(accumulate), taps, _st()), "conv_wgrad")
+    _chk(_lib.d3d_conv_wgrad3(g.data_ptr(), x.data_ptr(), ws.data_ptr(), dW.data_ptr(), _ptr(db), N, H, W, IC, OH,
+                              OW, OC, stride, s.value, pps.value, int(accumulate), taps, float(scale), _st()),
+         "conv_wgrad")
     return dW, db
 
 
@@ -521,7 +563,7 @@ class _Conv(torch.autograd.Function):
     via the split-K transpose-read kernel, bias grads via channel sums."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias, res_period, taps, gn=None):
+    def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias, res_period, taps, gn=None, res_slot=None):
         x = x.contiguous()
         N, H, W, IC = x.shape
         OC = weight.shape[0]
@@ -542,6 +584,7 @@ class _Conv(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.cfg = (stride, out_scale, residual is not None, row_bias is not None, bias is not None, res_period, taps)
         ctx.bias_param = bias
+        ctx.res_slot = res_slot
         SINK.use(weight, ctx.needs_input_grad[1])
         SINK.use(bias, ctx.needs_input_grad[2])
         return out
@@ -554,19 +597,27 @@ class _Conv(torch.autograd.Function):
         OC = weight.shape[0]
         dy = dy.contiguous()
         _, OH, OW, _ = dy.shape
-        if scale != 1.0:
+        bias = ctx.bias_param
+        need_w, need_b = ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]
+        # out = scale * (conv + residual): the gradient of both is scale * dy.
+        # Fold the scale into the kernels (dgrad epilogue, wgrad reduction,
+        # the GroupNorm that takes the residual's share) instead of writing a
+        # scaled copy of dy, whenever every consumer can take it that way.
+        slot = ctx.res_slot
+        lazy = scale != 1.0 and not has_rb and not res_period and (need_w or not need_b) and \
+            (not has_res or not ctx.needs_input_grad[4] or (slot is not None and not slot.consumed))
+        if scale != 1.0 and not lazy:
             g = torch.empty_like(dy)
             _chk(_lib.d3d_add_scale(dy.data_ptr(), None, g.data_ptr(), float(scale), dy.numel(), _st()), "scale")
+            ks = 1.0
         else:
-            g = dy
+            g, ks = dy, scale
         dx = None
         if ctx.needs_input_grad[0]:
             wt = packed_weight(weight, True, taps)
             dx = torch.empty_like(x)
-            _conv_fwd(g, wt, None, None, None, dx, N, OH, OW, OC, _up(OC, 64), H, W, IC, IC, stride, True, 1.0, 0,
+            _conv_fwd(g, wt, None, None, None, dx, N, OH, OW, OC, _up(OC, 64), H, W, IC, IC, stride, True, ks, 0,
                       taps)
-        bias = ctx.bias_param
-        need_w, need_b = ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]
         dW = db = drb = None
         tw = SINK.target(weight) if need_w else None
         tb = SINK.target(bias) if need_b else None
@@ -586,12 +637,12 @@ class _Conv(torch.autograd.Function):
             if direct:
                 with SINK.producer(g.device, g, x):
                     _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, dW=tw.view(OC, IC, taps),
-                           db=tb if need_b else None, accumulate=True)
+                           db=tb if need_b else None, accumulate=True, scale=ks)
                 SINK.done(weight)
                 if need_b:
                     SINK.done(bias)
             else:
-                dW, db2 = _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, want_bias=need_b)
+                dW, db2 = _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, want_bias=need_b, scale=ks)
                 dW = dW.reshape(weight.shape)
                 if need_b:
                     db = db2
@@ -599,13 +650,17 @@ class _Conv(torch.autograd.Function):
             gg = g if taps == 9 else g.reshape(1, N * OH * OW, 1, OC)
             db = _chansum(gg, False)[1]
         dres = None
-        if has_res:
-            dres = g if not res_period else \
-                g.reshape(N // res_period, res_period, *g.shape[1:]).sum(0, dtype=F32).to(g.dtype)
-        return dx, dW, db, None, dres, None, drb, None, None, None
+        if has_res and ctx.needs_input_grad[4]:
+            if res_period:
+                dres = g.reshape(N // res_period, res_period, *g.shape[1:]).sum(0, dtype=F32).to(g.dtype)
+            elif slot is None or not slot.deposit(g, ks):
+                assert ks == 1.0            # (lazy only when the slot takes it)
+                dres = g
+        return dx, dW, db, None, dres, None, drb, None, None, None, None
 
 
-def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=None, res_period=0, gn_groups=0):
+def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=None, res_period=0, gn_groups=0,
+            res_slot=None):
     """3x3 conv.  gn_groups > 0: the output feeds a GroupNorm with that many
     groups -- the conv epilogue then also emits the GroupNorm's partial
     statistics when its kernel can (attached to the output as ``_d3d_gnpart``
@@ -614,7 +669,7 @@ def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=No
     OC, IC = weight.shape[0], weight.shape[1]
     if IC % 8 == 0 and OC % 8 == 0:
         gn = {"groups": int(gn_groups)} if gn_groups else None
-        y = _Conv.apply(x, weight, bias, stride, residual, out_scale, row_bias, res_period, 9, gn)
+        y = _Conv.apply(x, weight, bias, stride, residual, out_scale, row_bias, res_period, 9, gn, res_slot)
         if gn is not None and "part" in gn:
             y._d3d_gnpart = (gn["part"][0], int(gn_groups), gn["part"][1])
         return y
@@ -763,7 +818,7 @@ class _Linear(torch.autograd.Function):
     residual/scale epilogue done by a fused HIP elementwise kernel."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, out_scale):
+    def forward(ctx, x, weight, bias, residual, out_scale, res_slot=None, in_slot=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         wb = bf16_weight(weight)
@@ -778,6 +833,7 @@ class _Linear(torch.autograd.Function):
         ctx.save_for_backward(x2, weight)
         ctx.cfg = (shp, out_scale, residual is not None, bias is not None)
         ctx.bias_param = bias
+        ctx.slots = (res_slot, in_slot)
         if shp[-1] % 8 == 0 and wb.shape[0] % 8 == 0:
             SINK.use(weight, ctx.needs_input_grad[1])
             SINK.use(bias, ctx.needs_input_grad[2])
@@ -788,33 +844,51 @@ class _Linear(torch.autograd.Function):
         x2, weight = ctx.saved_tensors
         shp, scale, has_res, has_b = ctx.cfg
         g = dy.reshape(-1, dy.shape[-1])
-        if scale != 1.0:
+        wb = bf16_weight(weight)
+        OC, IC = g.shape[-1], x2.shape[-1]
+        rows = g.shape[0]
+        dW = db = None
+        bias = ctx.bias_param
+        need_w, need_b = ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]
+        res_slot, in_slot = ctx.slots
+        # gradient of out = scale * (x W^T + b + residual) is scale * dy: the
+        # scale rides on the GEMM alpha, the wgrad reduction and the residual
+        # hand-off instead of a scaled copy of dy (same rule as _Conv)
+        mma = IC % 8 == 0 and OC % 8 == 0
+        lazy = scale != 1.0 and mma and need_w and \
+            (not has_res or not ctx.needs_input_grad[3] or (res_slot is not None and not res_slot.consumed))
+        ks = 1.0
+        if scale != 1.0 and not lazy:
             gs = torch.empty_like(g)
             _chk(_lib.d3d_add_scale(g.contiguous().data_ptr(), None, gs.data_ptr(), float(scale), g.numel(), _st()),
                  "scale")
             g = gs
-        wb = bf16_weight(weight)
-        OC, IC = g.shape[-1], x2.shape[-1]
-        rows = g.shape[0]
-        dx = torch.mm(g, wb).reshape(shp) if ctx.needs_input_grad[0] else None
-        dW = db = None
-        bias = ctx.bias_param
-        need_w, need_b = ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]
-        if IC % 8 == 0 and OC % 8 == 0 and need_w:
+        elif lazy:
+            ks = scale
+        if ctx.needs_input_grad[0]:
+            if ks != 1.0:
+                dx = torch.empty(rows, IC, dtype=g.dtype, device=g.device).addmm_(g, wb, beta=0.0, alpha=ks)
+            else:
+                dx = torch.mm(g, wb)
+            dx = dx.reshape(shp)
+        else:
+            dx = None
+        if mma and need_w:
             g = g.contiguous()
             g4, x4 = g.reshape(rows, 1, 1, OC), x2.contiguous().reshape(rows, 1, 1, IC)
             tw = SINK.target(weight)
             tb = SINK.target(bias) if need_b else None
             if tw is not None and (not need_b or tb is not None):
                 with SINK.producer(g.device, g4, x4):
-                    _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, dW=tw.view(OC, IC, 1), db=tb, accumulate=True)
+                    _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, dW=tw.view(OC, IC, 1), db=tb, accumulate=True,
+                           scale=ks)
                 SINK.done(weight)
                 if need_b:
                     SINK.done(bias)
             else:
-                dW, db = _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, want_bias=need_b)
+                dW, db = _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, want_bias=need_b, scale=ks)
                 dW = dW.reshape(weight.shape)
-        elif IC % 8 == 0 and OC % 8 == 0:
+        elif mma:
             if need_b:
                 db = _chansum(g.contiguous().reshape(1, rows, 1, OC), False)[1]
         else:
@@ -822,8 +896,13 @@ class _Linear(torch.autograd.Function):
                 dW = _mm_f32(g.t(), x2).reshape(weight.shape)
             if has_b and ctx.needs_input_grad[2]:
                 db = g.float().sum(0)
-        dres = g.reshape(*shp[:-1], OC) if has_res else None
-        return dx, dW, db, dres, None
+        dres = None
+        if has_res and ctx.needs_input_grad[3] and (res_slot is None or not res_slot.deposit(g, ks)):
+            assert ks == 1.0
+            dres = g.reshape(*shp[:-1], OC)
+        if dx is not None and in_slot is not None and in_slot.deposit(dx):
+            dx = None
+        return dx, dW, db, dres, None, None, None
 
 
 class _FiLMSlot:
@@ -957,14 +1036,14 @@ def film_batch(semb, weights, biases):
     return outs
 
 
-def linear(x, weight, bias, residual=None, out_scale=1.0):
+def linear(x, weight, bias, residual=None, out_scale=1.0, res_slot=None, in_slot=None):
     """Per-pixel dense layer.  Forward and input-gradient are plain GEMMs on
     hipBLASLt (≈1 PF/s on these shapes); the weight gradient -- a GEMM whose
     reduction runs over every pixel of the batch (K up to 5e5), where
     hipBLASLt drops to 45-240 TF/s -- uses the split-K MFMA kernel, and the
     bias / residual epilogues are fused HIP kernels."""
     _need_bf16(x, residual)
-    return _Linear.apply(x, weight, bias, residual, out_scale)
+    return _Linear.apply(x, weight, bias, residual, out_scale, res_slot, in_slot)
 
 
 # ------------------------------------------------------------ attention ----

@@ -589,3 +589,39 @@ def test_training_step_bitwise_deterministic():
     for r in runs[1:]:
         assert runs[0][0] == r[0], runs
         assert torch.equal(runs[0][1], r[1]), (runs[0][1] - r[1]).abs().max().item()
+
+
+@pytest.mark.parametrize("kind", ["conv_res", "linear_res", "nin_input"])
+def test_residual_grad_slot(H, kind):
+    """ResGradSlot: the residual branch's gradient of x handed to the
+    GroupNorm backward kernel == autograd summing the two branches."""
+    torch.manual_seed(5)
+    C, Co = 128, (256 if kind == "nin_input" else 128)
+    x = torch.randn(4, 16, 16, C, device=DEV).to(BF).requires_grad_(True)
+    gam = torch.rand(C, device=DEV) + 0.5
+    bet = torch.randn(C, device=DEV) * 0.1
+    w = torch.randn(Co, C, 3, 3, device=DEV) / math.sqrt(9 * C)
+    wl = torch.randn(Co, C, device=DEV) / math.sqrt(C)
+    bl = torch.randn(Co, device=DEV) * 0.1
+    go = torch.randn(4, 16, 16, Co, device=DEV).to(BF)
+
+    def run(use):
+        x.grad = None
+        slot = H.ResGradSlot() if use else None
+        if kind == "conv_res":
+            h = H.group_norm(x, gam, bet, 32, 1e-5, True, slot)
+            y = H.conv3x3(h, w, None, residual=x, out_scale=1 / math.sqrt(2), res_slot=slot)
+        elif kind == "linear_res":
+            h = H.group_norm(x, gam, bet, 32, 1e-5, False, slot)
+            y = H.linear(h, wl, bl, residual=x, out_scale=1 / math.sqrt(2), res_slot=slot)
+        else:
+            h = H.group_norm(x, gam, bet, 32, 1e-5, True, slot)
+            s = H.linear(x, wl, bl, in_slot=slot)
+            y = H.conv3x3(h, w, None, residual=s, out_scale=1 / math.sqrt(2))
+        y.backward(go)
+        if use:
+            assert slot.consumed and slot.g is None
+        return x.grad.float().clone()
+
+    a, b = run(True), run(False)
+    assert rel(a, b) < 1e-2, rel(a, b)
