@@ -2006,11 +2006,19 @@ conv_wgrad_w8_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* 
 // reduce wrote OIHW 36 B apart (one read-modify-write per 4-B element): ~86
 // us for a 2-split 512x512 weight, now bandwidth-bound.  Blocks past
 // nblk_w sum the bias partials (brows rows) into db.
+template <int TG>
 __global__ void __launch_bounds__(256) wgrad_reduce9_k(const float* __restrict__ ws, int OC, int IC, int splits,
                                                        int accumulate, const float* __restrict__ bws, int brows,
                                                        float* __restrict__ dW, float* __restrict__ db, int nblk_w,
                                                        float scale) {
-  __shared__ float tile[64 * 9];
+  // block = (co, 64 input channels, TG taps); 256 threads = 64 channels x 4
+  // split lanes, each lane folding every 4th split of all TG taps at once
+  // (TG x 2 independent loads in flight), lanes merged in fixed order
+  // through LDS.  TG < 9 spreads the taps over more blocks when the grid
+  // would otherwise be small (many splits over few weights: the 64x64-level
+  // wgrad at 16 examples per GPU reduces 108 slabs).
+  __shared__ float red[4][TG][64];
+  __shared__ float tile[64 * TG];
   const int tid = threadIdx.x;
   if ((int)blockIdx.x >= nblk_w) {
     const int c = ((int)blockIdx.x - nblk_w) * 256 + tid;
@@ -2022,32 +2030,57 @@ __global__ void __launch_bounds__(256) wgrad_reduce9_k(const float* __restrict__
     }
     return;
   }
+  constexpr int NTG = 9 / TG;
   const int ncg = (IC + 63) / 64;
-  const int co = blockIdx.x / ncg, ci0 = (blockIdx.x % ncg) * 64;
+  const int co = blockIdx.x / (ncg * NTG);
+  const int rem = blockIdx.x % (ncg * NTG);
+  const int ci0 = (rem / NTG) * 64, tap0 = (rem % NTG) * TG;
   const int nci = min(64, IC - ci0);
   const long total = (long)OC * 9 * IC;
-  const long rowbase = (long)co * 9 * IC;
-  for (int k = tid; k < 9 * 64; k += 256) {
-    const int tap = k >> 6, ci = k & 63;
-    float sum = 0.f;
-    if (ci < nci) {
-      const float* src = ws + rowbase + (long)tap * IC + ci0 + ci;
-      int s = 0;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-      for (; s + 4 <= splits; s += 4) {           // independent loads in flight
-        a0 += src[(long)s * total];
-        a1 += src[(long)(s + 1) * total];
-        a2 += src[(long)(s + 2) * total];
-        a3 += src[(long)(s + 3) * total];
-      }
-      for (; s < splits; ++s) a0 += src[(long)s * total];
-      sum = ((a0 + a1) + (a2 + a3)) * scale;
+  const int ci = tid & 63, ln = tid >> 6;
+  constexpr int NC = TG == 1 ? 8 : (TG == 3 ? 4 : 2);     // independent chains per tap
+  float a[TG][NC];
+#pragma unroll
+  for (int t = 0; t < TG; ++t)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) a[t][c] = 0.f;
+  if (ci < nci) {
+    const float* src = ws + (long)co * 9 * IC + (long)tap0 * IC + ci0 + ci;
+    int sp = ln;
+    for (; sp + 4 * (NC - 1) < splits; sp += 4 * NC) {
+#pragma unroll
+      for (int t = 0; t < TG; ++t)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) a[t][c] += src[(long)(sp + 4 * c) * total + (long)t * IC];
     }
-    tile[ci * 9 + tap] = sum;
+    for (int c = 0; sp < splits; sp += 4, ++c) {
+#pragma unroll
+      for (int t = 0; t < TG; ++t) a[t][0] += src[(long)sp * total + (long)t * IC];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TG; ++t) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) v += a[t][c];
+    red[ln][t][ci] = v;
   }
   __syncthreads();
-  float* dst = dW + ((long)co * IC + ci0) * 9;
-  for (int m = tid; m < nci * 9; m += 256) dst[m] = accumulate ? dst[m] + tile[m] : tile[m];
+  for (int k = tid; k < TG * 64; k += 256) {
+    const int t = k >> 6, c = k & 63;
+    tile[c * TG + t] = (((red[0][t][c] + red[1][t][c]) + red[2][t][c]) + red[3][t][c]) * scale;
+  }
+  __syncthreads();
+  if (TG == 9) {                                 // 576 contiguous floats of OIHW
+    float* dst = dW + ((long)co * IC + ci0) * 9;
+    for (int m = tid; m < nci * 9; m += 256) dst[m] = accumulate ? dst[m] + tile[m] : tile[m];
+  } else {
+    for (int m = tid; m < nci * TG; m += 256) {
+      const int c = m / TG, t = m - c * TG;
+      float* d = dW + ((long)co * IC + ci0 + c) * 9 + tap0 + t;
+      *d = accumulate ? *d + tile[m] : tile[m];
+    }
+  }
 }
 
 // sum the split slabs and write dW in OIHW fp32 layout (optionally accumulate)
@@ -2573,10 +2606,15 @@ static void launch_reduce2(const float* ws, int OC, int IC, int taps, int splits
                            int brows, float* dW, float* db, WSegs sg, bool want_bias, hipStream_t st,
                            float scale = 1.f) {
   if (taps == 9 && sg.n == 0) {
-    const int nblk_w = OC * ((IC + 63) / 64);
+    // split the taps over more blocks while the grid is below ~1024 blocks
+    const long base = (long)OC * ((IC + 63) / 64);
+    const int tg = base >= 1024 ? 9 : (base * 3 >= 1024 ? 3 : 1);
+    const int nblk_w = (int)(base * (9 / tg));
     const int nblk_b = want_bias ? (OC + 255) / 256 : 0;
-    hipLaunchKernelGGL(wgrad_reduce9_k, dim3(nblk_w + nblk_b), dim3(256), 0, st, ws, OC, IC, splits, accumulate, bws,
-                       brows, dW, db, nblk_w, scale);
+#define R9(TGv) hipLaunchKernelGGL(wgrad_reduce9_k<TGv>, dim3(nblk_w + nblk_b), dim3(256), 0, st, ws, OC, IC, splits, \
+                                  accumulate, bws, brows, dW, db, nblk_w, scale)
+    if (tg == 9) R9(9); else if (tg == 3) R9(3); else R9(1);
+#undef R9
     return;
   }
   int SL = 1;
