@@ -931,9 +931,9 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
 // fused GroupNorm partials) is the same.
 constexpr int HALO_CH = 32;
 
-template <int OWT>
+template <int OWT, int BNT = 512>
 struct HaloGeom {
-  static constexpr int TR = 512 / OWT;                        // image rows per tile
+  static constexpr int TR = BNT / OWT;                        // image rows per tile
   static constexpr int HW2 = OWT + 2;                          // halo row length
   static constexpr int HP = (TR + 2) * HW2;                    // halo pixels
   static constexpr int HPW = (HP + 127) / 128;                 // 1-KiB pieces per wave (16 pixels each)
@@ -958,14 +958,14 @@ __device__ __forceinline__ void halo_issue_b(bf16* sH, const bf16* I, int in_byt
                                              hoff[k] + (unsigned)cbyte, 0, 0, 0);
 }
 
-template <int OWT, bool TRANS>
+template <int OWT, bool TRANS, int BNT = 512>
 __global__ void __launch_bounds__(512, 1)
 conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
             int w_bytes, int Nimg, int OH, int IC, int ICp, int OC, float scale, int res_nmod,
             float* __restrict__ gnp, int gn_groups) {
-  typedef HaloGeom<OWT> Gm;
-  constexpr int BM = 128, BN = 512, WM = 64, WN = 128, TM = 4, TN = 8;
+  typedef HaloGeom<OWT, BNT> Gm;
+  constexpr int BM = 128, BN = BNT, WM = 64, WN = BN / 4, TM = 4, TN = WN / 16;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * Gm::HBUF + 4 * Gm::ABUF];
   bf16* const sH = smem;                       // [2][HBUF]
   bf16* const sAr = smem + 2 * Gm::HBUF;       // [4][ABUF]
@@ -2391,6 +2391,10 @@ D3D_API int d3d_pack_all(const void* descs, const int* blk_desc, int total_block
 // 32-wide images on the halo kernel too (measured 2-7 % slower than conv_w8_k
 // there, profiles/kbench_conv_halo.jsonl; kept selectable for the sweep)
 static int g_halo32 = getenv("D3D_HALO32") ? atoi(getenv("D3D_HALO32")) : 0;
+// 256-pixel halo tiles for grids the 512-pixel ones cannot fill: measured
+// 10-15 % slower than the 4-wave 128x128 kernel on the 32x32 level at 16
+// examples per GPU (profiles/kbench_conv_halo256.jsonl); selectable only
+static int g_halo256 = getenv("D3D_HALO256") ? atoi(getenv("D3D_HALO256")) : 0;
 static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline, 2: buffer-descriptor LDS-DMA
 static int g_conv_korder = 1;     // glds k-step order: 1 channel-chunk major, 0 tap major
 static int g_wgrad_impl = 5;      // 0: register-staged; 1-4: glds (PK,NS) = (64,2) (32,2) (32,3) (64,3); 5: bufl
@@ -2450,24 +2454,41 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM), (unsigned)nsplit);
   const long in_bytes = (long)N * IH * IW * IC * 2, w_bytes = (long)((OC + 127) / 128 * 128) * taps * ICp * 2;
   if (g_conv_impl == 8 && taps == 9 && stride == 1 && IW == OW && IH == OH && ldo == OC && IC % HALO_CH == 0 &&
-      OC % 128 == 0 && (OW == 64 || OW == 128 || (OW == 32 && g_halo32)) && OH % (512 / OW) == 0 &&
-      in_bytes < (1L << 31) &&
-      w_bytes < (1L << 31) && (long)N * (OH / (512 / OW)) * (OC / 128) >= 256) {
-    dim3 gh((unsigned)(N * (OH / (512 / OW))), (unsigned)(OC / 128), 1);
-#define HALO(OWv, TR)                                                                                              \
-  hipLaunchKernelGGL((conv_halo_k<OWv, TR>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias, row_bias, \
-                     (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale, res_nmod,  \
-                     gnp, gn_groups)
-    if (OW == 32) {
-      if (trans) HALO(32, true); else HALO(32, false);
-    } else if (OW == 64) {
-      if (trans) HALO(64, true); else HALO(64, false);
-    } else {
-      if (trans) HALO(128, true); else HALO(128, false);
-    }
+      OC % 128 == 0 && (OW == 32 || OW == 64 || OW == 128) && in_bytes < (1L << 31) && w_bytes < (1L << 31)) {
+    // 512-pixel tiles where they fill the chip (64/128-wide images; 32-wide
+    // only on request: conv_w8_k is faster there at large batch), else
+    // 256-pixel tiles when those do (the 32x32 level at 16 examples per GPU)
+    auto nblk = [&](int bn) { return OH % (bn / OW) ? 0L : (long)N * (OH / (bn / OW)) * (OC / 128); };
+    int bn = 0;
+    if ((OW != 32 || g_halo32) && nblk(512) >= 256) bn = 512;
+    else if (g_halo256 && nblk(512) < 256 && nblk(256) >= 256) bn = 256;
+    if (bn) {
+      dim3 gh((unsigned)(N * (OH / (bn / OW))), (unsigned)(OC / 128), 1);
+#define HALO(OWv, TR, BNv)                                                                                         \
+  hipLaunchKernelGGL((conv_halo_k<OWv, TR, BNv>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias,     \
+                     row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale,  \
+                     res_nmod, gnp, gn_groups)
+      if (bn == 512) {
+        if (OW == 32) {
+          if (trans) HALO(32, true, 512); else HALO(32, false, 512);
+        } else if (OW == 64) {
+          if (trans) HALO(64, true, 512); else HALO(64, false, 512);
+        } else {
+          if (trans) HALO(128, true, 512); else HALO(128, false, 512);
+        }
+      } else {
+        if (OW == 32) {
+          if (trans) HALO(32, true, 256); else HALO(32, false, 256);
+        } else if (OW == 64) {
+          if (trans) HALO(64, true, 256); else HALO(64, false, 256);
+        } else {
+          if (trans) HALO(128, true, 256); else HALO(128, false, 256);
+        }
+      }
 #undef HALO
-    if (gn_done && gnp) *gn_done = 1;
-    return (int)hipGetLastError();
+      if (gn_done && gnp) *gn_done = 1;
+      return (int)hipGetLastError();
+    }
   }
   if (g_conv_impl >= 4 && (!trans || stride == 1) && in_bytes < (1L << 31) && w_bytes < (1L << 31) && OC >= 64) {
     // large-tile 8-wave kernel when its grid still covers every CU

@@ -171,6 +171,23 @@ def test_conv3x3_w8(H, impl, N, Hh, W, Ci, Co, s, res, rb, scale):
         H.set_conv_impl(os.environ.get("D3D_CONV_IMPL", "halo"))
 
 
+@pytest.mark.parametrize("N,Hh,Ci,Co", [(32, 32, 256, 256), (64, 32, 128, 256), (16, 64, 128, 128)])
+def test_conv3x3_halo_variants(N, Hh, Ci, Co):
+    """The opt-in halo tile variants (32-wide 512-pixel tiles, 256-pixel
+    tiles) against the torch composition, in a child process (the switches
+    are read once at library load)."""
+    import subprocess
+    import sys
+    code = ("import math, torch\n"
+            "from tests.test_ops_gpu import test_conv3x3\n"
+            "from distributed_3d_diffusion_pytorch_amd.ops import hip_impl as H\n"
+            f"H.set_conv_impl('halo'); test_conv3x3(H, {N}, {Hh}, {Hh}, {Ci}, {Co}, 1, True, False, 0.5)\n")
+    env = dict(os.environ, D3D_HALO32="1", D3D_HALO256="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 WGRAD_W8_SHAPES = [
     # 3x3 stride-1 weight gradients on the 8-wave kernel (impl "w8")
     (8, 32, 32, 256, 256, 1, False, False, 1.0),                  # 256 x 256 tiles
