@@ -12,12 +12,15 @@ Layout of one step (MI355X, one process per GPU):
       X-UNet forward -> backward; HIP weight-gradient kernels deposit into the
       flat fp32 gradient buffer (GradSink), the micro-batch loss is added to a
       device accumulator.  Inputs are copied into static buffers first.
-  [world > 1] eager RCCL all-reduce of the flat gradient (one collective: the
-      graph cannot contain the hook-driven bucketed launches, and a single
-      547 MB ring all-reduce over xGMI is ~3 ms against a ~40 ms step).
-  graph B: fused Adam reading its per-step hyper-parameters from a device
-      block (lr warmup / bias correction change every step) -> batched weight
-      repack -> gradient / loss-accumulator zeroing.
+  [world > 1] eager RCCL all-reduce of the flat gradient in D3D_AR_CHUNKS
+      (default 4) async collectives, each chunk's Adam launched as soon as
+      its collective lands, so the optimizer pass (~0.7 ms) hides behind the
+      remaining chunks' reduction (~3 ms for 547 MB over xGMI against a ~33
+      ms step), then the batched weight repack and the zeroing.  (The graph
+      cannot hold the hook-driven bucketed launches of the eager step.)
+  graph B (world == 1): fused Adam reading its per-step hyper-parameters
+      from a device block (lr warmup / bias correction change every step) ->
+      batched weight repack -> gradient / loss-accumulator zeroing.
 
 Per-step values that a replay cannot see from Python travel through device
 words refreshed before the replays: the dropout seed (``hip_impl._SEED_DEV``,
@@ -26,6 +29,7 @@ added to every mask kernel's baked seed) and the Adam block ``hp``.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -118,6 +122,24 @@ class GraphedTrainStep:
         return torch.tensor([b1, b2, eps, wd, lr / bc1, bc2_sqrt, grad_scale, 1.0 - o.ema_decay],
                             dtype=torch.float32)
 
+    def _reduce_update_chunked(self) -> None:
+        """fp32 all-reduce in chunks, each chunk's Adam behind its own
+        collective (overlaps the optimizer with the remaining reduction)."""
+        o = self.tr.optim
+        p, g, m, v, ema = o.flat.data, o.flat.grad, o.exp_avg, o.exp_avg_sq, o.ema
+        n = g.numel()
+        k = max(1, int(os.environ.get("D3D_AR_CHUNKS", "4")))
+        cuts = [0] + [min(n, (n * i // k + 255) // 256 * 256) for i in range(1, k)] + [n]
+        spans = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+        works = [dist.all_reduce(g[a:b], async_op=True) for a, b in spans]
+        for (a, b), w in zip(spans, works):
+            w.wait()
+            self.H.adam_flat_dev(p[a:b], g[a:b], m[a:b], v[a:b], ema[a:b] if ema is not None else None, self.hp,
+                                 refresh=False)
+        self.H.refresh_weights()
+        g.zero_()
+        self.loss_acc.zero_()
+
     def step(self, img, R, T, K) -> torch.Tensor:
         tr = self.tr
         if self.gA is None:
@@ -142,7 +164,11 @@ class GraphedTrainStep:
                 dist.all_reduce(gb)
                 g.copy_(gb)
             else:
-                dist.all_reduce(g)
+                self.hp.copy_(self._hparams(1.0 / tr.ctx.world))
+                self._reduce_update_chunked()
+                for cb in tr.optim.on_step:
+                    cb()
+                return loss
         self.hp.copy_(self._hparams(1.0 / tr.ctx.world))
         self.gB.replay()
         for cb in tr.optim.on_step:

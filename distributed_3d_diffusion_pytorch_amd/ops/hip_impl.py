@@ -1222,12 +1222,15 @@ def adam_flat(p, g, m, v, ema, lr, b1, b2, eps, wd, step_size, bc2_sqrt, grad_sc
     refresh_weights()
 
 
-def adam_flat_dev(p, g, m, v, ema, hp):
+def adam_flat_dev(p, g, m, v, ema, hp, refresh=True):
     """Adam with its per-step hyper-parameters read from the device block
-    ``hp`` (graph-replay form; see d3d_adam_dev)."""
+    ``hp`` (graph-replay form; see d3d_adam_dev).  Works on any contiguous
+    span of the flat buffers (refresh=False: the caller repacks the bf16
+    operand caches once after the last span)."""
     _chk(_lib.d3d_adam_dev(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(ema), p.numel(),
                            hp.data_ptr(), _st()), "adam_dev")
-    refresh_weights()
+    if refresh:
+        refresh_weights()
 
 
 # ------------------------------------------------------------- sampler ---
