@@ -1167,10 +1167,18 @@ __global__ void __launch_bounds__(256) conv_splitk_epi_gn_k(const float* __restr
   const long slab = Mpix * OC;
   const int Cg = OC / G;
   float sum = 0.f, sq = 0.f;
-  for (int k = 0; k < 64 / PPI; ++k) {
+  constexpr int KP = 64 / PPI;
+  f32x4 acc[KP];                                   // all pixels' slab loads in flight together
+#pragma unroll
+  for (int k = 0; k < KP; ++k) acc[k] = *reinterpret_cast<const f32x4*>(part + (pix0 + k * PPI + r) * OC + co);
+  for (int sp = 1; sp < nsplit; ++sp)
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+      acc[k] += *reinterpret_cast<const f32x4*>(part + sp * slab + (pix0 + k * PPI + r) * OC + co);
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
     const long pix = pix0 + k * PPI + r;
-    f32x4 a = *reinterpret_cast<const f32x4*>(part + pix * OC + co);
-    for (int sp = 1; sp < nsplit; ++sp) a += *reinterpret_cast<const f32x4*>(part + sp * slab + pix * OC + co);
+    f32x4 a = acc[k];
     const int img = (int)(pix / OHW);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
