@@ -2029,12 +2029,24 @@ __global__ void __launch_bounds__(256) wgrad_reduce9_k(const float* __restrict__
   __shared__ float tile[64 * TG];
   const int tid = threadIdx.x;
   if ((int)blockIdx.x >= nblk_w) {
-    const int c = ((int)blockIdx.x - nblk_w) * 256 + tid;
+    // bias: 64 channels x 4 row lanes x 8 independent accumulators (a single
+    // dependent chain over the ~200 partial rows cost ~60 us per launch)
+    const int c = ((int)blockIdx.x - nblk_w) * 64 + (tid & 63), ln = tid >> 6;
+    float a[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a[q] = 0.f;
     if (c < OC && db) {
-      float s = 0.f;
-      for (int k = 0; k < brows; ++k) s += bws[(long)k * OC + c];
-      s *= scale;
-      db[c] = accumulate ? db[c] + s : s;
+      int k = ln;
+      for (; k + 28 < brows; k += 32)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] += bws[(long)(k + 4 * q) * OC + c];
+      for (; k < brows; k += 4) a[0] += bws[(long)k * OC + c];
+    }
+    red[ln][0][tid & 63] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    __syncthreads();
+    if (ln == 0 && c < OC && db) {
+      const float sv = (((red[0][0][tid] + red[1][0][tid]) + red[2][0][tid]) + red[3][0][tid]) * scale;
+      db[c] = accumulate ? db[c] + sv : sv;
     }
     return;
   }
@@ -2203,7 +2215,14 @@ __global__ void __launch_bounds__(256) wgrad_reduce2_k(const float* __restrict__
   f32x4 a = {0.f, 0.f, 0.f, 0.f};
   if (base < total) {
     if (base + 3 < total) {
-      for (int k = sl; k < nrows; k += SL) a += *reinterpret_cast<const f32x4*>(src + (long)k * total + base);
+      f32x4 b2 = {0.f, 0.f, 0.f, 0.f};          // two chains: up to ~30 rows per lane for bias partials
+      int k = sl;
+      for (; k + SL < nrows; k += 2 * SL) {
+        a += *reinterpret_cast<const f32x4*>(src + (long)k * total + base);
+        b2 += *reinterpret_cast<const f32x4*>(src + (long)(k + SL) * total + base);
+      }
+      if (k < nrows) a += *reinterpret_cast<const f32x4*>(src + (long)k * total + base);
+      a += b2;
     } else {
       for (int k = sl; k < nrows; k += SL)
         for (int e = 0; e < 4 && base + e < total; ++e) a[e] += src[(long)k * total + base + e];
@@ -2639,7 +2658,7 @@ static void launch_reduce2(const float* ws, int OC, int IC, int taps, int splits
     const long base = (long)OC * ((IC + 63) / 64);
     const int tg = base >= 1024 ? 9 : (base * 3 >= 1024 ? 3 : 1);
     const int nblk_w = (int)(base * (9 / tg));
-    const int nblk_b = want_bias ? (OC + 255) / 256 : 0;
+    const int nblk_b = want_bias ? (OC + 63) / 64 : 0;
 #define R9(TGv) hipLaunchKernelGGL(wgrad_reduce9_k<TGv>, dim3(nblk_w + nblk_b), dim3(256), 0, st, ws, OC, IC, splits, \
                                   accumulate, bws, brows, dW, db, nblk_w, scale)
     if (tg == 9) R9(9); else if (tg == 3) R9(3); else R9(1);
