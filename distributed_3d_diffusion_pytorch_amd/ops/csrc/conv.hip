@@ -2275,7 +2275,17 @@ __global__ void chansum_k(const bf16* __restrict__ dy, float* __restrict__ part,
   if (cv < CV) {
     int rows = (P + nchunks - 1) / nchunks;
     int r0 = chunk * rows, r1 = min(P, r0 + rows);
-    for (int r = r0 + rl; r < r1; r += 8) s += ld8(dy + ((long)img * P + r) * C + cv * 8);
+    const bf16* src = dy + (long)img * P * C + cv * 8;
+    f32x8 s1 = {}, s2 = {}, s3 = {};              // four independent chains of row loads
+    int r = r0 + rl;
+    for (; r + 24 < r1; r += 32) {
+      s += ld8(src + (long)r * C);
+      s1 += ld8(src + (long)(r + 8) * C);
+      s2 += ld8(src + (long)(r + 16) * C);
+      s3 += ld8(src + (long)(r + 24) * C);
+    }
+    for (; r < r1; r += 8) s += ld8(src + (long)r * C);
+    s = (s + s1) + (s2 + s3);
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[rl][threadIdx.x & 31][e] = s[e];
@@ -2295,9 +2305,16 @@ __global__ void chansum_img_k(const float* __restrict__ part, float* __restrict_
   long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (t >= (long)Nimg * C) return;
   int n = (int)(t / C), c = (int)(t % C);
-  float s = 0.f;
-  for (int k = 0; k < nchunks; ++k) s += part[((long)k * Nimg + n) * C + c];
-  per_img[t] = s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int k = 0;
+  for (; k + 3 < nchunks; k += 4) {
+    s0 += part[((long)k * Nimg + n) * C + c];
+    s1 += part[((long)(k + 1) * Nimg + n) * C + c];
+    s2 += part[((long)(k + 2) * Nimg + n) * C + c];
+    s3 += part[((long)(k + 3) * Nimg + n) * C + c];
+  }
+  for (; k < nchunks; ++k) s0 += part[((long)k * Nimg + n) * C + c];
+  per_img[t] = (s0 + s1) + (s2 + s3);
 }
 
 // weight packing: OIHW fp32 -> [OCp][9][ICp] bf16 (forward) or
