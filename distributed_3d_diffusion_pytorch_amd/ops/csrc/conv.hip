@@ -958,7 +958,7 @@ __device__ __forceinline__ void halo_issue_b(bf16* sH, const bf16* I, int in_byt
                                              hoff[k] + (unsigned)cbyte, 0, 0, 0);
 }
 
-template <int OWT, bool TRANS, int BNT = 512>
+template <int OWT, bool TRANS, int BNT = 512, bool PF = false>
 __global__ void __launch_bounds__(512, 1)
 conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
@@ -1026,6 +1026,65 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     hp0[j] = (p / OWT) * Gm::HW2 + (p % OWT);
   }
 
+  auto frags = [&](bf16x8 (&af)[TM], bf16x8 (&bfr)[TN], const bf16* a, const bf16* hb, int t) {
+    const int kh = TRANS ? 2 - t / 3 : t / 3, kw = TRANS ? 2 - t % 3 : t % 3;
+    const int dsh = kh * Gm::HW2 + kw;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int hp = hp0[j] + dsh;
+      bfr[j] = *reinterpret_cast<const bf16x8*>(hb + hp * HALO_CH + ((fq ^ ((hp >> 2) & 3)) << 3));
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * WM + i * 16 + fr;
+      af[i] = *reinterpret_cast<const bf16x8*>(a + row * HALO_CH + ((fq ^ ((row >> 2) & 3)) << 3));
+    }
+  };
+  if constexpr (PF) {
+    // fragment double-buffering: step s+1's weights are waited for at step
+    // s's barrier (ring issue distance 4), so its LDS fragment reads go out
+    // while step s's MFMAs run instead of in front of them
+    halo_issue_b<Gm::HPW>(sH, I, in_bytes, hoff, 0, wave);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) halo_issue_a(sAr + k * Gm::ABUF, Wp, w_bytes, aoff, a_soff(k), wave);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    bf16x8 af[TM], bfr[TN];
+    frags(af, bfr, sAr, sH, 0);
+    int s = 0;
+    for (int c = 0; c < NCH; ++c) {
+#pragma unroll 1
+      for (int t = 0; t < 9; ++t, ++s) {
+        if (t >= 1 && t <= 3) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + Gm::HPW) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        halo_issue_a(sAr + ((s + 4) & 3) * Gm::ABUF, Wp, w_bytes, aoff, a_soff(s + 4), wave);
+        if (t == 0) {
+          const int cn = c + 1 < NCH ? c + 1 : NCH - 1;
+          halo_issue_b<Gm::HPW>(sH + ((c + 1) & 1) * Gm::HBUF, I, in_bytes, hoff, cn * HALO_CH * 2, wave);
+        }
+        bf16x8 an[TM], bn[TN];
+        if (s + 1 < S) {
+          const int cn = t == 8 ? c + 1 : c, tn = t == 8 ? 0 : t + 1;
+          frags(an, bn, sAr + ((s + 1) & 3) * Gm::ABUF, sH + (cn & 1) * Gm::HBUF, tn);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = an[i];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = bn[j];
+      }
+    }
+  } else {
   halo_issue_b<Gm::HPW>(sH, I, in_bytes, hoff, 0, wave);
   halo_issue_a(sAr, Wp, w_bytes, aoff, a_soff(0), wave);
   halo_issue_a(sAr + Gm::ABUF, Wp, w_bytes, aoff, a_soff(1), wave);
@@ -1071,6 +1130,7 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
+  }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tail re-loads drained before exit
 
@@ -2439,6 +2499,9 @@ static int g_halo32 = getenv("D3D_HALO32") ? atoi(getenv("D3D_HALO32")) : 0;
 // 10-15 % slower than the 4-wave 128x128 kernel on the 32x32 level at 16
 // examples per GPU (profiles/kbench_conv_halo256.jsonl); selectable only
 static int g_halo256 = getenv("D3D_HALO256") ? atoi(getenv("D3D_HALO256")) : 0;
+// fragment double-buffering in the halo conv (PF): measured 4-15 % slower
+// (249 VGPRs, the extra copies outweigh the overlap; profiles/ab_halo_prefetch.txt)
+static int g_halo_pf = getenv("D3D_HALO_PF") ? atoi(getenv("D3D_HALO_PF")) : 0;
 static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline, 2: buffer-descriptor LDS-DMA
 static int g_conv_korder = 1;     // glds k-step order: 1 channel-chunk major, 0 tap major
 static int g_wgrad_impl = 5;      // 0: register-staged; 1-4: glds (PK,NS) = (64,2) (32,2) (32,3) (64,3); 5: bufl
@@ -2509,9 +2572,14 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
     if (bn) {
       dim3 gh((unsigned)(N * (OH / (bn / OW))), (unsigned)(OC / 128), 1);
 #define HALO(OWv, TR, BNv)                                                                                         \
-  hipLaunchKernelGGL((conv_halo_k<OWv, TR, BNv>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias,     \
-                     row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale,  \
-                     res_nmod, gnp, gn_groups)
+  if (g_halo_pf && BNv == 512 && OWv == 64)                                                                         \
+    hipLaunchKernelGGL((conv_halo_k<OWv, TR, BNv, true>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp,   \
+                       bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, \
+                       scale, res_nmod, gnp, gn_groups);                                                            \
+  else                                                                                                              \
+    hipLaunchKernelGGL((conv_halo_k<OWv, TR, BNv>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias,   \
+                       row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale, \
+                       res_nmod, gnp, gn_groups)
       if (bn == 512) {
         if (OW == 32) {
           if (trans) HALO(32, true, 512); else HALO(32, false, 512);
