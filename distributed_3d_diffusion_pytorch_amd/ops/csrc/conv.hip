@@ -2532,8 +2532,9 @@ D3D_API int d3d_conv_plan(int N, int OH, int OW, int OC, int ICp, int taps) {
   long Mpix = (long)N * OH * OW;
   long blocks = ((Mpix + BN - 1) / BN) * ((OC + BM - 1) / BM);
   int nk = taps * ICp / 64;
+  static const int target = getenv("D3D_CONV_SPLIT_TARGET") ? atoi(getenv("D3D_CONV_SPLIT_TARGET")) : 512;
   if (blocks >= 384 || (OC & 3) || g_conv_impl < 1) return 1;
-  long want = 512 / blocks;         // rounded down: no nearly empty extra round of blocks
+  long want = target / blocks;      // rounded down: no nearly empty extra round of blocks
   long maxs = nk / 6;
   if (want > maxs) want = maxs;
   if (want > 16) want = 16;
