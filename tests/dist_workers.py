@@ -157,3 +157,36 @@ def gpu_graph_vs_eager(out_dir):
     with open(os.path.join(out_dir, f"gr{ctx.rank}.txt"), "w") as f:
         f.write(f"{d} {de} {dg} {max(abs(a - b) for a, b in zip(le, lg))}")
     cleanup()
+
+
+def two_node_emulation(out_dir):
+    """4 ranks laid out as 2 "nodes" x 2 local ranks (LOCAL_RANK != RANK on the
+    second node, as torchrun exports it on a multi-node job): 2 steps, rank-0
+    checkpoint, then every rank resumes from it into a fresh trainer and steps
+    again -- replicas must agree after the resume too (SURVEY §4 distributed tier)."""
+    rank = int(os.environ["RANK"])
+    os.environ["LOCAL_RANK"] = str(rank % 2)
+    os.environ["LOCAL_WORLD_SIZE"] = "2"
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup, check_replicas_in_sync
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    ctx = init_distributed("gloo", 60, use_gpu=False)
+    assert ctx.local_rank == rank % 2 and ctx.world == 4
+    cfg = make_config(None, dict(TINY_OV, **{"global_batch": 8, "out_dir": out_dir}))
+    tr = Trainer(cfg, ctx)
+    assert tr.local_batch == 2
+    data = SyntheticBatches(tr.local_batch, 16, "cpu", seed=ctx.rank)
+    for _ in range(2):
+        tr.train_step(*next(data))
+    ok = check_replicas_in_sync(tr.flat)
+    tr.save("latest.pt", epoch=0)
+    dist.barrier()
+    cfg2 = make_config(None, dict(TINY_OV, **{"global_batch": 8, "out_dir": out_dir, "transfer": out_dir}))
+    tr2 = Trainer(cfg2, ctx)
+    same = bool(torch.equal(tr2.flat.data, tr.flat.data)) and tr2.step == tr.step == 2
+    tr2.train_step(*next(data))
+    ok2 = check_replicas_in_sync(tr2.flat) and tr2.step == 3
+    with open(os.path.join(out_dir, f"node{ctx.rank}.txt"), "w") as f:
+        f.write(f"{int(ok)} {int(same)} {int(ok2)}")
+    cleanup()

@@ -29,3 +29,19 @@ def test_dead_rank_is_detected(tmp_path):
     with pytest.raises(Exception):
         spawn(W.fault_injection, 2, (str(tmp_path),))
     assert not os.path.exists(tmp_path / "survived0.txt")
+
+
+def test_four_ranks_two_node_layout_resume(tmp_path):
+    spawn(W.two_node_emulation, 4, (str(tmp_path),))
+    res = [open(tmp_path / f"node{r}.txt").read() for r in range(4)]
+    assert res == ["1 1 1"] * 4, res
+
+
+@pytest.mark.parametrize("n,world", [(8, 1), (8, 3), (64, 8), (5, 8)])
+def test_sampler_chain_shards_disjoint_covering(n, world):
+    from distributed_3d_diffusion_pytorch_amd.engine.sampler import shard_range
+    spans = [shard_range(n, r, world) for r in range(world)]
+    idx = [i for a, b in spans for i in range(a, b)]
+    assert idx == list(range(n))
+    sizes = [b - a for a, b in spans]
+    assert max(sizes) - min(sizes) <= 1
