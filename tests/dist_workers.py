@@ -9,6 +9,10 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+# several ranks share this host's CPUs: one intra-op pool per rank of the full
+# CPU count oversubscribes it many times over
+torch.set_num_threads(max(1, (os.cpu_count() or 8) // 4))
+
 TINY_OV = {"model.ch": 32, "model.emb_ch": 64, "model.H": 16, "model.W": 16, "data.imgsize": 16,
            "dtype": "fp32", "backend": "torch", "log_every": 0, "ckpt_every": 0, "data.synthetic": True,
            "dist.timeout_s": 20.0}
