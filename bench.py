@@ -5,8 +5,14 @@ Metric (BASELINE.json): train imgs/sec for the whole node, SRN cars 64x64,
 global batch 128 (reference: ≈29.9 examples/s on 8x RTX 3090, README.md:39).
 One "example" = one 2-view training pair.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W          (self-spawns N ranks)
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Launch: under torchrun (WORLD_SIZE set) every process is one rank.  Without
+it and with ``--gpus N > 1`` this process becomes a launcher: it starts N fresh
+child interpreters (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* on
+127.0.0.1), never touches the GPU itself, and exits with the worst child status
+(reference launcher: ``mp.spawn`` in `train.py:189-193`).
 
 Scaling is *strong* by default: the global batch stays 128 (the published
 config) and each of the N ranks trains on 128/N examples per step, so every
@@ -29,6 +35,37 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_EX_PER_S = 29.9  # 101,000 steps x 128 / 432,000 s on 8x RTX 3090
+
+
+def _launch(nprocs: int) -> int:
+    """Start ``nprocs`` ranks of this script as child processes (fresh
+    interpreters: the launcher itself never initialises the GPU) and wait.
+    A failing rank takes the others down (by their exact PIDs)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_WORLD_SIZE=str(nprocs),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:              # one rank died: end the job instead of hanging in a collective
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
 
 
 def main() -> None:
@@ -54,16 +91,22 @@ def main() -> None:
                     help="sample: 256-step stochastic-conditioning CFG sampling wall-clock (BASELINE config 5)")
     ap.add_argument("--sample_batch", type=int, default=64)
     ap.add_argument("--timesteps", type=int, default=256)
+    ap.add_argument("--device", default="auto", choices=["auto", "cpu"],
+                    help="cpu: gloo ranks on the host (launcher / plumbing tests)")
+    ap.add_argument("--ch", type=int, default=128, help="model width (128 = the benchmarked architecture)")
+    ap.add_argument("--emb_ch", type=int, default=1024)
     args = ap.parse_args()
     if args.mode == "sample":
         return bench_sample(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_launch(args.gpus))
 
     from distributed_3d_diffusion_pytorch_amd.config import make_config
     from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup, barrier
     from distributed_3d_diffusion_pytorch_amd.engine import Trainer
     from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
 
-    ctx = init_distributed("auto", timeout_s=900)
+    ctx = init_distributed("auto", timeout_s=900, use_gpu=False if args.device == "cpu" else None)
     N = ctx.world
     if args.gpus and args.gpus != N and ctx.rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={N}", file=sys.stderr)
@@ -82,6 +125,7 @@ def main() -> None:
     else:
         graph = bool(int(args.graph))
     cfg = make_config(None, {"model.H": args.imgsize, "model.W": args.imgsize, "data.imgsize": args.imgsize,
+                             "model.ch": args.ch, "model.emb_ch": args.emb_ch,
                              "global_batch": global_batch, "micro_batch": mb, "data.synthetic": True,
                              "backend": args.backend, "dtype": args.dtype, "log_every": 0, "ckpt_every": 0,
                              "dist.bucket_mb": args.bucket_mb, "dist.grad_dtype": args.grad_dtype,
@@ -134,13 +178,16 @@ def main() -> None:
             "value": round(value, 3), "unit": "examples/s", "n_gpus": N, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": scaling,
-            "vs_baseline": round(value / BASELINE_EX_PER_S, 3) if args.imgsize == 64 else None,
+            "vs_baseline": round(value / BASELINE_EX_PER_S, 3) if (args.imgsize == 64 and args.ch == 128) else None,
             "dtype": args.dtype, "data": "synthetic (on-device SRN-shaped batches, random-init weights)",
-            "config": {"model": "XUNet ch128 ch_mult(1,2,2,4) 136.7M params (3DiM, reference xunet.py)",
+            "config": {"model": (f"XUNet ch{args.ch} ch_mult(1,2,2,4) "
+                                 f"{sum(p.numel() for p in trainer.model.parameters()) / 1e6:.1f}M params "
+                                 "(3DiM, reference xunet.py)"),
                        "global_batch": global_batch, "seq_len": args.imgsize * args.imgsize,
                        "image_size": args.imgsize, "per_gpu_batch": local, "micro_batch": mb or local,
                        "hip_graph": graph,
-                       "parallelism": f"dp{N}",
+                       "parallelism": f"dp{N}", "dist_backend": ctx.backend,
+                       "graph_comm": getattr(trainer._graphed, "comm_mode", None),
                        "backend": "hip" if (ctx.device.type == "cuda" and use_hip(probe)) else "torch"},
             "final_loss": lv,
         }

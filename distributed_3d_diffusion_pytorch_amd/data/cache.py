@@ -23,7 +23,7 @@ from typing import Dict, List, Optional
 import numpy as np
 from torch.utils.data import Dataset
 
-from .srn import load_index, scan_index, split_ids, read_matrix
+from .srn import load_index, scan_index, split_ids, read_matrix, split_key
 
 
 def build_cache(root: str, out: str, imgsize: int, index: str = "", workers: int = 8) -> str:
@@ -90,10 +90,11 @@ class CachedSRNDataset(Dataset):
     def __len__(self) -> int:
         return len(self.ids)
 
-    def __getitem__(self, idx: int):
+    def __getitem__(self, key):
+        epoch, idx = split_key(key, self.epoch)
         images, poses, counts, Ks = self._load()
         r = self.rows[idx]
-        rng = random.Random((self.seed * 1000003 + self.epoch) * 1000003 + idx)
+        rng = random.Random((self.seed * 1000003 + epoch) * 1000003 + idx)
         pair = rng.sample(range(int(counts[r])), 2)
         imgs = np.stack([images[r, j] for j in pair]).astype(np.float32) / 255.0 * 2.0 - 1.0
         imgs = imgs.transpose(0, 3, 1, 2).copy()

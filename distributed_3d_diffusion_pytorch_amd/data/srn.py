@@ -12,7 +12,11 @@ Contract kept from the reference:
 
 Differences by design: the pair draw uses a per-(epoch, index) RNG (the
 reference uses the process-global ``random`` module, so pairs differ per
-worker), the index may also be JSON or discovered by scanning, and pickled
+worker).  The epoch travels WITH each index: :class:`ShardSampler` (``with_epoch``)
+yields ``(epoch, idx)`` keys, so persistent DataLoader workers -- which hold
+their own copy of the dataset and never see ``set_epoch`` on the main
+process's copy -- still draw a fresh view pair every epoch.  The index may
+also be JSON or discovered by scanning, and pickled
 indices are read with a restricted unpickler that only admits plain
 containers of strings (no code execution).
 """
@@ -85,6 +89,14 @@ def load_image(path: str, imgsize: int) -> np.ndarray:
     return arr.transpose(2, 0, 1)[:3].astype(np.float32)
 
 
+def split_key(key, default_epoch: int):
+    """Dataset key -> (epoch, index): ``(epoch, idx)`` from an epoch-carrying
+    sampler, or a plain index drawn under the dataset's own epoch."""
+    if isinstance(key, (tuple, list)):
+        return int(key[0]), int(key[1])
+    return default_epoch, int(key)
+
+
 class SRNDataset(Dataset):
     """``SRNDataset(split, path, index, imgsize)`` -> (imgs, R, T, K)."""
 
@@ -107,11 +119,12 @@ class SRNDataset(Dataset):
     def __len__(self) -> int:
         return len(self.ids)
 
-    def __getitem__(self, idx: int):
+    def __getitem__(self, key):
+        epoch, idx = split_key(key, self.epoch)
         inst = self.ids[idx]
         views = self.index[inst]
         K = read_matrix(os.path.join(self.path, inst, "intrinsics", views[0][:-4] + ".txt"), (3, 3))
-        rng = random.Random((self.seed * 1000003 + self.epoch) * 1000003 + idx)
+        rng = random.Random((self.seed * 1000003 + epoch) * 1000003 + idx)
         pair = rng.sample(views, 2)
         imgs, poses = [], []
         for v in pair:
@@ -125,21 +138,28 @@ class SRNDataset(Dataset):
 class ShardSampler(Sampler):
     """DistributedSampler-equivalent (fixes D1: the reference passes the
     sampler *as the dataset*).  Shuffles with (seed, epoch), pads to a multiple
-    of world size, returns this rank's strided shard."""
+    of world size, returns this rank's strided shard.  ``with_epoch``: yield
+    ``(epoch, idx)`` keys so the dataset's pair draw follows the epoch even
+    inside persistent worker processes."""
 
     def __init__(self, n: int, rank: int = 0, world: int = 1, shuffle: bool = True, seed: int = 0,
-                 drop_last: bool = False):
+                 drop_last: bool = False, with_epoch: bool = False):
         self.n, self.rank, self.world = n, rank, world
+        self.with_epoch = with_epoch
         self.shuffle, self.seed, self.drop_last = shuffle, seed, drop_last
         self.epoch = 0
+        self.start = 0
         if drop_last:
             self.num = n // world
         else:
             self.num = (n + world - 1) // world
         self.total = self.num * world
 
-    def set_epoch(self, epoch: int) -> None:
+    def set_epoch(self, epoch: int, start: int = 0) -> None:
+        """``start``: skip this rank's first ``start`` indices of the epoch
+        (mid-epoch resume continues where the checkpoint left off)."""
         self.epoch = epoch
+        self.start = max(0, min(int(start), self.num))
 
     def __iter__(self):
         if self.shuffle:
@@ -151,10 +171,13 @@ class ShardSampler(Sampler):
         if self.total > len(idx):
             idx = idx + idx[: self.total - len(idx)]
         idx = idx[: self.total]
-        return iter(idx[self.rank: self.total: self.world])
+        mine = idx[self.rank: self.total: self.world][self.start:]
+        if self.with_epoch:
+            return iter([(self.epoch, i) for i in mine])
+        return iter(mine)
 
     def __len__(self) -> int:
-        return self.num
+        return self.num - self.start
 
 
 def collate(items):

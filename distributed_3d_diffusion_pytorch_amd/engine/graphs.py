@@ -12,15 +12,23 @@ Layout of one step (MI355X, one process per GPU):
       X-UNet forward -> backward; HIP weight-gradient kernels deposit into the
       flat fp32 gradient buffer (GradSink), the micro-batch loss is added to a
       device accumulator.  Inputs are copied into static buffers first.
-  [world > 1] eager RCCL all-reduce of the flat gradient in D3D_AR_CHUNKS
-      (default 4) async collectives, each chunk's Adam launched as soon as
-      its collective lands, so the optimizer pass (~0.7 ms) hides behind the
-      remaining chunks' reduction (~3 ms for 547 MB over xGMI against a ~33
-      ms step), then the batched weight repack and the zeroing.  (The graph
-      cannot hold the hook-driven bucketed launches of the eager step.)
-  graph B (world == 1): fused Adam reading its per-step hyper-parameters
-      from a device block (lr warmup / bias correction change every step) ->
-      batched weight repack -> gradient / loss-accumulator zeroing.
+  [world > 1, comm_mode "graph"] the bucketed RCCL all-reduces are captured
+      INTO graph A: the same gradient hooks / sink notifications that drive
+      the eager reducer (parallel/ddp.py) fire during capture, so each bucket's
+      collective is recorded on RCCL's stream as soon as its last gradient is
+      deposited, with event edges from the compute stream; on replay the
+      reduction of bucket k runs concurrently with the backward kernels of
+      the layers below it, exactly like the eager overlapped step, and only
+      the last (small, first-layer) buckets are exposed.  Graph A ends by
+      joining RCCL's stream (work.wait() captured as an edge).
+  [world > 1, comm_mode "post"] fallback when a probe capture of an RCCL
+      collective fails (or D3D_GRAPH_COMM=0, or gloo): eager all-reduce of the
+      flat gradient after graph A in D3D_AR_CHUNKS (default 4) async chunks,
+      each chunk's Adam launched as soon as its collective lands.
+  graph B: fused Adam reading its per-step hyper-parameters from a device
+      block (lr warmup / bias correction change every step; the 1/world
+      gradient average is folded in) -> batched weight repack -> gradient /
+      loss-accumulator zeroing.
 
 Per-step values that a replay cannot see from Python travel through device
 words refreshed before the replays: the dropout seed (``hip_impl._SEED_DEV``,
@@ -28,12 +36,47 @@ added to every mask kernel's baked seed) and the Adam block ``hp``.
 """
 from __future__ import annotations
 
-import math
 import os
 from typing import Optional
 
 import torch
 import torch.distributed as dist
+
+
+def probe_graph_collective(device: torch.device) -> bool:
+    """True when an RCCL all-reduce can be captured in a HIP graph and replayed
+    correctly on every rank.  Run once, eagerly, before the step capture; the
+    verdict is agreed over the group (MIN), so all ranks take the same path."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_backend() != "nccl":
+        return False
+    ok = 1.0
+    try:
+        world = dist.get_world_size()
+        x = torch.zeros(4096, device=device)
+        s = torch.cuda.Stream(device=device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):          # warm the collective outside the capture
+            dist.all_reduce(x)
+        torch.cuda.current_stream(device).wait_stream(s)
+        torch.cuda.synchronize(device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            w = dist.all_reduce(x, async_op=True)
+            w.wait()
+            x.mul_(2.0)
+        for rep in range(2):
+            x.fill_(float(dist.get_rank() + 1 + rep))
+            g.replay()
+        torch.cuda.synchronize(device)
+        want = 2.0 * (world * (world + 1) / 2 + world)
+        ok = float(bool(torch.all(x == want).item()))
+    except Exception as e:                   # noqa: BLE001 -- any failure means "do not capture"
+        print(f"[graphs] RCCL graph-capture probe failed ({type(e).__name__}: {e}); "
+              "all-reduce runs after the graph", flush=True)
+        ok = 0.0
+    flag = torch.tensor([ok], device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item() > 0.5)
 
 
 class GraphedTrainStep:
@@ -51,23 +94,39 @@ class GraphedTrainStep:
         self.K = torch.zeros((micro_batch,) + tuple(K.shape[1:]), dtype=K.dtype, device=dev)
         self.frac = torch.ones((), device=dev)
         self.loss_acc = torch.zeros((), device=dev)
-        self.seed = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.seed = torch.zeros(3, dtype=torch.int64, device=dev)    # [dropout word, draw word, example offset]
         self.hp = torch.zeros(8, device=dev)
         self.pool = torch.cuda.graph_pool_handle()
-        self.gA: Optional[torch.cuda.CUDAGraph] = None
+        self.gA: Optional[torch.cuda.CUDAGraph] = None      # fwd+bwd (+ captured all-reduce)
+        self.gA0: Optional[torch.cuda.CUDAGraph] = None     # fwd+bwd without comm (leading micro-batches)
         self.gB: Optional[torch.cuda.CUDAGraph] = None
+        world = trainer.ctx.world
+        self.comm_mode = None
+        if world > 1:
+            want = os.environ.get("D3D_GRAPH_COMM", "1") != "0" and trainer.cfg.dist.grad_dtype != "bf16"
+            self.comm_mode = "graph" if (want and probe_graph_collective(dev)) else "post"
 
     # ------------------------------------------------------------------
-    def _body(self) -> None:
+    def _body(self, comm: bool = False) -> None:
         tr = self.tr
         if tr.sink is not None:
             tr.sink.reset()
-        batch, mask, eps = tr.diffusion_inputs(self.img, self.R, self.T, self.K)
-        eps_hat = tr.model(batch, cond_mask=mask)
-        from ..diffusion import diffusion_loss
-        loss = diffusion_loss(eps, eps_hat, tr.cfg.diffusion.loss_type)
+        red = tr.reducer
+        if red is not None:
+            red.enabled = comm
+            red.reset()
+        # step word 0 / offset 0 baked: the per-step words and the micro-batch
+        # offset come from the device block self.seed (see step())
+        batch, mask, eps = tr.diffusion_inputs(self.img, self.R, self.T, self.K, 0, step_word=0)
+        y = tr.model(batch, cond_mask=mask, head_nhwc=True)
+        from .. import ops
+        loss = ops.diff_loss_nhwc(y, eps, tr.cfg.diffusion.loss_type)
         (loss * self.frac).backward()
         self.loss_acc.add_(loss.detach() * self.frac)
+        if red is not None and comm:
+            red.finish()            # remaining buckets + the join of RCCL's stream (captured edges)
+        if red is not None:
+            red.enabled = False
 
     def _update(self) -> None:
         o = self.tr.optim
@@ -75,13 +134,12 @@ class GraphedTrainStep:
         o.flat.grad.zero_()
         self.loss_acc.zero_()
 
-    def capture(self) -> None:
+    def capture(self, nchunks: int = 1) -> None:
         tr = self.tr
         tr.model.train()
         tr.model.set_dropout_seed(0)             # baked; the per-step part is self.seed
         self.H.set_device_seed(self.seed)
-        if tr.reducer is not None:
-            tr.reducer.enabled = False           # the all-reduce runs between the graphs
+        comm = self.comm_mode == "graph"
         self.img.normal_()
         self.R.copy_(torch.eye(3, device=self.R.device).expand_as(self.R))
         self.K.copy_(torch.eye(3, device=self.K.device).expand_as(self.K))
@@ -93,35 +151,33 @@ class GraphedTrainStep:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                self._body()
+                self._body(comm)
         torch.cuda.current_stream().wait_stream(s)
         self.H.refresh_weights()                 # descriptor table final before capture
         torch.cuda.synchronize()
+        mode = "thread_local" if comm else "global"     # RCCL's watchdog thread keeps querying events
         self.gA = torch.cuda.CUDAGraph()
         self.gA.register_generator_state(tr.gen)
-        with torch.cuda.graph(self.gA, pool=self.pool):
-            self._body()
+        with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
+            self._body(comm)
+        if comm and nchunks > 1:
+            self.gA0 = torch.cuda.CUDAGraph()
+            self.gA0.register_generator_state(tr.gen)
+            with torch.cuda.graph(self.gA0, pool=self.pool):
+                self._body(False)
         self.gB = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.gB, pool=self.pool):
             self._update()
         torch.cuda.synchronize()
         tr.gen.set_state(gstate)
+        # scope the device seed word to the replays (an eager forward after
+        # this must not add a stale device seed to its dropout seed)
+        self.H.set_device_seed(None)
         # warm-up / capture left partial gradients behind
         tr.flat.zero_grad()
         self.loss_acc.zero_()
 
     # ------------------------------------------------------------------
-    def _hparams(self, grad_scale: float) -> torch.Tensor:
-        o = self.tr.optim
-        g = o.param_groups[0]
-        lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
-        o.step_count += 1
-        t = o.step_count
-        bc1 = 1.0 - b1 ** t
-        bc2_sqrt = math.sqrt(1.0 - b2 ** t)
-        return torch.tensor([b1, b2, eps, wd, lr / bc1, bc2_sqrt, grad_scale, 1.0 - o.ema_decay],
-                            dtype=torch.float32)
-
     def _reduce_update_chunked(self) -> None:
         """fp32 all-reduce in chunks, each chunk's Adam behind its own
         collective (overlaps the optimizer with the remaining reduction)."""
@@ -140,37 +196,52 @@ class GraphedTrainStep:
         g.zero_()
         self.loss_acc.zero_()
 
-    def step(self, img, R, T, K) -> torch.Tensor:
+    def step(self, img, R, T, K, want_norm: bool = False) -> torch.Tensor:
         tr = self.tr
-        if self.gA is None:
-            self.capture()
         B = img.shape[0]
         mb = self.mb
         assert B % mb == 0, (B, mb)
-        self.seed.fill_(tr.step * tr.ctx.world + tr.ctx.rank + 1)
         nchunks = B // mb
+        if self.gA is None:
+            self.capture(nchunks)
+        # same seeds as the eager step (Trainer.train_step): the captured
+        # kernels carry the base seeds and add these device words
+        word = tr.step * tr.ctx.world + tr.ctx.rank
         self.frac.fill_(1.0 / nchunks)
-        for s in range(0, B, mb):
+        for ci, s in enumerate(range(0, B, mb)):
+            from .trainer import dropout_word
+            for j, v in enumerate((dropout_word(word, ci), word, s)):     # kernel-argument fills, no H2D copy
+                self.seed[j].fill_(v)
             self.img.copy_(img[s:s + mb])
             self.R.copy_(R[s:s + mb])
             self.T.copy_(T[s:s + mb])
             self.K.copy_(K[s:s + mb])
-            self.gA.replay()
+            last = ci == nchunks - 1
+            (self.gA if (last or self.gA0 is None) else self.gA0).replay()
         loss = self.loss_acc.clone()
-        if tr.ctx.world > 1:
+        world = tr.ctx.world
+        o = tr.optim
+        clip = tr.cfg.optim.grad_clip
+        self.hp.copy_(o.hparams(1.0 / world), non_blocking=True)
+        post = world > 1 and self.comm_mode != "graph"
+        if post and (clip > 0 or want_norm or tr.cfg.dist.grad_dtype == "bf16"):
             g = tr.flat.grad
             if tr.cfg.dist.grad_dtype == "bf16":
                 gb = g.to(torch.bfloat16)
                 dist.all_reduce(gb)
                 g.copy_(gb)
             else:
-                self.hp.copy_(self._hparams(1.0 / tr.ctx.world))
-                self._reduce_update_chunked()
-                for cb in tr.optim.on_step:
-                    cb()
-                return loss
-        self.hp.copy_(self._hparams(1.0 / tr.ctx.world))
-        self.gB.replay()
-        for cb in tr.optim.on_step:
+                dist.all_reduce(g)
+            post = False
+        if want_norm or clip > 0:
+            norm = o.grad_norm(1.0 / world)
+            tr.last_grad_norm = norm
+            if clip > 0:
+                self.hp[6:7].mul_(o.clip_coef(norm, clip))
+        if post:
+            self._reduce_update_chunked()
+        else:
+            self.gB.replay()
+        for cb in o.on_step:
             cb()
         return loss

@@ -42,24 +42,64 @@ class FusedAdam(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = False) -> None:  # noqa: D401 - torch API
         self.flat.zero_grad()
 
-    @torch.no_grad()
-    def step(self, closure=None, grad_scale: float = 1.0):
-        loss = closure() if closure is not None else None
+    def grad_norm(self, grad_scale: float = 1.0) -> torch.Tensor:
+        """L2 norm of the (averaged) flat gradient, as a device scalar (no sync)."""
+        return torch.linalg.vector_norm(self.flat.grad, dtype=torch.float32) * grad_scale
+
+    def hparams(self, grad_scale: float) -> torch.Tensor:
+        """Advance the step counter and return the per-step hyper-parameter
+        block of the device-side Adam kernel (adam.hip ``d3d_adam_dev``):
+        [b1, b2, eps, wd, lr/bc1, sqrt(bc2), grad_scale, 1-ema_decay]."""
         g = self.param_groups[0]
         lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
         self.step_count += 1
         t = self.step_count
-        bc1 = 1.0 - b1 ** t
-        bc2_sqrt = math.sqrt(1.0 - b2 ** t)
-        step_size = lr / bc1
+        return torch.tensor([b1, b2, eps, wd, lr / (1.0 - b1 ** t), math.sqrt(1.0 - b2 ** t), grad_scale,
+                             1.0 - self.ema_decay], dtype=torch.float32)
+
+    @staticmethod
+    def clip_coef(norm: torch.Tensor, max_norm: float) -> torch.Tensor:
+        """min(1, max_norm / norm) on the device (torch clip_grad_norm_ rule)."""
+        return torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: float = 1.0, max_norm: float = 0.0,
+             norm: Optional[torch.Tensor] = None):
+        """One update.  ``max_norm > 0`` clips the averaged gradient to that
+        global L2 norm (``norm``: its precomputed value, else computed here);
+        the clip coefficient stays on the device and scales the gradient
+        inside the Adam kernel."""
+        loss = closure() if closure is not None else None
         p, gr = self.flat.data, self.flat.grad
+        coef = None
+        if max_norm > 0:
+            if norm is None:
+                norm = self.grad_norm(grad_scale)
+            coef = self.clip_coef(norm, max_norm)
         from .. import ops
         if p.is_cuda and ops.use_hip(p, any_dtype=True):
             from ..ops import hip_impl
-            hip_impl.adam_flat(p, gr, self.exp_avg, self.exp_avg_sq, self.ema, lr, b1, b2, eps, wd,
-                               step_size, bc2_sqrt, grad_scale, self.ema_decay)
+            if coef is not None:
+                hp = self.hparams(grad_scale).to(p.device, non_blocking=True)
+                hp[6:7].mul_(coef)
+                hip_impl.adam_flat_dev(p, gr, self.exp_avg, self.exp_avg_sq, self.ema, hp)
+            else:
+                g = self.param_groups[0]
+                lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
+                self.step_count += 1
+                t = self.step_count
+                hip_impl.adam_flat(p, gr, self.exp_avg, self.exp_avg_sq, self.ema, lr, b1, b2, eps, wd,
+                                   lr / (1.0 - b1 ** t), math.sqrt(1.0 - b2 ** t), grad_scale, self.ema_decay)
         else:
+            g = self.param_groups[0]
+            lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
+            self.step_count += 1
+            t = self.step_count
+            bc2_sqrt = math.sqrt(1.0 - b2 ** t)
+            step_size = lr / (1.0 - b1 ** t)
             grad = gr if grad_scale == 1.0 else gr * grad_scale
+            if coef is not None:
+                grad = grad * coef
             if wd != 0.0:
                 grad = grad.add(p, alpha=wd)
             self.exp_avg.lerp_(grad, 1.0 - b1)
@@ -111,6 +151,32 @@ class FusedAdam(torch.optim.Optimizer):
             return None
         names = [n for n, _ in model.named_parameters()]
         return {n: self.flat.view(self.ema, i).clone() for i, n in enumerate(names)}
+
+    @torch.no_grad()
+    def reset_ema(self) -> None:
+        """Restart the EMA from the current weights (after loading pretrained
+        / transferred weights, so the average never starts from random init)."""
+        if self.ema is not None:
+            self.ema.copy_(self.flat.data)
+
+    @torch.no_grad()
+    def load_ema_state_dict(self, model: torch.nn.Module, sd) -> bool:
+        """Restore a saved EMA (``ema_state_dict`` format, optional ``module.``
+        prefix).  Returns False (EMA restarted from the weights) when the
+        checkpoint has none or it does not cover every parameter."""
+        if self.ema is None:
+            return False
+        if not sd:
+            self.reset_ema()
+            return False
+        sd = {(k[7:] if k.startswith("module.") else k): v for k, v in sd.items()}
+        names = [n for n, _ in model.named_parameters()]
+        if any(n not in sd for n in names):
+            self.reset_ema()
+            return False
+        for i, n in enumerate(names):
+            self.flat.view(self.ema, i).copy_(sd[n].reshape(self.flat.params[i].shape))
+        return True
 
 
 def ema_decay_for(batch_size: int, halflife_examples: float) -> float:

@@ -25,12 +25,17 @@ import torch
 
 from .. import ops
 from ..config import TrainConfig, dumps, to_dict
-from ..diffusion import logsnr_schedule_cosine, q_sample, diffusion_loss
 from ..models import XUNet
 from ..parallel import (DistContext, FlatParams, GradReducer, get_context, check_replicas_in_sync)
 from ..utils import (save_checkpoint, load_checkpoint, load_model_weights, find_resume, MetricsLogger,
                      StepTimer, train_flops_per_example, range_push, check_finite)
 from .optim import FusedAdam, ema_decay_for, warmup_lr
+
+
+def dropout_word(step_word: int, chunk: int) -> int:
+    """Dropout seed word of micro-batch ``chunk`` of a step (distinct per
+    micro-batch: the masks are element-indexed within each launch)."""
+    return step_word + (chunk << 40)
 
 
 class _null:
@@ -91,11 +96,13 @@ class Trainer:
         self.logger = MetricsLogger(os.path.join(self.out_dir, "metrics.jsonl") if self.ctx.is_main else None)
         self.fault_step = int(os.environ.get("D3D_FAULT_AT_STEP", "-1"))
         self.fault_rank = int(os.environ.get("D3D_FAULT_RANK", "-1"))
+        self.epoch_pos = 0          # batches of self.epoch already consumed (mid-epoch resume)
         if cfg.pretrained and not cfg.transfer:
             ck = load_checkpoint(cfg.pretrained, map_location="cpu")
             load_model_weights(self.model, ck["model"])
             if "optim" in ck:
                 self.optim.load_state_dict(ck["optim"])
+            self.optim.reset_ema()          # EMA starts from the loaded weights, not random init
         if cfg.transfer:
             self.resume(cfg.transfer)
         if self.reducer is not None:
@@ -110,20 +117,41 @@ class Trainer:
         load_model_weights(self.model, ck["model"])
         if "optim" in ck:
             self.optim.load_state_dict(ck["optim"])
+        self.optim.load_ema_state_dict(self.model, ck.get("ema"))
         self.step = int(ck.get("step", 0))
-        self.epoch = int(ck.get("epoch", -1)) + 1 if "epoch" in ck else 0
-        if "rng" in ck and ck["rng"] is not None and self.ctx.world == int(ck.get("world_size", 1)):
-            try:
-                self.gen.set_state(ck["rng"][self.ctx.rank].to(self.gen.get_state().device))
-            except Exception:
-                pass
+        if "sampler_epoch" in ck:           # mid-epoch checkpoint (after_warmup.pt)
+            self.epoch = int(ck["sampler_epoch"])
+            self.epoch_pos = int(ck.get("epoch_pos", 0))
+        else:                               # end-of-epoch checkpoint (latest.pt) or reference file
+            self.epoch = int(ck.get("epoch", -1)) + 1 if "epoch" in ck else 0
+            self.epoch_pos = 0
+        rng = ck.get("rng")
+        if rng is not None and self.ctx.world == int(ck.get("world_size", 1)) and self.ctx.rank < len(rng):
+            self.gen.set_state(rng[self.ctx.rank].to(torch.uint8).cpu())
         return True
 
-    def save(self, name: str, epoch: Optional[int] = None) -> Optional[str]:
+    def _gather_rng(self):
+        """Every rank's generator state (collective: all ranks call it)."""
+        st = self.gen.get_state()
+        if self.ctx.world == 1:
+            return [st]
+        import torch.distributed as dist
+        out = [None] * self.ctx.world
+        dist.all_gather_object(out, st)
+        return out
+
+    def save(self, name: str, epoch: Optional[int] = None, epoch_pos: Optional[int] = None) -> Optional[str]:
+        """Collective (every rank calls it: the RNG states are gathered);
+        rank 0 writes.  ``epoch``: completed epoch (reference ``latest.pt``);
+        ``epoch_pos``: mid-epoch position of the current epoch."""
+        rng = self._gather_rng()
         if not self.ctx.is_main:
             return None
         path = os.path.join(self.out_dir, name)
-        extra = {"config": to_dict(self.cfg), "world_size": self.ctx.world}
+        extra = {"config": to_dict(self.cfg), "world_size": self.ctx.world, "rng": rng}
+        if epoch_pos is not None:
+            extra["sampler_epoch"] = int(self.epoch)
+            extra["epoch_pos"] = int(epoch_pos)
         ema = self.optim.ema_state_dict(self.model)
         if ema is not None:
             extra["ema"] = {k: v.cpu() for k, v in ema.items()}
@@ -131,37 +159,46 @@ class Trainer:
         return path
 
     # ------------------------------------------------------------------
-    def diffusion_inputs(self, img, R, T, K):
-        """q_sample + CFG dropout (`train.py:80-100`), all on device."""
-        B = img.shape[0]
-        dev = img.device
-        x, z = img[:, 0].float(), img[:, 1].float()
-        t = torch.rand(B, generator=self.gen, device=dev)
+    def step_seed(self, step_word: Optional[int] = None) -> int:
+        """64-bit RNG seed of the training-input draw of one step on this
+        rank: base + (step * world + rank) * golden (the graph step bakes the
+        base and supplies the step word on the device; ops.diffusion_inputs)."""
+        base = (self.cfg.seed * 0x2545F4914F6CDD1D + 0x1234567) & 0xFFFFFFFFFFFFFFFF
+        if step_word is None:
+            step_word = self.step * self.ctx.world + self.ctx.rank
+        return (base + step_word * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+
+    def diffusion_inputs(self, img, R, T, K, e0: int = 0, step_word: Optional[int] = None):
+        """q_sample + CFG dropout (`train.py:80-100`) for examples e0.. of this
+        rank's batch, on device: one fused launch on the HIP path.  The draw is
+        counter-based in (step seed, example index), so micro-batching and
+        graph replay see exactly the numbers of the full-batch eager step."""
         dc = self.cfg.diffusion
-        logsnr = logsnr_schedule_cosine(t, logsnr_min=dc.logsnr_min, logsnr_max=dc.logsnr_max)
-        eps = torch.randn(z.shape, generator=self.gen, device=dev)
-        z_t = q_sample(z, logsnr, eps)
-        cond_mask = torch.rand(B, generator=self.gen, device=dev) > dc.cond_prob
-        x_cond = torch.where(cond_mask[:, None, None, None], x,
-                             torch.randn(x.shape, generator=self.gen, device=dev))
-        lam0 = logsnr_schedule_cosine(torch.zeros_like(logsnr), logsnr_min=dc.logsnr_min, logsnr_max=dc.logsnr_max)
-        batch = {"x": x_cond, "z": z_t, "logsnr": torch.stack([lam0, logsnr], 1), "R": R, "t": T, "K": K}
-        return batch, cond_mask, eps
+        xz, eps, logsnr, keep = ops.diffusion_inputs(img, self.step_seed(step_word), e0, dc.cond_prob,
+                                                     dc.logsnr_min, dc.logsnr_max, self.dtype)
+        batch = {"xz": xz, "logsnr": logsnr, "R": R, "t": T, "K": K}
+        return batch, keep, eps
 
-    def loss_fn(self, img, R, T, K) -> torch.Tensor:
-        batch, mask, eps = self.diffusion_inputs(img, R, T, K)
-        self.model.set_dropout_seed(self.step * self.ctx.world + self.ctx.rank)
-        eps_hat = self.model(batch, cond_mask=mask)
-        return diffusion_loss(eps, eps_hat, self.cfg.diffusion.loss_type)
+    def loss_fn(self, img, R, T, K, e0: int = 0, chunk: int = 0) -> torch.Tensor:
+        batch, mask, eps = self.diffusion_inputs(img, R, T, K, e0)
+        self.model.set_dropout_seed(dropout_word(self.step * self.ctx.world + self.ctx.rank, chunk))
+        y = self.model(batch, cond_mask=mask, head_nhwc=True)
+        return ops.diff_loss_nhwc(y, eps, self.cfg.diffusion.loss_type)
 
-    def train_step(self, img, R, T, K) -> torch.Tensor:
+    last_grad_norm: Optional[torch.Tensor] = None    # device scalar, set when measured / clipping
+    last_allreduce_ms: float = 0.0
+
+    def train_step(self, img, R, T, K, want_stats: bool = False) -> torch.Tensor:
+        """One optimizer step.  ``want_stats``: also measure the gradient norm
+        (``last_grad_norm``) and the time the optimizer waited on the gradient
+        all-reduce (``last_allreduce_ms``, device events) -- log steps only."""
         if self.step == self.fault_step and self.ctx.rank == self.fault_rank:
             os._exit(13)  # fault-injection hook for the failure-detection tests
         g = self.optim.param_groups[0]
         if self.sched is None:
             g["lr"] = warmup_lr(self.step, self.warmup_steps, self.cfg.optim.lr)
         if self.cfg.graph and self.device.type == "cuda" and self.sink is not None:
-            return self._graph_train_step(img, R, T, K)
+            return self._graph_train_step(img, R, T, K, want_stats)
         self.model.train()
         if self.sink is not None:
             self.sink.reset()
@@ -174,17 +211,31 @@ class Trainer:
                 last_chunk = ci == len(chunks) - 1
                 ctx = self.reducer.no_sync() if (self.reducer is not None and not last_chunk) else _null()
                 with ctx:
-                    loss = self.loss_fn(img[s:e], R[s:e], T[s:e], K[s:e])
+                    loss = self.loss_fn(img[s:e], R[s:e], T[s:e], K[s:e], e0=s, chunk=ci)
                     (loss * ((e - s) / B)).backward() if len(chunks) > 1 else loss.backward()
                 l = loss.detach() * ((e - s) / B)
                 total = l if total is None else total + l
         loss = total
+        timing = want_stats and self.device.type == "cuda" and self.reducer is not None
+        if timing:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
         if self.reducer is not None:
             with range_push("allreduce_wait"):
                 self.reducer.finish()
+        if timing:
+            ev1.record()
+        scale = 1.0 / self.ctx.world
+        clip = self.cfg.optim.grad_clip
+        norm = self.optim.grad_norm(scale) if (want_stats or clip > 0) else None
+        if norm is not None:
+            self.last_grad_norm = norm
         with range_push("optimizer"):
-            self.optim.step(grad_scale=1.0 / self.ctx.world)
+            self.optim.step(grad_scale=scale, max_norm=clip, norm=norm)
             self.optim.zero_grad()
+        if timing:
+            ev1.synchronize()
+            self.last_allreduce_ms = ev0.elapsed_time(ev1)
         if self.sched is not None:
             self.sched.step()
         self.step += 1
@@ -195,7 +246,7 @@ class Trainer:
 
     _graphed = None
 
-    def _graph_train_step(self, img, R, T, K) -> torch.Tensor:
+    def _graph_train_step(self, img, R, T, K, want_stats: bool = False) -> torch.Tensor:
         """Same step, replayed from captured HIP graphs (engine/graphs.py)."""
         from .graphs import GraphedTrainStep
         B = img.shape[0]
@@ -203,7 +254,7 @@ class Trainer:
         if self._graphed is None or self._graphed.mb != mb:
             self._graphed = GraphedTrainStep(self, mb, (img, R, T, K))
         self.model.train()
-        loss = self._graphed.step(img, R, T, K)
+        loss = self._graphed.step(img, R, T, K, want_norm=want_stats)
         if self.sched is not None:
             self.sched.step()
         self.step += 1
@@ -225,7 +276,8 @@ class Trainer:
             ds = CachedSRNDataset("train", dc.cache, seed=dc.seed)
         else:
             ds = SRNDataset("train", dc.path, dc.index, dc.imgsize, seed=dc.seed)
-        sampler = ShardSampler(len(ds), self.ctx.rank, self.ctx.world, shuffle=True, seed=dc.seed)
+        sampler = ShardSampler(len(ds), self.ctx.rank, self.ctx.world, shuffle=True, seed=dc.seed,
+                               with_epoch=True)
         loader = MultiEpochsDataLoader(ds, batch_size=self.local_batch, sampler=sampler,
                                        num_workers=dc.num_workers, drop_last=True,
                                        pin_memory=self.device.type == "cuda")
@@ -247,35 +299,46 @@ class Trainer:
         done = False
         for epoch in range(self.epoch, cfg.num_epochs):
             self.epoch = epoch
+            n = self.epoch_pos if epoch == self.epoch else 0
             if sampler is not None:
-                sampler.set_epoch(epoch)
+                sampler.set_epoch(epoch, start=n * self.local_batch)
                 ds.set_epoch(epoch)
+            self.epoch_pos = 0
             it = iter(data)
-            n = 0
+            data_wait = 0.0
             while True:
                 if steps_per_epoch and n >= steps_per_epoch:
                     break
+                t_wait = time.perf_counter()
                 try:
                     batch = next(it)
                 except StopIteration:
                     break
+                data_wait += time.perf_counter() - t_wait
                 self._profile_hook(self.step)
-                loss = self.train_step(*self._to_dev(batch))
+                log_now = bool(cfg.log_every) and (self.step + 1) % cfg.log_every == 0
+                loss = self.train_step(*self._to_dev(batch), want_stats=log_now)
                 timer.tick()
                 n += 1
-                if cfg.log_every and self.step % cfg.log_every == 0:
+                if log_now:
                     lv = float(loss)
                     check_finite(loss, self.step)
                     rep = timer.report()
+                    gn = float(self.last_grad_norm) if self.last_grad_norm is not None else float("nan")
                     last = {"step": self.step, "epoch": epoch, "loss": lv,
-                            "lr": self.optim.param_groups[0]["lr"], **rep}
+                            "lr": self.optim.param_groups[0]["lr"], **rep, "grad_norm": gn,
+                            "allreduce_wait_ms": self.last_allreduce_ms,
+                            "data_wait_ms": 1e3 * data_wait / max(rep["steps"], 1),
+                            "hbm_peak_gib": (torch.cuda.max_memory_allocated(self.device) / 2 ** 30
+                                             if self.device.type == "cuda" else 0.0)}
+                    data_wait = 0.0
                     if self.ctx.is_main:
                         print(f"[step {self.step}] loss {lv:.5f} {rep['examples_per_s']:.1f} ex/s "
                               f"{rep['tflops']:.1f} TFLOP/s", flush=True)
                         self.logger.log(**last)
                     timer.start()
                 if cfg.ckpt_every and self.step % cfg.ckpt_every == 0:
-                    self.save("after_warmup.pt")
+                    self.save("after_warmup.pt", epoch_pos=n)
                 if cfg.max_steps and self.step >= cfg.max_steps:
                     done = True
                     break

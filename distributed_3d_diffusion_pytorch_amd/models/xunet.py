@@ -248,7 +248,7 @@ class ConditioningProcessor(nn.Module):
 
     def forward(self, batch: Dict[str, torch.Tensor], cond_mask: torch.Tensor,
                 dtype: torch.dtype) -> List[torch.Tensor]:
-        B = batch["x"].shape[0]
+        B = batch["logsnr"].shape[0]
         assert cond_mask.shape == (B,), (cond_mask.shape, B)
         logsnr_emb = self.logsnr_embedding(batch["logsnr"])
         # Data-dependent part: NeRF-encoded camera rays (masked), no gradient.
@@ -371,14 +371,29 @@ class XUNet(nn.Module):
             if isinstance(m, ResnetBlock):
                 m._base_seed = int(seed)
 
-    def forward(self, batch: Dict[str, torch.Tensor], *, cond_mask: torch.Tensor) -> torch.Tensor:
-        x, z = batch["x"], batch["z"]
-        B, C, H, W = x.shape
+    def forward(self, batch: Dict[str, torch.Tensor], *, cond_mask: torch.Tensor,
+                head_nhwc: bool = False) -> torch.Tensor:
+        """``batch``: the reference dict {x, z, logsnr, R, t, K} (`xunet.py:477`),
+        or with ``xz`` -- the already stacked NHWC stem input [2B,H,W,C>=3]
+        (frames interleaved; extra channels zero) drawn by
+        ``ops.diffusion_inputs`` -- in place of x and z.  ``head_nhwc``: return
+        the head conv's NHWC output (channel-padded on the HIP path) for
+        ``ops.diff_loss_nhwc`` instead of eps [B,3,H,W]."""
+        xz = batch.get("xz")
+        if xz is not None:
+            B = xz.shape[0] // 2
+            H, W = xz.shape[1], xz.shape[2]
+            xdt = xz.dtype
+        else:
+            x, z = batch["x"], batch["z"]
+            B, C, H, W = x.shape
+            xdt = x.dtype
         for key, v in batch.items():
-            assert v.shape[0] == B, f"{key} should have batch size {B}, not {v.shape[0]}"
+            if key != "xz":
+                assert v.shape[0] == B, f"{key} should have batch size {B}, not {v.shape[0]}"
         assert cond_mask.shape[0] == B
         assert (H, W) == (self.H, self.W), ((H, W), (self.H, self.W))
-        dt = self.compute_dtype or x.dtype
+        dt = self.compute_dtype or xdt
 
         sembs = self.conditioningprocessor(batch, cond_mask, dt)
         if self.batch_film:
@@ -390,7 +405,10 @@ class XUNet(nn.Module):
                                       [b.film.dense.bias for b in blocks])
                 for b, o in zip(blocks, outs):
                     b.__dict__["_ss"] = o
-        h = torch.stack([x, z], dim=1).reshape(2 * B, C, H, W).permute(0, 2, 3, 1).to(dt).contiguous()
+        if xz is not None:
+            h = xz.to(dt)
+        else:
+            h = torch.stack([x, z], dim=1).reshape(2 * B, C, H, W).permute(0, 2, 3, 1).to(dt).contiguous()
         h = ops.conv3x3(h, self.conv.weight, self.conv.bias)
 
         L = self.num_resolutions
@@ -412,13 +430,22 @@ class XUNet(nn.Module):
         assert not hs
         # only frame 1 (the target view) is returned by the reference
         h1 = self.lastgn(h[1::2].contiguous(), silu=True)
-        out = ops.conv3x3(h1, self.lastconv.weight, self.lastconv.bias)
+        out = ops.conv3x3(h1, self.lastconv.weight, self.lastconv.bias, keep_pad=head_nhwc)
+        if head_nhwc:
+            return out
         return out.permute(0, 3, 1, 2)
 
 
+_GOLDEN = 0x9E3779B97F4A7C15
+
+
 def _next_seed(block: ResnetBlock) -> int:
+    """64-bit dropout seed of one block: slot part + base * golden ratio.  The
+    HIP mask kernels of a graph replay add ``device_word * golden`` to a baked
+    slot part (base 0), so eager and replayed steps draw identical masks when
+    the device word equals the eager base seed (engine/graphs.py)."""
     base = getattr(block, "_base_seed", 0)
-    return (base * 1000003 + block._seed_slot * 7919 + 17) & 0x7FFFFFFF
+    return (block._seed_slot * 7919 + 17 + base * _GOLDEN) & 0xFFFFFFFFFFFFFFFF
 
 
 def count_params(model: nn.Module) -> int:

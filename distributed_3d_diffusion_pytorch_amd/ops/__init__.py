@@ -39,13 +39,20 @@ def gn_film(x, weight, bias, ss, groups: int = 32, eps: float = 1e-5, dropout_p:
 
 def conv3x3(x, weight, bias, stride: int = 1, residual: Optional[torch.Tensor] = None,
             out_scale: float = 1.0, row_bias: Optional[torch.Tensor] = None, res_period: int = 0,
-            gn_groups: int = 0, res_slot=None):
+            gn_groups: int = 0, res_slot=None, keep_pad: bool = False):
     """gn_groups: the output feeds a GroupNorm with that many groups (the HIP
     path then fuses that GroupNorm's statistics into the conv epilogue).
     res_slot / in_slot (HIP path; :class:`ResGradSlot`): hand the residual's /
-    the input's gradient to the GroupNorm that reads the same tensor."""
+    the input's gradient to the GroupNorm that reads the same tensor.
+    keep_pad: (IC or OC not a multiple of 8, i.e. stem / head) the HIP path
+    returns the channel-padded output (the fused loss reads it in place).
+    Inputs may carry zero channels beyond the weight's IC (pre-padded stem
+    input)."""
     if use_hip(x):
-        return _h().conv3x3(x, weight, bias, stride, residual, out_scale, row_bias, res_period, gn_groups, res_slot)
+        return _h().conv3x3(x, weight, bias, stride, residual, out_scale, row_bias, res_period, gn_groups, res_slot,
+                            keep_pad)
+    if x.shape[-1] > weight.shape[1]:
+        x = x[..., :weight.shape[1]]
     return _t.conv3x3(x, weight, bias, stride, residual, out_scale, row_bias, res_period)
 
 
@@ -91,6 +98,21 @@ def attention(qkv, heads: int, cross: bool):
     return _t.attention(qkv, heads, cross)
 
 
+def diffusion_inputs(img, seed: int, e0: int = 0, cond_prob: float = 0.1, logsnr_min: float = -20.0,
+                     logsnr_max: float = 20.0, dtype=torch.float32):
+    """Counter-based training-input draw (see torch_impl.diffusion_inputs);
+    one HIP launch for bf16 GPU runs."""
+    if dtype == torch.bfloat16 and img.is_cuda and use_hip(img, any_dtype=True):
+        return _h().diffusion_inputs(img, seed, e0, cond_prob, logsnr_min, logsnr_max, dtype)
+    return _t.diffusion_inputs(img, seed, e0, cond_prob, logsnr_min, logsnr_max, dtype)
+
+
+def diff_loss_nhwc(y, eps, loss_type: str = "l2"):
+    if use_hip(y):
+        return _h().diff_loss_nhwc(y, eps, loss_type)
+    return _t.diff_loss_nhwc(y, eps, loss_type)
+
+
 def avgpool2(x):
     if use_hip(x):
         return _h().avgpool2(x)
@@ -122,7 +144,7 @@ posenc_ddpm = _t.posenc_ddpm
 camera_rays = _t.camera_rays
 posenc_nerf = _t.posenc_nerf
 
-__all__ = ["group_norm", "gn_film", "conv3x3", "linear", "film_batch", "cat_gn_silu_dense", "cond_conv", "ray_posenc_dir",
+__all__ = ["diffusion_inputs", "diff_loss_nhwc", "group_norm", "gn_film", "conv3x3", "linear", "film_batch", "cat_gn_silu_dense", "cond_conv", "ray_posenc_dir",
            "ray_origin_pe", "attention", "avgpool2", "upsample2",
            "silu", "ray_posenc", "posenc_ddpm", "camera_rays", "posenc_nerf", "set_backend",
            "use_hip", "load_library", "library_error", "lib_path"]

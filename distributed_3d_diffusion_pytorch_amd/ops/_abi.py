@@ -31,7 +31,9 @@ SIGNATURES = {
     "d3d_upsample2": [P, P, I, I, I, I, I, P],
     "d3d_add_scale": [P, P, P, F, L, P],
     "d3d_sampler_step": [P, P, P, P, P, I, I, F, F, F, F, F, I, U64, P],
-    "d3d_diffusion_fwd": [P, P, P, P, P, P, P, I, I, U64, P],
+    "d3d_diffusion_fwd2": [P, I, I, U64, P, L, F, F, F, P, P, P, P, P],
+    "d3d_diff_loss": [P, P, I, I, I, I, P, P, P],
+    "d3d_diff_loss_bwd": [P, P, P, I, I, I, I, P, P],
     # adam.hip
     "d3d_adam": [P, P, P, P, P, L, F, F, F, F, F, F, F, F, P],
     "d3d_adam_dev": [P, P, P, P, P, L, P, P],

@@ -7,7 +7,11 @@
 //   add_scale                     : (a + b) * s residual epilogue (xunet.py:152,220)
 //   sampler_step                  : CFG combine + x0 clamp + posterior + noise
 //                                   (train.py:140-166 / sampling.py:85-127, on device)
-//   diffusion_fwd                 : q_sample + CFG-drop input noise (train.py:50-60,95-96)
+//   diffusion_fwd2                : the whole training-input draw of one step in one launch:
+//                                   t ~ U[0,1), lambda(t), eps, z_t = q_sample, CFG drop
+//                                   (train.py:50-60,80-100) -> the stem's NHWC bf16 input
+//   diff_loss / diff_loss_bwd     : l2 / l1 epsilon loss read straight from the padded
+//                                   NHWC head output (train.py:102-112)
 #include "common.h"
 
 namespace {
@@ -139,18 +143,117 @@ __global__ void sampler_step_k(const float* __restrict__ z, const float* __restr
   }
 }
 
-// q_sample + CFG drop on fp32 [B, D] images:
-//   z_t = alpha_b z + sigma_b eps ;  x' = mask_b ? x : N(0,1)
-__global__ void diffusion_fwd_k(const float* __restrict__ x, const float* __restrict__ z,
-                                const float* __restrict__ eps, const float* __restrict__ logsnr,
-                                const uint8_t* __restrict__ mask, float* __restrict__ zt, float* __restrict__ xc,
-                                int D, long total, uint64_t seed) {
-  GRID_LOOP(i, total) {
-    int b = (int)(i / D);
-    float l = logsnr[b];
-    float alpha = sqrtf(sigmoidf_(l)), sigma = sqrtf(sigmoidf_(-l));
-    zt[i] = alpha * z[i] + sigma * eps[i];
-    xc[i] = mask[b] ? x[i] : normal01(seed, (uint64_t)i);
+// Training-input draw (train.py:80-100), counter-based so that it is
+// reproducible per (step seed, global example index) -- micro-batches,
+// graph replays and the torch reference (ops/torch_impl.py
+// diffusion_inputs) all draw the same numbers:
+//   t_g    = u01(s, 4g)                 lambda = -2 log tan(a t + b)
+//   keep_g = u01(s, 4g + 1) > cond_prob
+//   eps    = N(s ^ K_EPS, g*3HW + c*HW + p)   x_noise = N(s ^ K_XN, same index)
+// Outputs: eps [B,3,H,W] fp32 (loss target), logsnr [B,2] (frame 0 = lambda(0)),
+// keep [B] u8, and the stem input xz [2B,H,W,8] bf16 (frame 0 = keep ? x :
+// x_noise, frame 1 = alpha z + sigma eps, channels 3..7 zero).
+// Graph replays pass seed_dev = the step's device seed block [dropout word,
+// draw word, example offset]: s = seed + sd[1] * golden, e0 += sd[2].
+#define K_EPS 0x5851F42D4C957F2Dull
+#define K_XN 0x14057B7EF767814Full
+__global__ void diffusion_fwd2_k(const float* __restrict__ img, int B, int HW, uint64_t seed,
+                                 const uint64_t* __restrict__ seed_dev, long e0, float cond_prob, float a, float b0,
+                                 float* __restrict__ eps_out, float* __restrict__ logsnr_out,
+                                 uint8_t* __restrict__ keep_out, bf16* __restrict__ xz) {
+  uint64_t s = seed;
+  if (seed_dev) {
+    s += seed_dev[1] * 0x9E3779B97F4A7C15ull;
+    e0 += (long)seed_dev[2];
+  }
+  const float lam0 = -2.f * logf(tanf(b0));
+  GRID_LOOP(i, (long)B * HW) {
+    const int bb = (int)(i / HW);
+    const int p = (int)(i - (long)bb * HW);
+    const uint64_t g = (uint64_t)(e0 + bb);
+    const float t = (hash_u32(s, 4 * g) >> 8) * (1.0f / 16777216.0f);
+    const float lam = -2.f * logf(tanf(a * t + b0));
+    const bool keep = (hash_u32(s, 4 * g + 1) >> 8) * (1.0f / 16777216.0f) > cond_prob;
+    const float alpha = sqrtf(1.f / (1.f + expf(-lam))), sigma = sqrtf(1.f / (1.f + expf(lam)));
+    const float* x = img + (size_t)bb * 6 * HW;
+    const float* z = x + 3 * (size_t)HW;
+    bf16x8 ox, oz;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { ox[c] = (bf16)0.f; oz[c] = (bf16)0.f; }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const uint64_t idx = g * 3 * (uint64_t)HW + (uint64_t)c * HW + p;
+      const float e = normal01(s ^ K_EPS, idx);
+      eps_out[(size_t)bb * 3 * HW + (size_t)c * HW + p] = e;
+      ox[c] = (bf16)(keep ? x[(size_t)c * HW + p] : normal01(s ^ K_XN, idx));
+      oz[c] = (bf16)(alpha * z[(size_t)c * HW + p] + sigma * e);
+    }
+    *reinterpret_cast<bf16x8*>(xz + ((size_t)2 * bb * HW + p) * 8) = ox;
+    *reinterpret_cast<bf16x8*>(xz + ((size_t)(2 * bb + 1) * HW + p) * 8) = oz;
+    if (p == 0) {
+      logsnr_out[2 * bb] = lam0;
+      logsnr_out[2 * bb + 1] = lam;
+      keep_out[bb] = keep ? 1 : 0;
+    }
+  }
+}
+
+// Epsilon loss over the padded NHWC head output y [B,H,W,CP] bf16 (first 3
+// channels valid) against eps [B,3,H,W] fp32: per-block partial sums over a
+// fixed grid (deterministic), then one block sums the partials in order.
+// mode 0: mean (y - eps)^2, 1: mean |y - eps|.
+#define LOSS_BLOCKS 256
+__global__ void __launch_bounds__(256) diff_loss_part_k(const bf16* __restrict__ y, const float* __restrict__ eps,
+                                                        int B, int HW, int CP, int mode, float* __restrict__ part) {
+  float acc = 0.f;
+  const long n = (long)B * HW;
+  GRID_LOOP(i, n) {
+    const int bb = (int)(i / HW);
+    const int p = (int)(i - (long)bb * HW);
+    const bf16* yp = y + (size_t)i * CP;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float d = (float)yp[c] - eps[(size_t)bb * 3 * HW + (size_t)c * HW + p];
+      acc += mode ? fabsf(d) : d * d;
+    }
+  }
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(256) diff_loss_final_k(const float* __restrict__ part, int nparts, float inv_n,
+                                                         float* __restrict__ out) {
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) acc += part[i];
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = ((red[0] + red[1]) + (red[2] + red[3])) * inv_n;
+}
+
+// dy [B,H,W,CP] bf16 = dL * d/dy loss (channels >= 3 zero); dL read from the
+// device (the upstream gradient of the scalar loss, e.g. a micro-batch weight).
+__global__ void diff_loss_bwd_k(const bf16* __restrict__ y, const float* __restrict__ eps,
+                                const float* __restrict__ dloss, int B, int HW, int CP, int mode, float inv_n,
+                                bf16* __restrict__ dy) {
+  const float g = dloss[0] * inv_n;
+  GRID_LOOP(i, (long)B * HW) {
+    const int bb = (int)(i / HW);
+    const int p = (int)(i - (long)bb * HW);
+    const bf16* yp = y + (size_t)i * CP;
+    bf16x8 o;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o[c] = (bf16)0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float d = (float)yp[c] - eps[(size_t)bb * 3 * HW + (size_t)c * HW + p];
+      o[c] = (bf16)(mode ? g * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) : 2.f * g * d);
+    }
+    *reinterpret_cast<bf16x8*>(dy + (size_t)i * CP) = o;
   }
 }
 }  // namespace
@@ -194,11 +297,27 @@ D3D_API int d3d_sampler_step(const float* z, const float* ec, const float* eu, c
                      alpha, sigma, alpha_n, c, var_sqrt, add_noise, (uint64_t)seed);
   return (int)hipGetLastError();
 }
-D3D_API int d3d_diffusion_fwd(const float* x, const float* z, const float* eps, const float* logsnr,
-                              const unsigned char* mask, float* zt, float* xc, int B, int D, unsigned long long seed,
-                              hipStream_t st) {
-  long total = (long)B * D;
-  hipLaunchKernelGGL(diffusion_fwd_k, dim3(ew_grid(total / 8 + 1)), dim3(256), 0, st, x, z, eps, logsnr, mask, zt,
-                     xc, D, total, (uint64_t)seed);
+D3D_API int d3d_diffusion_fwd2(const float* img, int B, int HW, unsigned long long seed, const void* seed_dev,
+                               long e0, float cond_prob, float a, float b0, float* eps, float* logsnr,
+                               unsigned char* keep, void* xz, hipStream_t st) {
+  long total = (long)B * HW;
+  hipLaunchKernelGGL(diffusion_fwd2_k, dim3(ew_grid(total)), dim3(256), 0, st, img, B, HW, (uint64_t)seed,
+                     (const uint64_t*)seed_dev, e0, cond_prob, a, b0, eps, logsnr, keep, (bf16*)xz);
+  return (int)hipGetLastError();
+}
+D3D_API int d3d_diff_loss(const void* y, const float* eps, int B, int HW, int CP, int mode, float* part, float* out,
+                          hipStream_t st) {
+  if (CP != 8) return -1;
+  hipLaunchKernelGGL(diff_loss_part_k, dim3(LOSS_BLOCKS), dim3(256), 0, st, (const bf16*)y, eps, B, HW, CP, mode,
+                     part);
+  hipLaunchKernelGGL(diff_loss_final_k, dim3(1), dim3(256), 0, st, part, LOSS_BLOCKS, 1.f / (3.f * B * HW), out);
+  return (int)hipGetLastError();
+}
+D3D_API int d3d_diff_loss_bwd(const void* y, const float* eps, const float* dloss, int B, int HW, int CP, int mode,
+                              void* dy, hipStream_t st) {
+  if (CP != 8) return -1;
+  long total = (long)B * HW;
+  hipLaunchKernelGGL(diff_loss_bwd_k, dim3(ew_grid(total)), dim3(256), 0, st, (const bf16*)y, eps, dloss, B, HW, CP,
+                     mode, 1.f / (3.f * B * HW), (bf16*)dy);
   return (int)hipGetLastError();
 }

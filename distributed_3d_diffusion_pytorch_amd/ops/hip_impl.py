@@ -219,14 +219,16 @@ def bf16_weight(w: torch.Tensor) -> torch.Tensor:
     return _cached(w, "bf16", lambda: w.detach().reshape(w.shape[0], -1).to(BF16), desc)
 
 
-# Per-step dropout seed on the device (graph replay: a captured kernel cannot
-# see a new Python seed, so the mask kernels add this device word to their
-# baked seed).  None in eager mode.
+# Per-step seed block on the device (graph replay: a captured kernel cannot
+# see a new Python seed): int64 [dropout word, input-draw word, example
+# offset].  The mask kernels add word 0 (x golden) to their baked seed, the
+# input draw adds word 1 and offsets its example index by word 2.  None in
+# eager mode.
 _SEED_DEV = [None]
 
 
 def set_device_seed(t: Optional[torch.Tensor]) -> None:
-    assert t is None or (t.dtype == torch.int64 and t.is_cuda and t.numel() >= 1)
+    assert t is None or (t.dtype == torch.int64 and t.is_cuda and t.numel() >= 3)
     _SEED_DEV[0] = t
 
 
@@ -504,7 +506,7 @@ class _GNFiLM(torch.autograd.Function):
 def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=False, seed=0):
     _need_bf16(x, ss)
     p = float(dropout_p) if training else 0.0
-    return _GNFiLM.apply(x, weight, bias, ss, groups, eps, p, int(seed) & 0x7FFFFFFFFFFFFFFF)
+    return _GNFiLM.apply(x, weight, bias, ss, groups, eps, p, int(seed) & 0xFFFFFFFFFFFFFFFF)
 
 
 # ----------------------------------------------------------------- conv ----
@@ -660,7 +662,7 @@ class _Conv(torch.autograd.Function):
 
 
 def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=None, res_period=0, gn_groups=0,
-            res_slot=None):
+            res_slot=None, keep_pad=False):
     """3x3 conv.  gn_groups > 0: the output feeds a GroupNorm with that many
     groups -- the conv epilogue then also emits the GroupNorm's partial
     statistics when its kernel can (attached to the output as ``_d3d_gnpart``
@@ -676,13 +678,13 @@ def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=No
     # stem (IC=3) / head (OC=3): zero-pad channels to a multiple of 8 so every
     # access stays 16-byte vectorised; the padding costs < 0.1 % of FLOPs.
     ICe, OCe = _up(IC, 8), _up(OC, 8)
-    xe = F.pad(x, (0, ICe - IC)) if ICe != IC else x
+    xe = F.pad(x, (0, ICe - x.shape[-1])) if x.shape[-1] != ICe else x      # (the fused input draw is pre-padded)
     we = F.pad(weight, (0, 0, 0, 0, 0, ICe - IC, 0, OCe - OC))
     be = F.pad(bias, (0, OCe - OC)) if bias is not None else None
     re = F.pad(residual, (0, OCe - OC)) if residual is not None else None
     rbe = F.pad(row_bias, (0, OCe - OC)) if row_bias is not None else None
     y = _Conv.apply(xe, we, be, stride, re, out_scale, rbe, res_period, 9)
-    return y[..., :OC].contiguous() if OCe != OC else y
+    return y[..., :OC].contiguous() if (OCe != OC and not keep_pad) else y
 
 
 # ------------------------------------------------- conditioning conv ------
@@ -1231,6 +1233,62 @@ def adam_flat_dev(p, g, m, v, ema, hp, refresh=True):
                            hp.data_ptr(), _st()), "adam_dev")
     if refresh:
         refresh_weights()
+
+
+# ------------------------------------------- training input and loss ---
+def diffusion_inputs(img, seed, e0=0, cond_prob=0.1, logsnr_min=-20.0, logsnr_max=20.0, dtype=BF16):
+    """One launch (diffusion_fwd2_k): t, lambda, eps, z_t, CFG drop -> the
+    stem's NHWC bf16 input, eps, logsnr [B,2], keep mask.  Same numbers as
+    ``torch_impl.diffusion_inputs``; in a graph replay the per-step part of the
+    seed is the device word of :func:`set_device_seed`."""
+    assert dtype == BF16
+    img = img.float().contiguous()
+    B, _, C, H, W = img.shape
+    assert C == 3, img.shape
+    dev = img.device
+    xz = torch.empty(2 * B, H, W, 8, dtype=BF16, device=dev)
+    eps = torch.empty(B, 3, H, W, dtype=F32, device=dev)
+    lam = torch.empty(B, 2, dtype=F32, device=dev)
+    keep = torch.empty(B, dtype=torch.uint8, device=dev)
+    a, b = _t.schedule_ab(logsnr_min, logsnr_max)
+    _chk(_lib.d3d_diffusion_fwd2(img.data_ptr(), B, H * W, int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(_SEED_DEV[0]), int(e0),
+                                 float(cond_prob), float(a), float(b), eps.data_ptr(), lam.data_ptr(),
+                                 keep.data_ptr(), xz.data_ptr(), _st()), "diffusion_fwd2")
+    return xz, eps, lam, keep.view(torch.bool)
+
+
+_LOSS_MODES = {"l2": 0, "l1": 1}
+
+
+class _DiffLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, eps, mode):
+        B, H, W, CP = y.shape
+        part = torch.empty(256, dtype=F32, device=y.device)
+        out = torch.empty((), dtype=F32, device=y.device)
+        _chk(_lib.d3d_diff_loss(y.data_ptr(), eps.data_ptr(), B, H * W, CP, mode, part.data_ptr(), out.data_ptr(),
+                                _st()), "diff_loss")
+        ctx.save_for_backward(y, eps)
+        ctx.mode = mode
+        return out
+
+    @staticmethod
+    def backward(ctx, dl):
+        y, eps = ctx.saved_tensors
+        B, H, W, CP = y.shape
+        dl = dl.float().contiguous()
+        dy = torch.empty_like(y)
+        _chk(_lib.d3d_diff_loss_bwd(y.data_ptr(), eps.data_ptr(), dl.data_ptr(), B, H * W, CP, ctx.mode,
+                                    dy.data_ptr(), _st()), "diff_loss_bwd")
+        return dy, None, None
+
+
+def diff_loss_nhwc(y, eps, loss_type="l2"):
+    """Epsilon loss read straight from the channel-padded NHWC head output
+    (two launches forward, one backward; deterministic partial sums)."""
+    if loss_type not in _LOSS_MODES or y.shape[-1] != 8 or y.dtype != BF16:
+        return _t.diff_loss_nhwc(y, eps, loss_type)
+    return _DiffLoss.apply(y.contiguous(), eps.float().contiguous(), _LOSS_MODES[loss_type])
 
 
 # ------------------------------------------------------------- sampler ---

@@ -241,3 +241,94 @@ def cat_gn_silu_dense(a, b, gw, gb, dw, db, groups: int = 32, eps: float = 1e-5)
     """silu(GN(cat[a, b])) and dense(cat[a, b]) (decoder block entry, oracle)."""
     x = torch.cat([a, b], -1)
     return group_norm(x, gw, gb, groups, eps, True), linear(x, dw, db)
+
+
+# ------------------------------------------------ training-input draw ----
+# Counter-based RNG shared bit-for-bit with the HIP kernels (common.h
+# hash_u32 / normal01; elementwise.hip diffusion_fwd2_k): splitmix64 of
+# (seed, index) in wrapping int64 arithmetic with logical shifts.
+_M64 = (1 << 64) - 1
+GOLDEN = 0x9E3779B97F4A7C15
+K_EPS = 0x5851F42D4C957F2D
+K_XN = 0x14057B7EF767814F
+
+
+def _s64(v: int) -> int:
+    v &= _M64
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def _lsr(z: torch.Tensor, k: int) -> torch.Tensor:
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def hash_u32(seed: int, idx: torch.Tensor) -> torch.Tensor:
+    """common.h ``hash_u32`` on an int64 index tensor -> values in [0, 2^32)."""
+    z = idx.to(torch.int64) + _s64(seed * GOLDEN + 0x632BE59BD9B4E019)
+    z = (z ^ _lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = (z ^ _lsr(z, 27)) * _s64(0x94D049BB133111EB)
+    z = z ^ _lsr(z, 31)
+    return _lsr(z, 32)
+
+
+def u01(seed: int, idx: torch.Tensor) -> torch.Tensor:
+    return (hash_u32(seed, idx) >> 8).to(torch.float32) * (1.0 / 16777216.0)
+
+
+def normal01(seed: int, idx: torch.Tensor) -> torch.Tensor:
+    idx = idx.to(torch.int64)
+    u1 = ((hash_u32(seed, 2 * idx) >> 8) + 1).to(torch.float32) * torch.tensor(1.0 / 16777217.0)
+    u2 = (hash_u32(seed, 2 * idx + 1) >> 8).to(torch.float32) * (1.0 / 16777216.0)
+    return torch.sqrt(-2.0 * torch.log(u1)) * torch.cos(6.283185307179586 * u2)
+
+
+def schedule_ab(logsnr_min: float, logsnr_max: float):
+    b = math.atan(math.exp(-0.5 * logsnr_max))
+    a = math.atan(math.exp(-0.5 * logsnr_min)) - b
+    return a, b
+
+
+def diffusion_inputs(img: torch.Tensor, seed: int, e0: int = 0, cond_prob: float = 0.1,
+                     logsnr_min: float = -20.0, logsnr_max: float = 20.0, dtype=torch.float32):
+    """The training-input draw of `train.py:80-100` for examples
+    ``e0 .. e0+B-1`` of a step whose RNG seed is ``seed`` (same numbers as
+    ``diffusion_fwd2_k``).  img [B,2,3,H,W] -> (xz [2B,H,W,8] NHWC stem input
+    (frame 0 = CFG-dropped x, frame 1 = z_t; channels 3..7 zero), eps
+    [B,3,H,W] fp32, logsnr [B,2], keep [B] bool)."""
+    B, _, C, H, W = img.shape
+    HW = H * W
+    dev = img.device
+    s = seed & _M64
+    g = torch.arange(B, device=dev, dtype=torch.int64) + e0
+    a, b = schedule_ab(logsnr_min, logsnr_max)
+    af, bf = torch.tensor(a, dtype=torch.float32), torch.tensor(b, dtype=torch.float32)
+    t = u01(s, 4 * g)
+    lam = -2.0 * torch.log(torch.tan(af.to(dev) * t + bf.to(dev)))
+    keep = u01(s, 4 * g + 1) > cond_prob
+    lam0 = (-2.0 * torch.log(torch.tan(bf))).to(dev).expand(B)
+    idx = g[:, None, None] * (3 * HW) + torch.arange(3, device=dev)[None, :, None] * HW + \
+        torch.arange(HW, device=dev)[None, None, :]
+    eps = normal01(s ^ K_EPS, idx).reshape(B, 3, H, W)
+    xn = normal01(s ^ K_XN, idx).reshape(B, 3, H, W)
+    alpha = torch.sqrt(torch.sigmoid(lam)).view(B, 1, 1, 1)
+    sigma = torch.sqrt(torch.sigmoid(-lam)).view(B, 1, 1, 1)
+    x, z = img[:, 0].float(), img[:, 1].float()
+    xc = torch.where(keep.view(B, 1, 1, 1), x, xn)
+    zt = alpha * z + sigma * eps
+    xz = torch.zeros(B, 2, H, W, 8, dtype=dtype, device=dev)
+    xz[:, 0, ..., :3] = xc.permute(0, 2, 3, 1).to(dtype)
+    xz[:, 1, ..., :3] = zt.permute(0, 2, 3, 1).to(dtype)
+    return xz.reshape(2 * B, H, W, 8), eps, torch.stack([lam0, lam], 1), keep
+
+
+def diff_loss_nhwc(y: torch.Tensor, eps: torch.Tensor, loss_type: str = "l2") -> torch.Tensor:
+    """Epsilon loss (`train.py:102-112`) on the NHWC head output y [B,H,W,>=3]
+    (only the first 3 channels are the prediction) against eps [B,3,H,W]."""
+    yh = y[..., :3].permute(0, 3, 1, 2).float()
+    if loss_type == "l2":
+        return torch.mean((eps.float() - yh) ** 2)
+    if loss_type == "l1":
+        return torch.mean((eps.float() - yh).abs())
+    if loss_type == "huber":
+        return F.smooth_l1_loss(yh, eps.float())
+    raise NotImplementedError(loss_type)

@@ -124,6 +124,10 @@ class GradReducer:
         for w, tmp, view in self._works:
             w.wait()
             if tmp is not None:
+                if tmp.is_cuda:
+                    # tmp was allocated on the sink's side stream; without this
+                    # the allocator may recycle it before the copy below runs
+                    tmp.record_stream(torch.cuda.current_stream(tmp.device))
                 view.copy_(tmp)
         self.reset()
 

@@ -9,7 +9,11 @@ torchrun worker would spawn its own children, P2).  Here:
 * otherwise :func:`spawn` self-launches ``nprocs`` workers on 127.0.0.1;
 * backend ``nccl`` (= RCCL on ROCm) for GPU tensors, ``gloo`` on CPU, with a
   finite timeout so a dead rank surfaces as an error instead of a hang;
-* ``torch.cuda.set_device(local_rank)`` before anything touches the GPU (D4).
+* ``torch.cuda.set_device(local_rank)`` before anything touches the GPU (D4);
+* RCCL hardening (:func:`rccl_env_defaults`): asynchronous error handling
+  tears a rank down when a collective fails or exceeds the timeout (so the
+  launcher's "one rank died" path ends the job instead of a silent hang), and
+  the watchdog's heartbeat monitor dumps the flight recorder of a stuck rank.
 """
 from __future__ import annotations
 
@@ -51,6 +55,24 @@ def env_world() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
+def rccl_env_defaults() -> None:
+    """Defaults for the ``nccl`` (= RCCL) process group, set before it is
+    created; an explicit setting in the environment always wins.
+
+    * ``TORCH_NCCL_ASYNC_ERROR_HANDLING=1``: a failed / timed-out collective
+      aborts the communicator and raises in the rank instead of leaving the
+      other ranks blocked inside RCCL kernels;
+    * ``TORCH_NCCL_ENABLE_MONITORING=1`` with a heartbeat timeout above the
+      collective timeout: a rank whose watchdog itself hangs is killed;
+    * ``TORCH_NCCL_DUMP_ON_TIMEOUT=0``: no flight-recorder files in the repo.
+    """
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    os.environ.setdefault("TORCH_NCCL_ENABLE_MONITORING", "1")
+    os.environ.setdefault("TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC", "1200")
+    os.environ.setdefault("TORCH_NCCL_DUMP_ON_TIMEOUT", "0")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (the only mode the host driver has)
+
+
 def init_distributed(backend: str = "auto", timeout_s: float = 600.0, use_gpu: Optional[bool] = None
                      ) -> DistContext:
     """Initialise from the environment (torchrun-compatible).  Single-process
@@ -75,7 +97,8 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0, use_gpu: O
         kw = dict(backend=backend, rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
-            kw["device_id"] = device
+            rccl_env_defaults()
+            kw["device_id"] = device        # eager communicator creation (no lazy init inside graph capture)
         dist.init_process_group(**kw)
     _CTX = DistContext(rank, world, local_rank, device, backend if world > 1 else "none")
     return _CTX

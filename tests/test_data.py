@@ -76,3 +76,20 @@ def test_loader(srn_root):
         assert len(batches) == 2
         img, R, T, K = batches[0]
         assert img.shape == (4, 2, 3, 16, 16) and R.dtype == torch.float64 and K.shape == (4, 3, 3)
+
+
+def test_persistent_workers_draw_new_pairs_each_epoch(srn_root):
+    """Persistent workers hold their own dataset copy; the epoch must reach
+    them through the sampler keys (pairs were frozen at epoch 0)."""
+    ds = SRNDataset("train", srn_root, "", imgsize=16)
+    sampler = ShardSampler(len(ds), 0, 1, shuffle=False, with_epoch=True)
+    dl = MultiEpochsDataLoader(ds, batch_size=3, sampler=sampler, num_workers=2)
+    seen = []
+    for epoch in range(3):
+        sampler.set_epoch(epoch)
+        ds.set_epoch(epoch)             # main-process copy only (what the trainer does)
+        seen.append(torch.cat([b[0] for b in dl]))
+    assert not torch.equal(seen[0], seen[1]) and not torch.equal(seen[1], seen[2])
+    # and it is the in-process draw for the same (epoch, index) key
+    ref = torch.from_numpy(np.stack([ds[(1, i)][0] for i in range(seen[1].shape[0])]))
+    assert torch.equal(seen[1], ref)

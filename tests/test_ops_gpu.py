@@ -422,8 +422,9 @@ def test_film_batch_with_gn_film(H, chans, blas):
 
 
 def test_graph_train_step_matches_eager():
-    """HIP-graph replayed training step == eager step (dropout off, same
-    generator stream): losses and parameters after 3 steps."""
+    """HIP-graph replayed training step == eager step (dropout ON: the graph
+    adds the same per-step device words the eager step uses as host seeds;
+    counter-based input draw): losses and parameters after 3 steps."""
     from distributed_3d_diffusion_pytorch_amd.config import make_config
     from distributed_3d_diffusion_pytorch_amd.engine import Trainer
     from distributed_3d_diffusion_pytorch_amd.parallel import DistContext
@@ -431,7 +432,7 @@ def test_graph_train_step_matches_eager():
     ctx = DistContext(device=torch.device("cuda", 0))
 
     def make(graph):
-        cfg = make_config(None, {"model.H": 32, "model.W": 32, "model.dropout": 0.0, "data.imgsize": 32,
+        cfg = make_config(None, {"model.H": 32, "model.W": 32, "model.dropout": 0.1, "data.imgsize": 32,
                                  "global_batch": 4, "micro_batch": 2, "data.synthetic": True, "log_every": 0,
                                  "ckpt_every": 0, "graph": graph, "optim.warmup_examples": 8})
         return Trainer(cfg, ctx)
@@ -642,3 +643,123 @@ def test_residual_grad_slot(H, kind):
 
     a, b = run(True), run(False)
     assert rel(a, b) < 1e-2, rel(a, b)
+
+
+def test_diffusion_inputs_kernel_matches_torch(H):
+    """diffusion_fwd2_k (one launch: t, lambda, eps, q_sample, CFG drop, NHWC
+    stem input) == the torch composition of the same counter-based draw."""
+    torch.manual_seed(3)
+    img = (torch.rand(24, 2, 3, 32, 32, device=DEV) * 2 - 1)
+    xz, eps, lam, keep = H.diffusion_inputs(img, 0xDEADBEEF12345678, e0=5, cond_prob=0.3)
+    xr, er, lr, kr = T.diffusion_inputs(img, 0xDEADBEEF12345678, e0=5, cond_prob=0.3, dtype=torch.float32)
+    assert torch.equal(keep, kr) and 0 < int((~keep).sum()) < 24
+    assert (lam - lr).abs().max().item() < 2e-4 * 20
+    assert (eps - er).abs().max().item() < 1e-3
+    assert (xz.float() - xr).abs().max().item() < 2e-2
+    # graph form: baked seed + device words [dropout, draw word, offset]
+    word, off = 7, 3
+    seed_blk = torch.tensor([0, word, off], dtype=torch.int64, device=DEV)
+    base = 0x1111
+    H.set_device_seed(seed_blk)
+    try:
+        xg, eg, lg, kg = H.diffusion_inputs(img, base, e0=0)
+    finally:
+        H.set_device_seed(None)
+    xe, ee, le, ke = H.diffusion_inputs(img, (base + word * 0x9E3779B97F4A7C15) & (2 ** 64 - 1), e0=off)
+    assert torch.equal(eg, ee) and torch.equal(xg, xe) and torch.equal(lg, le) and torch.equal(kg, ke)
+
+
+@pytest.mark.parametrize("loss_type", ["l2", "l1"])
+def test_diff_loss_kernel(H, loss_type):
+    torch.manual_seed(4)
+    y = torch.randn(6, 32, 32, 8, device=DEV).to(BF)
+    y[..., 3:] = 0
+    eps = torch.randn(6, 3, 32, 32, device=DEV)
+    yh = leaf(y)
+    yr = leaf(y, torch.float32)
+    lh = H.diff_loss_nhwc(yh, eps, loss_type)
+    lr_ = T.diff_loss_nhwc(yr, eps, loss_type)
+    assert abs(lh.item() - lr_.item()) < 1e-5 * abs(lr_.item())
+    (lh * 0.37).backward()
+    (lr_ * 0.37).backward()
+    assert rel(yh.grad, yr.grad) < 1e-2
+    assert float(yh.grad[..., 3:].abs().max()) == 0.0
+
+
+def _probe_worker(out_dir):
+    import datetime
+    import torch.distributed as dist
+    from distributed_3d_diffusion_pytorch_amd.parallel import cleanup
+    from distributed_3d_diffusion_pytorch_amd.parallel.dist import rccl_env_defaults
+    from distributed_3d_diffusion_pytorch_amd.engine.graphs import probe_graph_collective
+    # a 1-rank RCCL group (init_distributed skips the group at world 1; RCCL
+    # refuses two ranks on one device, so 1 rank is all a 1-GPU box can run)
+    rccl_env_defaults()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, timeout=datetime.timedelta(seconds=120))
+    ok = probe_graph_collective(dev)
+    with open(os.path.join(out_dir, "probe.txt"), "w") as f:
+        f.write(f"{int(ok)} {dist.get_backend()}")
+    cleanup()
+
+
+def test_rccl_allreduce_graph_capture_probe(tmp_path):
+    """The RCCL ("nccl") process group on this stack can capture an
+    all-reduce into a HIP graph and replay it correctly (the mechanism the
+    multi-GPU graph step overlaps its gradient reduction with)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from distributed_3d_diffusion_pytorch_amd.parallel import spawn
+    import test_ops_gpu as me
+    spawn(me._probe_worker, 1, (str(tmp_path),))
+    ok, be = open(tmp_path / "probe.txt").read().split()
+    assert be == "nccl" and ok == "1"
+
+
+def _graph_comm_worker(out_dir):
+    """world=2 RCCL: the graph step with the all-reduce captured inside graph
+    A must equal the eager bucketed step."""
+    import torch.distributed as dist
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    ctx = init_distributed("nccl", 180)
+
+    def make(graph):
+        cfg = make_config(None, {"model.H": 32, "model.W": 32, "data.imgsize": 32, "global_batch": 8,
+                                 "data.synthetic": True, "log_every": 0, "ckpt_every": 0, "graph": graph,
+                                 "optim.warmup_examples": 16, "dist.bucket_mb": 16.0})
+        return Trainer(cfg, ctx)
+
+    data = SyntheticBatches(4, 32, "cuda", seed=11 + ctx.rank)
+    batches = [next(data) for _ in range(3)]
+    res = []
+    for graph in (False, True):
+        tr = make(graph)
+        losses = [float(tr.train_step(*b)) for b in batches]
+        mode = tr._graphed.comm_mode if tr._graphed is not None else "eager"
+        p = tr.flat.data.clone()
+        other = p.clone()
+        dist.broadcast(other, 0)
+        res.append((losses, p, (p - other).abs().max().item(), mode))
+        del tr
+    (le, pe, de, _), (lg, pg, dg, mode) = res
+    with open(os.path.join(out_dir, f"gc{ctx.rank}.txt"), "w") as f:
+        f.write(f"{(pe - pg).abs().max().item()} {de} {dg} {max(abs(a - b) for a, b in zip(le, lg))} {mode}")
+    cleanup()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs 2 GPUs (RCCL: one rank per device)")
+def test_graph_step_rccl_captured_allreduce_two_gpus(tmp_path):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from distributed_3d_diffusion_pytorch_amd.parallel import spawn
+    import test_ops_gpu as me
+    spawn(me._graph_comm_worker, 2, (str(tmp_path),))
+    for r in range(2):
+        d, de, dg, dl, mode = open(tmp_path / f"gc{r}.txt").read().split()
+        assert mode == "graph"
+        assert float(de) == 0.0 and float(dg) == 0.0
+        assert float(d) < 5e-4 and float(dl) < 2e-3
