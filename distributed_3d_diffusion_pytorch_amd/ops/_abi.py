@@ -31,6 +31,9 @@ SIGNATURES = {
     "d3d_upsample2": [P, P, I, I, I, I, I, P],
     "d3d_add_scale": [P, P, P, F, L, P],
     "d3d_sampler_step": [P, P, P, P, P, I, I, F, F, F, F, F, I, U64, P],
+    "d3d_sampler_inputs": [P, P, I, I, P, P, U64, L, P, P, P],
+    "d3d_sampler_step2": [P, P, P, I, I, P, P, U64, L, P],
+    "d3d_randn_hash": [P, L, U64, L, P],
     "d3d_diffusion_fwd2": [P, I, I, U64, P, L, F, F, F, P, P, P, P, P],
     "d3d_diff_loss": [P, P, I, I, I, I, P, P, P],
     "d3d_diff_loss_bwd": [P, P, P, I, I, I, I, P, P],

@@ -143,6 +143,73 @@ __global__ void sampler_step_k(const float* __restrict__ z, const float* __restr
   }
 }
 
+// ---- graph-replayed sampler (engine/sampler.py GraphedSampler) ----------
+// Per-step scalars live in a device block (a replay cannot see new host
+// values): prm = [lambda, alpha, sigma, alpha_next, c, sqrt(var), add_noise,
+// lambda0]; the step's RNG word is sd[0] (s = seed + sd[0] * golden).
+// Noise is counter-based in the GLOBAL chain index (c0 + chain), so a chain
+// draws the same numbers whatever the rank sharding.
+#define K_XU 0xA0761D6478BD642Full
+#define K_NZ 0xE7037ED1A0B428DBull
+// CFG batch of one step: xz [4b,H,W,8] bf16 = per example j in [0,2b): frame 0
+// = x_cond (j < b) or N(0,1) (j >= b: the unconditional pass), frame 1 = z;
+// logsnr [2b,2] = (lambda0, lambda).
+__global__ void sampler_inputs_k(const float* __restrict__ xc, const float* __restrict__ z, int b, int HW,
+                                 const float* __restrict__ prm, const uint64_t* __restrict__ sd, uint64_t seed,
+                                 long c0, bf16* __restrict__ xz, float* __restrict__ logsnr) {
+  const uint64_t s = seed + (sd ? sd[0] : 0ull) * 0x9E3779B97F4A7C15ull;
+  GRID_LOOP(i, (long)2 * b * HW) {
+    const int j = (int)(i / HW);
+    const int p = (int)(i - (long)j * HW);
+    const int jb = j < b ? j : j - b;
+    bf16x8 ox, oz;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { ox[c] = (bf16)0.f; oz[c] = (bf16)0.f; }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const size_t e = (size_t)jb * 3 * HW + (size_t)c * HW + p;
+      oz[c] = (bf16)z[e];
+      ox[c] = (bf16)(j < b ? xc[e] : normal01(s ^ K_XU, (uint64_t)(c0 + jb) * 3 * HW + (uint64_t)c * HW + p));
+    }
+    *reinterpret_cast<bf16x8*>(xz + ((size_t)2 * j * HW + p) * 8) = ox;
+    *reinterpret_cast<bf16x8*>(xz + ((size_t)(2 * j + 1) * HW + p) * 8) = oz;
+    if (p == 0) {
+      logsnr[2 * j] = prm[7];
+      logsnr[2 * j + 1] = prm[0];
+    }
+  }
+}
+
+// Ancestral CFG step reading eps straight from the padded NHWC head output
+// y [2b,H,W,8] bf16 (rows [0,b) conditional, [b,2b) unconditional); z fp32
+// [b,3,H,W] updated in place.
+__global__ void sampler_step2_k(float* __restrict__ z, const bf16* __restrict__ y, const float* __restrict__ w,
+                                int b, int HW, const float* __restrict__ prm, const uint64_t* __restrict__ sd,
+                                uint64_t seed, long c0) {
+  const uint64_t s = seed + (sd ? sd[0] : 0ull) * 0x9E3779B97F4A7C15ull;
+  const float alpha = prm[1], sigma = prm[2], alpha_n = prm[3], c = prm[4], var_sqrt = prm[5];
+  const bool noise = prm[6] != 0.f;
+  GRID_LOOP(i, (long)b * 3 * HW) {
+    const int j = (int)(i / (3 * HW));
+    const int r = (int)(i - (long)j * 3 * HW);
+    const int ch = r / HW, p = r - ch * HW;
+    const float ec = (float)y[((size_t)j * HW + p) * 8 + ch];
+    const float eu = (float)y[((size_t)(j + b) * HW + p) * 8 + ch];
+    const float wb = w[j];
+    const float e = (1.f + wb) * ec - wb * eu;
+    const float zi = z[i];
+    const float x0 = fminf(fmaxf((zi - sigma * e) / alpha, -1.f), 1.f);
+    float m = alpha_n * (zi * (1.f - c) / alpha + c * x0);
+    if (noise) m += var_sqrt * normal01(s ^ K_NZ, (uint64_t)(c0 + j) * 3 * HW + r);
+    z[i] = m;
+  }
+}
+
+// Counter-based N(0,1) fill: out[i] = N(seed ^ key, off + i)
+__global__ void randn_hash_k(float* __restrict__ out, long n, uint64_t seed, long off) {
+  GRID_LOOP(i, n) out[i] = normal01(seed, (uint64_t)(off + i));
+}
+
 // Training-input draw (train.py:80-100), counter-based so that it is
 // reproducible per (step seed, global example index) -- micro-batches,
 // graph replays and the torch reference (ops/torch_impl.py
@@ -295,6 +362,24 @@ D3D_API int d3d_sampler_step(const float* z, const float* ec, const float* eu, c
   long total = (long)b * D;
   hipLaunchKernelGGL(sampler_step_k, dim3(ew_grid(total / 8 + 1)), dim3(256), 0, st, z, ec, eu, w, out, D, total,
                      alpha, sigma, alpha_n, c, var_sqrt, add_noise, (uint64_t)seed);
+  return (int)hipGetLastError();
+}
+D3D_API int d3d_sampler_inputs(const float* xc, const float* z, int b, int HW, const float* prm, const void* sd,
+                               unsigned long long seed, long c0, void* xz, float* logsnr, hipStream_t st) {
+  long total = (long)2 * b * HW;
+  hipLaunchKernelGGL(sampler_inputs_k, dim3(ew_grid(total)), dim3(256), 0, st, xc, z, b, HW, prm,
+                     (const uint64_t*)sd, (uint64_t)seed, c0, (bf16*)xz, logsnr);
+  return (int)hipGetLastError();
+}
+D3D_API int d3d_sampler_step2(float* z, const void* y, const float* w, int b, int HW, const float* prm,
+                              const void* sd, unsigned long long seed, long c0, hipStream_t st) {
+  long total = (long)b * 3 * HW;
+  hipLaunchKernelGGL(sampler_step2_k, dim3(ew_grid(total)), dim3(256), 0, st, z, (const bf16*)y, w, b, HW, prm,
+                     (const uint64_t*)sd, (uint64_t)seed, c0);
+  return (int)hipGetLastError();
+}
+D3D_API int d3d_randn_hash(float* out, long n, unsigned long long seed, long off, hipStream_t st) {
+  hipLaunchKernelGGL(randn_hash_k, dim3(ew_grid(n)), dim3(256), 0, st, out, n, (uint64_t)seed, off);
   return (int)hipGetLastError();
 }
 D3D_API int d3d_diffusion_fwd2(const float* img, int B, int HW, unsigned long long seed, const void* seed_dev,

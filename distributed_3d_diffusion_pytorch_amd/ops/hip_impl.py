@@ -1292,6 +1292,29 @@ def diff_loss_nhwc(y, eps, loss_type="l2"):
 
 
 # ------------------------------------------------------------- sampler ---
+def sampler_inputs(xc, z, prm, sd, seed, c0, xz, logsnr):
+    b = z.shape[0]
+    HW = z.shape[-1] * z.shape[-2]
+    _chk(_lib.d3d_sampler_inputs(xc.data_ptr(), z.data_ptr(), b, HW, prm.data_ptr(), _ptr(sd),
+                                 int(seed) & 0xFFFFFFFFFFFFFFFF, int(c0), xz.data_ptr(), logsnr.data_ptr(), _st()),
+         "sampler_inputs")
+
+
+def sampler_step2(z, y, w, prm, sd, seed, c0):
+    b = z.shape[0]
+    HW = z.shape[-1] * z.shape[-2]
+    assert y.shape[-1] == 8 and y.shape[0] == 2 * b and z.is_contiguous()
+    _chk(_lib.d3d_sampler_step2(z.data_ptr(), y.data_ptr(), w.data_ptr(), b, HW, prm.data_ptr(), _ptr(sd),
+                                int(seed) & 0xFFFFFFFFFFFFFFFF, int(c0), _st()), "sampler_step2")
+
+
+def randn_hash(shape, seed, off, device):
+    out = torch.empty(shape, dtype=F32, device=device)
+    _chk(_lib.d3d_randn_hash(out.data_ptr(), out.numel(), int(seed) & 0xFFFFFFFFFFFFFFFF, int(off), _st()),
+         "randn_hash")
+    return out
+
+
 def sampler_step(z, eps_c, eps_u, w, alpha, sigma, alpha_n, c, var_sqrt, add_noise, seed):
     b = z.shape[0]
     D = z[0].numel()

@@ -251,6 +251,9 @@ _M64 = (1 << 64) - 1
 GOLDEN = 0x9E3779B97F4A7C15
 K_EPS = 0x5851F42D4C957F2D
 K_XN = 0x14057B7EF767814F
+K_XU = 0xA0761D6478BD642F       # sampler: unconditional-pass input noise
+K_NZ = 0xE7037ED1A0B428DB       # sampler: ancestral-step noise
+K_Z0 = 0x8EBC6AF09C88C6E3       # sampler: initial z
 
 
 def _s64(v: int) -> int:

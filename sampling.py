@@ -95,9 +95,10 @@ def run(args) -> None:
     s, e = shard_range(len(w_all), ctx.rank, ctx.world)
     w = w_all[s:e]
     b = len(w)
-    sampler = DiffusionSampler(model, args.timesteps, args.ref_quirk, seed=args.seed * 1000 + ctx.rank,
-                               device=dev)
-    sampler.choice_rng.seed(args.seed)        # identical record choices on every rank
+    # same seed on every rank: identical record choices, and the counter-based
+    # noise is keyed by the GLOBAL chain index (chain_offset), so the gathered
+    # result does not depend on the number of ranks
+    sampler = DiffusionSampler(model, args.timesteps, args.ref_quirk, seed=args.seed, device=dev, chain_offset=s)
     t = lambda a: torch.tensor(a, dtype=torch.float32, device=dev)  # noqa: E731
     record = [RecordEntry(t(imgs[0])[None].expand(b, -1, -1, -1).contiguous(), t(Rs[0]), t(Ts[0]))]
     if ctx.is_main:

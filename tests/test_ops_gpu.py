@@ -763,3 +763,52 @@ def test_graph_step_rccl_captured_allreduce_two_gpus(tmp_path):
         assert mode == "graph"
         assert float(de) == 0.0 and float(dg) == 0.0
         assert float(d) < 5e-4 and float(dl) < 2e-3
+
+
+def test_sampler_step2_matches_posterior(H):
+    """Graph-form CFG step (eps read from the padded NHWC head output, scalars
+    from the device block) == cfg_posterior + the counter-based noise."""
+    from distributed_3d_diffusion_pytorch_amd.diffusion import cfg_posterior
+    from distributed_3d_diffusion_pytorch_amd.engine import DiffusionSampler
+    torch.manual_seed(12)
+    b, S = 3, 16
+    y = torch.randn(2 * b, S, S, 8, device=DEV).to(BF)
+    z = torch.randn(b, 3, S, S, device=DEV)
+    w = torch.tensor([0.0, 2.0, 5.0], device=DEV)
+    smp = DiffusionSampler(torch.nn.Linear(1, 1).to(DEV), timesteps=8, seed=3, chain_offset=4)
+    for k in (2, 7):
+        prm = torch.tensor(smp.params(k), device=DEV)
+        zz = z.clone()
+        H.sampler_step2(zz, y, w, prm, None, smp.step_seed(k), 4)
+        ec = y[:b, ..., :3].float().permute(0, 3, 1, 2)
+        eu = y[b:, ..., :3].float().permute(0, 3, 1, 2)
+        mean, var = cfg_posterior(z, ec, eu, w, torch.tensor(smp.lam[k]), torch.tensor(smp.lam_next[k]))
+        if smp.add_noise(k):
+            mean = mean + var.sqrt() * smp._noise(T.K_NZ, k, (b, 3, S, S), torch.device(DEV))
+        assert (zz - mean).abs().max().item() < 1e-4
+
+
+def test_sampler_graph_replay_matches_eager():
+    """256-step sampler: the HIP-graph replayed step == the eager step with the
+    same kernels and seeds (a few steps, 2 record entries)."""
+    from distributed_3d_diffusion_pytorch_amd.models import XUNet
+    from distributed_3d_diffusion_pytorch_amd.engine import DiffusionSampler, RecordEntry
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    torch.manual_seed(13)
+    m = XUNet(H=32, W=32, ch=128).to(DEV)
+    with torch.no_grad():
+        for p in m.parameters():
+            if p.abs().sum() == 0:
+                p.normal_(0, 0.02)
+    m.compute_dtype = BF
+    m.eval()
+    img, R, t, K = next(SyntheticBatches(4, 32, DEV, seed=1))
+    rec = [RecordEntry(img[:, 0].contiguous(), R[0, 0].float(), t[0, 0].float()),
+           RecordEntry(img[:, 1].contiguous(), R[1, 0].float(), t[1, 0].float())]
+    w = torch.tensor([0.0, 1.0, 2.0, 3.0])
+    outs = []
+    for graph in (False, True):
+        smp = DiffusionSampler(m, timesteps=5, seed=9, device=torch.device(DEV), graph=graph)
+        outs.append(smp.sample(rec, R[2, 1].float(), t[2, 1].float(), K[0].float(), w))
+    assert torch.isfinite(outs[0]).all()
+    assert (outs[0] - outs[1]).abs().max().item() < 1e-3

@@ -95,10 +95,9 @@ def test_sampler_cfg_batched_equals_separate():
     from helpers import tiny_batch
     b = tiny_batch(B)
     R, T, K = b["R"], b["t"], b["K"]
-    smp.gen.manual_seed(5)
-    ec, eu = smp.denoise_eps(b["x"], b["z"], R, T, K, 1.0)
-    smp.gen.manual_seed(5)
-    x_unc = torch.randn(b["x"].shape, generator=smp.gen)
+    ec, eu = smp.denoise_eps(b["x"], b["z"], R, T, K, 1.0, k=3)
+    from distributed_3d_diffusion_pytorch_amd.ops import torch_impl as TI
+    x_unc = smp._noise(TI.K_XU, 3, tuple(b["x"].shape), b["x"].device)
     lam = torch.full((B,), 1.0)
     base = {"z": b["z"], "logsnr": torch.stack([torch.full_like(lam, smp.lam0), lam], 1), "R": R, "t": T, "K": K}
     ec2 = m(dict(base, x=b["x"]), cond_mask=torch.ones(B, dtype=torch.bool))
@@ -116,6 +115,23 @@ def test_sampler_quirk_and_shards():
         assert out.shape == (2, 3, 16, 16) and torch.isfinite(out).all()
     spans = [shard_range(8, r, 3) for r in range(3)]
     assert spans == [(0, 3), (3, 6), (6, 8)]
+
+
+def test_sampler_chains_independent_of_sharding():
+    """Counter-based noise keyed by the GLOBAL chain index: chains 2..4 of a
+    5-chain run equal a 3-chain run with chain_offset=2 (what rank r of a
+    multi-GPU sampling job computes)."""
+    m = tiny_model().eval()
+    K = torch.tensor([[20.0, 0, 8], [0, 20.0, 8], [0, 0, 1]])
+    img = torch.rand(5, 3, 16, 16) * 2 - 1
+    w = torch.tensor([0.0, 1.0, 2.0, 3.0, 4.0])
+    outs = []
+    for lo, hi in ((0, 5), (2, 5)):
+        smp = DiffusionSampler(m, timesteps=3, seed=7, chain_offset=lo)
+        rec = [RecordEntry(img[lo:hi], torch.eye(3), torch.tensor([0.0, 0.0, 1.3])),
+               RecordEntry(img[lo:hi].flip(-1), torch.eye(3), torch.tensor([0.0, 1.3, 0.0]))]
+        outs.append(smp.sample(rec, torch.eye(3), torch.tensor([1.3, 0.0, 0.0]), K, w[lo:hi]))
+    torch.testing.assert_close(outs[1], outs[0][2:], rtol=1e-4, atol=1e-5)
 
 
 def test_lightning_cli_layout(srn_root, tmp_path):

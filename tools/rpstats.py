@@ -12,6 +12,9 @@ def main():
     ap.add_argument("--steps", type=int, default=0, help="divide totals by K (per-step ms)")
     ap.add_argument("--top", type=int, default=45)
     ap.add_argument("--grid", action="store_true", help="split rows by grid size")
+    ap.add_argument("--window", type=float, default=0.0,
+                    help="only kernels that start within the last WINDOW ms of the trace (steady-state steps; "
+                         "warm-up / capture passes excluded)")
     ap.add_argument("--busy", type=float, default=0.0,
                     help="occupancy of the last BUSY ms of the trace: union of kernel intervals vs span vs the sum "
                          "of kernel times (>1 overlap factor = concurrent kernels)")
@@ -46,7 +49,11 @@ def main():
         return
     agg = defaultdict(lambda: [0.0, 0])
     t0, t1 = None, None
-    for r in db.execute(q):
+    rows = list(db.execute(q))
+    if a.window:
+        last = max(r[2] for r in rows)
+        rows = [r for r in rows if r[1] >= last - a.window * 1e6]
+    for r in rows:
         nm = r[0]
         short = nm.replace("(anonymous namespace)::", "").split("(")[0][:100]
         if a.grid and gx:
