@@ -89,6 +89,20 @@ def _need_bf16(*ts):
             raise TypeError(f"HIP kernels take bf16 activations, got {t.dtype}")
 
 
+# Shapes a HIP kernel does not cover run the torch composition instead; each
+# such (op, shape) is reported once on stderr and counted here so tests and
+# benchmarks can assert that the hot path never falls back.
+FALLBACKS: Dict[str, int] = {}
+
+
+def _fallback(op: str, why: str) -> None:
+    key = f"{op}: {why}"
+    if key not in FALLBACKS:
+        import sys
+        print(f"[d3d] HIP {op} falls back to the torch composition ({why})", file=sys.stderr, flush=True)
+    FALLBACKS[key] = FALLBACKS.get(key, 0) + 1
+
+
 def _up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
@@ -1028,6 +1042,7 @@ def film_batch(semb, weights, biases):
     K = semb.shape[-1]
     widths = [w.shape[0] for w in weights]
     if K % 8 or any(wd % 8 for wd in widths) or len(weights) > 16:
+        _fallback("film_batch", f"K={K} widths={widths}")
         return tuple(linear(semb, w, b) for w, b in zip(weights, biases))
     slot = _FiLMSlot(semb.shape[:-1], sum(widths), semb.device)
     outs = _FiLMBatch.apply(semb.contiguous(), slot, len(weights), *weights, *biases)
@@ -1085,7 +1100,8 @@ def attention(qkv, heads, cross):
     N, L, C3 = qkv.shape
     D = C3 // 3 // heads
     if L % 64 != 0 or D not in (64, 128) or (cross and N % 2):
-        return _t.attention(qkv, heads, cross)  # tiny test shapes only
+        _fallback("attention", f"L={L} head_dim={D} N={N} cross={cross}")
+        return _t.attention(qkv, heads, cross)
     return _Attention.apply(qkv, heads, cross)
 
 
