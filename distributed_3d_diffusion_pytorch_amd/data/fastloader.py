@@ -1,0 +1,123 @@
+"""Batch-level real-data feed for the GPU trainer (reference loader:
+`SRNdataset.py:12-95` -- per-item PNG decode in 16 worker processes).
+
+At the MI355X step rate (~500 examples/s per GPU at 16 per GPU, several
+thousand per node) a per-item decode pipeline is the bottleneck (SURVEY 7.3
+item 8).  This loader reads the preprocessed memory-mapped cache
+(:mod:`.cache`) a whole batch at a time:
+
+* one background thread per rank gathers the batch's view pairs with
+  vectorised fancy indexing straight from the ``uint8`` mmap (no decode, no
+  per-item Python tensors, no worker processes or IPC);
+* the batch crosses PCIe as ``uint8`` (4x fewer bytes than fp32) from a
+  pinned staging buffer, on a side HIP stream, one step AHEAD of the consumer
+  (the copy of batch k+1 overlaps the training step on batch k);
+* normalisation to [-1, 1] and the NHWC->NCHW view change run on the device,
+  on the consumer's stream after an event wait.
+
+Items are exactly those of :class:`.cache.CachedSRNDataset` for the same
+``(epoch, index)`` keys (same per-key pair draw), so switching loaders does
+not change the data a run sees.
+"""
+from __future__ import annotations
+
+import queue
+import random
+import threading
+from typing import Iterator, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .cache import CachedSRNDataset
+from .srn import split_key
+
+
+class CachedBatchLoader:
+    def __init__(self, ds: CachedSRNDataset, batch_size: int, sampler, device, drop_last: bool = True,
+                 prefetch: int = 2):
+        self.ds, self.B, self.sampler = ds, int(batch_size), sampler
+        self.device = torch.device(device)
+        self.drop_last = drop_last
+        self.prefetch = max(1, int(prefetch))
+
+    def __len__(self) -> int:
+        n = len(self.sampler)
+        return n // self.B if self.drop_last else (n + self.B - 1) // self.B
+
+    # ---------------------------------------------------------------- host
+    def gather(self, keys: Sequence) -> tuple:
+        """uint8 images [B,2,H,W,3], R [B,2,3,3] f64, T [B,2,3] f64, K [B,3,3]
+        f64 for a list of dataset keys (vectorised over the batch)."""
+        images, poses, counts, Ks = self.ds._load()
+        B = len(keys)
+        rows = np.empty(B, np.int64)
+        views = np.empty((B, 2), np.int64)
+        for i, key in enumerate(keys):
+            epoch, idx = split_key(key, self.ds.epoch)
+            r = self.ds.rows[idx]
+            rng = random.Random((self.ds.seed * 1000003 + epoch) * 1000003 + idx)
+            views[i] = rng.sample(range(int(counts[r])), 2)
+            rows[i] = r
+        rr = np.repeat(rows, 2)
+        img = images[rr, views.reshape(-1)].reshape(B, 2, *images.shape[2:])   # one fancy-index read
+        P = poses[rows[:, None], views]                                         # [B,2,4,4]
+        return img, P[:, :, :3, :3].copy(), P[:, :, :3, 3].copy(), Ks[rows].copy()
+
+    def _producer(self, batches: List[List], q: "queue.Queue") -> None:
+        try:
+            for keys in batches:
+                img, R, T, K = self.gather(keys)
+                t = torch.from_numpy(np.ascontiguousarray(img))
+                if self.device.type == "cuda":
+                    t = t.pin_memory()
+                q.put((t, torch.from_numpy(R), torch.from_numpy(T), torch.from_numpy(K)))
+        except BaseException as e:          # surface loader errors in the consumer
+            q.put(e)
+        q.put(None)
+
+    # -------------------------------------------------------------- device
+    def __iter__(self) -> Iterator[tuple]:
+        keys = list(iter(self.sampler))
+        nb = len(self)
+        batches = [keys[i * self.B:(i + 1) * self.B] for i in range(nb)]
+        q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
+        th = threading.Thread(target=self._producer, args=(batches, q), daemon=True)
+        th.start()
+        cuda = self.device.type == "cuda"
+        side = torch.cuda.Stream(device=self.device) if cuda else None
+
+        def upload(item):
+            u8, R, T, K = item
+            if not cuda:
+                return (u8, R, T, K), None
+            with torch.cuda.stream(side):
+                out = (u8.to(self.device, non_blocking=True), R.to(self.device, non_blocking=True),
+                       T.to(self.device, non_blocking=True), K.to(self.device, non_blocking=True))
+                ev = torch.cuda.Event()
+                ev.record(side)
+            return out, ev
+
+        def finish(dev_item, ev):
+            u8, R, T, K = dev_item
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                for t in dev_item:
+                    t.record_stream(torch.cuda.current_stream(self.device))
+            img = u8.permute(0, 1, 4, 2, 3).float().mul_(2.0 / 255.0).sub_(1.0)    # [B,2,3,H,W] in [-1,1]
+            return img, R, T, K
+
+        pending = None
+        while True:
+            item = q.get()
+            if isinstance(item, BaseException):
+                raise item
+            if item is None:
+                break
+            nxt = upload(item)              # H2D of batch k+1 is queued before batch k is consumed
+            if pending is not None:
+                yield finish(*pending)
+            pending = nxt
+        if pending is not None:
+            yield finish(*pending)
+        th.join()

@@ -271,13 +271,16 @@ class Trainer:
             it = SyntheticBatches(self.local_batch, dc.imgsize, self.device,
                                   seed=dc.seed * 7919 + self.ctx.rank)
             return it, None, None
-        from ..data import SRNDataset, ShardSampler, MultiEpochsDataLoader, CachedSRNDataset
+        from ..data import SRNDataset, ShardSampler, MultiEpochsDataLoader, CachedSRNDataset, CachedBatchLoader
         if dc.cache:
             ds = CachedSRNDataset("train", dc.cache, seed=dc.seed)
         else:
             ds = SRNDataset("train", dc.path, dc.index, dc.imgsize, seed=dc.seed)
         sampler = ShardSampler(len(ds), self.ctx.rank, self.ctx.world, shuffle=True, seed=dc.seed,
                                with_epoch=True)
+        if dc.cache:
+            # batch-level mmap gather + uint8 pinned H2D one step ahead (data/fastloader.py)
+            return CachedBatchLoader(ds, self.local_batch, sampler, self.device), ds, sampler
         loader = MultiEpochsDataLoader(ds, batch_size=self.local_batch, sampler=sampler,
                                        num_workers=dc.num_workers, drop_last=True,
                                        pin_memory=self.device.type == "cuda")

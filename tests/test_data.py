@@ -93,3 +93,36 @@ def test_persistent_workers_draw_new_pairs_each_epoch(srn_root):
     # and it is the in-process draw for the same (epoch, index) key
     ref = torch.from_numpy(np.stack([ds[(1, i)][0] for i in range(seen[1].shape[0])]))
     assert torch.equal(seen[1], ref)
+
+
+def test_cached_batch_loader_matches_dataset_and_feeds_fast(tmp_path):
+    """Batch loader over the uint8 mmap cache: identical items to
+    CachedSRNDataset for the same (epoch, index) keys; throughput far above
+    the per-GPU consumption (~500 pairs/s at 16 per GPU)."""
+    import time
+    from distributed_3d_diffusion_pytorch_amd.data import build_cache, CachedSRNDataset, CachedBatchLoader
+    root = str(tmp_path / "srn")
+    write_synthetic_srn(root, num_instances=40, num_views=6, size=64, seed=3)
+    cache = build_cache(root, str(tmp_path / "cache"), 64)
+    ds = CachedSRNDataset("train", cache, seed=1)
+    sampler = ShardSampler(len(ds), 0, 1, shuffle=True, seed=2, with_epoch=True)
+    sampler.set_epoch(3)
+    dl = CachedBatchLoader(ds, 8, sampler, "cpu")
+    keys = list(sampler)
+    got = list(dl)
+    assert len(got) == len(dl) == len(keys) // 8
+    for bi, (img, R, T, K) in enumerate(got):
+        assert img.shape == (8, 2, 3, 64, 64) and img.dtype == torch.float32
+        for j in range(8):
+            ref = ds[keys[bi * 8 + j]]
+            assert np.allclose(img[j].numpy(), ref[0], atol=1e-6)
+            assert np.allclose(R[j].numpy(), ref[1]) and np.allclose(T[j].numpy(), ref[2])
+            assert np.allclose(K[j].numpy(), ref[3])
+    # host-side gather rate (what one rank's producer thread sustains)
+    big = [(0, i % len(ds)) for i in range(4096)]
+    t0 = time.perf_counter()
+    for i in range(0, len(big), 16):
+        dl.gather(big[i:i + 16])
+    rate = len(big) / (time.perf_counter() - t0)
+    print(f"cached batch gather: {rate:.0f} pairs/s")
+    assert rate > 4000, rate
