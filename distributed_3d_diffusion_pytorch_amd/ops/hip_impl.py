@@ -829,38 +829,70 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         return torch.mm(a, b).float()
 
 
+# Dense-layer dispatch.  In isolation the MFMA implicit-GEMM kernels (taps =
+# 1) beat hipBLASLt on the small per-pixel GEMMs of the small-batch step (the
+# attention projections / 1x1 convs at 16 examples per GPU: 1-4 GFLOP, 16 vs
+# 24 us, profiles/kbench_linear_r2.txt) and fuse the residual / scale
+# epilogue -- but inside the replayed training step they measured SLOWER
+# (bs16 31.4 -> 32.2 ms for the input-gradient GEMMs, 32.2 -> 33.1 ms for the
+# forward ones, profiles/ab_linear_dispatch_r2.txt): off by default (0),
+# enabled per GEMM size by D3D_LIN_HIP_FWD_FLOP / D3D_LIN_HIP_DGRAD_FLOP.
+_LIN_HIP_FWD_FLOP = float(os.environ.get("D3D_LIN_HIP_FWD_FLOP", "0"))
+_LIN_HIP_DGRAD_FLOP = float(os.environ.get("D3D_LIN_HIP_DGRAD_FLOP", "0"))
+
+
+def _lin_hip_fwd(P: int, IC: int, OC: int) -> bool:
+    return _LIN_HIP_FWD_FLOP > 0 and IC % 8 == 0 and OC % 8 == 0 and OC >= 64 and 2.0 * P * IC * OC <= _LIN_HIP_FWD_FLOP
+
+
+def _lin_hip_dgrad(P: int, IC: int, OC: int) -> bool:
+    # the input-gradient GEMM reduces over OC: short reductions (OC < IC)
+    # leave the tiled kernel prologue-bound
+    return _LIN_HIP_DGRAD_FLOP > 0 and IC % 8 == 0 and OC % 8 == 0 and IC >= 64 and OC >= IC and 2.0 * P * IC * OC <= _LIN_HIP_DGRAD_FLOP
+
+
 class _Linear(torch.autograd.Function):
-    """Per-pixel dense layer on hipBLASLt (plain library GEMM) with the
-    residual/scale epilogue done by a fused HIP elementwise kernel."""
+    """Per-pixel dense layer: hand-written MFMA GEMM (conv kernels, taps=1)
+    with the bias / residual / scale epilogue fused for small problems, the
+    hipBLASLt library GEMM + a fused HIP epilogue kernel for large ones."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, residual, out_scale, res_slot=None, in_slot=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        wb = bf16_weight(weight)
-        if bias is not None:
-            y = torch.addmm(bf16_weight(bias), x2, wb.t())
+        P, IC = x2.shape
+        OC = weight.shape[0]
+        if _lin_hip_fwd(P, IC, OC):
+            x2 = x2.contiguous()
+            y = torch.empty(P, OC, dtype=BF16, device=x.device)
+            r = residual.reshape(P, OC).contiguous() if residual is not None else None
+            _conv_fwd(x2, packed_weight(weight, False, 1), bias, None, r, y, P, 1, 1, IC, _up(IC, 64), 1, 1, OC, OC,
+                      1, False, float(out_scale), 0, 1)
+            wb = None
         else:
-            y = torch.mm(x2, wb.t())
-        if residual is not None or out_scale != 1.0:
-            r = residual.reshape(y.shape).contiguous() if residual is not None else None
-            _chk(_lib.d3d_add_scale(y.data_ptr(), _ptr(r), y.data_ptr(), float(out_scale), y.numel(), _st()),
-                 "add_scale")
+            wb = bf16_weight(weight)
+            if bias is not None:
+                y = torch.addmm(bf16_weight(bias), x2, wb.t())
+            else:
+                y = torch.mm(x2, wb.t())
+            if residual is not None or out_scale != 1.0:
+                r = residual.reshape(y.shape).contiguous() if residual is not None else None
+                _chk(_lib.d3d_add_scale(y.data_ptr(), _ptr(r), y.data_ptr(), float(out_scale), y.numel(), _st()),
+                     "add_scale")
         ctx.save_for_backward(x2, weight)
         ctx.cfg = (shp, out_scale, residual is not None, bias is not None)
         ctx.bias_param = bias
         ctx.slots = (res_slot, in_slot)
-        if shp[-1] % 8 == 0 and wb.shape[0] % 8 == 0:
+        if shp[-1] % 8 == 0 and OC % 8 == 0:
             SINK.use(weight, ctx.needs_input_grad[1])
             SINK.use(bias, ctx.needs_input_grad[2])
-        return y.reshape(*shp[:-1], wb.shape[0])
+        return y.reshape(*shp[:-1], OC)
 
     @staticmethod
     def backward(ctx, dy):
         x2, weight = ctx.saved_tensors
         shp, scale, has_res, has_b = ctx.cfg
         g = dy.reshape(-1, dy.shape[-1])
-        wb = bf16_weight(weight)
         OC, IC = g.shape[-1], x2.shape[-1]
         rows = g.shape[0]
         dW = db = None
@@ -882,10 +914,16 @@ class _Linear(torch.autograd.Function):
         elif lazy:
             ks = scale
         if ctx.needs_input_grad[0]:
-            if ks != 1.0:
-                dx = torch.empty(rows, IC, dtype=g.dtype, device=g.device).addmm_(g, wb, beta=0.0, alpha=ks)
+            if _lin_hip_dgrad(rows, IC, OC):
+                gc = g.contiguous()
+                dx = torch.empty(rows, IC, dtype=g.dtype, device=g.device)
+                _conv_fwd(gc, packed_weight(weight, True, 1), None, None, None, dx, rows, 1, 1, OC, _up(OC, 64), 1, 1,
+                          IC, IC, 1, True, float(ks), 0, 1)
+            elif ks != 1.0:
+                dx = torch.empty(rows, IC, dtype=g.dtype, device=g.device).addmm_(g, bf16_weight(weight), beta=0.0,
+                                                                                   alpha=ks)
             else:
-                dx = torch.mm(g, wb)
+                dx = torch.mm(g, bf16_weight(weight))
             dx = dx.reshape(shp)
         else:
             dx = None

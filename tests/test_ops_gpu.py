@@ -206,13 +206,20 @@ def test_conv3x3_wgrad_w8(H, N, Hh, W, Ci, Co, s, res, rb, scale):
         H.set_wgrad_impl(os.environ.get("D3D_WGRAD_IMPL", "w8"))
 
 
-def test_linear(H):
+@pytest.mark.parametrize("hip_gemm", [False, True])
+@pytest.mark.parametrize("P,IC,OC", [(128, 256, 768), (8192, 256, 768), (2048, 512, 512), (2048, 512, 1536),
+                                     (4096, 384, 128), (32768, 1024, 512)])
+def test_linear(H, P, IC, OC, hip_gemm, monkeypatch):
+    """Both dispatch regimes: the MFMA kernel with the fused residual / scale
+    epilogue and hipBLASLt + the epilogue kernel."""
+    monkeypatch.setattr(H, "_LIN_HIP_FWD_FLOP", 1e12 if hip_gemm else 0.0)
+    monkeypatch.setattr(H, "_LIN_HIP_DGRAD_FLOP", 1e12 if hip_gemm else 0.0)
     torch.manual_seed(4)
-    x = torch.randn(2, 64, 256, device=DEV).to(BF)
-    w = torch.randn(768, 256, device=DEV) / 16
-    b = torch.randn(768, device=DEV) * 0.1
-    r = torch.randn(2, 64, 768, device=DEV).to(BF)
-    go = torch.randn(2, 64, 768, device=DEV)
+    x = torch.randn(2, P // 2, IC, device=DEV).to(BF)
+    w = torch.randn(OC, IC, device=DEV) / math.sqrt(IC)
+    b = torch.randn(OC, device=DEV) * 0.1
+    r = torch.randn(2, P // 2, OC, device=DEV).to(BF)
+    go = torch.randn(2, P // 2, OC, device=DEV)
     yh, yr, gh, gr = run_both(lambda x, w, b, r: H.linear(x, w, b, r, 0.7),
                               lambda x, w, b, r: T.linear(x, w, b, r, 0.7), [x, w, b, r], go)
     assert rel(yh, yr) < 2e-2
