@@ -26,7 +26,7 @@ _LOCK = threading.Lock()
 _FORCED: Optional[str] = None
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "ops", "libd3d_hip.so")
+LIB_PATH = os.environ.get("D3D_LIB_PATH") or os.path.join(PKG_DIR, "ops", "libd3d_hip.so")   # override: A/B builds
 
 
 def lib_path() -> str:

@@ -1291,6 +1291,29 @@ __device__ __forceinline__ s16x4 ds_tr(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
 }
 
+// The same transposed LDS read as inline asm.  The compiler's wait-count
+// pass cannot tell an LDS load from the LDS-DMA writes still in flight to
+// the OTHER pipeline stage, so in front of the first ds_read_tr of every
+// stage it inserted "s_waitcnt vmcnt(0)" -- i.e. each stage waited for the
+// NEXT stage's loads to land before computing, serialising DMA and MFMA.
+// With the read in asm the only waits are the kernels' own (counted vmcnt +
+// barrier before a stage is read; ds_tr_wait before the fragments are used,
+// which ties their registers so no MFMA is scheduled above it).
+__device__ __forceinline__ s16x4 ds_tr_asm(const bf16* p) {
+  s16x4 v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+template <int TM, int TN>
+__device__ __forceinline__ void ds_tr_wait(bf16x8 (&a)[TM], bf16x8 (&b)[TN]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(a[i]));
+#pragma unroll
+  for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(b[j]));
+}
+
 template <int BM, int BN, int TAPS>
 __global__ void __launch_bounds__(256, 2)
 conv_wgrad_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __restrict__ ws, int Nimg, int IH,
@@ -1818,18 +1841,19 @@ conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I0, floa
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        s16x4 lo = ds_tr(a + la[i] + kk * 32 * 128);
-        s16x4 hi = ds_tr(a + la[i] + kk * 32 * 128 + 16 * 128);
+        s16x4 lo = ds_tr_asm(a + la[i] + kk * 32 * 128);
+        s16x4 hi = ds_tr_asm(a + la[i] + kk * 32 * 128 + 16 * 128);
         s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[i] = __builtin_bit_cast(bf16x8, v);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        s16x4 lo = ds_tr(b + lb[j] + kk * 32 * 128);
-        s16x4 hi = ds_tr(b + lb[j] + kk * 32 * 128 + 16 * 128);
+        s16x4 lo = ds_tr_asm(b + lb[j] + kk * 32 * 128);
+        s16x4 hi = ds_tr_asm(b + lb[j] + kk * 32 * 128 + 16 * 128);
         s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         bfr[j] = __builtin_bit_cast(bf16x8, v);
       }
+      ds_tr_wait<TM, TN>(af, bfr);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -2016,18 +2040,19 @@ conv_wgrad_w8_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* 
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        s16x4 lo = ds_tr(b + lb[j] + kk * 32 * BN);
-        s16x4 hi = ds_tr(b + lb[j] + kk * 32 * BN + 16 * BN);
+        s16x4 lo = ds_tr_asm(b + lb[j] + kk * 32 * BN);
+        s16x4 hi = ds_tr_asm(b + lb[j] + kk * 32 * BN + 16 * BN);
         s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         bfr[j] = __builtin_bit_cast(bf16x8, v);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        s16x4 lo = ds_tr(a + la[i] + kk * 32 * BM);
-        s16x4 hi = ds_tr(a + la[i] + kk * 32 * BM + 16 * BM);
+        s16x4 lo = ds_tr_asm(a + la[i] + kk * 32 * BM);
+        s16x4 hi = ds_tr_asm(a + la[i] + kk * 32 * BM + 16 * BM);
         s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[i] = __builtin_bit_cast(bf16x8, v);
       }
+      ds_tr_wait<TM, TN>(af, bfr);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -2502,6 +2527,18 @@ static int g_halo256 = getenv("D3D_HALO256") ? atoi(getenv("D3D_HALO256")) : 0;
 // fragment double-buffering in the halo conv (PF): measured 4-15 % slower
 // (249 VGPRs, the extra copies outweigh the overlap; profiles/ab_halo_prefetch.txt)
 static int g_halo_pf = getenv("D3D_HALO_PF") ? atoi(getenv("D3D_HALO_PF")) : 0;
+// 64 x 64 no-split tiles (conv_small.hip) where the 128 x 128 kernels would
+// split K over a small grid (the low-resolution levels at small per-GPU batch)
+static int g_s64 = getenv("D3D_CONV_S64") ? atoi(getenv("D3D_CONV_S64")) : 0;
+extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias, const float* row_bias,
+                                const void* res, void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW,
+                                int OC, int ldo, int stride, int trans, float scale, int res_nmod, int taps,
+                                float* gnp, int gn_groups, int* gn_done, hipStream_t st);
+static bool s64_wanted(long Mpix, int OC, int ICp, int taps) {
+  const long blocks128 = ((Mpix + 127) / 128) * ((OC + 127) / 128);
+  const long blocks64 = ((Mpix + 63) / 64) * (OC / 64);
+  return g_s64 && OC % 64 == 0 && (taps * ICp) % 64 == 0 && blocks128 < 384 && blocks64 >= 128;
+}
 static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline, 2: buffer-descriptor LDS-DMA
 static int g_conv_korder = 1;     // glds k-step order: 1 channel-chunk major, 0 tap major
 static int g_wgrad_impl = 5;      // 0: register-staged; 1-4: glds (PK,NS) = (64,2) (32,2) (32,3) (64,3); 5: bufl
@@ -2534,6 +2571,7 @@ D3D_API int d3d_conv_plan(int N, int OH, int OW, int OC, int ICp, int taps) {
   int nk = taps * ICp / 64;
   static const int target = getenv("D3D_CONV_SPLIT_TARGET") ? atoi(getenv("D3D_CONV_SPLIT_TARGET")) : 512;
   if (blocks >= 384 || (OC & 3) || g_conv_impl < 1) return 1;
+  if (g_conv_impl >= 2 && s64_wanted(Mpix, OC, ICp, taps)) return 1;     // no-split small tiles instead
   long want = target / blocks;      // rounded down: no nearly empty extra round of blocks
   long maxs = nk / 6;
   if (want > maxs) want = maxs;
@@ -2559,6 +2597,11 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
   }
   constexpr int BM = 128, BN = 128;
   if (nsplit < 1 || !ws || g_conv_impl < 1) nsplit = 1;
+  if (g_conv_impl >= 2 && nsplit == 1 && s64_wanted(Mpix, OC, ICp, taps)) {
+    const int r = d3d_conv_s64_try(I, Wp, bias, row_bias, res, O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans,
+                                   scale, res_nmod, taps, gnp, gn_groups, gn_done, st);
+    if (r != 0) return r < 0 ? -r : 0;
+  }
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM), (unsigned)nsplit);
   const long in_bytes = (long)N * IH * IW * IC * 2, w_bytes = (long)((OC + 127) / 128 * 128) * taps * ICp * 2;
   if (g_conv_impl == 8 && taps == 9 && stride == 1 && IW == OW && IH == OH && ldo == OC && IC % HALO_CH == 0 &&

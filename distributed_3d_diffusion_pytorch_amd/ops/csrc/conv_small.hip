@@ -1,0 +1,310 @@
+// Small-grid implicit-GEMM 3x3 conv (and 1x1 / per-pixel dense) for the low
+// resolution levels at small per-GPU batch: the 8x8 / 16x16 levels at 16-32
+// examples per GPU, i.e. the per-GPU share of the global-batch-128 step on 4-8
+// GPUs (reference convs: xunet.py:114-126, ResnetBlock conv1/conv2).
+//
+// Why a separate kernel.  At 16 examples per GPU the 8x8 level is 2,048
+// output pixels x 512 channels: 64 blocks of the 128 x 128 tiles (conv_bufl_k),
+// so that kernel splits K = 9 x IC eight ways and a second launch sums eight
+// fp32 partial slabs (33 MB of partial traffic for a 2 MB output) -- ~36 us per
+// conv for 9.7 GFLOP.  Here a block owns a 64 x 64 output tile over the WHOLE
+// K: 256 blocks fill the chip with no split, no partial slabs and no epilogue
+// launch; the epilogue (bias / per-image bias / residual / scale / GroupNorm
+// partial statistics) is fused as in the other conv kernels.
+//
+//   * 4 waves as 2 (channels) x 2 (pixels), 32 x 32 each: 2 x 2
+//     v_mfma_f32_16x16x32_bf16 per 32-deep slice, 8 per 64-deep k-step;
+//   * operands land in LDS by buffer-descriptor DMA (buffer_load ... lds,
+//     range-checked zero fill for padding taps / tile overhang, XOR chunk
+//     swizzle: conflict-free 16-row fragment reads), in a 4-stage ring with
+//     one barrier per k-step and counted vmcnt waits, so three k-steps of
+//     loads are in flight behind the MFMAs (a 64 x 64 tile is L2-bound: 16 KiB
+//     per k-step for 8 MFMA per wave -- the deep ring keeps the L2 pipe full);
+//   * XCD-aware block order (consecutive tiles of one channel slab on one XCD
+//     share its L2 copy of the weight rows);
+//   * GroupNorm partials: the two pixel-half waves of a 64-pixel slot combine
+//     through LDS, so the slot layout is the one the GN kernels consume
+//     (gn_part_store: [N][G][HW/64] x (sum, sum of squares)).
+#include "common.h"
+
+namespace {
+
+// LDS fragment read by inline asm: the compiler's wait-count pass treats every
+// LDS load as possibly aliasing any in-flight LDS-DMA write and would put a
+// full "s_waitcnt vmcnt(0)" in front of it -- serialising the whole DMA ring
+// against the MFMAs.  Ordering here is explicit instead: the counted vmcnt
+// wait + barrier before a stage is read, and lds_wait() (which also ties the
+// fragment registers, so no MFMA can be scheduled above it) before use.
+__device__ __forceinline__ bf16x8 lds_rd128(const bf16* p) {
+  bf16x8 v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_wait(bf16x8 (&a)[2], bf16x8 (&b)[2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]) :: "memory");
+}
+
+constexpr int S64_BM = 64, S64_BN = 64, S64_BK = 64, S64_NS = 4;
+
+template <int TAPS, bool TRANS>
+__global__ void __launch_bounds__(256, 2)
+conv_s64_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
+           const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
+           int w_bytes, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
+           float scale, int res_nmod, float* __restrict__ gnp, int gn_groups) {
+  constexpr int BM = S64_BM, BN = S64_BN, BK = S64_BK, NS = S64_NS;
+  constexpr int STAGE = (BM + BN) * BK;                 // elements
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
+  __shared__ float gn_x[2][2][2][4];                    // [wm][i][s|q][fq] pixel-half-1 partials
+  typedef __attribute__((address_space(3))) void lds_void;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const long Mpix = (long)Nimg * OH * OW;
+  // XCD-aware order over the (pixel tile, channel tile) grid, pixel-major
+  // within a channel slab
+  const int nbx = gridDim.x, nby = gridDim.y;
+  int bid = blockIdx.x + nbx * blockIdx.y;
+  {
+    const int T = nbx * nby, q = T / 8, r = T % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const long n0 = (long)(bid % nbx) * BN;
+  const int m0 = (bid / nbx) * BM;
+  const int Kp = TAPS * ICp;
+
+  // loader: one 1-KiB DMA piece = 8 rows x 64 k (8 x 16-B chunks); each wave
+  // issues 2 pieces of A (weights) and 2 of B (im2col rows) per stage
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;
+  const __amdgpu_buffer_rsrc_t rI = __builtin_amdgcn_make_buffer_rsrc((void*)I, (short)0, in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, w_bytes, 0x00020000);
+  int boff[2], aoff[2];
+  unsigned vmask[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int prow = (wave * 2 + i) * 8 + lrow;
+    const long p = n0 + prow;
+    const bool pv = p < Mpix;
+    const unsigned pp = pv ? (unsigned)p : 0u;      // Mpix < 2^31 (host checks operand sizes)
+    const int pw = (int)(pp % (unsigned)OW);
+    const unsigned t = pp / (unsigned)OW;
+    const int poh = (int)(t % (unsigned)OH);
+    const int pn = (int)(t / (unsigned)OH);
+    const int oh0 = TRANS ? poh : poh * stride, ow0 = TRANS ? pw : pw * stride;
+    boff[i] = (((pn * IH + oh0) * IW + ow0) * IC + lchunk * 8) * 2;
+    unsigned m = 0;
+#pragma unroll
+    for (int tp = 0; tp < TAPS; ++tp) {
+      const int kh = TAPS == 9 ? tp / 3 : 1, kw = TAPS == 9 ? tp % 3 : 1;
+      const int ih = TRANS ? oh0 + 1 - kh : oh0 + kh - 1, iw = TRANS ? ow0 + 1 - kw : ow0 + kw - 1;
+      if (pv && ih >= 0 && ih < IH && iw >= 0 && iw < IW) m |= 1u << tp;
+    }
+    vmask[i] = m;
+    // weight rows past the packed tensor (OC overhang) read as zeros
+    aoff[i] = ((m0 + prow) * Kp + lchunk * 8) * 2;
+  }
+  const int lane_cmax = IC - lchunk * 8;
+
+  auto issue = [&](int kstep, int stage) {
+    // k-step order: channel chunk major over the nine taps (as conv_bufl_k korder 1)
+    const int tap = TAPS == 9 ? kstep % 9 : 0;
+    const int c0 = (TAPS == 9 ? kstep / 9 : kstep) * BK;
+    const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
+    const int tapoff = (TRANS ? ((1 - kh) * IW + (1 - kw)) : ((kh - 1) * IW + (kw - 1))) * IC;
+    const int ubyte = (tapoff + c0) * 2;
+    const int soffA = (tap * ICp + c0) * 2;
+    bf16* sA = smem + stage * STAGE;
+    bf16* sB = sA + BM * BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sA + (wave * 2 + i) * 8 * BK), 16, aoff[i], soffA, 0, 0);
+    const bool cok = c0 < lane_cmax;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const unsigned okb = (unsigned)cok & (vmask[i] >> tap) & 1u;   // failed test -> bit 31: zero fill
+      const unsigned vo = (unsigned)(boff[i] + ubyte) | ((okb - 1u) & 0x80000000u);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rI, (lds_void*)(sB + (wave * 2 + i) * 8 * BK), 16, vo, 0, 0, 0);
+    }
+  };
+  auto swz = [](int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = Kp / BK;
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int ks = 0; ks < nk; ++ks) {
+    // stages ks .. ks + NS - 2 are in flight (4 DMA pieces each): retire ks
+    const int after = nk - 1 - ks < NS - 2 ? nk - 1 - ks : NS - 2;
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // stage ks landed for every wave, and every wave is done reading the
+    // buffer the next issue overwrites (it held stage ks - 1)
+    __builtin_amdgcn_s_barrier();
+    if (ks + NS - 1 < nk) issue(ks + NS - 1, (ks + NS - 1) % NS);
+    const bf16* a = smem + (ks % NS) * STAGE;
+    const bf16* b = a + BM * BK;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = lds_rd128(a + swz(wm * 32 + i * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = lds_rd128(b + swz(wn * 32 + j * 16 + fr, kk * 4 + fq));
+      lds_wait(af, bfr);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  // ---- epilogue: bias / per-image bias / residual / scale, GN partials
+  const int OHW = OH * OW;
+  float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const long pix = n0 + wn * 32 + j * 16 + fr;
+    if (pix >= Mpix) continue;
+    const int img = (int)(pix / OHW);
+    const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co = m0 + wm * 32 + i * 16 + fq * 4;
+      if (co >= OC) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int cc = co + e < OC ? co + e : OC - 1;
+        float t = acc[i][j][e] + (bias ? bias[cc] : 0.f);
+        if (row_bias) t += row_bias[(long)img * OC + cc];
+        v[e] = t;
+      }
+      bf16* dst = O + pix * ldo + co;
+      if (co + 3 < OC && (ldo & 3) == 0) {
+        if (res) {
+          const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+        }
+        bf16x4 o4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o4[e] = (bf16)(v[e] * scale);
+          const float y = (float)o4[e];
+          gs[i] += y;
+          gq[i] += y * y;
+        }
+        *reinterpret_cast<bf16x4*>(dst) = o4;
+      } else {
+        for (int e = 0; e < 4 && co + e < OC; ++e) {
+          float t = v[e];
+          if (res) t += (float)res[rpix * ldo + co + e];
+          dst[e] = (bf16)(t * scale);
+          const float y = (float)dst[e];
+          gs[i] += y;
+          gq[i] += y * y;
+        }
+      }
+    }
+  }
+  if (!gnp) return;
+  // (sum, sum of squares) of the 64-pixel slot per channel group.  Per lane:
+  // its 2 pixel columns x 4 channels (already summed).  Reduce the 16 pixels
+  // of a fragment column (lanes fr), then the 4-channel lane groups (fq) up to
+  // the group width; pixel half wn = 1 hands its sums to wn = 0 through LDS.
+  const int Cg = OC / gn_groups;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) {
+      gs[i] += __shfl_xor(gs[i], m, 64);
+      gq[i] += __shfl_xor(gq[i], m, 64);
+    }
+    if (Cg >= 8) {
+      gs[i] += __shfl_xor(gs[i], 16, 64);
+      gq[i] += __shfl_xor(gq[i], 16, 64);
+    }
+    if (Cg >= 16) {
+      gs[i] += __shfl_xor(gs[i], 32, 64);
+      gq[i] += __shfl_xor(gq[i], 32, 64);
+    }
+  }
+  if (wn == 1 && fr == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      gn_x[wm][i][0][fq] = gs[i];
+      gn_x[wm][i][1][fq] = gq[i];
+    }
+  }
+  __syncthreads();
+  if (wn != 0 || fr != 0) return;
+  const long p = n0;                                   // the slot: pixels n0 .. n0 + 63 (64 | OHW)
+  if (p >= Mpix) return;
+  const long n = p / OHW;
+  const int t = (int)(p - n * OHW) / 64;
+  const int nparts = OHW / 64;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int co = m0 + wm * 32 + i * 16 + fq * 4;
+    float a = gs[i] + gn_x[wm][i][0][fq], b = gq[i] + gn_x[wm][i][1][fq];
+    if (Cg >= 32) {                                    // 32-channel groups: both row tiles of the wave
+      if (i != 0 || fq != 0) continue;
+      a += gs[1] + gn_x[wm][1][0][0];
+      b += gq[1] + gn_x[wm][1][1][0];
+    } else if (fq % (Cg / 4) != 0) {
+      continue;
+    }
+    if (co >= OC) continue;
+    float* d = gnp + ((n * gn_groups + co / Cg) * nparts + t) * 2;
+    d[0] = a;
+    d[1] = b;
+  }
+}
+
+}  // namespace
+
+// Launch the small-tile kernel when it applies; returns 1 if launched (and
+// *gn_done = 1 when the GroupNorm partials were written), 0 if not applicable.
+extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias, const float* row_bias,
+                                const void* res, void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW,
+                                int OC, int ldo, int stride, int trans, float scale, int res_nmod, int taps,
+                                float* gnp, int gn_groups, int* gn_done, hipStream_t st) {
+  const long Mpix = (long)N * OH * OW;
+  const long in_bytes = (long)N * IH * IW * IC * 2;
+  const long w_bytes = (long)((OC + 127) / 128 * 128) * taps * ICp * 2;
+  if ((trans && stride != 1) || in_bytes >= (1L << 31) || w_bytes >= (1L << 31) || OC % 64 || (taps * ICp) % 64)
+    return 0;
+  if (gnp) {
+    const int Cg = gn_groups > 0 && OC % gn_groups == 0 ? OC / gn_groups : 0;
+    if (!((Cg == 4 || Cg == 8 || Cg == 16 || Cg == 32) && (OH * OW) % 64 == 0 && ldo == OC)) gnp = nullptr;
+  }
+  dim3 grid((unsigned)((Mpix + 63) / 64), (unsigned)(OC / 64), 1);
+#define S64(TP, TR)                                                                                             \
+  hipLaunchKernelGGL((conv_s64_k<TP, TR>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias, row_bias, \
+                     (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, OC, ldo, \
+                     stride, scale, res_nmod, gnp, gn_groups)
+  if (taps == 9) {
+    if (trans) S64(9, true); else S64(9, false);
+  } else {
+    if (trans) S64(1, true); else S64(1, false);
+  }
+#undef S64
+  if (gn_done) *gn_done = gnp ? 1 : 0;
+  const int e = (int)hipGetLastError();
+  return e ? -e : 1;
+}

@@ -171,6 +171,23 @@ def test_conv3x3_w8(H, impl, N, Hh, W, Ci, Co, s, res, rb, scale):
         H.set_conv_impl(os.environ.get("D3D_CONV_IMPL", "halo"))
 
 
+S64_SHAPES = [
+    # small grids that the 128x128 kernels would split over K: the 64x64
+    # no-split tiles of conv_small.hip (16-32 examples per GPU, levels 2-3)
+    (32, 8, 8, 512, 512, 1, True, False, 1 / math.sqrt(2)),
+    (32, 16, 16, 256, 256, 1, False, False, 1.0),
+    (32, 8, 8, 1024, 512, 1, True, False, 1 / math.sqrt(2)),
+    (32, 16, 16, 768, 256, 1, False, False, 1.0),
+    (32, 16, 16, 144, 1024, 2, False, True, 1.0),       # strided conditioning conv
+    (20, 8, 8, 256, 512, 1, False, True, 0.5),          # partial pixel tiles (1280 px)
+]
+
+
+@pytest.mark.parametrize("N,Hh,W,Ci,Co,s,res,rb,scale", S64_SHAPES)
+def test_conv3x3_small_tiles(H, N, Hh, W, Ci, Co, s, res, rb, scale):
+    test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale)
+
+
 @pytest.mark.parametrize("N,Hh,Ci,Co", [(32, 32, 256, 256), (64, 32, 128, 256), (16, 64, 128, 128)])
 def test_conv3x3_halo_variants(N, Hh, Ci, Co):
     """The opt-in halo tile variants (32-wide 512-pixel tiles, 256-pixel
@@ -556,7 +573,10 @@ def test_batched_weight_refresh_matches_pack(H, OC, IC, taps):
     (16, 32, 1024, 1024, True, False),    # 32-channel groups span two MFMA row tiles
     (64, 8, 512, 512, True, True),        # split-K grid: statistics from the split-K epilogue
     (2, 16, 128, 256, True, False),       # split-K, 8-channel groups
-    (2, 16, 64, 96, False, False)])       # OC % 64 != 0 under split-K: separate statistics pass
+    (2, 16, 64, 96, False, False),        # OC % 64 != 0 under split-K: separate statistics pass
+    (32, 8, 512, 512, True, True),        # 64x64 small tiles (conv_small.hip), 16-channel groups
+    (32, 8, 1024, 1024, True, False),     # small tiles, 32-channel groups
+    (32, 16, 256, 256, True, True)])      # small tiles, 8-channel groups
 def test_conv_fused_gn_stats(H, N, Hh, Ci, Co, fused, res):
     """GroupNorm statistics emitted by the conv epilogue (w8 / bufl / split-K
     epilogue paths) == the separate statistics pass: GN+SiLU and GN-FiLM."""

@@ -32,20 +32,24 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def sources():
-    return sorted(os.path.join(SRC, f) for f in os.listdir(SRC) if f.endswith(".hip"))
+def sources(src: str = SRC):
+    return sorted(os.path.join(src, f) for f in os.listdir(src) if f.endswith(".hip"))
 
 
-def build(force: bool = False, jobs: int = 8, debug: bool = False, verbose: bool = True) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build(force: bool = False, jobs: int = 8, debug: bool = False, verbose: bool = True, src: str = SRC,
+          out: str = OUT, obj: str = OBJ) -> str:
+    """``src`` / ``out`` / ``obj``: build another source tree (e.g. an older
+    revision for an in-process A/B, loaded through D3D_LIB_PATH) elsewhere."""
+    SRC_, OUT_, OBJ_ = src, out, obj
+    os.makedirs(OBJ_, exist_ok=True)
     cc = hipcc()
-    hdrs = [os.path.join(SRC, f) for f in os.listdir(SRC) if f.endswith(".h")]
+    hdrs = [os.path.join(SRC_, f) for f in os.listdir(SRC_) if f.endswith(".h")]
     hdr_mtime = max((os.path.getmtime(h) for h in hdrs), default=0)
     flags = ["-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
     flags += ["-O0", "-g"] if debug else ["-O3"]
 
     def compile_one(src: str) -> str:
-        obj = os.path.join(OBJ, os.path.basename(src)[:-4] + ".o")
+        obj = os.path.join(OBJ_, os.path.basename(src)[:-4] + ".o")
         if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
             return obj
         cmd = [cc, *flags, "-c", src, "-o", obj]
@@ -56,17 +60,17 @@ def build(force: bool = False, jobs: int = 8, debug: bool = False, verbose: bool
             print(f"[build] {os.path.basename(src)}", flush=True)
         return obj
 
-    srcs = sources()
+    srcs = sources(SRC_)
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
         objs = list(ex.map(compile_one, srcs))
-    if force or not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(o) for o in objs):
-        cmd = [cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT]
+    if force or not os.path.exists(OUT_) or os.path.getmtime(OUT_) < max(os.path.getmtime(o) for o in objs):
+        cmd = [cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT_]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stderr}")
         if verbose:
-            print(f"[build] linked {OUT}", flush=True)
-    return OUT
+            print(f"[build] linked {OUT_}", flush=True)
+    return OUT_
 
 
 def main() -> None:
@@ -74,7 +78,23 @@ def main() -> None:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--rev", default="", help="build ops/csrc as of this git revision into build/ab/<rev>/ "
+                                              "(load it with D3D_LIB_PATH for an in-process A/B)")
     a = ap.parse_args()
+    if a.rev:
+        d = os.path.join(ROOT, "build", "ab", a.rev)
+        src = os.path.join(d, "csrc")
+        os.makedirs(src, exist_ok=True)
+        rel = os.path.relpath(SRC, ROOT)
+        files = subprocess.run(["git", "-C", ROOT, "ls-tree", "--name-only", f"{a.rev}:{rel}"], check=True,
+                               capture_output=True, text=True).stdout.split()
+        for f in files:
+            blob = subprocess.run(["git", "-C", ROOT, "show", f"{a.rev}:{rel}/{f}"], check=True,
+                                  capture_output=True).stdout
+            with open(os.path.join(src, f), "wb") as fh:
+                fh.write(blob)
+        print(build(True, a.jobs, a.debug, src=src, out=os.path.join(d, "libd3d_hip.so"), obj=os.path.join(d, "obj")))
+        return
     build(a.force, a.jobs, a.debug)
 
 
