@@ -188,6 +188,7 @@ def main() -> None:
                        "hip_graph": graph,
                        "parallelism": f"dp{N}", "dist_backend": ctx.backend,
                        "graph_comm": getattr(trainer._graphed, "comm_mode", None),
+                       "tuned_gemms": bool(getattr(trainer, "tuned_gemms", False)),
                        "backend": "hip" if (ctx.device.type == "cuda" and use_hip(probe)) else "torch"},
             "final_loss": lv,
         }

@@ -7,7 +7,9 @@ the CPU, D11):
   * q_sample                -> `train.py:50-60`
   * cfg posterior           -> `train.py:131-166`, `sampling.py:78-112`
   * ancestral step          -> `train.py:118-128`, `sampling.py:115-127`
-The on-device fused forms live in ``ops.diffusion_forward`` / ``ops.sampler_step``.
+The on-device fused forms are ``ops.diffusion_inputs`` (t, lambda, eps, q_sample and CFG drop in
+one launch) and the sampler kernels driven by ``engine.sampler`` (CFG combine, x0 clamp,
+posterior and noise in one launch per step).
 """
 from __future__ import annotations
 

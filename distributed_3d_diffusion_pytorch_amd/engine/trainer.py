@@ -54,6 +54,9 @@ class Trainer:
         self.device = dev
         if cfg.backend != "auto":
             ops.set_backend(cfg.backend)
+        if dev.type == "cuda":
+            from ..utils.gemm_tuning import enable_tuned_gemms
+            self.tuned_gemms = enable_tuned_gemms()
         if cfg.deterministic:
             torch.use_deterministic_algorithms(True, warn_only=True)
         torch.manual_seed(cfg.seed)

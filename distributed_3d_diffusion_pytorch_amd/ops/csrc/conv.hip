@@ -1827,51 +1827,110 @@ conv_wgrad_bufl_k(const bf16* __restrict__ dY, const bf16* __restrict__ I0, floa
   float bacc = 0.f;
   // bias: thread -> column tid&127, rows half*(PK/2) .. +PK/2 (swizzled reads)
   const int bcol = tid & 127, bhalf = tid >> 7;
-  auto compute = [&](const bf16* a) {
-    const bf16* b = a + PK * BM;
-    if (do_bias) {
-#pragma unroll
-      for (int r = 0; r < PK / 2; ++r) {
-        const int row = bhalf * (PK / 2) + r;
-        bacc += (float)a[row * 128 + ((((bcol >> 3) ^ (2 * (row & 7)))) << 3) + (bcol & 7)];
+  // FAST (stride-1, power-of-two images: every large layer): the issue-then-
+  // compute order below, in which the compiler waits for the next stage's DMA
+  // before reading this one -- the two co-resident blocks per CU cover each
+  // other's waits, and in-graph A/B (profiles/ab_wgrad_order_r2.txt) had it
+  // 1.3-1.6x faster than reads-first ordering on these shapes.  Strided /
+  // generic addressing: reads-first (-10..15 % on the conditioning convs).
+  if constexpr (FAST) {
+    auto compute = [&](const bf16* a) {
+      const bf16* b = a + PK * BM;
+      if (do_bias) {
+  #pragma unroll
+        for (int r = 0; r < PK / 2; ++r) {
+          const int row = bhalf * (PK / 2) + r;
+          bacc += (float)a[row * 128 + ((((bcol >> 3) ^ (2 * (row & 7)))) << 3) + (bcol & 7)];
+        }
       }
+  #pragma unroll
+      for (int kk = 0; kk < PK / 32; ++kk) {
+        bf16x8 af[TM], bfr[TN];
+  #pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          s16x4 lo = ds_tr(a + la[i] + kk * 32 * 128);
+          s16x4 hi = ds_tr(a + la[i] + kk * 32 * 128 + 16 * 128);
+          s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          af[i] = __builtin_bit_cast(bf16x8, v);
+        }
+  #pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          s16x4 lo = ds_tr(b + lb[j] + kk * 32 * 128);
+          s16x4 hi = ds_tr(b + lb[j] + kk * 32 * 128 + 16 * 128);
+          s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bfr[j] = __builtin_bit_cast(bf16x8, v);
+        }
+  #pragma unroll
+        for (int i = 0; i < TM; ++i)
+  #pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    };
+    // one barrier per step: wait for this step's DMA, barrier (every wave's
+    // DMA landed AND every wave done reading the other slot), issue the next
+    // step into the other slot, compute.
+    if (nsteps > 0) issue(p_begin, 0);
+    for (long s = 0; s < nsteps; ++s) {
+      const int st = (int)(s & 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (s + 1 < nsteps) issue(p_begin + (s + 1) * PK, st ^ 1);
+      compute(smem + st * STAGE);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-#pragma unroll
-    for (int kk = 0; kk < PK / 32; ++kk) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        s16x4 lo = ds_tr_asm(a + la[i] + kk * 32 * 128);
-        s16x4 hi = ds_tr_asm(a + la[i] + kk * 32 * 128 + 16 * 128);
-        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, v);
+  } else {
+    // Per stage: read EVERY fragment of the stage, THEN issue the next stage's
+    // LDS-DMA, then run the MFMAs.  With the DMA issued after the reads, the
+    // compiler's wait-count pass sees no LDS-DMA in flight at any LDS read (the
+    // stage's own DMA is retired by the s_waitcnt builtin below, which the pass
+    // accounts for, unlike inline asm), so it inserts no "vmcnt(0)" that would
+    // wait for the NEXT stage; the DMA of stage s+1 overlaps stage s's MFMAs
+    // while the compiler keeps its fine-grained read / MFMA interleave.
+    constexpr int KK = PK / 32;
+    auto frags = [&](const bf16* a, bf16x8 (&af)[KK][TM], bf16x8 (&bfr)[KK][TN]) {
+      const bf16* b = a + PK * BM;
+      if (do_bias) {
+  #pragma unroll
+        for (int r = 0; r < PK / 2; ++r) {
+          const int row = bhalf * (PK / 2) + r;
+          bacc += (float)a[row * 128 + ((((bcol >> 3) ^ (2 * (row & 7)))) << 3) + (bcol & 7)];
+        }
       }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        s16x4 lo = ds_tr_asm(b + lb[j] + kk * 32 * 128);
-        s16x4 hi = ds_tr_asm(b + lb[j] + kk * 32 * 128 + 16 * 128);
-        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8, v);
+  #pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+  #pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          s16x4 lo = ds_tr(a + la[i] + kk * 32 * 128);
+          s16x4 hi = ds_tr(a + la[i] + kk * 32 * 128 + 16 * 128);
+          s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          af[kk][i] = __builtin_bit_cast(bf16x8, v);
+        }
+  #pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          s16x4 lo = ds_tr(b + lb[j] + kk * 32 * 128);
+          s16x4 hi = ds_tr(b + lb[j] + kk * 32 * 128 + 16 * 128);
+          s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bfr[kk][j] = __builtin_bit_cast(bf16x8, v);
+        }
       }
-      ds_tr_wait<TM, TN>(af, bfr);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    };
+    if (nsteps > 0) issue(p_begin, 0);
+    for (long s = 0; s < nsteps; ++s) {
+      const int st = (int)(s & 1);
+      __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0): this stage landed
+      __builtin_amdgcn_s_barrier();                    // ... everywhere; the other slot is free
+      bf16x8 af[KK][TM], bfr[KK][TN];
+      frags(smem + st * STAGE, af, bfr);
+      if (s + 1 < nsteps) issue(p_begin + (s + 1) * PK, st ^ 1);
+  #pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+  #pragma unroll
+        for (int i = 0; i < TM; ++i)
+  #pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
     }
-  };
-  // one barrier per step: wait for this step's DMA, barrier (every wave's
-  // DMA landed AND every wave done reading the other slot), issue the next
-  // step into the other slot, compute.
-  if (nsteps > 0) issue(p_begin, 0);
-  for (long s = 0; s < nsteps; ++s) {
-    const int st = (int)(s & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (s + 1 < nsteps) issue(p_begin + (s + 1) * PK, st ^ 1);
-    compute(smem + st * STAGE);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   if (do_bias) {
     if (m0 + bcol < OC) bws[((long)split * 2 + bhalf) * OC + m0 + bcol] = bacc;

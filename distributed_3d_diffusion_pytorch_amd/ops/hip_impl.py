@@ -122,6 +122,7 @@ _REV = [0]
 def invalidate_weight_cache() -> None:
     _EPOCH[0] += 1
     _WCACHE.clear()
+    _CATBUF.clear()
     _REV[0] += 1
 
 
@@ -224,6 +225,34 @@ def packed_weight_slice(w: torch.Tensor, ic0: int, nic: int, ICp: int) -> torch.
 
 def packed_conv_weight(w: torch.Tensor, trans: bool) -> torch.Tensor:
     return packed_weight(w, trans, 9)
+
+
+_CATBUF: Dict[Tuple, torch.Tensor] = {}
+
+
+def bf16_cat(params, kind: str) -> torch.Tensor:
+    """bf16 copy of ``cat([p.reshape(p.shape[0], -1) for p in params])`` kept
+    as ONE persistent buffer: every parameter's slice is a cache entry whose
+    descriptor points into the buffer, so the batched repack after each
+    optimizer step refreshes it in place and a forward never concatenates
+    (the level-batched FiLM projection weights / biases)."""
+    key = (kind,) + tuple((p.data_ptr(), tuple(p.shape)) for p in params)
+    buf = _CATBUF.get(key)
+    rows = [p.shape[0] for p in params]
+    cols = params[0].numel() // params[0].shape[0]
+    if buf is None:
+        buf = torch.empty(sum(rows), cols, dtype=BF16, device=params[0].device)
+        _CATBUF[key] = buf
+    off = 0
+    for p, r in zip(params, rows):
+        view = buf[off: off + r]
+
+        def build(p=p, view=view):
+            view.copy_(p.detach().reshape(view.shape))
+            return view
+        _cached(p, f"{kind}@{buf.data_ptr()}", build, (p.numel(), 1, 1, 1, 1, 2))
+        off += r
+    return buf if cols > 1 else buf.reshape(-1)
 
 
 def bf16_weight(w: torch.Tensor) -> torch.Tensor:
@@ -989,8 +1018,8 @@ class _FiLMBatch(torch.autograd.Function):
         shp = semb.shape
         K = shp[-1]
         x2 = semb.reshape(-1, K)
-        wcat = torch.cat([bf16_weight(w) for w in Ws], 0)
-        bcat = torch.cat([bf16_weight(b) for b in Bs], 0)
+        wcat = bf16_cat(Ws, "filmW")
+        bcat = bf16_cat(list(Bs), "filmB")
         y = torch.addmm(bcat, x2, wcat.t()).view(*shp[:-1], wcat.shape[0])
         ctx.save_for_backward(x2, wcat)
         ctx.n, ctx.slot, ctx.shp = n, slot, shp
