@@ -34,14 +34,18 @@ def enable_tuned_gemms(path: str = TABLE) -> bool:
     if os.environ.get("D3D_TUNED_GEMMS", "1") == "0" or not torch.cuda.is_available() or not os.path.exists(path):
         return False
     tun = torch.cuda.tunable
-    # work on a private copy: TunableOp may rewrite its results file at exit,
-    # and the repository copy must stay what the tuning run produced
-    tmp = os.path.join(tempfile.gettempdir(), f"d3d_tunableop_{os.getpid()}.csv")
-    shutil.copyfile(path, tmp)
-    tun.enable(True)
-    tun.tuning_enable(False)
-    tun.set_filename(tmp)
-    ok = tun.read_file(tmp)
+    try:
+        # work on a private copy: TunableOp may rewrite its results file at
+        # exit, and the repository copy must stay what the tuning run produced
+        tmp = os.path.join(tempfile.gettempdir(), f"d3d_tunableop_{os.getpid()}.csv")
+        shutil.copyfile(path, tmp)
+        tun.enable(True)
+        tun.tuning_enable(False)
+        tun.record_untuned_enable(False)
+        tun.set_filename(tmp)
+        ok = bool(tun.read_file(tmp))
+    except Exception:                       # noqa: BLE001 -- a table problem must never stop training
+        ok = False
     if not ok:
         tun.enable(False)
-    return bool(ok)
+    return ok
