@@ -25,12 +25,18 @@ see the same ordering as a single stream.  Collectives over the deposited
 gradients are issued from behind the side stream (:meth:`collective`).
 Per-parameter accumulation order is unchanged (one side stream, launch
 order), so results stay bitwise reproducible.  ``D3D_WGRAD_STREAM=0`` runs
-everything on the compute stream.  Not used inside HIP-graph capture: there
-the replayed step is already back-to-back on the GPU (99 % kernel-busy at 16
-examples per GPU, profiles/busy_bs16_side_stream.txt) and each cross-stream
-edge of the graph costs ~7 us of dependency latency, which ate the overlap
-(eager bs128: 761 -> 786 examples/s with the side stream; graph bs16: 444 ->
-440).
+everything on the compute stream.
+
+Inside HIP-graph capture (:meth:`submit`, ``D3D_GRAPH_WGRAD_STREAM``): a fork
+per weight gradient cost ~7 us of graph dependency latency per edge -- ~1,600
+edges ate the concurrency (busy 88.7 %, profiles/busy_bs16_side_stream.txt).
+There the weight-gradient jobs are DEFERRED instead: queued as closures and
+flushed onto the side stream ``D3D_WGRAD_DEFER_BATCH`` (default 4) at a time
+behind ONE fork each, and joined once at the end of backward, so the graph
+holds a few dozen cross-stream edges while the weight-gradient branch runs
+concurrently with the input-gradient chain.  Deferred operands stay alive in
+the closures; the allocator defers frees of side-stream-recorded blocks to
+the end of the capture.
 """
 from __future__ import annotations
 
@@ -50,6 +56,9 @@ class GradSink:
         self.seen = set()
         self.notify: Optional[Callable[[int], None]] = None
         self.stream_enabled = os.environ.get("D3D_WGRAD_STREAM", "1") != "0"
+        self.graph_defer = os.environ.get("D3D_GRAPH_WGRAD_STREAM", "1") != "0"
+        self.defer_batch = max(1, int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "4")))
+        self._queue = []
         self._streams: Dict[int, "torch.cuda.Stream"] = {}
         self._forked = set()
         self._cb_queued = False
@@ -128,7 +137,55 @@ class GradSink:
 
     def _end_of_backward(self) -> None:
         self._cb_queued = False
+        self.flush()
         self.join()
+
+    def _queue_end_callback(self) -> None:
+        if not self._cb_queued:
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+                self._cb_queued = True
+            except RuntimeError:        # not inside a backward pass
+                pass
+
+    # ------------------------------------------------ weight-gradient jobs
+    def submit(self, dev: torch.device, fn: Callable[[], None], keep=(), done=()) -> None:
+        """Run one weight-gradient job: ``fn()`` launches kernels that deposit
+        into sink targets, then the parameters in ``done`` are reported.
+        Eager: now, on the side stream (:meth:`producer`).  Graph capture with
+        deferral on: queued and flushed in batches behind one fork each."""
+        if (self.stream_enabled and self.graph_defer and dev.type == "cuda"
+                and torch.cuda.is_current_stream_capturing()):
+            self._queue.append((fn, tuple(t for t in keep if t is not None), tuple(p for p in done if p is not None)))
+            self._queue_end_callback()
+            if len(self._queue) >= self.defer_batch:
+                self.flush()
+            return
+        with self.producer(dev, *keep):
+            fn()
+        for p in done:
+            if p is not None:
+                self.done(p)
+
+    def flush(self) -> None:
+        """Issue the queued weight-gradient jobs on the side stream behind ONE
+        wait on the compute stream, then report their parameters."""
+        if not self._queue:
+            return
+        q, self._queue = self._queue, []
+        idx = torch.cuda.current_device()
+        side = self._side(idx)
+        side.wait_stream(torch.cuda.current_stream(idx))
+        with torch.cuda.stream(side):
+            for fn, _, _ in q:
+                fn()
+        for _, keep, _ in q:
+            for t in keep:
+                t.record_stream(side)
+        self._forked.add(idx)
+        for _, _, done in q:
+            for p in done:
+                self.done(p)
 
     def join(self) -> None:
         """Make the current stream wait for every deposited gradient."""
@@ -153,6 +210,7 @@ class GradSink:
     def reset(self) -> None:
         self.uses = {}
         self.seen = set()
+        self._queue = []
 
 
 SINK = GradSink()

@@ -465,8 +465,7 @@ class _CatGNDense(torch.autograd.Function):
         # one weight-gradient GEMM over the virtual concat (the kernel picks
         # the source per 128-channel tile); two GEMMs when it cannot
         _ensure_impl()
-        side = SINK.producer(g.device, g2, a, b) if direct else contextlib.nullcontext()
-        with side:
+        def job():
             sp, pps = ctypes.c_int(), ctypes.c_int()
             _lib.d3d_conv_wgrad_plan2(rows, 1, 1, OC, C, 1, ctypes.byref(sp), ctypes.byref(pps))
             ws = torch.empty(sp.value * OC * C + 2 * sp.value * OC, dtype=F32, device=g.device)
@@ -483,10 +482,9 @@ class _CatGNDense(torch.autograd.Function):
             else:
                 _chk(rc, "wgrad_cat")
         if direct:
-            SINK.done(dwp)
-            if has_db:
-                SINK.done(dbp)
+            SINK.submit(g.device, job, (g2, a, b), (dwp, dbp if has_db else None))
         else:
+            job()
             gW = dWt.view(dwp.shape)
             gB = dbt
         return da, db_in, dgw, dgb, gW, gB, None, None
@@ -680,12 +678,10 @@ class _Conv(torch.autograd.Function):
         if need_w:
             direct = tw is not None and (not need_b or tb is not None)
             if direct:
-                with SINK.producer(g.device, g, x):
-                    _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, dW=tw.view(OC, IC, taps),
-                           db=tb if need_b else None, accumulate=True, scale=ks)
-                SINK.done(weight)
-                if need_b:
-                    SINK.done(bias)
+                def job(g=g, x=x, tw=tw, tb=tb if need_b else None, ks=ks):
+                    _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, dW=tw.view(OC, IC, taps), db=tb,
+                           accumulate=True, scale=ks)
+                SINK.submit(g.device, job, (g, x), (weight, bias if need_b else None))
             else:
                 dW, db2 = _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, want_bias=need_b, scale=ks)
                 dW = dW.reshape(weight.shape)
@@ -962,12 +958,10 @@ class _Linear(torch.autograd.Function):
             tw = SINK.target(weight)
             tb = SINK.target(bias) if need_b else None
             if tw is not None and (not need_b or tb is not None):
-                with SINK.producer(g.device, g4, x4):
+                def job(g4=g4, x4=x4, tw=tw, tb=tb, ks=ks):
                     _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, dW=tw.view(OC, IC, 1), db=tb, accumulate=True,
                            scale=ks)
-                SINK.done(weight)
-                if need_b:
-                    SINK.done(bias)
+                SINK.submit(g.device, job, (g4, x4), (weight, bias if need_b else None))
             else:
                 dW, db = _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, want_bias=need_b, scale=ks)
                 dW = dW.reshape(weight.shape)
@@ -1070,8 +1064,7 @@ class _FiLMBatch(torch.autograd.Function):
                 tw = [torch.zeros(w.shape, dtype=F32, device=x2.device) for w in Ws]
                 tb = [torch.zeros(b.shape, dtype=F32, device=x2.device) for b in Bs]
             _ensure_impl()
-            side = SINK.producer(x2.device, dy, x2) if direct else contextlib.nullcontext()
-            with side:
+            def job():
                 row0 = (ctypes.c_int * n)(*offs[:n])
                 wd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tw])
                 bd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tb])
@@ -1093,10 +1086,9 @@ class _FiLMBatch(torch.autograd.Function):
                     _chk(_lib.d3d_conv_wgrad_seg(dy.data_ptr(), x2.data_ptr(), ws.data_ptr(), rows, 1, 1, K, 1, 1, S,
                                                  1, sp.value, pps.value, 1, 1, n, row0, wd, bd, _st()), "film_wgrad")
             if direct:
-                for w, b in zip(Ws, Bs):
-                    SINK.done(w)
-                    SINK.done(b)
+                SINK.submit(x2.device, job, (dy, x2), [p for wb in zip(Ws, Bs) for p in wb])
             else:
+                job()
                 grads_w = [t.view(w.shape) for t, w in zip(tw, Ws)]
                 grads_b = tb
         return (dx, None, None, *grads_w, *grads_b)
