@@ -185,7 +185,7 @@ def main() -> None:
                                  "(3DiM, reference xunet.py)"),
                        "global_batch": global_batch, "seq_len": args.imgsize * args.imgsize,
                        "image_size": args.imgsize, "per_gpu_batch": local, "micro_batch": mb or local,
-                       "hip_graph": graph,
+                       "hip_graph": bool(trainer.cfg.graph),
                        "parallelism": f"dp{N}", "dist_backend": ctx.backend,
                        "graph_comm": getattr(trainer._graphed, "comm_mode", None),
                        "tuned_gemms": bool(getattr(trainer, "tuned_gemms", False)),

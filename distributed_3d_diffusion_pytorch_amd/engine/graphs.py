@@ -79,6 +79,11 @@ def probe_graph_collective(device: torch.device) -> bool:
     return bool(flag.item() > 0.5)
 
 
+class GraphCaptureError(RuntimeError):
+    """The training step could not be captured (on this rank or any other):
+    the trainer falls back to the eager step on every rank."""
+
+
 class GraphedTrainStep:
     def __init__(self, trainer, micro_batch: int, example):
         from ..ops import hip_impl
@@ -135,6 +140,29 @@ class GraphedTrainStep:
         self.loss_acc.zero_()
 
     def capture(self, nchunks: int = 1) -> None:
+        """Capture the graphs; on failure (here or on any rank) raise
+        GraphCaptureError on every rank, so all ranks take the same path."""
+        err = None
+        try:
+            self._capture(nchunks)
+        except Exception as e:            # noqa: BLE001
+            err = e
+            self.gA = self.gA0 = self.gB = None
+            self.H.set_device_seed(None)
+            torch.cuda.synchronize()
+        tr = self.tr
+        if tr.ctx.world > 1 and dist.is_initialized():
+            flag = torch.tensor([0.0 if err is not None else 1.0], device=tr.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if flag.item() < 0.5 and err is None:
+                err = RuntimeError("graph capture failed on another rank")
+                self.gA = self.gA0 = self.gB = None
+        if err is not None:
+            tr.flat.zero_grad()
+            self.loss_acc.zero_()
+            raise GraphCaptureError(f"{type(err).__name__}: {err}") from err
+
+    def _capture(self, nchunks: int = 1) -> None:
         tr = self.tr
         tr.model.train()
         tr.model.set_dropout_seed(0)             # baked; the per-step part is self.seed

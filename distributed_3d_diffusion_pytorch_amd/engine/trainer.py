@@ -201,7 +201,16 @@ class Trainer:
         if self.sched is None:
             g["lr"] = warmup_lr(self.step, self.warmup_steps, self.cfg.optim.lr)
         if self.cfg.graph and self.device.type == "cuda" and self.sink is not None:
-            return self._graph_train_step(img, R, T, K, want_stats)
+            from .graphs import GraphCaptureError
+            try:
+                return self._graph_train_step(img, R, T, K, want_stats)
+            except GraphCaptureError as e:
+                # every rank raises together (GraphedTrainStep.capture): all
+                # continue with the eager step
+                if self.ctx.is_main:
+                    print(f"[trainer] HIP-graph capture failed ({e}); continuing with the eager step", flush=True)
+                self.cfg.graph = False
+                self._graphed = None
         self.model.train()
         if self.sink is not None:
             self.sink.reset()
