@@ -50,6 +50,7 @@ import torch
 class GradSink:
     def __init__(self) -> None:
         self.enabled = False
+        self.owners: Dict[int, torch.Tensor] = {}
         self.views: Dict[int, torch.Tensor] = {}
         self.index: Dict[int, int] = {}
         self.uses: Dict[int, int] = {}
@@ -64,6 +65,10 @@ class GradSink:
         self._cb_queued = False
 
     def attach(self, params, views, notify: Optional[Callable[[int], None]] = None) -> None:
+        # the parameter objects themselves are kept: a key is only trusted
+        # when it still names the same object (ids are reused once a model
+        # that attached earlier is gone)
+        self.owners = {id(p): p for p in params}
         self.views = {id(p): v for p, v in zip(params, views)}
         self.index = {id(p): i for i, p in enumerate(params)}
         self.uses = {}
@@ -72,10 +77,10 @@ class GradSink:
 
     def detach(self) -> None:
         self.enabled = False
-        self.views, self.index, self.uses, self.notify = {}, {}, {}, None
+        self.views, self.index, self.uses, self.notify, self.owners = {}, {}, {}, None, {}
 
     def managed(self, p) -> bool:
-        return self.enabled and p is not None and id(p) in self.views
+        return self.enabled and p is not None and self.owners.get(id(p)) is p
 
     def target(self, p) -> Optional[torch.Tensor]:
         if not self.managed(p):
@@ -93,7 +98,7 @@ class GradSink:
 
     def was_used(self, p) -> bool:
         """True when this step's gradient of p is delivered by the sink."""
-        return self.enabled and id(p) in self.seen
+        return self.enabled and id(p) in self.seen and self.owners.get(id(p)) is p
 
     def done(self, p) -> None:
         if not self.managed(p):
