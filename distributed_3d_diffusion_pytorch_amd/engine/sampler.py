@@ -19,6 +19,12 @@ Differences by design (same math, §2.5 of SURVEY):
   all 256 steps: the per-step scalars come from a device table row and the
   step's RNG word from a device word, the stochastic-conditioning choice is a
   device-to-device copy into the graph's static input before each replay;
+* all b chains of a step condition on the same (record view, target view)
+  poses and logSNR pair, so the conditioning is computed for the 2 distinct
+  classes (cond / uncond) only -- 4 conditioning images instead of 4b -- and
+  shared by the GN-FiLM kernels through a row -> class map
+  (``XUNet.forward(shared_cond=)``; ``share_cond=False`` restores the
+  per-example forward);
 * D9 (noise skipped at t=0.5 where logsnr_next == 0) is opt-in via
   ``ref_quirk``; default adds noise on every step but the last.
 """
@@ -46,10 +52,13 @@ class RecordEntry:
 class DiffusionSampler:
     def __init__(self, model: torch.nn.Module, timesteps: int = 256, ref_quirk: bool = False,
                  logsnr_min: float = -20.0, logsnr_max: float = 20.0, seed: int = 0, device=None,
-                 chain_offset: int = 0, graph: Optional[bool] = None):
+                 chain_offset: int = 0, graph: Optional[bool] = None, share_cond: bool = True):
         """``chain_offset``: global index of this sampler's first chain (its
         rank's shard start).  ``graph``: replay the step from a HIP graph
-        (default: on for the bf16 HIP path)."""
+        (default: on for the bf16 HIP path).  ``share_cond``: compute the
+        conditioning once per class instead of once per chain in
+        :meth:`sample` (identical result)."""
+        self.share_cond = bool(share_cond)
         self.model = model
         self.T = timesteps
         self.ref_quirk = ref_quirk
@@ -100,37 +109,59 @@ class DiffusionSampler:
         idx = torch.arange(int(torch.Size(shape).numel()), device=device, dtype=torch.int64) + self.c0 * D
         return TI.normal01(s, idx).reshape(shape)
 
+    # ------------------------------------------------ shared conditioning
+    @staticmethod
+    def shared_cond(R1, T1, K1, logsnr: torch.Tensor, b: int) -> dict:
+        """The 2 distinct conditioning examples of a CFG batch whose b chains
+        share one pose pair: class 0 conditional, class 1 unconditional
+        (rays masked).  R1 [2,3,3], T1 [2,3], K1 [3,3], logsnr [2,2] (or a
+        view of any 2 rows of the batch's identical [lambda0, lambda] rows)."""
+        dev = R1.device
+        return {"R": R1[None].expand(2, 2, 3, 3), "t": T1[None].expand(2, 2, 3),
+                "K": K1.reshape(1, 3, 3).expand(2, 3, 3), "logsnr": logsnr,
+                "cond_mask": torch.tensor([True, False], device=dev),
+                "example_class": torch.cat([torch.zeros(b, dtype=torch.int32, device=dev),
+                                            torch.ones(b, dtype=torch.int32, device=dev)])}
+
     # ------------------------------------------------------- eager step
     @torch.no_grad()
-    def denoise_eps(self, x_cond, z, R, T, K, logsnr: float, k: int = 0):
+    def denoise_eps(self, x_cond, z, R, T, K, logsnr: float, k: int = 0, shared: bool = False):
         """CFG pair in one forward: rows [0,b) conditional, [b,2b) unconditional
         (x replaced by the step-k counter-based noise, rays zeroed via
-        cond_mask=False)."""
+        cond_mask=False).  ``shared``: R/T/K are the same for every chain
+        (as in :meth:`sample`): condition once per class."""
         from ..ops import torch_impl as TI
         b = z.shape[0]
         dev = z.device
         x_unc = self._noise(TI.K_XU, k, tuple(x_cond.shape), dev).to(x_cond.dtype)
         lam = torch.full((2 * b,), float(logsnr), device=dev)
-        batch = {"x": torch.cat([x_cond, x_unc]), "z": torch.cat([z, z]),
-                 "logsnr": torch.stack([torch.full_like(lam, self.lam0), lam], 1),
-                 "R": torch.cat([R, R]), "t": torch.cat([T, T]), "K": torch.cat([K, K])}
-        mask = torch.cat([torch.ones(b, dtype=torch.bool, device=dev), torch.zeros(b, dtype=torch.bool, device=dev)])
-        eps = self.model(batch, cond_mask=mask).float()
+        logsnr2 = torch.stack([torch.full_like(lam, self.lam0), lam], 1)
+        batch = {"x": torch.cat([x_cond, x_unc]), "z": torch.cat([z, z])}
+        if shared:
+            eps = self.model(batch, shared_cond=self.shared_cond(R[0], T[0], K[0], logsnr2[:2], b)).float()
+        else:
+            batch.update({"logsnr": logsnr2, "R": torch.cat([R, R]), "t": torch.cat([T, T]),
+                          "K": torch.cat([K, K])})
+            mask = torch.cat([torch.ones(b, dtype=torch.bool, device=dev),
+                              torch.zeros(b, dtype=torch.bool, device=dev)])
+            eps = self.model(batch, cond_mask=mask).float()
         return eps[:b], eps[b:]
 
     @torch.no_grad()
-    def step(self, z, x_cond, R, T, K, w, k: int):
+    def step(self, z, x_cond, R, T, K, w, k: int, shared: bool = False):
+        """One ancestral CFG step for b chains.  ``shared``: every chain has
+        the same R/T/K (conditioning computed once per class)."""
         from ..ops import torch_impl as TI
         if self._hip(z):
-            return self._hip_step(z, x_cond, R, T, K, w, k)
-        eps_c, eps_u = self.denoise_eps(x_cond, z, R, T, K, self.lam[k], k)
+            return self._hip_step(z, x_cond, R, T, K, w, k, shared)
+        eps_c, eps_u = self.denoise_eps(x_cond, z, R, T, K, self.lam[k], k, shared)
         mean, var = cfg_posterior(z, eps_c, eps_u, w, torch.tensor(self.lam[k]), torch.tensor(self.lam_next[k]))
         if not self.add_noise(k):
             return mean
         return mean + var.sqrt() * self._noise(TI.K_NZ, k, tuple(z.shape), z.device)
 
     @torch.no_grad()
-    def _hip_step(self, z, x_cond, R, T, K, w, k):
+    def _hip_step(self, z, x_cond, R, T, K, w, k, shared=False):
         """Eager form of the graphed step (same kernels, host seed)."""
         from ..ops import hip_impl
         b, _, H, W = z.shape
@@ -140,9 +171,15 @@ class DiffusionSampler:
         logsnr = torch.empty(2 * b, 2, dtype=torch.float32, device=dev)
         z = z.float().contiguous().clone()
         hip_impl.sampler_inputs(x_cond.float().contiguous(), z, prm, None, self.step_seed(k), self.c0, xz, logsnr)
-        mask = torch.cat([torch.ones(b, dtype=torch.bool, device=dev), torch.zeros(b, dtype=torch.bool, device=dev)])
-        batch = {"xz": xz, "logsnr": logsnr, "R": torch.cat([R, R]), "t": torch.cat([T, T]), "K": torch.cat([K, K])}
-        y = self.model(batch, cond_mask=mask, head_nhwc=True)
+        if shared:
+            sc = self.shared_cond(R[0].float(), T[0].float(), K[0].float(), logsnr[:2], b)
+            y = self.model({"xz": xz}, shared_cond=sc, head_nhwc=True)
+        else:
+            mask = torch.cat([torch.ones(b, dtype=torch.bool, device=dev),
+                              torch.zeros(b, dtype=torch.bool, device=dev)])
+            batch = {"xz": xz, "logsnr": logsnr, "R": torch.cat([R, R]), "t": torch.cat([T, T]),
+                     "K": torch.cat([K, K])}
+            y = self.model(batch, cond_mask=mask, head_nhwc=True)
         hip_impl.sampler_step2(z, y, w.float().contiguous(), prm, None, self.step_seed(k), self.c0)
         return z
 
@@ -153,11 +190,13 @@ class DiffusionSampler:
         g = {"b": b, "H": H, "W": W}
         g["xc"] = torch.zeros(b, 3, H, W, device=dev)
         g["z"] = torch.zeros(b, 3, H, W, device=dev)
-        g["R"] = torch.zeros(2 * b, 2, 3, 3, device=dev)
-        g["t"] = torch.zeros(2 * b, 2, 3, device=dev)
+        shared = g["shared"] = self.share_cond
+        nb = 1 if shared else 2 * b                 # pose rows the graph reads
+        g["R"] = torch.zeros(nb, 2, 3, 3, device=dev)
+        g["t"] = torch.zeros(nb, 2, 3, device=dev)
         g["R"][:, 1] = target_R.to(dev).float()
         g["t"][:, 1] = target_T.to(dev).float()
-        g["K"] = K.to(dev).float().reshape(1, 3, 3).expand(2 * b, 3, 3).contiguous()
+        g["K"] = K.to(dev).float().reshape(1, 3, 3).expand(nb, 3, 3).contiguous()
         g["w"] = w.to(dev).float().contiguous()
         g["prm_table"] = torch.tensor([self.params(k) for k in range(self.T)], dtype=torch.float32).to(dev)
         g["prm"] = g["prm_table"][0].clone()
@@ -168,11 +207,17 @@ class DiffusionSampler:
                                torch.zeros(b, dtype=torch.bool, device=dev)])
         g["target"] = (target_R.detach().clone(), target_T.detach().clone(), K.detach().clone(), w.detach().clone())
 
+        if shared:
+            g["sc"] = self.shared_cond(g["R"][0], g["t"][0], g["K"][0], g["logsnr"][:2], b)
+
         def body():
             hip_impl.sampler_inputs(g["xc"], g["z"], g["prm"], g["sd"], self.seed_base, self.c0, g["xz"],
                                     g["logsnr"])
-            batch = {"xz": g["xz"], "logsnr": g["logsnr"], "R": g["R"], "t": g["t"], "K": g["K"]}
-            y = self.model(batch, cond_mask=g["mask"], head_nhwc=True)
+            if shared:
+                y = self.model({"xz": g["xz"]}, shared_cond=g["sc"], head_nhwc=True)
+            else:
+                batch = {"xz": g["xz"], "logsnr": g["logsnr"], "R": g["R"], "t": g["t"], "K": g["K"]}
+                y = self.model(batch, cond_mask=g["mask"], head_nhwc=True)
             hip_impl.sampler_step2(g["z"], y, g["w"], g["prm"], g["sd"], self.seed_base, self.c0)
 
         z_keep = g["z"].clone()
@@ -195,7 +240,7 @@ class DiffusionSampler:
 
     def _graph_ok(self, b, H, W, K, w, target_R, target_T) -> bool:
         g = self._g
-        if g is None or g["b"] != b or g["H"] != H or g["W"] != W:
+        if g is None or g["b"] != b or g["H"] != H or g["W"] != W or g["shared"] != self.share_cond:
             return False
         tR, tT, tK, tw = g["target"]
         return bool(torch.equal(tK.to(K.device), K) and torch.equal(tw.to(w.device), w))
@@ -245,7 +290,7 @@ class DiffusionSampler:
                 e = record[self.choice_rng.randrange(len(record))]
                 R = torch.stack([e.R.to(dev), target_R.to(dev)], 0)[None].expand(b, 2, 3, 3).contiguous()
                 T = torch.stack([e.T.to(dev), target_T.to(dev)], 0)[None].expand(b, 2, 3).contiguous()
-                z = self.step(z, e.img.to(dev), R, T, Kb, w, k)
+                z = self.step(z, e.img.to(dev), R, T, Kb, w, k, shared=self.share_cond)
         if model_was_training:
             self.model.train()
         return z

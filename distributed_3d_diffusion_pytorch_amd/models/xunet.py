@@ -110,9 +110,12 @@ class ResnetBlock(nn.Module):
         ss = self.__dict__.pop("_ss", None)     # precomputed by the level-batched FiLM
         if ss is None:
             ss = self.film(semb)
+        # shared conditioning: ss holds one modulation per conditioning class,
+        # image n reads class ss_map[n] (XUNet.forward(shared_cond=))
+        ss_map = self.__dict__.get("_ss_map")
         h = ops.gn_film(h, self.groupnorm1.gn.weight, self.groupnorm1.gn.bias, ss,
                         self.groupnorm1.gn.num_groups, self.groupnorm1.gn.eps,
-                        self.dropout_p, self.training, _next_seed(self))
+                        self.dropout_p, self.training, _next_seed(self), ss_map=ss_map)
         rslot = None
         if skip is None:
             if self.in_features != self.features:
@@ -371,14 +374,26 @@ class XUNet(nn.Module):
             if isinstance(m, ResnetBlock):
                 m._base_seed = int(seed)
 
-    def forward(self, batch: Dict[str, torch.Tensor], *, cond_mask: torch.Tensor,
-                head_nhwc: bool = False) -> torch.Tensor:
+    def forward(self, batch: Dict[str, torch.Tensor], *, cond_mask: Optional[torch.Tensor] = None,
+                head_nhwc: bool = False, shared_cond: Optional[Dict[str, torch.Tensor]] = None) -> torch.Tensor:
         """``batch``: the reference dict {x, z, logsnr, R, t, K} (`xunet.py:477`),
         or with ``xz`` -- the already stacked NHWC stem input [2B,H,W,C>=3]
         (frames interleaved; extra channels zero) drawn by
         ``ops.diffusion_inputs`` -- in place of x and z.  ``head_nhwc``: return
         the head conv's NHWC output (channel-padded on the HIP path) for
-        ``ops.diff_loss_nhwc`` instead of eps [B,3,H,W]."""
+        ``ops.diff_loss_nhwc`` instead of eps [B,3,H,W].
+
+        ``shared_cond`` (inference only): when many examples share the same
+        conditioning -- CFG sampling, where all b chains use the same poses
+        and logSNR pair and differ only in cond / uncond -- pass the Bc
+        DISTINCT conditioning examples ``{"logsnr": [Bc,2], "R", "t", "K",
+        "cond_mask": [Bc], "example_class": [B] int}`` instead of per-example
+        R/t/K/logsnr: the conditioning processor and the FiLM projections run
+        on 2Bc images instead of 2B and the GN-FiLM kernels read the
+        modulation of class ``example_class[n]``.  Same result as the
+        per-example forward; removes ~38 % of the sampler's FLOPs at b=8."""
+        if shared_cond is not None:
+            return self._forward_shared(batch, shared_cond, head_nhwc)
         xz = batch.get("xz")
         if xz is not None:
             B = xz.shape[0] // 2
@@ -391,12 +406,40 @@ class XUNet(nn.Module):
         for key, v in batch.items():
             if key != "xz":
                 assert v.shape[0] == B, f"{key} should have batch size {B}, not {v.shape[0]}"
-        assert cond_mask.shape[0] == B
+        assert cond_mask is not None and cond_mask.shape[0] == B
         assert (H, W) == (self.H, self.W), ((H, W), (self.H, self.W))
         dt = self.compute_dtype or xdt
-
         sembs = self.conditioningprocessor(batch, cond_mask, dt)
-        if self.batch_film:
+        return self._trunk(batch, sembs, B, H, W, dt, head_nhwc, None)
+
+    def _forward_shared(self, batch, sc, head_nhwc):
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise RuntimeError("shared_cond is an inference path: run it under torch.no_grad()")
+        xz = batch.get("xz")
+        if xz is not None:
+            B, H, W = xz.shape[0] // 2, xz.shape[1], xz.shape[2]
+            xdt = xz.dtype
+        else:
+            B, _, H, W = batch["x"].shape
+            xdt = batch["x"].dtype
+        assert (H, W) == (self.H, self.W), ((H, W), (self.H, self.W))
+        ecls = sc["example_class"]
+        assert ecls.shape == (B,), (ecls.shape, B)
+        Bc = sc["logsnr"].shape[0]
+        for key in ("R", "t", "K", "cond_mask"):
+            assert sc[key].shape[0] == Bc, (key, sc[key].shape, Bc)
+        dt = self.compute_dtype or xdt
+        sembs = self.conditioningprocessor(sc, sc["cond_mask"], dt)
+        # image (example e, frame f) -> conditioning image (class of e, frame f)
+        fr = torch.arange(2, device=ecls.device, dtype=torch.int32)
+        ss_map = (2 * ecls.to(torch.int32)[:, None] + fr).reshape(-1)
+        return self._trunk(batch, sembs, B, H, W, dt, head_nhwc, ss_map)
+
+    def _trunk(self, batch, sembs, B, H, W, dt, head_nhwc, ss_map):
+        for blocks in self._film_groups():
+            for b in blocks:
+                b.__dict__["_ss_map"] = ss_map
+        if ss_map is not None or self.batch_film:
             # every FiLM projection of a level reads the same embedding: run
             # them as one GEMM per level (ops.film_batch) and hand each
             # ResnetBlock its modulation slice
@@ -405,9 +448,12 @@ class XUNet(nn.Module):
                                       [b.film.dense.bias for b in blocks])
                 for b, o in zip(blocks, outs):
                     b.__dict__["_ss"] = o
+        xz = batch.get("xz")
         if xz is not None:
             h = xz.to(dt)
         else:
+            x, z = batch["x"], batch["z"]
+            C = x.shape[1]
             h = torch.stack([x, z], dim=1).reshape(2 * B, C, H, W).permute(0, 2, 3, 1).to(dt).contiguous()
         h = ops.conv3x3(h, self.conv.weight, self.conv.bias)
 

@@ -31,10 +31,12 @@ def group_norm(x, weight, bias, groups: int = 32, eps: float = 1e-5, silu: bool 
 
 
 def gn_film(x, weight, bias, ss, groups: int = 32, eps: float = 1e-5, dropout_p: float = 0.0,
-            training: bool = False, seed: int = 0):
+            training: bool = False, seed: int = 0, ss_map: Optional[torch.Tensor] = None):
+    """ss_map (int32 [N], inference): image n is modulated by ss[ss_map[n]]
+    (shared conditioning, XUNet.forward(shared_cond=))."""
     if use_hip(x):
-        return _h().gn_film(x, weight, bias, ss, groups, eps, dropout_p, training, seed)
-    return _t.gn_film(x, weight, bias, ss, groups, eps, dropout_p, training, seed)
+        return _h().gn_film(x, weight, bias, ss, groups, eps, dropout_p, training, seed, ss_map)
+    return _t.gn_film(x, weight, bias, ss, groups, eps, dropout_p, training, seed, ss_map)
 
 
 def conv3x3(x, weight, bias, stride: int = 1, residual: Optional[torch.Tensor] = None,

@@ -22,7 +22,7 @@ SIGNATURES = {
     "d3d_ray_dir": [P, P, P, P, I, I, I, I, P],
     "d3d_border_fix": [P, P, I, I, I, I, I, I, I, P],
     "d3d_border_sums": [P, P, I, I, I, I, P],
-    "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, I, P],
+    "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, I, P, P],
     "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P, F, P],
     # elementwise.hip
     "d3d_silu": [P, P, L, P],

@@ -402,7 +402,8 @@ __global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, co
                                                   const float* __restrict__ beta, const bf16* __restrict__ ss,
                                                   bf16* __restrict__ y, int P, int C, int G, int rows, int nchunks,
                                                   float eps, float p_drop, uint64_t seed, int ssld,
-                                                  const uint64_t* __restrict__ seed_dev, Cat cat, int conv_parts) {
+                                                  const uint64_t* __restrict__ seed_dev, Cat cat, int conv_parts,
+                                                  const int* __restrict__ ss_map) {
   constexpr int U = MODE == 2 ? 2 : UNR;      // rows in flight per thread
   __shared__ float s_st[2 * 1024];
   const int chunk = blockIdx.x, n = blockIdx.y;
@@ -428,6 +429,9 @@ __global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, co
   }
   const RowSrc src = row_src(x, cat, c0, C);
   const long pix0 = (long)n * P;
+  // shared conditioning (sampling): image n reads the modulation of
+  // conditioning class ss_map[n] (engine/sampler.py)
+  const long spix0 = (MODE == 2 && ss_map) ? (long)ss_map[n] * P : pix0;
   const int r1 = min(P, chunk * rows + rows);
   for (int r = chunk * rows + roff; r < r1; r += U * rpi) {
     f32x8 a[U], sc[U], sf[U];
@@ -438,8 +442,8 @@ __global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, co
         const long pix = pix0 + rr;
         a[u] = ld8(src.p + pix * src.ld);
         if (MODE == 2) {
-          sc[u] = ld8(ss + pix * ssld + c0);
-          sf[u] = ld8(ss + pix * ssld + C + c0);
+          sc[u] = ld8(ss + (spix0 + rr) * ssld + c0);
+          sf[u] = ld8(ss + (spix0 + rr) * ssld + C + c0);
         }
       }
     }
@@ -806,7 +810,7 @@ D3D_API int d3d_gn_stats(const void* x, int N, int P, int C, int G, float eps, f
 D3D_API int d3d_gn_apply2(int mode, const void* x, const float* part, float* stats_out, const float* gamma,
                           const float* beta, const void* ss, void* y, int N, int P, int C, int G, float eps,
                           float p_drop, unsigned long long seed, int ssld, const void* seed_dev, const void* x2,
-                          int C1, int conv_parts, hipStream_t st) {
+                          int C1, int conv_parts, const int* ss_map, hipStream_t st) {
   if (G > 1024) return (int)hipErrorInvalidValue;
   Cat cat{(const bf16*)x2, nullptr, C1};
   Plan p = make_plan(N, P, C);
@@ -814,7 +818,7 @@ D3D_API int d3d_gn_apply2(int mode, const void* x, const float* part, float* sta
 #define AP(M)                                                                                                   \
   hipLaunchKernelGGL(gn_apply2_k<M>, dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, part, stats_out, gamma, \
                      beta, (const bf16*)ss, (bf16*)y, P, C, G, p.rows, p.nchunks, eps, p_drop, (uint64_t)seed, ssld, \
-                     (const uint64_t*)seed_dev, cat, conv_parts)
+                     (const uint64_t*)seed_dev, cat, conv_parts, ss_map)
   if (mode == 0) AP(0);
   else if (mode == 1) AP(1);
   else AP(2);

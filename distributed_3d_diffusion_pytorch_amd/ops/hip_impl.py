@@ -293,7 +293,7 @@ def _gn_stats(x, G, eps):
     return stats
 
 
-def _gn_fwd(mode, x, w, b, G, eps, ss=None, ssld=0, p=0.0, seed=0, x2=None):
+def _gn_fwd(mode, x, w, b, G, eps, ss=None, ssld=0, p=0.0, seed=0, x2=None, ss_map=None):
     """Statistics pass + fused finalize/apply (mode 0 GN, 1 GN+SiLU, 2 GN+FiLM):
     two launches; returns (y, stats) with stats = per-(image, group) mean/rstd.
     With x2, the input is the virtual channel concat [x | x2]."""
@@ -313,7 +313,8 @@ def _gn_fwd(mode, x, w, b, G, eps, ss=None, ssld=0, p=0.0, seed=0, x2=None):
     y = torch.empty(N, H, W, C, dtype=x.dtype, device=x.device)
     _chk(_lib.d3d_gn_apply2(mode, x.data_ptr(), part.data_ptr(), stats.data_ptr(), w.data_ptr(), b.data_ptr(),
                             _ptr(ss), y.data_ptr(), N, P, C, G, float(eps), float(p), int(seed), int(ssld),
-                            _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), C1, int(conv_parts), _st()),
+                            _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), C1, int(conv_parts),
+                            _ptr(ss_map), _st()),
          "gn_apply2")
     return y, stats
 
@@ -516,12 +517,16 @@ def _ss_layout(ss: torch.Tensor, C: int):
 
 class _GNFiLM(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, ss, groups, eps, p, seed):
+    def forward(ctx, x, weight, bias, ss, groups, eps, p, seed, ss_map=None):
         x = x.contiguous()
         N, H, W, C = x.shape
         slot = getattr(ss, "_d3d_slot", None)
         ss, ld = _ss_layout(ss, C)
-        y, stats = _gn_fwd(2, x, weight, bias, groups, eps, ss, ld, p, seed)
+        if ss_map is not None:
+            assert ss_map.dtype == torch.int32 and ss_map.is_contiguous() and ss_map.shape == (N,), \
+                (ss_map.dtype, ss_map.shape, N)
+            assert ss.shape[1:3] == (H, W), (ss.shape, x.shape)
+        y, stats = _gn_fwd(2, x, weight, bias, groups, eps, ss, ld, p, seed, ss_map=ss_map)
         ctx.save_for_backward(x, weight, bias, ss, stats)
         ctx.cfg = (groups, p, seed, ld)
         ctx.slot = slot if ld != 2 * C or slot is not None else None
@@ -541,13 +546,16 @@ class _GNFiLM(torch.autograd.Function):
             dss = holder.grad_slice(off, x.shape[-1])
             ld = holder.width
         dx, dss, dg, db = _gn_bwd(2, x, dy.contiguous(), ss, stats, w, b, G, p, seed, dss=dss, ssld=ld)
-        return dx, dg, db, dss, None, None, None, None
+        return dx, dg, db, dss, None, None, None, None, None
 
 
-def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=False, seed=0):
+def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=False, seed=0, ss_map=None):
     _need_bf16(x, ss)
     p = float(dropout_p) if training else 0.0
-    return _GNFiLM.apply(x, weight, bias, ss, groups, eps, p, int(seed) & 0xFFFFFFFFFFFFFFFF)
+    if ss_map is not None and torch.is_grad_enabled() and \
+            any(t is not None and t.requires_grad for t in (x, weight, bias, ss)):
+        raise RuntimeError("gn_film(ss_map=) is inference-only")
+    return _GNFiLM.apply(x, weight, bias, ss, groups, eps, p, int(seed) & 0xFFFFFFFFFFFFFFFF, ss_map)
 
 
 # ----------------------------------------------------------------- conv ----

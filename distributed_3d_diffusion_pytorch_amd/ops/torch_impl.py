@@ -47,11 +47,14 @@ def dropout_mask(shape, p: float, seed: int, device) -> torch.Tensor:
 
 def gn_film(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, ss: torch.Tensor,
             groups: int = 32, eps: float = 1e-5, dropout_p: float = 0.0,
-            training: bool = False, seed: int = 0) -> torch.Tensor:
+            training: bool = False, seed: int = 0, ss_map: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dropout(GN(x) * (1 + scale) + shift); ``ss = [scale | shift]`` on the
-    channel axis (FiLM, `xunet.py:74-87`; ResBlock ordering `xunet.py:140-146`)."""
+    channel axis (FiLM, `xunet.py:74-87`; ResBlock ordering `xunet.py:140-146`).
+    ``ss_map``: image n takes the modulation ss[ss_map[n]]."""
     C = x.shape[-1]
     h = group_norm(x, weight, bias, groups, eps).float()
+    if ss_map is not None:
+        ss = ss.index_select(0, ss_map.long())
     ssf = ss.float()
     y = h * (1.0 + ssf[..., :C]) + ssf[..., C:]
     if training and dropout_p > 0.0:

@@ -75,6 +75,25 @@ def test_gn_film(H, N, Hh, W, C):
         assert rel(a, c) < 3e-2
 
 
+def test_gn_film_ss_map(H):
+    """Shared-conditioning GN-FiLM: image n modulated by class ss_map[n] of a
+    strided level-batched modulation == the torch op on the gathered ss."""
+    torch.manual_seed(4)
+    N, Hh, C = 6, 8, 256
+    x = torch.randn(N, Hh, Hh, C, device=DEV).to(BF)
+    w = torch.randn(C, device=DEV) * 0.5 + 1
+    b = torch.randn(C, device=DEV) * 0.1
+    parent = (torch.randn(4, Hh, Hh, 3 * 2 * C, device=DEV) * 0.5).to(BF)
+    ss = parent[..., 2 * C:4 * C]                    # channel slice, ld = 6C
+    smap = torch.tensor([0, 1, 2, 3, 0, 3], dtype=torch.int32, device=DEV)
+    with torch.no_grad():
+        y = H.gn_film(x, w, b, ss, 32, 1e-5, 0.0, False, 0, smap)
+        yr = T.gn_film(x.float(), w, b, ss.float()[smap.long()], 32, 1e-5, 0.0, False, 0)
+    assert rel(y, yr) < 1e-2
+    with pytest.raises(RuntimeError):
+        H.gn_film(x, w.clone().requires_grad_(True), b, ss, 32, 1e-5, 0.0, False, 0, smap)
+
+
 def test_gn_film_dropout(H):
     torch.manual_seed(2)
     N, Hh, W, C, p = 2, 16, 16, 128, 0.1
@@ -839,6 +858,40 @@ def test_sampler_graph_replay_matches_eager():
         outs.append(smp.sample(rec, R[2, 1].float(), t[2, 1].float(), K[0].float(), w))
     assert torch.isfinite(outs[0]).all()
     assert (outs[0] - outs[1]).abs().max().item() < 1e-3
+
+
+def test_sampler_shared_cond_matches_per_chain():
+    """HIP sampler step with the conditioning computed per class (4
+    conditioning images, GN-FiLM through the row -> class map) == the
+    per-chain step, to bf16 accuracy.  Compared on single mid-schedule steps:
+    a whole short-schedule run is ill-conditioned (x0 = (z - sigma eps) /
+    alpha with alpha ~ 5e-5 at logsnr -20 amplifies bf16 rounding to the
+    x0 clamp), so bitwise agreement is only expected between identical
+    kernel sequences (test_sampler_graph_replay_matches_eager)."""
+    from distributed_3d_diffusion_pytorch_amd.models import XUNet
+    from distributed_3d_diffusion_pytorch_amd.engine import DiffusionSampler
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    torch.manual_seed(14)
+    m = XUNet(H=32, W=32, ch=128).to(DEV)
+    with torch.no_grad():
+        for p in m.parameters():
+            if p.abs().sum() == 0:
+                p.normal_(0, 0.02)
+    m.compute_dtype = BF
+    m.eval()
+    b = 4
+    img, R, t, K = next(SyntheticBatches(b, 32, DEV, seed=2))
+    Rb = torch.stack([R[0, 0], R[1, 1]])[None].expand(b, 2, 3, 3).float().contiguous()
+    Tb = torch.stack([t[0, 0], t[1, 1]])[None].expand(b, 2, 3).float().contiguous()
+    Kb = K[0].float()[None].expand(b, 3, 3).contiguous()
+    w = torch.tensor([0.0, 1.0, 2.0, 3.0], device=DEV)
+    smp = DiffusionSampler(m, timesteps=256, seed=9, device=torch.device(DEV))
+    z = torch.randn(b, 3, 32, 32, device=DEV)
+    for k in (100, 128, 200):
+        za = smp.step(z, img[:, 0], Rb, Tb, Kb, w, k, shared=False)
+        zb = smp.step(z, img[:, 0], Rb, Tb, Kb, w, k, shared=True)
+        assert torch.isfinite(zb).all()
+        assert rel(zb, za) < 1e-2, (k, rel(zb, za))
 
 
 def test_full_model_64px_matches_fp32_oracle():

@@ -134,6 +134,58 @@ def test_sampler_chains_independent_of_sharding():
     torch.testing.assert_close(outs[1], outs[0][2:], rtol=1e-4, atol=1e-5)
 
 
+def _signal_model():
+    """tiny_model with its zero-init layers randomised, so the output depends
+    on the conditioning through every path."""
+    m = tiny_model().eval()
+    torch.manual_seed(3)
+    with torch.no_grad():
+        for p in m.parameters():
+            if p.abs().sum() == 0:
+                p.normal_(0, 0.05)
+    return m
+
+
+def test_shared_cond_forward_matches_per_example():
+    """XUNet.forward(shared_cond=) -- conditioning per class, FiLM read
+    through the row -> class map -- equals the per-example forward."""
+    from helpers import tiny_batch
+    m = _signal_model()
+    b = tiny_batch(1)
+    B = 5
+    R = torch.cat([b["R"]] * B)
+    T = torch.cat([b["t"]] * B)
+    K = torch.cat([b["K"]] * B)
+    x = torch.rand(B, 3, 16, 16) * 2 - 1
+    z = torch.randn(B, 3, 16, 16)
+    lg = torch.tensor([[20.0, -1.5]] * B)
+    cls = torch.tensor([0, 1, 1, 0, 1], dtype=torch.int32)
+    mask = cls == 0
+    with torch.no_grad():
+        ref = m({"x": x, "z": z, "logsnr": lg, "R": R, "t": T, "K": K}, cond_mask=mask)
+        sc = {"R": R[:2], "t": T[:2], "K": K[:2], "logsnr": lg[:2], "cond_mask": torch.tensor([True, False]),
+              "example_class": cls}
+        out = m({"x": x, "z": z}, shared_cond=sc)
+    assert ref.abs().max() > 1e-3
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-5)
+    with pytest.raises(RuntimeError):
+        m({"x": x, "z": z}, shared_cond=sc)      # inference only
+
+
+def test_sampler_shared_cond_matches_per_chain():
+    m = _signal_model()
+    K = torch.tensor([[20.0, 0, 8], [0, 20.0, 8], [0, 0, 1]])
+    img = torch.rand(3, 3, 16, 16) * 2 - 1
+    w = torch.tensor([0.0, 1.0, 3.0])
+    outs = []
+    for share in (False, True):
+        smp = DiffusionSampler(m, timesteps=3, seed=5, share_cond=share)
+        rec = [RecordEntry(img, torch.eye(3), torch.tensor([0.0, 0.0, 1.3])),
+               RecordEntry(img.flip(-1), torch.eye(3), torch.tensor([0.0, 1.3, 0.0]))]
+        outs.append(smp.sample(rec, torch.eye(3), torch.tensor([1.3, 0.0, 0.0]), K, w))
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-4, atol=1e-5)
+
+
 def test_lightning_cli_layout(srn_root, tmp_path):
     """`lightning/train.py` (reference T3): cars.pickle index inside --train_data,
     --transfer initialises from a checkpoint FILE and restarts at step 0,
