@@ -2004,7 +2004,10 @@ __device__ __forceinline__ void wgrad_w8_issue(bf16* sA, bf16* sB, const bf16* _
   }
 }
 
-template <int BM, int BN>
+// TAPS = 1: per-pixel dense weight gradient dY^T X over P rows (the level-
+// batched FiLM projections, attention projections, NIN skips); no padding
+// tests, any row count.
+template <int BM, int BN, int TAPS = 9>
 __global__ void __launch_bounds__(512, 1)
 conv_wgrad_w8_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* __restrict__ ws, long in_pix,
                 int Nimg, int IH, int IW, int IC, int OH, int OW, int OC, int pix_per_split, int ncb,
@@ -2029,11 +2032,11 @@ conv_wgrad_w8_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* 
     by = (int)((R / gx) % gy);
     bz = (int)(R / ((long)gx * gy));
   }
-  const int tap = bx / ncb;
+  const int tap = TAPS == 9 ? bx / ncb : 0;
   const int ci0 = (bx % ncb) * BN;
   const int m0 = by * BM;
   const int split = bz;
-  const int kh = tap / 3, kw = tap % 3;
+  const int kh = TAPS == 9 ? tap / 3 : 1, kw = TAPS == 9 ? tap % 3 : 1;
   const long P = (long)Nimg * OH * OW;
   const long p_begin = (long)split * pix_per_split;
   const long p_end = p_begin + pix_per_split < P ? p_begin + pix_per_split : P;
@@ -2135,7 +2138,7 @@ conv_wgrad_w8_k(const bf16* __restrict__ dY, const bf16* __restrict__ I, float* 
   }
   if (do_bias && m0 + bcol < OC) bws[((long)split * 2 + bhalf) * OC + m0 + bcol] = bacc;
   const int fr = lane & 15, fq = lane >> 4;
-  const long KW = 9L * IC;
+  const long KW = (long)TAPS * IC;
   float* slab = ws + (long)split * OC * KW;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -2953,12 +2956,23 @@ D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps
 // conv_wgrad_w8_k takes a 3x3 stride-1 same-size power-of-two shape when
 // at least one of its channel counts fills a 256-wide tile side (the 128x128
 // level-0 convs stay on the 4-wave kernel); impl 6 enables it.
+// taps == 1 (per-pixel GEMMs, D3D_WGRAD_W8_1X1, default on): any geometry,
+// long reductions (the FiLM projections over every pixel of a level) are
+// where the 4-wave kernel's 16-MFMA stages stall most.
+static bool wgrad_w8_1x1() {
+  static const int v = getenv("D3D_WGRAD_W8_1X1") ? atoi(getenv("D3D_WGRAD_W8_1X1")) : 1;
+  return v != 0;
+}
+
 static bool wgrad_w8_ok(int taps, int IH, int IW, int OH, int OW, int IC, int OC, int stride, long in_elems, int* bm,
                         int* bn) {
   auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
-  if (g_wgrad_impl != 6 || taps != 9 || stride != 1 || IH != OH || IW != OW || !pow2(OH) || !pow2(OW) ||
-      IC % 128 || OC % 8 || in_elems * 2 >= (1L << 30))
+  if (g_wgrad_impl != 6 || IC % 128 || OC % 8 || in_elems * 2 >= (1L << 30)) return false;
+  if (taps == 1) {
+    if (!wgrad_w8_1x1() || stride != 1 || IH != OH || IW != OW) return false;
+  } else if (taps != 9 || stride != 1 || IH != OH || IW != OW || !pow2(OH) || !pow2(OW)) {
     return false;
+  }
   // 256 output channels per tile: the 128-row form (384 -> 128) measured
   // 1.5x slower than the 4-wave kernel at its 1024-block plan
   *bm = 256;
@@ -2968,10 +2982,12 @@ static bool wgrad_w8_ok(int taps, int IH, int IW, int OH, int OW, int IC, int OC
   // ~one block per CU >= 16 stages each: the 4-wave kernel is faster there
   // (kbench batch 16: 268 vs 196 TF/s at 16x16, 256 channels)
   const long P = in_elems / IC;
-  const int tiles = 9 * ((IC + *bn - 1) / *bn) * ((OC + *bm - 1) / *bm);
+  const int tiles = taps * ((IC + *bn - 1) / *bn) * ((OC + *bm - 1) / *bm);
   long splits = 256 / tiles;
   if (splits > P / 1024) splits = P / 1024;
   if (splits < 1) splits = 1;
+  // the dY descriptor spans one split: its byte count must fit 31 bits
+  if ((P + splits - 1) / splits * OC * 2 >= (1L << 31) - (1L << 20)) return false;
   return tiles * splits >= 128;
 }
 
@@ -2983,7 +2999,7 @@ D3D_API int d3d_conv_wgrad_plan3(int N, int IH, int IW, int OH, int OW, int OC, 
   if (!wgrad_w8_ok(taps, IH, IW, OH, OW, IC, OC, stride, (long)N * IH * IW * IC, &bm, &bn))
     return d3d_conv_wgrad_plan2(N, OH, OW, OC, IC, taps, splits, pix_per_split);
   const long P = (long)N * OH * OW;
-  const int tiles = 9 * ((IC + bn - 1) / bn) * ((OC + bm - 1) / bm);
+  const int tiles = taps * ((IC + bn - 1) / bn) * ((OC + bm - 1) / bm);
   // at one block per CU a grid just past 256 blocks runs a second, nearly
   // empty round: round the split count DOWN to fit one wave of blocks
   long want = 256 / tiles;
@@ -2995,6 +3011,22 @@ D3D_API int d3d_conv_wgrad_plan3(int N, int IH, int IW, int OH, int OW, int OC, 
   *pix_per_split = (int)pps;
   *splits = (int)((P + pps - 1) / pps);
   return 0;
+}
+
+static void launch_wgrad_w8(const void* dY, const void* I, float* ws, int N, int IH, int IW, int IC, int OH, int OW,
+                            int OC, int pps, int splits, float* bws, int lw, int lh, int taps, int bn,
+                            hipStream_t st) {
+  const int ncb = (IC + bn - 1) / bn;
+  dim3 g8(taps * ncb, (OC + 255) / 256, splits);
+#define WW(BNv, TP)                                                                                              \
+  hipLaunchKernelGGL((conv_wgrad_w8_k<256, BNv, TP>), g8, dim3(512), 0, st, (const bf16*)dY, (const bf16*)I, ws,  \
+                     (long)N * IH * IW, N, IH, IW, IC, OH, OW, OC, pps, ncb, bws, lw, lh)
+  if (taps == 9) {
+    if (bn == 256) WW(256, 9); else WW(128, 9);
+  } else {
+    if (bn == 256) WW(256, 1); else WW(128, 1);
+  }
+#undef WW
 }
 
 D3D_API int d3d_conv_wgrad_plan(int N, int OH, int OW, int OC, int IC, int* splits, int* pix_per_split) {
@@ -3018,14 +3050,7 @@ D3D_API int d3d_conv_wgrad3(const void* dY, const void* I, float* ws, float* dW,
   if (lw < 0 || lh < 0) lw = lh = -1;
   int bm, bn;
   if (wgrad_w8_ok(taps, IH, IW, OH, OW, IC, OC, stride, (long)N * IH * IW * IC, &bm, &bn)) {
-    const int ncb = (IC + bn - 1) / bn;
-    dim3 g8(9 * ncb, (OC + bm - 1) / bm, splits);
-#define WW(BMv, BNv)                                                                                             \
-  hipLaunchKernelGGL((conv_wgrad_w8_k<BMv, BNv>), g8, dim3(512), 0, st, (const bf16*)dY, (const bf16*)I, ws,       \
-                     (long)N * IH * IW, N, IH, IW, IC, OH, OW, OC, pix_per_split, ncb, bws, lw, lh)
-    if (bn == 256) WW(256, 256);
-    else WW(256, 128);
-#undef WW
+    launch_wgrad_w8(dY, I, ws, N, IH, IW, IC, OH, OW, OC, pix_per_split, splits, bws, lw, lh, taps, bn, st);
   } else {
     int ncb = (IC + BN - 1) / BN;
     dim3 grid(taps * ncb, (OC + BM - 1) / BM, splits);
@@ -3097,7 +3122,11 @@ D3D_API int d3d_conv_wgrad_seg(const void* dY, const void* I, float* ws, int N, 
   auto lg2 = [](int v) { int l = 0; while ((1 << l) < v) ++l; return (1 << l) == v ? l : -1; };
   int lw = lg2(OW), lh = lg2(OH);
   if (lw < 0 || lh < 0) lw = lh = -1;
-  launch_wgrad(dY, I, ws, N, IH, IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh, taps, grid, st);
+  int bm, bn;
+  if (wgrad_w8_ok(taps, IH, IW, OH, OW, IC, OC, stride, (long)N * IH * IW * IC, &bm, &bn))
+    launch_wgrad_w8(dY, I, ws, N, IH, IW, IC, OH, OW, OC, pix_per_split, splits, bws, lw, lh, taps, bn, st);
+  else
+    launch_wgrad(dY, I, ws, N, IH, IW, IC, OH, OW, OC, stride, pix_per_split, ncb, bws, lw, lh, taps, grid, st);
   launch_reduce2(ws, OC, IC, taps, splits, accumulate, bws, splits * (256 / BM), (float*)nullptr, (float*)nullptr, sg,
                  bws != nullptr, st);
   return (int)hipGetLastError();

@@ -423,13 +423,14 @@ def test_sampler_step_matches_posterior(H):
 
 
 @pytest.mark.parametrize("blas", [True, False])
-@pytest.mark.parametrize("chans", [[128, 128, 256], [512, 512]])
-def test_film_batch_with_gn_film(H, chans, blas):
+@pytest.mark.parametrize("chans,N,Hh", [([128, 128, 256], 4, 8), ([512, 512], 4, 8),
+                                        ([128, 256, 384], 32, 32)])   # 32768 rows: 8-wave 1x1 wgrad
+def test_film_batch_with_gn_film(H, chans, N, Hh, blas):
     """Level-batched FiLM projection feeding strided GN-FiLM: forward, the
     shared d(scale|shift) buffer and the segmented weight-gradient scatter
     against per-block fp32 linears."""
     torch.manual_seed(0)
-    N, Hh, K = 4, 8, 1024
+    K = 1024
     semb = (torch.randn(N, Hh, Hh, K, device=DEV)).to(BF)
     Ws = [torch.randn(2 * c, K, device=DEV) / 32 for c in chans]
     Bs = [torch.randn(2 * c, device=DEV) * 0.1 for c in chans]
