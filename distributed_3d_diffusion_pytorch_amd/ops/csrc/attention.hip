@@ -23,7 +23,10 @@
 // S = Q K^T and dP = dO V^T with KEYS on the lane, so P and dS are already the
 // A operands of dV = P^T dO and dK = dS^T Q; dQ = dS K goes through LDS once
 // into a per-key-block fp32 slab, and the slabs are summed in fixed order
-// (deterministic, no atomics).
+// (deterministic, no atomics).  The softmax-backward row term
+// D = rowsum(dO * O) is formed in the kernel while the query tile loads (no
+// preprocessing launch), and a single-key-block sequence (L = 64: the 8x8
+// level) writes bf16 dQ directly (no slab, no conversion launch).
 #include "common.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -159,32 +162,10 @@ __global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, 
   if (g == 0) lse[((long)n * heads + h) * L + q] = (m + log2f(l)) / LOG2E;
 }
 
-// ------------------------------------------------------- bwd preprocess --
-// Dv[n][h][q] = sum_d dO * O
-__global__ void attn_bwd_pre_k(const bf16* __restrict__ out, const bf16* __restrict__ dout, float* __restrict__ Dv,
-                               int N, int L, int C, int heads, int D) {
-  long total = (long)N * L * heads;
-  long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (t >= total) return;
-  int h = (int)(t % heads);
-  long r = t / heads;           // n*L + q
-  int q = (int)(r % L);
-  int n = (int)(r / L);
-  const bf16* o = out + r * C + h * D;
-  const bf16* d = dout + r * C + h * D;
-  float s = 0.f;
-  for (int k = 0; k < D; k += 8) {
-    f32x8 a = ld8(o + k), b = ld8(d + k);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += a[j] * b[j];
-  }
-  Dv[((long)n * heads + h) * L + q] = s;
-}
-
 // --------------------------------------------------------------- backward --
 template <int D>
 __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                  const float* __restrict__ lse, const float* __restrict__ Dv,
+                                                  const float* __restrict__ lse, const bf16* __restrict__ out,
                                                   float* __restrict__ dq_acc, bf16* __restrict__ dqkv, int L, int C,
                                                   int heads, int cross, float scale) {
   constexpr int KC = D / 32, DT = D / 16;
@@ -227,7 +208,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
     dv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const float* lse_nh = lse + ((long)n * heads + h) * L;
-  const float* D_nh = Dv + ((long)n * heads + h) * L;
+  const bool direct_dq = L == 64;                 // one key block: dQ is complete here
 
   for (int q0 = 0; q0 < L; q0 += 32) {
     __syncthreads();
@@ -243,9 +224,25 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
             *reinterpret_cast<const bf16x8*>(dout + row * C + h * D + c * 8);
       }
     }
-    if (tid < 32) {
-      lse_s[tid] = lse_nh[q0 + tid] * LOG2E;
-      D_s[tid] = D_nh[q0 + tid];
+    if (tid < 32) lse_s[tid] = lse_nh[q0 + tid] * LOG2E;
+    {
+      // D[q] = sum_d dO[q, d] O[q, d]: 8 adjacent lanes per query row
+      constexpr int PER = D / 8;                  // elements per lane (8 or 16)
+      const int r = tid >> 3, part = tid & 7;
+      const long row = (long)n * L + q0 + r;
+      const bf16* o = out + row * C + h * D + part * PER;
+      const bf16* d = dout + row * C + h * D + part * PER;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < PER; k += 8) {
+        const f32x8 a = ld8(o + k), b = ld8(d + k);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += a[j] * b[j];
+      }
+      acc += __shfl_xor(acc, 1, 64);
+      acc += __shfl_xor(acc, 2, 64);
+      acc += __shfl_xor(acc, 4, 64);
+      if (part == 0) D_s[r] = acc;
     }
     __syncthreads();
     f32x4 p[2], ds[2];
@@ -305,11 +302,19 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
       // This key block's dQ contribution goes to its own slab (plain stores,
       // every element written once); dq_convert_k sums the slabs in key-block
       // order, so dQ is bitwise reproducible (fp32 atomics were not)
-      float* slab = dq_acc + (long)kblk * gridDim.z * L * C;
+      if (direct_dq) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        long row = (long)n * L + q0 + 16 * qt + 4 * g + i;
-        slab[row * C + h * D + 16 * t + fr] = acc[i] * scale;
+        for (int i = 0; i < 4; ++i) {
+          long row = (long)n * L + q0 + 16 * qt + 4 * g + i;
+          dqkv[row * C3 + h * D + 16 * t + fr] = (bf16)(acc[i] * scale);
+        }
+      } else {
+        float* slab = dq_acc + (long)kblk * gridDim.z * L * C;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          long row = (long)n * L + q0 + 16 * qt + 4 * g + i;
+          slab[row * C + h * D + 16 * t + fr] = acc[i] * scale;
+        }
       }
     }
   }
@@ -356,24 +361,22 @@ D3D_API int d3d_attn_fwd(const void* qkv, void* out, float* lse, int N, int L, i
 }
 
 // dq_acc: [L/64, N, L, C] fp32 workspace (one slab per key block, fully
-// written); Dv: [N, heads, L] fp32 workspace; dqkv: [N, L, 3C] bf16 output
-// (every element written).
-D3D_API int d3d_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* Dv,
-                         float* dq_acc, void* dqkv, int N, int L, int C, int heads, int cross, float scale,
-                         hipStream_t st) {
+// written; unused and may be null when L == 64); dqkv: [N, L, 3C] bf16
+// output (every element written).
+D3D_API int d3d_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* dq_acc,
+                         void* dqkv, int N, int L, int C, int heads, int cross, float scale, hipStream_t st) {
   int D = C / heads;
-  long total = (long)N * L * heads;
-  hipLaunchKernelGGL(attn_bwd_pre_k, dim3((int)((total + 255) / 256)), dim3(256), 0, st, (const bf16*)out,
-                     (const bf16*)dout, Dv, N, L, C, heads, D);
+  if (L % 64 || (L > 64 && dq_acc == nullptr)) return (int)hipErrorInvalidValue;
   dim3 grid(L / 64, heads, N);
   if (D == 64)
-    hipLaunchKernelGGL(attn_bwd_k<64>, grid, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse, Dv, dq_acc,
-                       (bf16*)dqkv, L, C, heads, cross, scale);
+    hipLaunchKernelGGL(attn_bwd_k<64>, grid, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse,
+                       (const bf16*)out, dq_acc, (bf16*)dqkv, L, C, heads, cross, scale);
   else if (D == 128)
-    hipLaunchKernelGGL(attn_bwd_k<128>, grid, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse, Dv,
-                       dq_acc, (bf16*)dqkv, L, C, heads, cross, scale);
+    hipLaunchKernelGGL(attn_bwd_k<128>, grid, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse,
+                       (const bf16*)out, dq_acc, (bf16*)dqkv, L, C, heads, cross, scale);
   else
     return (int)hipErrorInvalidValue;
+  if (L == 64) return (int)hipGetLastError();
   long rows = (long)N * L;
   long g = (rows * C / 8 + 255) / 256;
   if (g > 4096) g = 4096;

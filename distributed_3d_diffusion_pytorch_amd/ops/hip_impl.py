@@ -1089,7 +1089,7 @@ class _FiLMBatch(torch.autograd.Function):
                                                 _st()), "film_wgrad_scatter")
                 else:
                     sp, pps = ctypes.c_int(), ctypes.c_int()
-                    _lib.d3d_conv_wgrad_plan2(rows, 1, 1, S, K, 1, ctypes.byref(sp), ctypes.byref(pps))
+                    _lib.d3d_conv_wgrad_plan3(rows, 1, 1, 1, 1, S, K, 1, 1, ctypes.byref(sp), ctypes.byref(pps))
                     ws = torch.empty(sp.value * S * K + 2 * sp.value * S, dtype=F32, device=x2.device)
                     _chk(_lib.d3d_conv_wgrad_seg(dy.data_ptr(), x2.data_ptr(), ws.data_ptr(), rows, 1, 1, K, 1, 1, S,
                                                  1, sp.value, pps.value, 1, 1, n, row0, wd, bd, _st()), "film_wgrad")
@@ -1153,12 +1153,12 @@ class _Attention(torch.autograd.Function):
         N, L, C3 = qkv.shape
         C = C3 // 3
         dout = dout.contiguous()
-        Dv = torch.empty(N, heads, L, dtype=F32, device=qkv.device)
-        # one fp32 dQ slab per 64-key block, summed in fixed order (deterministic)
-        dq = torch.empty(L // 64, N, L, C, dtype=F32, device=qkv.device)
+        # one fp32 dQ slab per 64-key block, summed in fixed order
+        # (deterministic); a single key block (L = 64) writes dQ directly
+        dq = torch.empty(L // 64, N, L, C, dtype=F32, device=qkv.device) if L > 64 else None
         dqkv = torch.empty_like(qkv)
-        _chk(_lib.d3d_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), Dv.data_ptr(),
-                               dq.data_ptr(), dqkv.data_ptr(), N, L, C, heads, int(cross), scale, _st()), "attn_bwd")
+        _chk(_lib.d3d_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), _ptr(dq),
+                               dqkv.data_ptr(), N, L, C, heads, int(cross), scale, _st()), "attn_bwd")
         return dqkv, None, None
 
 
