@@ -582,9 +582,34 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   const int k1 = (int)((long)(blockIdx.z + 1) * nk_all / gridDim.z);
   const int nk = k1 - k0;
   const int fr = lane & 15, fq = lane >> 4;
+  const int OHW = OH * OW;
+  // residual prefetch (see conv_halo_k); not on split-K partial launches
+  bf16x4 rres[TM][TN];
+  const bool pre_res = res != nullptr && part == nullptr && (ldo & 3) == 0;
+  if (pre_res) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const long pix = n0 + wn * WN + j * 16 + fr;
+      const long pc = pix < Mpix ? pix : 0;
+      const int img = (int)(pc / OHW);
+      const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pc - (long)img * OHW) : pc;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int co = m0 + wm * WM + i * 16 + fq * 4;
+        rres[i][j] = (pix < Mpix && co + 3 < OC) ? *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co)
+                                                 : bf16x4{};
+      }
+    }
+  }
   issue(k0, 0);
   if (ONEBAR) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (pre_res) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(__builtin_bit_cast(unsigned long long, rres[i][j])));
+    }
     __builtin_amdgcn_s_barrier();
   }
   for (int ks = 0; ks < nk; ++ks) {
@@ -629,7 +654,6 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     __builtin_amdgcn_s_barrier();                             // stage st free for reuse
   }
 
-  const int OHW = OH * OW;
   if (part) {
     float* slab = part + (long)blockIdx.z * Mpix * OC;
 #pragma unroll
@@ -648,6 +672,13 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   float gs[TM][1], gq[TM][1];                     // fused GroupNorm partials (gn_part_store)
 #pragma unroll
   for (int i = 0; i < TM; ++i) gs[i][0] = gq[i][0] = 0.f;
+  float cb[TM][4];                                // bias, once per row tile
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cb[i][e] = (bias && co + e < OC) ? bias[co + e] : 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     long pix = n0 + wn * WN + j * 16 + fr;
@@ -662,16 +693,21 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         int cc = co + e < OC ? co + e : OC - 1;
-        float t = acc[i][j][e] + (bias ? bias[cc] : 0.f);
+        float t = acc[i][j][e] + cb[i][e];
         if (row_bias) t += row_bias[(long)img * OC + cc];
         v[e] = t;
       }
       bf16* dst = O + pix * ldo + co;
       if (co + 3 < OC && (ldo & 3) == 0) {
         if (res) {
-          bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co);
+          if (pre_res) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+            for (int e = 0; e < 4; ++e) v[e] += (float)rres[i][j][e];
+          } else {
+            const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+          }
         }
         bf16x4 o4;
 #pragma unroll
@@ -820,8 +856,34 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
 
   const int nk = Kp / BKk;
   const int fr = lane & 15, fq = lane >> 4;
+  const int OHW = OH * OW;
+  // residual prefetch (see conv_halo_k): issued ahead of the first stage,
+  // drained with it, held in registers through the K loop
+  bf16x4 rres[TM][TN];
+  const bool vec_out = (ldo & 3) == 0;
+  if (res && vec_out) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const long pix = n0 + wn * WN + j * 16 + fr;
+      const long pc = pix < Mpix ? pix : 0;
+      const int img = (int)(pc / OHW);
+      const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pc - (long)img * OHW) : pc;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int co = m0 + wm * WM + i * 16 + fq * 4;
+        rres[i][j] = (pix < Mpix && co + 3 < OC) ? *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co)
+                                                 : bf16x4{};
+      }
+    }
+  }
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (res && vec_out) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(__builtin_bit_cast(unsigned long long, rres[i][j])));
+  }
   __builtin_amdgcn_s_barrier();
   for (int ks = 0; ks < nk; ++ks) {
     const int st = ks & 1;
@@ -849,13 +911,19 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
     __builtin_amdgcn_s_barrier();
   }
 
-  const int OHW = OH * OW;
   constexpr int NH = WN / 64;                     // 64-pixel GroupNorm partial slots per wave slice
   float gs[TM][NH], gq[TM][NH];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int h = 0; h < NH; ++h) gs[i][h] = gq[i][h] = 0.f;
+  float cb[TM][4];                                // bias, once per row tile
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cb[i][e] = (bias && co + e < OC) ? bias[co + e] : 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const long pix = n0 + wn * WN + j * 16 + fr;
@@ -870,16 +938,15 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int cc = co + e < OC ? co + e : OC - 1;
-        float t = acc[i][j][e] + (bias ? bias[cc] : 0.f);
+        float t = acc[i][j][e] + cb[i][e];
         if (row_bias) t += row_bias[(long)img * OC + cc];
         v[e] = t;
       }
       bf16* dst = O + pix * ldo + co;
-      if (co + 3 < OC && (ldo & 3) == 0) {
+      if (co + 3 < OC && vec_out) {
         if (res) {
-          bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * ldo + co);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+          for (int e = 0; e < 4; ++e) v[e] += (float)rres[i][j][e];
         }
         bf16x4 o4;
 #pragma unroll
@@ -1025,6 +1092,25 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     const int p = wn * WN + j * 16 + fr;
     hp0[j] = (p / OWT) * Gm::HW2 + (p % OWT);
   }
+  const int OHW = OH * OW;
+  // Residual prefetch: issued ahead of the first operand DMA and drained by
+  // its full wait, then held in registers through the K loop.  In the
+  // epilogue the 8-byte residual reads (16 pixels x 32 B per instruction)
+  // were fully exposed -- one block per CU, nothing left to overlap them --
+  // and cost +30 % on the level-0 conv (tools/kbench_conv_epi.py).
+  bf16x4 rres[TM][TN];
+  if (res) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const long pix = n0 + wn * WN + j * 16 + fr;
+      const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int co = m0 + wm * WM + i * 16 + fq * 4;
+        rres[i][j] = co < OC ? *reinterpret_cast<const bf16x4*>(res + rpix * OC + co) : bf16x4{};
+      }
+    }
+  }
 
   auto frags = [&](bf16x8 (&af)[TM], bf16x8 (&bfr)[TN], const bf16* a, const bf16* hb, int t) {
     const int kh = TRANS ? 2 - t / 3 : t / 3, kw = TRANS ? 2 - t % 3 : t % 3;
@@ -1090,6 +1176,13 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   halo_issue_a(sAr + Gm::ABUF, Wp, w_bytes, aoff, a_soff(1), wave);
   halo_issue_a(sAr + 2 * Gm::ABUF, Wp, w_bytes, aoff, a_soff(2), wave);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (res) {
+    // pin the prefetched values here (keeps the loads ahead of the K loop)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(__builtin_bit_cast(unsigned long long, rres[i][j])));
+  }
 
   for (int c = 0; c < NCH; ++c) {
     const bf16* hb = sH + (c & 1) * Gm::HBUF;
@@ -1134,32 +1227,40 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tail re-loads drained before exit
 
-  const int OHW = OH * OW;
   constexpr int NH = WN / 64;
   float gs[TM][NH], gq[TM][NH];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int h = 0; h < NH; ++h) gs[i][h] = gq[i][h] = 0.f;
+  // per-channel additive terms, once per row tile (not per element)
+  float cb[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = 0.f;
+      if (co + e < OC) {
+        if (bias) t += bias[co + e];
+        if (row_bias) t += row_bias[(long)img * OC + co + e];
+      }
+      cb[i][e] = t;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const long pix = n0 + wn * WN + j * 16 + fr;
-    const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int co = m0 + wm * WM + i * 16 + fq * 4;
       if (co >= OC) continue;
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float tv = acc[i][j][e] + (bias ? bias[co + e] : 0.f);
-        if (row_bias) tv += row_bias[(long)img * OC + co + e];
-        v[e] = tv;
-      }
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + cb[i][e];
       if (res) {
-        bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * OC + co);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+        for (int e = 0; e < 4; ++e) v[e] += (float)rres[i][j][e];
       }
       bf16x4 o4;
 #pragma unroll
