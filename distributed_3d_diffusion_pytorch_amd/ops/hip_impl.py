@@ -9,6 +9,7 @@ graph.
 from __future__ import annotations
 
 import contextlib
+import collections
 import ctypes
 import os
 import math
@@ -78,9 +79,35 @@ def _st() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+# Launch-checking debug mode (the counterpart of
+# CUDA_LAUNCH_BLOCKING for the native kernels): D3D_SYNC_CHECK=1 synchronises
+# the device after every native launch outside graph capture, so an
+# asynchronous fault (out-of-bounds access, trap) is reported at the op that
+# caused it, and keeps a ring of the last launches for the post-mortem.
+_SYNC_CHECK = os.environ.get("D3D_SYNC_CHECK", "0") == "1"
+_RECENT = collections.deque(maxlen=64)
+
+
+def set_sync_check(on: bool) -> None:
+    global _SYNC_CHECK
+    _SYNC_CHECK = bool(on)
+
+
+def recent_launches() -> list:
+    """Names of the last native launches (recorded with D3D_SYNC_CHECK=1)."""
+    return list(_RECENT)
+
+
 def _chk(rc: int, name: str) -> None:
     if rc != 0:
         raise RuntimeError(f"{name} failed with hipError {rc}")
+    if _SYNC_CHECK:
+        _RECENT.append(name)
+        if not torch.cuda.is_current_stream_capturing():
+            try:
+                torch.cuda.synchronize()
+            except RuntimeError as e:
+                raise RuntimeError(f"{name}: device fault after launch (recent: {list(_RECENT)[-8:]}): {e}") from e
 
 
 def _need_bf16(*ts):

@@ -948,3 +948,21 @@ def test_full_model_64px_matches_fp32_oracle():
     med_h, med_t = hv[len(hv) // 2], tv[len(tv) // 2]
     assert hv[-1] < 0.12, max(gh.items(), key=lambda kv: kv[1])
     assert med_h < 1.5 * med_t + 5e-3, (med_h, med_t)
+
+
+def test_sync_check_mode(H):
+    """D3D_SYNC_CHECK debug mode: every native launch is synchronised and
+    recorded; results are unchanged."""
+    torch.manual_seed(3)
+    x = torch.randn(2, 16, 16, 128, device=DEV).to(BF)
+    w = torch.randn(128, 128, 3, 3, device=DEV) / 34
+    ref = H.conv3x3(x, w, None)
+    H.set_sync_check(True)
+    try:
+        y = H.conv3x3(x, w, None)
+        g = H.group_norm(y, torch.ones(128, device=DEV), torch.zeros(128, device=DEV), 32, 1e-5, True)
+    finally:
+        H.set_sync_check(False)
+    assert torch.equal(y, ref) and torch.isfinite(g.float()).all()
+    names = H.recent_launches()
+    assert "conv" in names and "gn_apply2" in names, names
