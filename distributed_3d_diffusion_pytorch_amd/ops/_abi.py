@@ -67,12 +67,15 @@ SIGNATURES = {
     "d3d_ray_posenc": [P, P, P, P, P, P, P, P, I, I, I, P],
     # attention.hip
     "d3d_attn_fwd": [P, P, P, I, I, I, I, I, F, P],
+    "d3d_set_splitk_counters": [P, I],
     "d3d_attn_bwd": [P, P, P, P, P, P, I, I, I, I, I, F, P],
 }
 
 
 def declare(lib: C.CDLL) -> None:
     for name, args in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:          # an older build (A/B runs via D3D_LIB_PATH): calls fail when made
+            continue
         fn.argtypes = args
         fn.restype = C.c_int
