@@ -184,15 +184,17 @@ class GraphedTrainStep:
         self.H.refresh_weights()                 # descriptor table final before capture
         torch.cuda.synchronize()
         mode = "thread_local" if comm else "global"     # RCCL's watchdog thread keeps querying events
-        self.gA = torch.cuda.CUDAGraph()
-        self.gA.register_generator_state(tr.gen)
-        with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
-            self._body(comm)
+        # graphs sharing a memory pool are captured in their replay order
+        # (leading micro-batches first)
         if comm and nchunks > 1:
             self.gA0 = torch.cuda.CUDAGraph()
             self.gA0.register_generator_state(tr.gen)
             with torch.cuda.graph(self.gA0, pool=self.pool):
                 self._body(False)
+        self.gA = torch.cuda.CUDAGraph()
+        self.gA.register_generator_state(tr.gen)
+        with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
+            self._body(comm)
         self.gB = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.gB, pool=self.pool):
             self._update()

@@ -67,7 +67,6 @@ SIGNATURES = {
     "d3d_ray_posenc": [P, P, P, P, P, P, P, P, I, I, I, P],
     # attention.hip
     "d3d_attn_fwd": [P, P, P, I, I, I, I, I, F, P],
-    "d3d_set_splitk_counters": [P, I],
     "d3d_attn_bwd": [P, P, P, P, P, P, I, I, I, I, I, F, P],
 }
 

@@ -13,5 +13,6 @@ for B in 16 32; do
   python3 /root/repo/tools/rpstats.py "$db" --window $W --steps 10 --top 90 > $O/bs${B}_stats.txt
   python3 /root/repo/tools/rpstats.py "$db" --window $W --steps 10 --top 160 --grid > $O/bs${B}_grid.txt
   python3 /root/repo/tools/rpstats.py "$db" --busy $W >> $O/bs${B}_stats.txt
+  python3 /root/repo/tools/rpstats.py "$db" --solo $W --steps 10 --top 60 > $O/bs${B}_solo.txt
   find $O/rp$B -name '*.db' -delete
 done

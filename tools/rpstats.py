@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--busy", type=float, default=0.0,
                     help="occupancy of the last BUSY ms of the trace: union of kernel intervals vs span vs the sum "
                          "of kernel times (>1 overlap factor = concurrent kernels)")
+    ap.add_argument("--solo", type=float, default=0.0,
+                    help="over the last SOLO ms: per kernel, the time it ran ALONE on the device (exposed, on the "
+                         "critical path) vs overlapped with another kernel (hidden behind / sharing the chip)")
     a = ap.parse_args()
     db = sqlite3.connect(a.db)
     cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
@@ -46,6 +49,40 @@ def main():
               f"kernel sum {tot * 1e-6:.2f} ms (overlap x{tot / max(busy, 1):.2f}), {len(iv)} kernels, "
               f"{len(gaps)} gaps, median gap {gaps[len(gaps) // 2] * 1e-3 if gaps else 0:.2f} us, "
               f"gap sum {sum(gaps) * 1e-6:.2f} ms")
+        return
+    if a.solo:
+        rows = [(r[0].replace("(anonymous namespace)::", "").split("(")[0][:100], r[1], r[2])
+                for r in db.execute(f"select {name_col}, start, end from kernels")]
+        end = max(r[2] for r in rows)
+        lo = end - a.solo * 1e6
+        ev = []
+        for i, (nm, s0, e) in enumerate(rows):
+            if e <= lo:
+                continue
+            ev.append((max(s0, lo), 1, i))
+            ev.append((e, -1, i))
+        ev.sort()
+        active, last_t = set(), None
+        solo, shared = defaultdict(float), defaultdict(float)
+        for t, kind, i in ev:
+            if last_t is not None and active and t > last_t:
+                dt = t - last_t
+                if len(active) == 1:
+                    solo[rows[next(iter(active))][0]] += dt
+                else:
+                    for j in active:
+                        shared[rows[j][0]] += dt / len(active)
+            if kind == 1:
+                active.add(i)
+            else:
+                active.discard(i)
+            last_t = t
+        div = a.steps or 1
+        ts, tsh = sum(solo.values()), sum(shared.values())
+        print(f"solo (exposed) {ts * 1e-6 / div:.2f} ms, overlapped share {tsh * 1e-6 / div:.2f} ms "
+              f"(per {'step' if a.steps else 'window'})")
+        for k in sorted(solo, key=lambda k: -solo[k])[: a.top]:
+            print(f"{solo[k] * 1e-6 / div:9.3f} ms solo  {shared[k] * 1e-6 / div:9.3f} ms shared  {k}")
         return
     agg = defaultdict(lambda: [0.0, 0])
     t0, t1 = None, None
