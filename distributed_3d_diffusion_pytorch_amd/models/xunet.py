@@ -170,9 +170,11 @@ class AttnBlock(nn.Module):
         slot = ops.res_slot(x) if torch.is_grad_enabled() and x.requires_grad else None
         hn = self.groupnorm(x, res_slot=slot).reshape(N, H * W, C)
         o = self.attn_layer(hn, cross=(self.attn_type == "cross"))
+        # the output feeds the next GroupNorm (the cross-attention block's, or
+        # the next ResnetBlock's GN0): its statistics come out of this epilogue
         y = ops.linear(o, self.linear.weight, self.linear.bias, residual=x.reshape(N, H * W, C),
-                       out_scale=INV_SQRT2, res_slot=slot)
-        return y.reshape(N, H, W, C)
+                       out_scale=INV_SQRT2, res_slot=slot, gn_groups=self.groupnorm.gn.num_groups)
+        return ops.carry_gn_stats(y, y.reshape(N, H, W, C))
 
 
 class XUNetBlock(nn.Module):

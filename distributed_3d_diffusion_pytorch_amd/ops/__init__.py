@@ -59,10 +59,20 @@ def conv3x3(x, weight, bias, stride: int = 1, residual: Optional[torch.Tensor] =
 
 
 def linear(x, weight, bias, residual: Optional[torch.Tensor] = None, out_scale: float = 1.0, res_slot=None,
-           in_slot=None):
+           in_slot=None, gn_groups: int = 0):
+    """gn_groups: the output feeds a GroupNorm with that many groups (the HIP
+    epilogue then also emits its partial statistics)."""
     if use_hip(x):
-        return _h().linear(x, weight, bias, residual, out_scale, res_slot, in_slot)
+        return _h().linear(x, weight, bias, residual, out_scale, res_slot, in_slot, gn_groups)
     return _t.linear(x, weight, bias, residual, out_scale)
+
+
+def carry_gn_stats(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """A reshaped view keeps the fused GroupNorm statistics of its source."""
+    part = getattr(src, "_d3d_gnpart", None)
+    if part is not None:
+        dst._d3d_gnpart = part
+    return dst
 
 
 def cond_conv(rays_dir, orig_pe, weight, bias, stride: int, row_bias=None, residual=None, res_period: int = 0):

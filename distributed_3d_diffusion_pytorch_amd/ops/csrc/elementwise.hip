@@ -124,6 +124,65 @@ __global__ void add_scale_k(const bf16* __restrict__ a, const bf16* __restrict__
   }
 }
 
+// y = (a + b) * s fused with the partial statistics of the GroupNorm that
+// consumes y (the attention block output feeding the next block's
+// GroupNorm: xunet.py:220 then :140) -- the layout of conv.hip
+// gn_part_store, [N][G][P/64] x (sum, sum of squares) over the STORED bf16
+// values, so that GroupNorm skips its statistics pass exactly as after a conv.
+// One block per (64-pixel part, 64-channel slab): 16 threads per pixel x 4
+// channels, 16 pixels per pass; a slab holds whole groups (Cg <= 32) of one
+// image, so every (image, group, part) slot is written by exactly one block.
+// In place (y == a) is allowed: each element is read and written by one thread.
+__global__ void __launch_bounds__(256) add_scale_gn_k(const bf16* a, const bf16* __restrict__ b, bf16* y, float s,
+                                                      int C, int P, int G, float* __restrict__ gnp) {
+  constexpr int CB = 64, TPC = CB / 4, PPI = 256 / TPC, KP = 64 / PPI;
+  __shared__ float s_s[PPI][TPC], s_q[PPI][TPC];
+  const int tid = threadIdx.x, r = tid / TPC, cq = tid % TPC;
+  const long pix0 = (long)blockIdx.x * 64;
+  const int co = blockIdx.y * CB + cq * 4;
+  bf16x4 av[KP], bv[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {                 // every load of the block in flight together
+    const long off = (pix0 + k * PPI + r) * C + co;
+    av[k] = *reinterpret_cast<const bf16x4*>(a + off);
+    if (b) bv[k] = *reinterpret_cast<const bf16x4*>(b + off);
+  }
+  float sum = 0.f, sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    bf16x4 o4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = (float)av[k][e];
+      if (b) v += (float)bv[k][e];
+      o4[e] = (bf16)(v * s);
+      const float q = (float)o4[e];
+      sum += q;
+      sq += q * q;
+    }
+    *reinterpret_cast<bf16x4*>(y + (pix0 + k * PPI + r) * C + co) = o4;
+  }
+  s_s[r][cq] = sum;
+  s_q[r][cq] = sq;
+  __syncthreads();
+  const int Cg = C / G, ng = CB / Cg;
+  if (tid < ng) {
+    const int q4 = Cg / 4;
+    float u = 0.f, w = 0.f;
+    for (int rr = 0; rr < PPI; ++rr)
+      for (int j = 0; j < q4; ++j) {
+        u += s_s[rr][tid * q4 + j];
+        w += s_q[rr][tid * q4 + j];
+      }
+    const long n = pix0 / P;
+    const int t = (int)(pix0 - n * P) / 64;
+    const int g = (blockIdx.y * CB) / Cg + tid;
+    float* d = gnp + ((n * G + g) * (P / 64) + t) * 2;
+    d[0] = u;
+    d[1] = w;
+  }
+}
+
 // CFG ancestral step for fp32 z [b, D]:
 //   eps = (1+w) ec - w eu;  x0 = clamp((z - sigma eps)/alpha, -1, 1)
 //   mean = alpha_n (z (1-c)/alpha + c x0);  z' = mean + sqrt(var) * N(0,1) * add_noise
@@ -351,6 +410,19 @@ D3D_API int d3d_upsample2(const void* x, void* y, int N, int H, int W, int C, in
     hipLaunchKernelGGL(upsample2_k, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, N, H, W, C);
   return (int)hipGetLastError();
 }
+// y = (a + b) * s over [rows, C] with the GroupNorm partials of y (images of
+// P rows, G groups) in gnp [rows/P][G][P/64][2].  Returns -1 (nothing
+// launched) when the shape is not covered (the caller then uses
+// d3d_add_scale and the statistics pass runs as usual).
+D3D_API int d3d_add_scale_gn(const void* a, const void* b, void* y, float s, long rows, int C, int P, int G,
+                             float* gnp, hipStream_t st) {
+  const int Cg = G > 0 && C % G == 0 ? C / G : 0;
+  if (!(Cg == 4 || Cg == 8 || Cg == 16 || Cg == 32) || C % 64 || P % 64 || rows % P) return -1;
+  hipLaunchKernelGGL(add_scale_gn_k, dim3((unsigned)(rows / 64), (unsigned)(C / 64)), dim3(256), 0, st,
+                     (const bf16*)a, (const bf16*)b, (bf16*)y, s, C, P, G, gnp);
+  return (int)hipGetLastError();
+}
+
 D3D_API int d3d_add_scale(const void* a, const void* b, void* y, float s, long n, hipStream_t st) {
   hipLaunchKernelGGL(add_scale_k, dim3(ew_grid(n / 8)), dim3(256), 0, st, (const bf16*)a, (const bf16*)b, (bf16*)y,
                      s, n / 8);

@@ -917,7 +917,7 @@ class _Linear(torch.autograd.Function):
     hipBLASLt library GEMM + a fused HIP epilogue kernel for large ones."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, out_scale, res_slot=None, in_slot=None):
+    def forward(ctx, x, weight, bias, residual, out_scale, res_slot=None, in_slot=None, gn=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         P, IC = x2.shape
@@ -937,8 +937,21 @@ class _Linear(torch.autograd.Function):
                 y = torch.mm(x2, wb.t())
             if residual is not None or out_scale != 1.0:
                 r = residual.reshape(y.shape).contiguous() if residual is not None else None
-                _chk(_lib.d3d_add_scale(y.data_ptr(), _ptr(r), y.data_ptr(), float(out_scale), y.numel(), _st()),
-                     "add_scale")
+                done = False
+                if gn is not None and len(shp) == 3:
+                    # the epilogue also emits the consuming GroupNorm's partials
+                    L, G = shp[1], gn["groups"]
+                    gnp = torch.empty((P // L) * G * (L // 64) * 2 if L % 64 == 0 else 0, dtype=F32,
+                                      device=x.device)
+                    rc = _lib.d3d_add_scale_gn(y.data_ptr(), _ptr(r), y.data_ptr(), float(out_scale), P, OC, L, G,
+                                               gnp.data_ptr(), _st()) if gnp.numel() else -1
+                    if rc >= 0:
+                        _chk(rc, "add_scale_gn")
+                        gn["part"] = (gnp, L // 64)
+                        done = True
+                if not done:
+                    _chk(_lib.d3d_add_scale(y.data_ptr(), _ptr(r), y.data_ptr(), float(out_scale), y.numel(),
+                                            _st()), "add_scale")
         ctx.save_for_backward(x2, weight)
         ctx.cfg = (shp, out_scale, residual is not None, bias is not None)
         ctx.bias_param = bias
@@ -1014,7 +1027,7 @@ class _Linear(torch.autograd.Function):
             dres = g.reshape(*shp[:-1], OC)
         if dx is not None and in_slot is not None and in_slot.deposit(dx):
             dx = None
-        return dx, dW, db, dres, None, None, None
+        return dx, dW, db, dres, None, None, None, None
 
 
 class _FiLMSlot:
@@ -1147,14 +1160,32 @@ def film_batch(semb, weights, biases):
     return outs
 
 
-def linear(x, weight, bias, residual=None, out_scale=1.0, res_slot=None, in_slot=None):
+_EPI_GN_STATS = os.environ.get("D3D_EPI_GN_STATS", "1") != "0"     # A/B switch of the fused statistics
+
+
+def linear(x, weight, bias, residual=None, out_scale=1.0, res_slot=None, in_slot=None, gn_groups=0):
     """Per-pixel dense layer.  Forward and input-gradient are plain GEMMs on
     hipBLASLt (≈1 PF/s on these shapes); the weight gradient -- a GEMM whose
     reduction runs over every pixel of the batch (K up to 5e5), where
     hipBLASLt drops to 45-240 TF/s -- uses the split-K MFMA kernel, and the
-    bias / residual epilogues are fused HIP kernels."""
+    bias / residual epilogues are fused HIP kernels.  ``gn_groups`` (x of
+    shape [N, L, C] with a residual / scale epilogue): the epilogue also emits
+    the partial statistics of the GroupNorm that reads the output (attached as
+    ``_d3d_gnpart``; see :func:`carry_gn_stats` across reshapes)."""
     _need_bf16(x, residual)
-    return _Linear.apply(x, weight, bias, residual, out_scale, res_slot, in_slot)
+    gn = {"groups": int(gn_groups)} if (gn_groups and _EPI_GN_STATS) else None
+    y = _Linear.apply(x, weight, bias, residual, out_scale, res_slot, in_slot, gn)
+    if gn is not None and "part" in gn:
+        y._d3d_gnpart = (gn["part"][0], int(gn_groups), gn["part"][1])
+    return y
+
+
+def carry_gn_stats(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """Keep fused GroupNorm partials on a reshaped view of the same data."""
+    part = getattr(src, "_d3d_gnpart", None)
+    if part is not None:
+        dst._d3d_gnpart = part
+    return dst
 
 
 # ------------------------------------------------------------ attention ----

@@ -966,3 +966,31 @@ def test_sync_check_mode(H):
     assert torch.equal(y, ref) and torch.isfinite(g.float()).all()
     names = H.recent_launches()
     assert "conv" in names and "gn_apply2" in names, names
+
+
+@pytest.mark.parametrize("N,L,C", [(4, 256, 256), (8, 64, 512), (2, 64, 128)])
+def test_linear_residual_fused_gn_stats(H, N, L, C):
+    """Attention-output epilogue (residual + scale) emitting the consuming
+    GroupNorm's partial statistics == the statistics pass (GN+SiLU and
+    GN-FiLM), and the output itself == the plain epilogue."""
+    torch.manual_seed(17)
+    x = torch.randn(N, L, C, device=DEV).to(BF)
+    w = torch.randn(C, C, device=DEV) / math.sqrt(C)
+    b = torch.randn(C, device=DEV) * 0.2
+    r = torch.randn(N, L, C, device=DEV).to(BF)
+    y = H.linear(x, w, b, r, 1 / math.sqrt(2), gn_groups=32)
+    y0 = H.linear(x, w, b, r, 1 / math.sqrt(2))
+    assert torch.equal(y, y0)
+    assert hasattr(y, "_d3d_gnpart")
+    Hh = int(math.isqrt(L))
+    y4 = H.carry_gn_stats(y, y.reshape(N, Hh, Hh, C))
+    plain = y4.detach().clone()
+    gam = torch.rand(C, device=DEV) + 0.5
+    bet = torch.randn(C, device=DEV) * 0.1
+    a1 = H.group_norm(y4, gam, bet, 32, 1e-5, True)
+    r1 = H.group_norm(plain, gam, bet, 32, 1e-5, True)
+    assert rel(a1, r1) < 1e-2, rel(a1, r1)
+    ss = (torch.randn(N, Hh, Hh, 2 * C, device=DEV) * 0.5).to(BF)
+    a2 = H.gn_film(y4, gam, bet, ss, 32, 1e-5, 0.0, False, 0)
+    r2 = H.gn_film(plain, gam, bet, ss, 32, 1e-5, 0.0, False, 0)
+    assert rel(a2, r2) < 1e-2, rel(a2, r2)
