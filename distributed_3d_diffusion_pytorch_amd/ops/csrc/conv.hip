@@ -2692,15 +2692,20 @@ static int g_halo256 = getenv("D3D_HALO256") ? atoi(getenv("D3D_HALO256")) : 0;
 static int g_halo_pf = getenv("D3D_HALO_PF") ? atoi(getenv("D3D_HALO_PF")) : 0;
 // 64 x 64 no-split tiles (conv_small.hip) where the 128 x 128 kernels would
 // split K over a small grid (the low-resolution levels at small per-GPU batch)
-static int g_s64 = getenv("D3D_CONV_S64") ? atoi(getenv("D3D_CONV_S64")) : 0;
+static int g_s64 = getenv("D3D_CONV_S64") ? atoi(getenv("D3D_CONV_S64")) : 1;
 extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias, const float* row_bias,
                                 const void* res, void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW,
                                 int OC, int ldo, int stride, int trans, float scale, int res_nmod, int taps,
                                 float* gnp, int gn_groups, int* gn_done, hipStream_t st);
+// 64x64 no-split tiles (conv_small.hip) on grids of at most D3D_S64_MAXB
+// 128x128 blocks (default 160): the 16x16 / 8x8 levels at 16 examples per GPU
+// and the 8x8 level at 32 (in-graph A/B: +1.1 % at bs16; the 16x16 level at
+// bs32, 256 such blocks, stays on split-K bufl, which is faster there)
+static const long g_s64_maxb = getenv("D3D_S64_MAXB") ? atol(getenv("D3D_S64_MAXB")) : 160;
 static bool s64_wanted(long Mpix, int OC, int ICp, int taps) {
   const long blocks128 = ((Mpix + 127) / 128) * ((OC + 127) / 128);
   const long blocks64 = ((Mpix + 63) / 64) * (OC / 64);
-  return g_s64 && OC % 64 == 0 && (taps * ICp) % 64 == 0 && blocks128 < 384 && blocks64 >= 128;
+  return g_s64 && OC % 64 == 0 && (taps * ICp) % 64 == 0 && blocks128 <= g_s64_maxb && blocks64 >= 128;
 }
 static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline, 2: buffer-descriptor LDS-DMA
 static int g_conv_korder = 1;     // glds k-step order: 1 channel-chunk major, 0 tap major

@@ -31,7 +31,7 @@ Inside HIP-graph capture (:meth:`submit`, ``D3D_GRAPH_WGRAD_STREAM``): a fork
 per weight gradient cost ~7 us of graph dependency latency per edge -- ~1,600
 edges ate the concurrency (busy 88.7 %, profiles/busy_bs16_side_stream.txt).
 There the weight-gradient jobs are DEFERRED instead: queued as closures and
-flushed onto the side stream ``D3D_WGRAD_DEFER_BATCH`` (default 4) at a time
+flushed onto the side stream ``D3D_WGRAD_DEFER_BATCH`` (default 8; 4 measured 1.5 % slower at bs16) at a time
 behind ONE fork each, and joined once at the end of backward, so the graph
 holds a few dozen cross-stream edges while the weight-gradient branch runs
 concurrently with the input-gradient chain.  Deferred operands stay alive in
@@ -58,7 +58,7 @@ class GradSink:
         self.notify: Optional[Callable[[int], None]] = None
         self.stream_enabled = os.environ.get("D3D_WGRAD_STREAM", "1") != "0"
         self.graph_defer = os.environ.get("D3D_GRAPH_WGRAD_STREAM", "1") != "0"
-        self.defer_batch = max(1, int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "4")))
+        self.defer_batch = max(1, int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "8")))
         self._queue = []
         self._streams: Dict[int, "torch.cuda.Stream"] = {}
         self._forked = set()
