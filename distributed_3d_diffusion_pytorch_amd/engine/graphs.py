@@ -79,6 +79,9 @@ def probe_graph_collective(device: torch.device) -> bool:
     return bool(flag.item() > 0.5)
 
 
+_FUSED_UPDATE = os.environ.get("D3D_FUSED_UPDATE", "1") != "0"
+
+
 class GraphCaptureError(RuntimeError):
     """The training step could not be captured (on this rank or any other):
     the trainer falls back to the eager step on every rank."""
@@ -135,7 +138,11 @@ class GraphedTrainStep:
 
     def _update(self) -> None:
         o = self.tr.optim
-        self.H.adam_flat_dev(o.flat.data, o.flat.grad, o.exp_avg, o.exp_avg_sq, o.ema, self.hp)
+        if _FUSED_UPDATE:
+            # Adam + operand repack fused (ops.hip_impl.adam_update_all)
+            self.H.adam_update_all(o.flat, o.exp_avg, o.exp_avg_sq, o.ema, self.hp)
+        else:
+            self.H.adam_flat_dev(o.flat.data, o.flat.grad, o.exp_avg, o.exp_avg_sq, o.ema, self.hp)
         o.flat.grad.zero_()
         self.loss_acc.zero_()
 
@@ -182,6 +189,8 @@ class GraphedTrainStep:
                 self._body(comm)
         torch.cuda.current_stream().wait_stream(s)
         self.H.refresh_weights()                 # descriptor table final before capture
+        if _FUSED_UPDATE:
+            self.H.prepare_fused_update(tr.flat)
         torch.cuda.synchronize()
         mode = "thread_local" if comm else "global"     # RCCL's watchdog thread keeps querying events
         # graphs sharing a memory pool are captured in their replay order

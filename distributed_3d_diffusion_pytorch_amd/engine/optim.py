@@ -17,11 +17,14 @@ checkpoints load unchanged.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
 
 from ..parallel.flat import FlatParams
+
+FUSED_UPDATE = os.environ.get("D3D_FUSED_UPDATE", "1") != "0"
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -79,10 +82,14 @@ class FusedAdam(torch.optim.Optimizer):
         from .. import ops
         if p.is_cuda and ops.use_hip(p, any_dtype=True):
             from ..ops import hip_impl
-            if coef is not None:
+            if coef is not None or FUSED_UPDATE:
                 hp = self.hparams(grad_scale).to(p.device, non_blocking=True)
-                hp[6:7].mul_(coef)
-                hip_impl.adam_flat_dev(p, gr, self.exp_avg, self.exp_avg_sq, self.ema, hp)
+                if coef is not None:
+                    hp[6:7].mul_(coef)
+                if FUSED_UPDATE:        # Adam + bf16 operand repack in one pass over the tiles
+                    hip_impl.adam_update_all(self.flat, self.exp_avg, self.exp_avg_sq, self.ema, hp)
+                else:
+                    hip_impl.adam_flat_dev(p, gr, self.exp_avg, self.exp_avg_sq, self.ema, hp)
             else:
                 g = self.param_groups[0]
                 lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]

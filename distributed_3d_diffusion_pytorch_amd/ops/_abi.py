@@ -68,6 +68,7 @@ SIGNATURES = {
     "d3d_ray_posenc": [P, P, P, P, P, P, P, P, I, I, I, P],
     # attention.hip
     "d3d_attn_fwd": [P, P, P, I, I, I, I, I, F, P],
+    "d3d_adam_fused": [P, P, P, P, P, P, P, P, I, P, P, I, P],
     "d3d_attn_bwd": [P, P, P, P, P, P, I, I, I, I, I, F, P],
 }
 

@@ -71,7 +71,149 @@ __global__ void adam_dev_k(float* __restrict__ p, const float* __restrict__ g, f
     }
   }
 }
+
+__device__ __forceinline__ float adam_elem(float pp, float gg, float& mm, float& vv, float b1, float b2, float eps,
+                                           float wd, float step_size, float inv_bc2, float grad_scale) {
+  float gj = gg * grad_scale;
+  if (wd != 0.f) gj += wd * pp;
+  mm = mm + (1.f - b1) * (gj - mm);
+  vv = vv * b2 + (1.f - b2) * gj * gj;
+  const float denom = sqrtf(vv) * inv_bc2 + eps;
+  return pp - step_size * (mm / denom);
+}
+
+// ---- fused update + bf16 repack (graph step and eager step) ----------------
+// Adam over a table of flat ranges (the parameters that have no packed MFMA
+// operand): block -> (range, 4096-element chunk) through a host-built map.
+struct AdamRange {
+  long start, len;
+  int blk0, pad;
+};
+
+__global__ void __launch_bounds__(256) adam_ranges_k(float* __restrict__ p, const float* __restrict__ g,
+                                                     float* __restrict__ m, float* __restrict__ v,
+                                                     float* __restrict__ ema, const float* __restrict__ hp,
+                                                     const AdamRange* __restrict__ ranges,
+                                                     const int* __restrict__ blk_range) {
+  const AdamRange r = ranges[blk_range[blockIdx.x]];
+  const long base = r.start + (long)(blockIdx.x - r.blk0) * 4096;
+  const long end = r.start + r.len;
+  const float b1 = hp[0], b2 = hp[1], eps = hp[2], wd = hp[3], step_size = hp[4], inv_bc2 = 1.0f / hp[5],
+              grad_scale = hp[6], ema_w = hp[7];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const long i = base + ((long)k * 256 + threadIdx.x) * 4;     // ranges are 64-element aligned
+    if (i >= end) break;
+    f32x4 pp = *reinterpret_cast<f32x4*>(p + i);
+    const f32x4 gg = *reinterpret_cast<const f32x4*>(g + i);
+    f32x4 mm = *reinterpret_cast<f32x4*>(m + i);
+    f32x4 vv = *reinterpret_cast<f32x4*>(v + i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float mj = mm[j], vj = vv[j];
+      pp[j] = adam_elem(pp[j], gg[j], mj, vj, b1, b2, eps, wd, step_size, inv_bc2, grad_scale);
+      mm[j] = mj;
+      vv[j] = vj;
+    }
+    *reinterpret_cast<f32x4*>(p + i) = pp;
+    *reinterpret_cast<f32x4*>(m + i) = mm;
+    *reinterpret_cast<f32x4*>(v + i) = vv;
+    if (ema) {
+      f32x4 ee = *reinterpret_cast<f32x4*>(ema + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ee[j] = ee[j] + ema_w * (pp[j] - ee[j]);
+      *reinterpret_cast<f32x4*>(ema + i) = ee;
+    }
+  }
+}
+
+// Adam of one (32 output x 16 input channel x taps) tile of an OIHW weight
+// fused with its bf16 MFMA operands: the updated tile is staged in LDS and
+// written as the forward pack [OCp][taps][ICp] and / or the transposed pack
+// [ICp][taps][OCp] (the layouts of conv.hip pack_all_k; padding lanes are
+// left untouched -- they hold the zeros written when the operand was built).
+// Saves the repack's second read of the fp32 masters.
+struct AdamTile {
+  long off;                    // flat index of the weight
+  bf16* dst0;                  // forward pack (or null)
+  bf16* dst1;                  // transposed pack (or null)
+  int OC, IC, taps, ICp0, OCp1, blk0;
+};
+
+__global__ void __launch_bounds__(256) adam_pack_tiles_k(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v,
+                                                         float* __restrict__ ema, const float* __restrict__ hp,
+                                                         const AdamTile* __restrict__ tiles,
+                                                         const int* __restrict__ blk_tile) {
+  __shared__ float tile[32 * 16 * 9];
+  const AdamTile d = tiles[blk_tile[blockIdx.x]];
+  const int local = blockIdx.x - d.blk0, tid = threadIdx.x, T = d.taps;
+  const int nct = (d.OC + 31) / 32;
+  const int co0 = (local % nct) * 32, ci0 = (local / nct) * 16;
+  const int nci = min(16, d.IC - ci0), nco = min(32, d.OC - co0);
+  const float b1 = hp[0], b2 = hp[1], eps = hp[2], wd = hp[3], step_size = hp[4], inv_bc2 = 1.0f / hp[5],
+              grad_scale = hp[6], ema_w = hp[7];
+  // tile element k -> (row r, q = ci * T + tap); each row's 16 * T elements
+  // are contiguous in the OIHW master (16 * 9 floats = 576 B)
+  const int RW = 16 * T;
+  for (int k = tid; k < 32 * RW; k += 256) {
+    const int r = k / RW, q = k - r * RW;
+    const int ci = q / T;
+    if (r >= nco || ci >= nci) continue;
+    const long i = d.off + ((long)(co0 + r) * d.IC + ci0) * T + q;
+    float mm = m[i], vv = v[i];
+    const float pn = adam_elem(p[i], g[i], mm, vv, b1, b2, eps, wd, step_size, inv_bc2, grad_scale);
+    p[i] = pn;
+    m[i] = mm;
+    v[i] = vv;
+    if (ema) ema[i] = ema[i] + ema_w * (pn - ema[i]);
+    tile[k] = pn;
+  }
+  __syncthreads();
+  if (d.dst1) {
+    // dst1[ci][tap][co0 .. co0+31]: 8 consecutive output channels per store
+    for (int k = tid; k < 16 * T * 4; k += 256) {
+      const int c8 = (k & 3) * 8, rt = k >> 2;
+      const int ci = rt / T, tap = rt % T;
+      if (ci >= nci || c8 >= nco) continue;
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16)(c8 + e < nco ? tile[(c8 + e) * RW + ci * T + tap] : 0.f);
+      *reinterpret_cast<bf16x8*>(d.dst1 + ((long)(ci0 + ci) * T + tap) * d.OCp1 + co0 + c8) = o;
+    }
+  }
+  if (d.dst0) {
+    // dst0[co][tap][ci0 .. ci0+15]: two 8-channel stores per (co, tap)
+    for (int k = tid; k < 32 * T * 2; k += 256) {
+      const int h = k & 1, rt = k >> 1;
+      const int r = rt / T, tap = rt % T;
+      if (r >= nco || h * 8 >= nci) continue;
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ci = h * 8 + e;
+        o[e] = (bf16)(ci < nci ? tile[r * RW + ci * T + tap] : 0.f);
+      }
+      *reinterpret_cast<bf16x8*>(d.dst0 + ((long)(co0 + r) * T + tap) * d.ICp0 + ci0 + h * 8) = o;
+    }
+  }
+}
 }  // namespace
+
+// One optimizer step over the flat buffers, repacking the MFMA operands of
+// the tile-table weights on the way (the repack of every other cached
+// operand -- plain casts, channel slices -- follows as d3d_pack_all).
+D3D_API int d3d_adam_fused(float* p, const float* g, float* m, float* v, float* ema, const float* hp,
+                           const void* ranges, const int* blk_range, int range_blocks, const void* tiles,
+                           const int* blk_tile, int tile_blocks, hipStream_t st) {
+  if (range_blocks > 0)
+    hipLaunchKernelGGL(adam_ranges_k, dim3(range_blocks), dim3(256), 0, st, p, g, m, v, ema, hp,
+                       (const AdamRange*)ranges, blk_range);
+  if (tile_blocks > 0)
+    hipLaunchKernelGGL(adam_pack_tiles_k, dim3(tile_blocks), dim3(256), 0, st, p, g, m, v, ema, hp,
+                       (const AdamTile*)tiles, blk_tile);
+  return (int)hipGetLastError();
+}
 
 D3D_API int d3d_adam_dev(float* p, const float* g, float* m, float* v, float* ema, long n, const float* hp,
                          hipStream_t st) {

@@ -178,6 +178,19 @@ def _pack_blocks(OC: int, OCp: int, ICp: int, mode: int) -> int:
     return (OC + 2047) // 2048
 
 
+def _desc_tensors(rows, blk):
+    """Device descriptor table (conv.hip PackDesc rows) + block -> row map."""
+    import numpy as np
+    dt = np.dtype([("src", np.uint64), ("dst", np.uint64), ("OC", np.int32), ("IC", np.int32),
+                   ("OCp", np.int32), ("ICp", np.int32), ("taps", np.int32), ("mode", np.int32),
+                   ("blk0", np.int32), ("ICs", np.int32)])
+    arr = np.array(rows, dtype=dt)
+    host = torch.from_numpy(arr.view(np.uint8).copy())
+    counts = np.diff(np.append(arr["blk0"], blk))
+    bmap = torch.from_numpy(np.repeat(np.arange(len(rows), dtype=np.int32), counts))
+    return host.to("cuda"), bmap.to("cuda")
+
+
 def refresh_weights() -> None:
     """After an optimizer update of the master weights: one launch repacks
     every cached operand; cache tokens advance to the new epoch."""
@@ -185,7 +198,6 @@ def refresh_weights() -> None:
     if not _WCACHE:
         return
     if _DESC_TABLE[2] != _REV[0]:
-        import numpy as np
         rows = []
         blk = 0
         for key, (tok, t, (p, desc)) in _WCACHE.items():
@@ -196,14 +208,7 @@ def refresh_weights() -> None:
             ics = desc[7] if len(desc) > 7 else 0            # source IC stride
             rows.append((p.data_ptr() + src_off, t.data_ptr(), OC, IC, OCp, ICp, taps, mode, blk, ics))
             blk += _pack_blocks(OC, OCp, ICp, mode)
-        dt = np.dtype([("src", np.uint64), ("dst", np.uint64), ("OC", np.int32), ("IC", np.int32),
-                       ("OCp", np.int32), ("ICp", np.int32), ("taps", np.int32), ("mode", np.int32),
-                       ("blk0", np.int32), ("ICs", np.int32)])
-        arr = np.array(rows, dtype=dt)
-        host = torch.from_numpy(arr.view(np.uint8).copy())
-        _DESC_TABLE[0] = host.to("cuda", non_blocking=False)
-        counts = np.diff(np.append(arr["blk0"], blk))
-        _DESC_TABLE[1] = torch.from_numpy(np.repeat(np.arange(len(rows), dtype=np.int32), counts)).to("cuda")
+        _DESC_TABLE[0], _DESC_TABLE[1] = _desc_tensors(rows, blk)
         _DESC_TABLE[2] = _REV[0]
         _DESC_TABLE[3] = blk
     _chk(_lib.d3d_pack_all(_DESC_TABLE[0].data_ptr(), _DESC_TABLE[1].data_ptr(), _DESC_TABLE[3], _st()), "pack_all")
@@ -1363,6 +1368,114 @@ def adam_flat(p, g, m, v, ema, lr, b1, b2, eps, wd, step_size, bc2_sqrt, grad_sc
     _chk(_lib.d3d_adam(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(ema), p.numel(), b1, b2, eps, wd,
                        step_size, bc2_sqrt, grad_scale, ema_decay, _st()), "adam")
     refresh_weights()
+
+
+# Fused optimizer step + operand repack (adam.hip d3d_adam_fused).  Tables
+# (built on the host when the weight cache changes, never inside a capture):
+#   tiles  -- weights whose cached MFMA operands are plain forward / transposed
+#             packs: their Adam runs tile by tile and writes the packs from the
+#             updated tile (the repack never re-reads their fp32 masters);
+#   ranges -- every other span of the flat buffer: plain vectorised Adam;
+#   rest   -- the remaining cached operands (bf16 casts, channel slices):
+#             repacked by pack_all after both.
+_FUSED = {}
+
+
+def _fused_tables(flat):
+    import numpy as np
+    key = id(flat)
+    ent = _FUSED.get(key)
+    if ent is not None and ent["rev"] == _REV[0] and ent["flat"] is flat:
+        return ent
+    pidx = {id(p): i for i, p in enumerate(flat.params)}
+    per = {}                                   # param index -> {"0": (t, desc), "1": (t, desc)}
+    absorbed = set()
+    for ckey, (tok, t, (p, desc)) in _WCACHE.items():
+        i = pidx.get(id(p))
+        if i is None or desc is None or len(desc) > 6 or desc[5] not in (0, 1):
+            continue
+        OC, IC, OCp, ICp, taps, mode = desc[:6]
+        if p.shape[0] != OC or p.numel() != OC * IC * taps or taps > 9:
+            continue
+        slot = per.setdefault(i, {})
+        if str(mode) in slot:
+            continue
+        slot[str(mode)] = (t, desc)
+        absorbed.add(ckey)
+    # tile table
+    trows, tblk = [], 0
+    for i, slot in sorted(per.items()):
+        prm = flat.params[i]
+        t0 = slot.get("0")
+        t1 = slot.get("1")
+        d = (t0 or t1)[1]
+        OC, IC, taps = d[0], d[1], d[4]
+        trows.append((flat.offsets[i], t0[0].data_ptr() if t0 else 0, t1[0].data_ptr() if t1 else 0, OC, IC, taps,
+                      t0[1][3] if t0 else 0, t1[1][2] if t1 else 0, tblk))
+        tblk += ((OC + 31) // 32) * ((IC + 15) // 16)
+    # range table: the complement of the tile weights' spans
+    tiled = sorted((flat.offsets[i], flat.span(i)[1]) for i in per)
+    rrows, rblk, pos = [], 0, 0
+    for a, b in tiled + [(flat.numel, flat.numel)]:
+        if a > pos:
+            rrows.append((pos, a - pos, rblk, 0))
+            rblk += (a - pos + 4095) // 4096
+        pos = max(pos, b)
+    dev = flat.data.device
+    tdt = np.dtype([("off", np.int64), ("dst0", np.uint64), ("dst1", np.uint64), ("OC", np.int32),
+                    ("IC", np.int32), ("taps", np.int32), ("ICp0", np.int32), ("OCp1", np.int32), ("blk0", np.int32)])
+    rdt = np.dtype([("start", np.int64), ("len", np.int64), ("blk0", np.int32), ("pad", np.int32)])
+
+    def table(rows, dt, nblk):
+        if not rows:
+            return None, None
+        arr = np.array(rows, dtype=dt)
+        counts = np.diff(np.append(arr["blk0"], nblk))
+        bmap = np.repeat(np.arange(len(rows), dtype=np.int32), counts)
+        return (torch.from_numpy(arr.view(np.uint8).copy()).to(dev), torch.from_numpy(bmap).to(dev))
+    tt, tb = table(trows, tdt, tblk)
+    rt, rb = table(rrows, rdt, rblk)
+    rest_rows, rest_blk = [], 0
+    for ckey, (tok, t, (p, desc)) in _WCACHE.items():
+        if desc is None or ckey in absorbed:
+            continue
+        OC, IC, OCp, ICp, taps, mode = desc[:6]
+        src_off = desc[6] if len(desc) > 6 else 0
+        ics = desc[7] if len(desc) > 7 else 0
+        rest_rows.append((p.data_ptr() + src_off, t.data_ptr(), OC, IC, OCp, ICp, taps, mode, rest_blk, ics))
+        rest_blk += _pack_blocks(OC, OCp, ICp, mode)
+    rd, rm = _desc_tensors(rest_rows, rest_blk) if rest_rows else (None, None)
+    ent = {"rev": _REV[0], "flat": flat, "tiles": (tt, tb, tblk), "ranges": (rt, rb, rblk),
+           "rest": (rd, rm, rest_blk)}
+    _FUSED[key] = ent
+    return ent
+
+
+def prepare_fused_update(flat) -> None:
+    """Build the fused-update tables now (host work; call before a capture)."""
+    _fused_tables(flat)
+
+
+def adam_update_all(flat, m, v, ema, hp) -> None:
+    """One optimizer step over the whole flat buffer with the cached bf16
+    operands repacked from the updated weights (replaces adam_flat_dev +
+    refresh_weights).  Inside a graph capture the tables must already exist
+    (:func:`prepare_fused_update`)."""
+    capturing = torch.cuda.is_current_stream_capturing()
+    ent = _FUSED.get(id(flat))
+    if ent is None or ent["rev"] != _REV[0] or ent["flat"] is not flat:
+        if capturing:
+            raise RuntimeError("fused update tables are stale inside a graph capture")
+        ent = _fused_tables(flat)
+    (tt, tb, tblk), (rt, rb, rblk), (rd, rm, rest_blk) = ent["tiles"], ent["ranges"], ent["rest"]
+    _chk(_lib.d3d_adam_fused(flat.data.data_ptr(), flat.grad.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(ema),
+                             hp.data_ptr(), _ptr(rt), _ptr(rb), int(rblk), _ptr(tt), _ptr(tb), int(tblk), _st()),
+         "adam_fused")
+    if rest_blk:
+        _chk(_lib.d3d_pack_all(rd.data_ptr(), rm.data_ptr(), rest_blk, _st()), "pack_all")
+    _EPOCH[0] += 1
+    for e in _WCACHE.values():
+        e[0] = (e[2][0]._version, _EPOCH[0])
 
 
 def adam_flat_dev(p, g, m, v, ema, hp, refresh=True):
