@@ -69,6 +69,10 @@ SIGNATURES = {
     # attention.hip
     "d3d_attn_fwd": [P, P, P, I, I, I, I, I, F, P],
     "d3d_adam_fused": [P, P, P, P, P, P, P, P, I, P, P, I, P],
+    "d3d_gemm_nt_ok": [I, I, I, I, I],
+    "d3d_gemm_tune": [I, I, I],
+    "d3d_gemm_nt": [P, P, P, P, P, I, I, I, I, I, I, I, F, F, P],
+    "d3d_gemm_nt_gn": [P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, I, I, P],
     "d3d_attn_bwd": [P, P, P, P, P, P, I, I, I, I, I, F, P],
 }
 

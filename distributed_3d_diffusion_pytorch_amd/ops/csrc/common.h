@@ -110,3 +110,68 @@ __device__ __forceinline__ Moments merge_moments(Moments a, Moments b) {
 }
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ----------------------------------------- fused GroupNorm statistics -----
+// GroupNorm partial statistics of a conv output, produced by the conv's
+// epilogue so the GroupNorm that consumes the output skips its statistics
+// pass (one full read of the activation).  Granularity: one group x 64
+// pixels of one image (HW % 64 == 0): gnp[((n * G + g) * nparts + t) * 2] =
+// (sum, sum of squares) of the bf16-rounded outputs, t = (pixel % HW) / 64,
+// nparts = HW / 64.  Every slot is written by exactly one wave: no atomics,
+// deterministic.  s/q: per (16-channel MFMA row tile i, 64-pixel half h)
+// lane sums over its 4 channels and its pixels.
+template <int TM, int NH>
+__device__ __forceinline__ void gn_part_store(float (&s)[TM][NH], float (&q)[TM][NH], int lane, int co_base,
+                                              long pix0, int OC, int G, int HW, long Mpix, float* __restrict__ gnp) {
+  const int fr = lane & 15, fq = lane >> 4;
+  const int Cg = OC / G;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      float a = s[i][h], b = q[i][h];
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {         // the 16 pixels of a fragment column
+        a += __shfl_xor(a, m, 64);
+        b += __shfl_xor(b, m, 64);
+      }
+      if (Cg >= 8) {                              // 4-channel lane groups -> 8 / 16 / 32-channel groups
+        a += __shfl_xor(a, 16, 64);
+        b += __shfl_xor(b, 16, 64);
+      }
+      if (Cg >= 16) {
+        a += __shfl_xor(a, 32, 64);
+        b += __shfl_xor(b, 32, 64);
+      }
+      s[i][h] = a;
+      q[i][h] = b;
+    }
+  if (fr != 0) return;
+  const int nparts = HW / 64;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int co = co_base + i * 16 + fq * 4;
+    if (Cg >= 32) {                               // 32-channel groups span two row tiles
+      if ((i & 1) || fq != 0) continue;
+    } else if (fq % (Cg / 4) != 0) {
+      continue;
+    }
+    if (co >= OC) continue;
+    const int g = co / Cg;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const long p = pix0 + h * 64;
+      if (p >= Mpix) continue;
+      float a = s[i][h], b = q[i][h];
+      if (Cg >= 32 && i + 1 < TM) {
+        a += s[i + 1][h];
+        b += q[i + 1][h];
+      }
+      const long n = p / HW;
+      const int t = (int)(p - n * HW) / 64;
+      float* d = gnp + ((n * G + g) * nparts + t) * 2;
+      d[0] = a;
+      d[1] = b;
+    }
+  }
+}

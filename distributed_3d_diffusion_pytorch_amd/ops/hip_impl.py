@@ -462,8 +462,15 @@ class _CatGNDense(torch.autograd.Function):
         wb = bf16_weight(dw)                                    # [OC, C1 + C2]
         OC = wb.shape[0]
         a2, b2 = a.reshape(-1, C1), b.reshape(-1, C2)
-        skip = torch.addmm(bf16_weight(db), a2, wb[:, :C1].t()) if db is not None else torch.mm(a2, wb[:, :C1].t())
-        skip.addmm_(b2, wb[:, C1:].t())
+        C = C1 + C2
+        if _LIN_PP and _pp_ok(OC, a2.shape[0], C1, C, C1) and _pp_ok(OC, b2.shape[0], C2, C, C2):
+            skip = torch.empty(a2.shape[0], OC, dtype=BF16, device=a.device)
+            gemm_nt(wb, a2, skip, OC, a2.shape[0], C1, C, C1, OC, bias=db.detach() if db is not None else None)
+            gemm_nt(wb[:, C1:], b2, skip, OC, b2.shape[0], C2, C, C2, OC, res=skip)
+        else:
+            skip = torch.addmm(bf16_weight(db), a2, wb[:, :C1].t()) if db is not None else \
+                torch.mm(a2, wb[:, :C1].t())
+            skip.addmm_(b2, wb[:, C1:].t())
         ctx.save_for_backward(a, b, gw, gb, stats, dw)
         ctx.cfg = (groups, db is not None)
         ctx.params = (dw, db)
@@ -483,9 +490,17 @@ class _CatGNDense(torch.autograd.Function):
         g = dskip.contiguous()
         OC = g.shape[-1]
         g2 = g.reshape(-1, OC)
-        wb = bf16_weight(dw)
-        da.view(-1, C1).addmm_(g2, wb[:, :C1])
-        db_in.view(-1, C2).addmm_(g2, wb[:, C1:])
+        OCp = _up(OC, 64)
+        rows_ = g2.shape[0]
+        if _LIN_PP and g2.is_contiguous() and _pp_ok(C1, rows_, OC, OCp, OC) and _pp_ok(C2, rows_, OC, OCp, OC):
+            pk = packed_weight(dw, True, 1)                      # [ICp][OCp]: rows = input channels
+            d2a, d2b = da.view(-1, C1), db_in.view(-1, C2)
+            gemm_nt(pk, g2, d2a, C1, rows_, OC, OCp, OC, C1, res=d2a)
+            gemm_nt(pk[C1 * OCp:], g2, d2b, C2, rows_, OC, OCp, OC, C2, res=d2b)
+        else:
+            wb = bf16_weight(dw)
+            da.view(-1, C1).addmm_(g2, wb[:, :C1])
+            db_in.view(-1, C2).addmm_(g2, wb[:, C1:])
         rows = g2.shape[0]
         C = C1 + C2
         dwp, dbp = ctx.params
@@ -906,6 +921,42 @@ _LIN_HIP_FWD_FLOP = float(os.environ.get("D3D_LIN_HIP_FWD_FLOP", "0"))
 _LIN_HIP_DGRAD_FLOP = float(os.environ.get("D3D_LIN_HIP_DGRAD_FLOP", "0"))
 
 
+# Hand-written ping-pong MFMA GEMM (ops/csrc/gemm.hip) for the dense layers:
+# "1" (default) routes the attention projections / NIN skips through it (fused
+# bias / residual / scale epilogue); the level-batched FiLM projections stay on
+# hipBLASLt unless D3D_FILM_PP=1 (kbench: 78-89 % of hipBLASLt on those,
+# profiles/kbench_gemm_pp_r2.txt).
+_LIN_PP = os.environ.get("D3D_LIN_PP", "0") != "0"
+_FILM_PP = os.environ.get("D3D_FILM_PP", "0") != "0"
+
+
+_PP_MIN_TILES = int(os.environ.get("D3D_LIN_PP_MIN_TILES", "128"))
+
+
+def _pp_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
+    # 256 x 256 output tiles: a GEMM of fewer tiles than ~half the CUs leaves
+    # the chip idle (the small per-GPU-batch layers stay on hipBLASLt's
+    # smaller tiles)
+    tiles = -(-M // 256) * -(-N // 256)
+    return tiles >= _PP_MIN_TILES and bool(_lib.d3d_gemm_nt_ok(M, N, K, lda, ldb))
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, M: int, N: int, K: int, lda: int, ldb: int, ldo: int,
+            bias: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None, ldr: int = 0,
+            alpha: float = 1.0, scale: float = 1.0, gnp: Optional[torch.Tensor] = None, gn_groups: int = 0,
+            gn_hw: int = 0) -> torch.Tensor:
+    """out[n][m] = (alpha * sum_k a[m][k] b[n][k] + bias[m] + res[n][m]) * scale
+    on the ping-pong MFMA kernel (bf16 operands / output, fp32 bias); ``gnp``:
+    the output's GroupNorm partial statistics (groups ``gn_groups`` over images
+    of ``gn_hw`` rows) from the same epilogue."""
+    if bias is not None:
+        assert bias.dtype == F32 and bias.is_contiguous()
+    _chk(_lib.d3d_gemm_nt_gn(a.data_ptr(), b.data_ptr(), out.data_ptr(), _ptr(bias), _ptr(res), M, N, K, lda, ldb,
+                             ldo, ldr or ldo, float(alpha), float(scale), _ptr(gnp), int(gn_groups), int(gn_hw),
+                             _st()), "gemm_nt")
+    return out
+
+
 def _lin_hip_fwd(P: int, IC: int, OC: int) -> bool:
     return _LIN_HIP_FWD_FLOP > 0 and IC % 8 == 0 and OC % 8 == 0 and OC >= 64 and 2.0 * P * IC * OC <= _LIN_HIP_FWD_FLOP
 
@@ -927,7 +978,20 @@ class _Linear(torch.autograd.Function):
         x2 = x.reshape(-1, shp[-1])
         P, IC = x2.shape
         OC = weight.shape[0]
-        if _lin_hip_fwd(P, IC, OC):
+        L = shp[1] if len(shp) == 3 else 0
+        gnp = None
+        if gn is not None and L % 64 == 0 and L and OC % 4 == 0 and OC % gn["groups"] == 0 and \
+                OC // gn["groups"] in (4, 8, 16, 32):
+            gnp = torch.empty((P // L) * gn["groups"] * (L // 64) * 2, dtype=F32, device=x.device)
+        if _LIN_PP and (gn is None or gnp is not None) and x2.is_contiguous() and _pp_ok(OC, P, IC, IC, IC):
+            wb = bf16_weight(weight)
+            y = torch.empty(P, OC, dtype=BF16, device=x.device)
+            r = residual.reshape(P, OC).contiguous() if residual is not None else None
+            gemm_nt(wb, x2, y, OC, P, IC, IC, IC, OC, bias=bias.detach() if bias is not None else None, res=r,
+                    scale=float(out_scale), gnp=gnp, gn_groups=gn["groups"] if gnp is not None else 0, gn_hw=L)
+            if gnp is not None:
+                gn["part"] = (gnp, L // 64)
+        elif _lin_hip_fwd(P, IC, OC):
             x2 = x2.contiguous()
             y = torch.empty(P, OC, dtype=BF16, device=x.device)
             r = residual.reshape(P, OC).contiguous() if residual is not None else None
@@ -992,7 +1056,11 @@ class _Linear(torch.autograd.Function):
         elif lazy:
             ks = scale
         if ctx.needs_input_grad[0]:
-            if _lin_hip_dgrad(rows, IC, OC):
+            pk = packed_weight(weight, True, 1) if (_LIN_PP and g.is_contiguous()) else None
+            if pk is not None and _pp_ok(IC, rows, OC, _up(OC, 64), OC):
+                dx = torch.empty(rows, IC, dtype=g.dtype, device=g.device)
+                gemm_nt(pk, g, dx, IC, rows, OC, _up(OC, 64), OC, IC, alpha=float(ks))
+            elif _lin_hip_dgrad(rows, IC, OC):
                 gc = g.contiguous()
                 dx = torch.empty(rows, IC, dtype=g.dtype, device=g.device)
                 _conv_fwd(gc, packed_weight(weight, True, 1), None, None, None, dx, rows, 1, 1, OC, _up(OC, 64), 1, 1,

@@ -242,14 +242,46 @@ def test_conv3x3_wgrad_w8(H, N, Hh, W, Ci, Co, s, res, rb, scale):
         H.set_wgrad_impl(os.environ.get("D3D_WGRAD_IMPL", "w8"))
 
 
-@pytest.mark.parametrize("hip_gemm", [False, True])
+@pytest.mark.parametrize("M,N,K,lda,ldb,ldo,bias,res,alpha,scale", [
+    (256, 256, 64, 64, 64, 256, False, False, 1.0, 1.0),
+    (768, 8192, 256, 256, 256, 768, True, False, 1.0, 1.0),
+    (200, 1000, 192, 200, 256, 208, True, True, 0.5, 0.7),        # M / N tails, padded rows
+    (1024, 4096, 4608, 4608, 4608, 1024, False, False, 1.0, 1.0),  # long reduction
+    (128, 70000, 256, 256, 256, 128, True, True, 1.0, 0.25),       # M < tile, many tiles per block
+    (4608, 2048, 1024, 1024, 1024, 4608, True, False, 1.0, 1.0),
+])
+def test_gemm_nt(H, M, N, K, lda, ldb, ldo, bias, res, alpha, scale):
+    """Ping-pong MFMA GEMM against the fp32 product (bias / residual / alpha /
+    scale epilogue, tails in M and N, row strides wider than K)."""
+    torch.manual_seed(11)
+    a = torch.randn(M, lda, device=DEV).to(BF)
+    b = torch.randn(N, ldb, device=DEV).to(BF)
+    bb = torch.randn(M, device=DEV) if bias else None
+    r = torch.randn(N, ldo, device=DEV).to(BF) if res else None
+    out = torch.full((N, ldo), 7.0, device=DEV).to(BF)
+    H.gemm_nt(a, b, out, M, N, K, lda, ldb, ldo, bias=bb, res=r, alpha=alpha, scale=scale)
+    ref = a[:, :K].float() @ b[:, :K].float().t() * alpha
+    ref = ref.t()
+    if bias:
+        ref = ref + bb
+    if res:
+        ref = ref + r[:, :M].float()
+    ref = ref * scale
+    assert rel(out[:, :M], ref) < 1e-2
+    if ldo > M:
+        assert (out[:, M:] == 7.0).all()          # columns past M untouched
+
+
+@pytest.mark.parametrize("impl", ["pp", "mfma", "blas"])
 @pytest.mark.parametrize("P,IC,OC", [(128, 256, 768), (8192, 256, 768), (2048, 512, 512), (2048, 512, 1536),
                                      (4096, 384, 128), (32768, 1024, 512)])
-def test_linear(H, P, IC, OC, hip_gemm, monkeypatch):
-    """Both dispatch regimes: the MFMA kernel with the fused residual / scale
-    epilogue and hipBLASLt + the epilogue kernel."""
-    monkeypatch.setattr(H, "_LIN_HIP_FWD_FLOP", 1e12 if hip_gemm else 0.0)
-    monkeypatch.setattr(H, "_LIN_HIP_DGRAD_FLOP", 1e12 if hip_gemm else 0.0)
+def test_linear(H, P, IC, OC, impl, monkeypatch):
+    """Every dispatch regime: the ping-pong GEMM with the fused bias /
+    residual / scale epilogue, the conv MFMA kernel (taps = 1) and hipBLASLt +
+    the epilogue kernel."""
+    monkeypatch.setattr(H, "_LIN_PP", impl == "pp")
+    monkeypatch.setattr(H, "_LIN_HIP_FWD_FLOP", 1e12 if impl == "mfma" else 0.0)
+    monkeypatch.setattr(H, "_LIN_HIP_DGRAD_FLOP", 1e12 if impl == "mfma" else 0.0)
     torch.manual_seed(4)
     x = torch.randn(2, P // 2, IC, device=DEV).to(BF)
     w = torch.randn(OC, IC, device=DEV) / math.sqrt(IC)

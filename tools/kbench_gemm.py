@@ -1,0 +1,106 @@
+"""Ping-pong MFMA GEMM (ops/csrc/gemm.hip) vs hipBLASLt (torch.mm) on the
+X-UNet's dense-layer shapes and a square reference GEMM: correctness against
+an fp32 product, then interleaved timing rounds in one process.
+
+    python tools/kbench_gemm.py [--rounds 3] [--iters 20] [--only fwd|dgrad]
+"""
+import argparse
+import json
+
+import torch
+
+from distributed_3d_diffusion_pytorch_amd.ops import hip_impl as H
+
+BF = torch.bfloat16
+
+# (label, M = output channels, N = pixels, K = reduction)
+SHAPES = [
+    ("sq8192", 8192, 8192, 8192),
+    ("film fwd P524288 1024->2048", 2048, 524288, 1024),
+    ("film fwd P131072 1024->4608", 4608, 131072, 1024),
+    ("film fwd P65536 1024->2048", 2048, 65536, 1024),
+    ("film fwd P16384 1024->4608", 4608, 16384, 1024),
+    ("k1024 M1024 P131072", 1024, 131072, 1024),
+    ("film dgrad P524288 2048->1024", 1024, 524288, 2048),
+    ("film dgrad P131072 4608->1024", 1024, 131072, 4608),
+    ("film dgrad P16384 4608->1024", 1024, 16384, 4608),
+    ("qkv fwd P131072 256->768", 768, 131072, 256),
+    ("qkv fwd P32768 512->1536", 1536, 32768, 512),
+    ("nin fwd P524288 256->128", 128, 524288, 256),
+    ("nin fwd P131072 512->256", 256, 131072, 512),
+    ("out fwd P32768 512->512", 512, 32768, 512),
+]
+
+
+def timeit(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--vers", default="2", help="comma list of kernel versions timed interleaved")
+    args = ap.parse_args()
+    H._ensure_impl()
+    lib = H._lib
+    torch.manual_seed(0)
+    for label, M, N, K in SHAPES:
+        if args.only and args.only not in label:
+            continue
+        w = (torch.rand(M, K, device="cuda") * 2 - 1).to(BF)
+        x = (torch.rand(N, K, device="cuda") * 2 - 1).to(BF)
+        bias = torch.randn(M, device="cuda")
+        y = torch.empty(N, M, dtype=BF, device="cuda")
+        st = H._st()
+
+        def ours(v=None):
+            if v is not None:
+                lib.d3d_gemm_tune(v, 0, 0)
+            rc = lib.d3d_gemm_nt(w.data_ptr(), x.data_ptr(), y.data_ptr(), bias.data_ptr(), None, M, N, K, K, K, M,
+                                 M, 1.0, 1.0, st)
+            assert rc == 0, rc
+
+        def blas():
+            return torch.addmm(bias.to(BF), x, w.t())
+
+        vers = [int(v) for v in args.vers.split(",")]
+        rows = torch.randint(0, N, (256,), device="cuda")
+        ref = x[rows].float() @ w.float().t() + bias
+        errs = {}
+        for v in vers:
+            y.zero_()
+            ours(v)
+            torch.cuda.synchronize()
+            errs[v] = ((y[rows].float() - ref).norm() / ref.norm()).item()
+        for _ in range(3):
+            ours()
+            blas()
+        torch.cuda.synchronize()
+        t_o, t_b = {v: [] for v in vers}, []
+        for _ in range(args.rounds):
+            for v in vers:
+                lib.d3d_gemm_tune(v, 0, 0)
+                t_o[v].append(timeit(ours, args.iters))
+            t_b.append(timeit(blas, args.iters))
+        fl = 2.0 * M * N * K
+        b = min(t_b)
+        rec = {"shape": label, "M": M, "N": N, "K": K, "blas_us": round(b, 1), "blas_tflops": round(fl / b / 1e6, 1)}
+        for v in vers:
+            o = min(t_o[v])
+            rec[f"v{v}_err"] = round(errs[v], 5)
+            rec[f"v{v}_us"] = round(o, 1)
+            rec[f"v{v}_tflops"] = round(fl / o / 1e6, 1)
+        print(json.dumps(rec), flush=True)
+        del w, x, y
+
+
+if __name__ == "__main__":
+    main()
