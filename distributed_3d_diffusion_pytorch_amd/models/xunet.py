@@ -231,13 +231,11 @@ class ConditioningProcessor(nn.Module):
         self.convs = nn.ModuleList([
             nn.Conv2d(D, emb_ch, kernel_size=3, stride=2 ** i, padding=1) for i in range(num_resolutions)])
 
-    def logsnr_embedding(self, logsnr: torch.Tensor) -> torch.Tensor:
-        """[B, 2] logSNR -> [2B, emb_ch] fp32 (clip +-20, DDPM posenc x1000, MLP)."""
-        l = torch.clamp(logsnr.float(), -20.0, 20.0)
-        e = ops.posenc_ddpm(l, self.emb_ch, max_time=1.0)
+    def logsnr_embedding(self, logsnr: torch.Tensor, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+        """[B, 2] logSNR -> [2B, emb_ch] fp32 (clip +-20, DDPM posenc x1000, MLP;
+        one fused HIP op in bf16 GPU runs)."""
         l0, act, l1 = self.logsnr_emb_emb
-        e = l1(torch.nn.functional.silu(l0(e)))
-        return e.reshape(-1, self.emb_ch)
+        return ops.logsnr_mlp(logsnr, l0.weight, l0.bias, l1.weight, l1.bias, max_time=1.0, dtype=dtype)
 
     def learned_embedding_image(self, dtype: torch.dtype) -> Optional[torch.Tensor]:
         """The learned part of the 144-ch conditioning input, identical for
@@ -255,7 +253,7 @@ class ConditioningProcessor(nn.Module):
                 dtype: torch.dtype) -> List[torch.Tensor]:
         B = batch["logsnr"].shape[0]
         assert cond_mask.shape == (B,), (cond_mask.shape, B)
-        logsnr_emb = self.logsnr_embedding(batch["logsnr"])
+        logsnr_emb = self.logsnr_embedding(batch["logsnr"], dtype)
         # Data-dependent part: NeRF-encoded camera rays (masked), no gradient.
         # A pinhole ray's origin is the camera centre, identical for every
         # pixel, so the 93 origin channels form a constant image per frame:

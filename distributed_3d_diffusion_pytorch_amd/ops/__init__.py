@@ -137,6 +137,15 @@ def upsample2(x):
     return _t.upsample2(x)
 
 
+def logsnr_mlp(logsnr, w1, b1, w2, b2, max_time: float = 1.0, dtype=None):
+    """posenc_ddpm(clamp(logsnr)) -> Linear -> SiLU -> Linear, [B, 2] -> [2B, E]
+    fp32.  HIP (``csrc/mlp.hip``) for bf16 GPU runs (``dtype``: the model's
+    activation dtype)."""
+    if dtype == torch.bfloat16 and logsnr.is_cuda and use_hip(logsnr, any_dtype=True):
+        return _h().logsnr_mlp(logsnr, w1, b1, w2, b2, max_time)
+    return _t.logsnr_mlp(logsnr, w1, b1, w2, b2, max_time)
+
+
 def silu(x):
     if use_hip(x):
         return _h().silu(x)
@@ -158,7 +167,7 @@ posenc_nerf = _t.posenc_nerf
 
 __all__ = ["diffusion_inputs", "diff_loss_nhwc", "group_norm", "gn_film", "conv3x3", "linear", "film_batch", "cat_gn_silu_dense", "cond_conv", "ray_posenc_dir",
            "ray_origin_pe", "attention", "avgpool2", "upsample2",
-           "silu", "ray_posenc", "posenc_ddpm", "camera_rays", "posenc_nerf", "set_backend",
+           "silu", "logsnr_mlp", "ray_posenc", "posenc_ddpm", "camera_rays", "posenc_nerf", "set_backend",
            "use_hip", "load_library", "library_error", "lib_path"]
 
 

@@ -69,6 +69,11 @@ SIGNATURES = {
     # attention.hip
     "d3d_attn_fwd": [P, P, P, I, I, I, I, I, F, P],
     "d3d_adam_fused": [P, P, P, P, P, P, P, P, I, P, P, I, P],
+    # mlp.hip
+    "d3d_mlp_ws": [I, I, I],
+    "d3d_mlp_pe": [P, I, I, F, P, P],
+    "d3d_mlp_mm": [P, P, I, I, I, I, I, I, P, P, P, P, P],
+    "d3d_mlp_wgrad": [P, P, I, I, I, I, P, P, I, P],
     "d3d_gemm_nt_ok": [I, I, I, I, I],
     "d3d_gemm_tune": [I, I, I],
     "d3d_gemm_nt": [P, P, P, P, P, I, I, I, I, I, I, I, F, F, P],
@@ -83,4 +88,7 @@ def declare(lib: C.CDLL) -> None:
         if fn is None:          # an older build (A/B runs via D3D_LIB_PATH): calls fail when made
             continue
         fn.argtypes = args
-        fn.restype = C.c_int
+        fn.restype = C.c_long if name in RET_LONG else C.c_int
+
+
+RET_LONG = {"d3d_mlp_ws"}

@@ -1303,6 +1303,76 @@ def attention(qkv, heads, cross):
     return _Attention.apply(qkv, heads, cross)
 
 
+# --------------------------------------------------- logSNR embedding ----
+class _LogSNRMLP(torch.autograd.Function):
+    """posenc_ddpm + Linear-SiLU-Linear of the logSNR embedding
+    (`xunet.py:273-277,305-308`) on ``csrc/mlp.hip``: posenc, two
+    split-K fp32 GEMMs with bias / SiLU-on-load epilogues; backward is one
+    input-gradient GEMM with the dSiLU epilogue and two weight-gradient
+    launches that deposit straight into the gradient sink."""
+
+    @staticmethod
+    def forward(ctx, logsnr, w1, b1, w2, b2, tscale):
+        l = logsnr.reshape(-1).float().contiguous()
+        R, E = l.numel(), w1.shape[0]
+        dev = l.device
+        pe = torch.empty(R, E, dtype=F32, device=dev)
+        a1 = torch.empty(R, E, dtype=F32, device=dev)
+        out = torch.empty(R, E, dtype=F32, device=dev)
+        ws = torch.empty(max(int(_lib.d3d_mlp_ws(R, E, E)), 1), dtype=F32, device=dev)
+        _chk(_lib.d3d_mlp_pe(l.data_ptr(), R, E, float(tscale), pe.data_ptr(), _st()), "mlp_pe")
+        _chk(_lib.d3d_mlp_mm(pe.data_ptr(), w1.detach().contiguous().data_ptr(), R, E, E, 0, 0, 0, _ptr(b1), None,
+                             ws.data_ptr(), a1.data_ptr(), _st()), "mlp_mm1")
+        _chk(_lib.d3d_mlp_mm(a1.data_ptr(), w2.detach().contiguous().data_ptr(), R, E, E, 1, 0, 0, _ptr(b2), None,
+                             ws.data_ptr(), out.data_ptr(), _st()), "mlp_mm2")
+        ctx.save_for_backward(pe, a1, w2)
+        ctx.params = (w1, b1, w2, b2)
+        for i, p in enumerate(ctx.params):
+            SINK.use(p, ctx.needs_input_grad[1 + i])
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        pe, a1, w2 = ctx.saved_tensors
+        w1p, b1p, w2p, b2p = ctx.params
+        g = dout.float().contiguous()
+        R, E = g.shape
+        dev = g.device
+        ws = torch.empty(max(int(_lib.d3d_mlp_ws(R, E, E)), 1), dtype=F32, device=dev)
+        da1 = torch.empty(R, E, dtype=F32, device=dev)
+        # da1 = (dout @ W2) * dsilu(a1)
+        _chk(_lib.d3d_mlp_mm(g.data_ptr(), w2.detach().contiguous().data_ptr(), R, E, E, 0, 1, 1, None, a1.data_ptr(),
+                             ws.data_ptr(), da1.data_ptr(), _st()), "mlp_dgrad")
+        targets = [SINK.target(p) for p in ctx.params]
+        if all(t is not None for t in targets):
+            tw1, tb1, tw2, tb2 = targets
+
+            def job(g=g, a1=a1, da1=da1, pe=pe):
+                _chk(_lib.d3d_mlp_wgrad(g.data_ptr(), a1.data_ptr(), R, E, E, 1, tw2.data_ptr(), tb2.data_ptr(), 1,
+                                        _st()), "mlp_wgrad2")
+                _chk(_lib.d3d_mlp_wgrad(da1.data_ptr(), pe.data_ptr(), R, E, E, 0, tw1.data_ptr(), tb1.data_ptr(), 1,
+                                        _st()), "mlp_wgrad1")
+            SINK.submit(dev, job, (g, a1, da1, pe), ctx.params)
+            return None, None, None, None, None, None
+        dw1 = torch.empty(E, E, dtype=F32, device=dev)
+        dw2 = torch.empty(E, E, dtype=F32, device=dev)
+        db1 = torch.empty(E, dtype=F32, device=dev)
+        db2 = torch.empty(E, dtype=F32, device=dev)
+        _chk(_lib.d3d_mlp_wgrad(g.data_ptr(), a1.data_ptr(), R, E, E, 1, dw2.data_ptr(), db2.data_ptr(), 0, _st()),
+             "mlp_wgrad2")
+        _chk(_lib.d3d_mlp_wgrad(da1.data_ptr(), pe.data_ptr(), R, E, E, 0, dw1.data_ptr(), db1.data_ptr(), 0, _st()),
+             "mlp_wgrad1")
+        return None, dw1, db1, dw2, db2, None
+
+
+def logsnr_mlp(logsnr, w1, b1, w2, b2, max_time=1.0):
+    E = w1.shape[0]
+    if tuple(w1.shape) != (E, E) or tuple(w2.shape) != (E, E) or E % 64 or b1 is None or b2 is None:
+        _fallback("logsnr_mlp", f"E={E}")
+        return _t.logsnr_mlp(logsnr, w1, b1, w2, b2, max_time)
+    return _LogSNRMLP.apply(logsnr, w1, b1, w2, b2, 1000.0 / max_time)
+
+
 # -------------------------------------------------------- elementwise ----
 class _SiLU(torch.autograd.Function):
     @staticmethod

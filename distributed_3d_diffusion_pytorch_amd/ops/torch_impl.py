@@ -181,6 +181,15 @@ def posenc_ddpm(t: torch.Tensor, emb_ch: int, max_time: float = 1.0) -> torch.Te
     return torch.cat([torch.sin(arg), torch.cos(arg)], dim=-1)
 
 
+def logsnr_mlp(logsnr: torch.Tensor, w1, b1, w2, b2, max_time: float = 1.0) -> torch.Tensor:
+    """[B, 2] logSNR -> [2B, E] fp32: clip +-20, DDPM posenc, Linear-SiLU-Linear
+    (`xunet.py:273-277,305-308`)."""
+    E = w1.shape[0]
+    l = torch.clamp(logsnr.float(), -20.0, 20.0)
+    e = posenc_ddpm(l, E, max_time=max_time).reshape(-1, E)
+    return torch.nn.functional.linear(torch.nn.functional.silu(torch.nn.functional.linear(e, w1, b1)), w2, b2)
+
+
 def ray_posenc(R: torch.Tensor, t: torch.Tensor, K: torch.Tensor, H: int, W: int,
                cond_mask: torch.Tensor, pos_emb: Optional[torch.Tensor],
                first_emb: Optional[torch.Tensor], other_emb: Optional[torch.Tensor],

@@ -1066,3 +1066,30 @@ def test_fused_update_matches_separate(graph, monkeypatch):
     for u, w in zip(a, b):
         d = (u - w).abs().max().item()
         assert d <= 1e-6 * max(1.0, u.abs().max().item()), d
+
+
+@pytest.mark.parametrize("R", [32, 128, 200])
+def test_logsnr_mlp(H, R):
+    """K10: fused posenc + Linear-SiLU-Linear (csrc/mlp.hip) vs the fp32 torch
+    composition, forward and all four parameter gradients (sink off)."""
+    torch.manual_seed(0)
+    E = 1024
+    logsnr = (torch.rand(R // 2, 2, device=DEV) * 50 - 25)      # includes clipped values
+    w1 = torch.randn(E, E, device=DEV) / 32
+    b1 = torch.randn(E, device=DEV) * 0.1
+    w2 = torch.randn(E, E, device=DEV) / 32
+    b2 = torch.randn(E, device=DEV) * 0.1
+    go = torch.randn(R, E, device=DEV)
+    ph = [leaf(t) for t in (w1, b1, w2, b2)]
+    pr = [leaf(t) for t in (w1, b1, w2, b2)]
+    yh = H.logsnr_mlp(logsnr, *ph)
+    yr = T.logsnr_mlp(logsnr, *pr)
+    assert H.FALLBACKS.get(f"logsnr_mlp: E={E}") is None
+    yh.backward(go)
+    yr.backward(go)
+    assert yh.shape == yr.shape == (R, E)
+    # fp32 throughout; the posenc arguments reach 2e4 rad, where one ulp of the
+    # device vs host exp() of a frequency moves sin/cos by ~1e-3
+    assert rel(yh, yr) < 1e-2
+    for a, b in zip(ph, pr):
+        assert rel(a.grad, b.grad) < 1e-2
