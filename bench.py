@@ -121,7 +121,10 @@ def main() -> None:
     local = global_batch // N
     mb = args.micro_batch
     if mb < 0:
-        mb = 0 if local <= 64 else 64
+        # one micro-batch whenever the rank's batch fits comfortably in HBM: at
+        # 64x64 the whole 128-example batch is one pass (~+8 % over two passes
+        # of 64, profiles/ab_bs128_modes_r2.txt); larger images split into 64s
+        mb = 0 if local * args.imgsize * args.imgsize <= 128 * 64 * 64 else 64
     if args.graph == "auto":
         graph = ctx.device.type == "cuda" and (mb or local) <= 32
     else:
@@ -193,6 +196,7 @@ def main() -> None:
                        "tuned_gemms": bool(getattr(trainer, "tuned_gemms", False)),
                        "backend": "hip" if (ctx.device.type == "cuda" and use_hip(probe)) else "torch"},
             "final_loss": lv,
+            "hbm_peak_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if ctx.device.type == "cuda" else None,
         }
         print(json.dumps(out), flush=True)
     cleanup()
