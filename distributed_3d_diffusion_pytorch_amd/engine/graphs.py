@@ -261,7 +261,7 @@ class GraphedTrainStep:
         world = tr.ctx.world
         o = tr.optim
         clip = tr.cfg.optim.grad_clip
-        self.hp.copy_(o.hparams(1.0 / world), non_blocking=True)
+        o.hparams_to(self.hp, 1.0 / world)        # kernel-argument write: no host wait
         post = world > 1 and self.comm_mode != "graph"
         if post and (clip > 0 or want_norm or tr.cfg.dist.grad_dtype == "bf16"):
             g = tr.flat.grad

@@ -49,7 +49,7 @@ class FusedAdam(torch.optim.Optimizer):
         """L2 norm of the (averaged) flat gradient, as a device scalar (no sync)."""
         return torch.linalg.vector_norm(self.flat.grad, dtype=torch.float32) * grad_scale
 
-    def hparams(self, grad_scale: float) -> torch.Tensor:
+    def hparams_list(self, grad_scale: float) -> list:
         """Advance the step counter and return the per-step hyper-parameter
         block of the device-side Adam kernel (adam.hip ``d3d_adam_dev``):
         [b1, b2, eps, wd, lr/bc1, sqrt(bc2), grad_scale, 1-ema_decay]."""
@@ -57,8 +57,18 @@ class FusedAdam(torch.optim.Optimizer):
         lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
         self.step_count += 1
         t = self.step_count
-        return torch.tensor([b1, b2, eps, wd, lr / (1.0 - b1 ** t), math.sqrt(1.0 - b2 ** t), grad_scale,
-                             1.0 - self.ema_decay], dtype=torch.float32)
+        return [b1, b2, eps, wd, lr / (1.0 - b1 ** t), math.sqrt(1.0 - b2 ** t), grad_scale, 1.0 - self.ema_decay]
+
+    def hparams(self, grad_scale: float) -> torch.Tensor:
+        """:meth:`hparams_list` as a host fp32 tensor."""
+        return torch.tensor(self.hparams_list(grad_scale), dtype=torch.float32)
+
+    def hparams_to(self, dst: torch.Tensor, grad_scale: float) -> torch.Tensor:
+        """Write the block into the device tensor ``dst`` without a host-to-
+        device copy (a kernel carries the values), so the host keeps running
+        ahead of the GPU across the optimizer step."""
+        from ..ops import hip_impl
+        return hip_impl.set_words(dst, self.hparams_list(grad_scale))
 
     @staticmethod
     def clip_coef(norm: torch.Tensor, max_norm: float) -> torch.Tensor:
@@ -83,7 +93,7 @@ class FusedAdam(torch.optim.Optimizer):
         if p.is_cuda and ops.use_hip(p, any_dtype=True):
             from ..ops import hip_impl
             if coef is not None or FUSED_UPDATE:
-                hp = self.hparams(grad_scale).to(p.device, non_blocking=True)
+                hp = self.hparams_to(torch.empty(8, dtype=torch.float32, device=p.device), grad_scale)
                 if coef is not None:
                     hp[6:7].mul_(coef)
                 if FUSED_UPDATE:        # Adam + bf16 operand repack in one pass over the tiles

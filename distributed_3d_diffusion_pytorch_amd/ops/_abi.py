@@ -30,6 +30,7 @@ SIGNATURES = {
     "d3d_avgpool2": [P, P, I, I, I, I, I, P],
     "d3d_upsample2": [P, P, I, I, I, I, I, P],
     "d3d_add_scale": [P, P, P, F, L, P],
+    "d3d_set_words": [P, I, F, F, F, F, F, F, F, F, P],
     "d3d_add_scale_gn": [P, P, P, F, L, I, I, I, P, P],
     "d3d_sampler_step": [P, P, P, P, P, I, I, F, F, F, F, F, I, U64, P],
     "d3d_sampler_inputs": [P, P, I, I, P, P, U64, L, P, P, P],

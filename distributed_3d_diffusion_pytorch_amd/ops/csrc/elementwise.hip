@@ -478,3 +478,24 @@ D3D_API int d3d_diff_loss_bwd(const void* y, const float* eps, const float* dlos
                      mode, 1.f / (3.f * B * HW), (bf16*)dy);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------- device words ----
+// Per-step scalars (the Adam hyper-parameter block, ...) written by a kernel
+// whose arguments carry the values: no host-to-device copy, so the host never
+// waits for the stream to drain (a pageable 32-byte H2D copy did, idling the
+// GPU for the host's latency once per step).
+struct Words8 {
+  float v[8];
+};
+
+__global__ void set_words_k(float* __restrict__ dst, int n, Words8 w) {
+  if ((int)threadIdx.x < n) dst[threadIdx.x] = w.v[threadIdx.x];
+}
+
+D3D_API int d3d_set_words(float* dst, int n, float a0, float a1, float a2, float a3, float a4, float a5, float a6,
+                          float a7, hipStream_t st) {
+  if (n < 0 || n > 8) return (int)hipErrorInvalidValue;
+  Words8 w{{a0, a1, a2, a3, a4, a5, a6, a7}};
+  hipLaunchKernelGGL(set_words_k, dim3(1), dim3(64), 0, st, dst, n, w);
+  return (int)hipGetLastError();
+}

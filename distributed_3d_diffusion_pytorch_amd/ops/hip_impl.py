@@ -1616,6 +1616,16 @@ def adam_update_all(flat, m, v, ema, hp) -> None:
         e[0] = (e[2][0]._version, _EPOCH[0])
 
 
+def set_words(dst: torch.Tensor, vals) -> torch.Tensor:
+    """dst[:len(vals)] = vals (fp32, <= 8) by a kernel whose arguments carry
+    the values: unlike a host-to-device copy from pageable memory this never
+    makes the host wait for the stream (graph-capture safe as well)."""
+    vals = [float(v) for v in vals]
+    assert dst.dtype == F32 and dst.is_cuda and dst.is_contiguous() and len(vals) <= min(8, dst.numel())
+    _chk(_lib.d3d_set_words(dst.data_ptr(), len(vals), *(vals + [0.0] * (8 - len(vals))), _st()), "set_words")
+    return dst
+
+
 def adam_flat_dev(p, g, m, v, ema, hp, refresh=True):
     """Adam with its per-step hyper-parameters read from the device block
     ``hp`` (graph-replay form; see d3d_adam_dev).  Works on any contiguous

@@ -1,0 +1,57 @@
+"""Host-side cost of replaying the captured bs16 training step (HIP graphs):
+how long graph.replay() occupies the calling thread vs how long the GPU needs.
+If the host time approaches the GPU time, the replayed step is host-bound."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.parallel import DistContext
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    ctx = DistContext(device=torch.device("cuda", 0))
+    cfg = make_config(None, {"model.H": 64, "model.W": 64, "data.imgsize": 64, "global_batch": B,
+                             "micro_batch": 0, "data.synthetic": True, "log_every": 0, "ckpt_every": 0,
+                             "graph": True})
+    tr = Trainer(cfg, ctx)
+    b = next(SyntheticBatches(B, 64, "cuda", seed=3))
+    for _ in range(4):
+        tr.train_step(*b)
+    torch.cuda.synchronize()
+    g = tr._graphed
+    for name, gr in (("A (fwd+bwd)", g.gA), ("B (update)", g.gB)):
+        hs, ts = [], []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            gr.replay()
+            t1 = time.perf_counter()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            hs.append(t1 - t0)
+            ts.append(t2 - t0)
+        print(f"graph {name}: host replay() {1e3 * min(hs):.3f} ms, replay+sync {1e3 * min(ts):.3f} ms", flush=True)
+    # the full step, back to back: host time per step vs wall per step
+    torch.cuda.synchronize()
+    n = 10
+    t0 = time.perf_counter()
+    hs = []
+    for _ in range(n):
+        a = time.perf_counter()
+        tr.train_step(*b)
+        hs.append(time.perf_counter() - a)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"train_step host time {1e3 * sum(hs) / n:.3f} ms/step (loop {1e3 * (t1 - t0) / n:.3f}), "
+          f"wall {1e3 * (t2 - t0) / n:.3f} ms/step", flush=True)
+
+
+if __name__ == "__main__":
+    main()

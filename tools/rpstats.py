@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--solo", type=float, default=0.0,
                     help="over the last SOLO ms: per kernel, the time it ran ALONE on the device (exposed, on the "
                          "critical path) vs overlapped with another kernel (hidden behind / sharing the chip)")
+    ap.add_argument("--gaps", type=float, default=0.0,
+                    help="over the last GAPS ms: device-idle gaps (no kernel running) summed by the (kernel before, "
+                         "kernel after) pair -- where the replayed step leaves the GPU idle")
     a = ap.parse_args()
     db = sqlite3.connect(a.db)
     cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
@@ -49,6 +52,27 @@ def main():
               f"kernel sum {tot * 1e-6:.2f} ms (overlap x{tot / max(busy, 1):.2f}), {len(iv)} kernels, "
               f"{len(gaps)} gaps, median gap {gaps[len(gaps) // 2] * 1e-3 if gaps else 0:.2f} us, "
               f"gap sum {sum(gaps) * 1e-6:.2f} ms")
+        return
+    if a.gaps:
+        rows = sorted((r[1], r[2], r[0].replace("(anonymous namespace)::", "").split("(")[0][:60])
+                      for r in db.execute(f"select {name_col}, start, end from kernels"))
+        end = max(r[1] for r in rows)
+        lo = end - a.gaps * 1e6
+        rows = [r for r in rows if r[1] > lo]
+        pair = defaultdict(lambda: [0.0, 0])
+        cur_e, cur_n = None, None
+        for s0, e, nm in rows:
+            if cur_e is not None and s0 > cur_e:
+                k = f"{cur_n}  ->  {nm}"
+                pair[k][0] += s0 - cur_e
+                pair[k][1] += 1
+            if cur_e is None or e > cur_e:
+                cur_e, cur_n = e, nm
+        div = a.steps or 1
+        tot = sum(v[0] for v in pair.values())
+        print(f"idle gaps {tot * 1e-6 / div:.3f} ms per {'step' if a.steps else 'window'}")
+        for k, (t, n) in sorted(pair.items(), key=lambda kv: -kv[1][0])[: a.top]:
+            print(f"{t * 1e-6 / div:8.3f} ms {n / div:7.1f} x {1e-3 * t / n:7.1f} us  {k}")
         return
     if a.solo:
         rows = [(r[0].replace("(anonymous namespace)::", "").split("(")[0][:100], r[1], r[2])
