@@ -22,6 +22,7 @@ re-designed:
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -32,6 +33,10 @@ from .. import ops
 from ..config import ModelConfig
 
 INV_SQRT2 = 1.0 / math.sqrt(2.0)
+
+
+_COND_STREAM = os.environ.get("D3D_COND_STREAM", "1") != "0"
+_COND_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
 
 
 class GroupNorm(nn.Module):
@@ -251,6 +256,11 @@ class ConditioningProcessor(nn.Module):
 
     def forward(self, batch: Dict[str, torch.Tensor], cond_mask: torch.Tensor,
                 dtype: torch.dtype) -> List[torch.Tensor]:
+        return list(self.levels(batch, cond_mask, dtype))
+
+    def levels(self, batch: Dict[str, torch.Tensor], cond_mask: torch.Tensor, dtype: torch.dtype):
+        """:meth:`forward` as a generator: yields the embedding of level 0, 1,
+        ... as soon as each is computed (the shared parts come first)."""
         B = batch["logsnr"].shape[0]
         assert cond_mask.shape == (B,), (cond_mask.shape, B)
         logsnr_emb = self.logsnr_embedding(batch["logsnr"], dtype)
@@ -269,14 +279,12 @@ class ConditioningProcessor(nn.Module):
         # first_emb / other_emb) is then a 2-image transposed conv instead of a
         # per-example one.
         emb_img = self.learned_embedding_image(dtype)
-        sembs = []
         for i, conv in enumerate(self.convs):
             s = 2 ** i
             e_emb = ops.conv3x3(emb_img, conv.weight, None, stride=s) if emb_img is not None else None
             e = ops.cond_conv(rays_dir, orig_pe, conv.weight, conv.bias, s, row_bias=logsnr_emb, residual=e_emb,
                               res_period=2 if e_emb is not None else 0)
-            sembs.append(ops.silu(e))
-        return sembs
+            yield ops.silu(e)
 
 
 class XUNet(nn.Module):
@@ -409,8 +417,31 @@ class XUNet(nn.Module):
         assert cond_mask is not None and cond_mask.shape[0] == B
         assert (H, W) == (self.H, self.W), ((H, W), (self.H, self.W))
         dt = self.compute_dtype or xdt
+        cs = self._cond_stream(batch.get("xz", batch.get("x")))
+        if cs is not None:
+            return self._trunk(batch, None, B, H, W, dt, head_nhwc, None,
+                               cond=(cs, batch, cond_mask))
         sembs = self.conditioningprocessor(batch, cond_mask, dt)
         return self._trunk(batch, sembs, B, H, W, dt, head_nhwc, None)
+
+    def _cond_stream(self, ref: Optional[torch.Tensor]):
+        """The conditioning side stream (HIP path, level-batched FiLM): the
+        camera-ray / logSNR conditioning and the FiLM projections of every
+        level depend only on the poses and logSNR, not on the trunk, so they
+        run on their own HIP stream -- level 0 first -- while the trunk's stem
+        and level-0 blocks run; the trunk waits on one event per level right
+        before that level's first block.  Autograd runs their backward on the
+        same stream.  D3D_COND_STREAM=0 keeps everything on one stream."""
+        if not (self.batch_film and _COND_STREAM and ref is not None and ref.is_cuda
+                and (self.compute_dtype or ref.dtype) == torch.bfloat16 and ops.use_hip(ref, any_dtype=True)):
+            return None
+        idx = ref.device.index if ref.device.index is not None else torch.cuda.current_device()
+        st = _COND_STREAMS.get(idx)
+        if st is None:
+            st = _COND_STREAMS[idx] = torch.cuda.Stream(device=idx)
+            from ..ops.gradsink import SINK
+            SINK.add_compute_stream(st)
+        return st
 
     def _forward_shared(self, batch, sc, head_nhwc):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
@@ -435,11 +466,34 @@ class XUNet(nn.Module):
         ss_map = (2 * ecls.to(torch.int32)[:, None] + fr).reshape(-1)
         return self._trunk(batch, sembs, B, H, W, dt, head_nhwc, ss_map)
 
-    def _trunk(self, batch, sembs, B, H, W, dt, head_nhwc, ss_map):
+    def _trunk(self, batch, sembs, B, H, W, dt, head_nhwc, ss_map, cond=None):
         for blocks in self._film_groups():
             for b in blocks:
                 b.__dict__["_ss_map"] = ss_map
-        if ss_map is not None or self.batch_film:
+        events = None
+        if cond is not None:
+            # conditioning + level-batched FiLM on the side stream, one event per level
+            cs, cbatch, cond_mask = cond
+            main = torch.cuda.current_stream()
+            cs.wait_stream(main)
+            for t in list(cbatch.values()) + [cond_mask]:
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(cs)
+            sembs, events = [], []
+            with torch.cuda.stream(cs):
+                for i, (semb, blocks) in enumerate(zip(self.conditioningprocessor.levels(cbatch, cond_mask, dt),
+                                                       self._film_groups())):
+                    outs = ops.film_batch(semb, [b.film.dense.weight for b in blocks],
+                                          [b.film.dense.bias for b in blocks])
+                    for o in outs:
+                        o.record_stream(main)       # read by the trunk's GN-FiLM kernels
+                    for b, o in zip(blocks, outs):
+                        b.__dict__["_ss"] = o
+                    ev = torch.cuda.Event()
+                    ev.record(cs)
+                    events.append(ev)
+                    sembs.append(semb)
+        elif ss_map is not None or self.batch_film:
             # every FiLM projection of a level reads the same embedding: run
             # them as one GEMM per level (ops.film_batch) and hand each
             # ResnetBlock its modulation slice
@@ -460,6 +514,8 @@ class XUNet(nn.Module):
         L = self.num_resolutions
         hs = [h]
         for i in range(L):
+            if events is not None:
+                torch.cuda.current_stream().wait_event(events[i])
             for j in range(self.num_res_blocks):
                 h = self.xunetblocks[i][j](h, sembs[i])
                 hs.append(h)

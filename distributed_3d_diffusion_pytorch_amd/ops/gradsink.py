@@ -60,6 +60,7 @@ class GradSink:
         self.graph_defer = os.environ.get("D3D_GRAPH_WGRAD_STREAM", "1") != "0"
         self.defer_batch = max(1, int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "8")))
         self._queue = []
+        self._compute = []
         self._streams: Dict[int, "torch.cuda.Stream"] = {}
         self._forked = set()
         self._cb_queued = False
@@ -140,6 +141,18 @@ class GradSink:
             except RuntimeError:        # not inside a backward pass: join now
                 self.join()
 
+    def add_compute_stream(self, st) -> None:
+        """Register another stream that runs forward / backward work (the
+        model's conditioning stream): collectives wait for it as well, and
+        the end-of-backward join rejoins it."""
+        if all(st is not s for s in self._compute):
+            self._compute.append(st)
+
+    def _wait_compute(self, st, idx) -> None:
+        for c in self._compute:
+            if c.device.index == idx and c != torch.cuda.current_stream(idx):
+                st.wait_stream(c)
+
     def _end_of_backward(self) -> None:
         self._cb_queued = False
         self.flush()
@@ -193,10 +206,14 @@ class GradSink:
                 self.done(p)
 
     def join(self) -> None:
-        """Make the current stream wait for every deposited gradient."""
+        """Make the current stream wait for every deposited gradient (and for
+        the registered compute streams)."""
         for idx in list(self._forked):
             torch.cuda.current_stream(idx).wait_stream(self._streams[idx])
         self._forked.clear()
+        if self._compute and torch.cuda.is_available() and torch.cuda.is_initialized():
+            idx = torch.cuda.current_device()
+            self._wait_compute(torch.cuda.current_stream(idx), idx)
 
     @contextlib.contextmanager
     def collective(self):
@@ -209,6 +226,7 @@ class GradSink:
         idx = torch.cuda.current_device()
         side = self._side(idx)
         side.wait_stream(torch.cuda.current_stream(idx))
+        self._wait_compute(side, idx)       # deposits made from the other compute stream(s)
         with torch.cuda.stream(side):
             yield
 

@@ -1166,6 +1166,9 @@ class _FiLMBatch(torch.autograd.Function):
                     break
         if ok:
             dy = buf.view(-1, S)
+            # written by the GN-FiLM backwards (trunk stream), read here -- on
+            # the conditioning stream when that is on (models/xunet.py)
+            buf.record_stream(torch.cuda.current_stream())
         else:
             dy = torch.zeros(x2.shape[0], S, dtype=BF16, device=x2.device)
             for g, o, wd in zip(gs, offs, ctx.widths):
