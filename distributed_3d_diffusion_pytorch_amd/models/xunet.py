@@ -37,6 +37,12 @@ INV_SQRT2 = 1.0 / math.sqrt(2.0)
 
 _COND_STREAM = os.environ.get("D3D_COND_STREAM", "1") != "0"
 _COND_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+# (level, event): parameters outside the early update part become valid at
+# `event` -- the trunk waits on it before encoder level `level` and the
+# conditioning stream before that level's FiLM projections (deferred,
+# overlapped optimizer step of the graph-replayed training step,
+# engine/graphs.py).  Set only around that step's forward.
+PARAM_FENCE: List = [None]
 
 
 class GroupNorm(nn.Module):
@@ -424,6 +430,34 @@ class XUNet(nn.Module):
         sembs = self.conditioningprocessor(batch, cond_mask, dt)
         return self._trunk(batch, sembs, B, H, W, dt, head_nhwc, None)
 
+    def update_parts(self):
+        """Split of the parameters for an optimizer step overlapped with the
+        next forward: ``(early, level)`` -- the parameters the forward reads
+        before encoder level ``level`` (conditioning processor, stem, encoder
+        levels below ``level`` and the FiLM projections of those levels,
+        decoder blocks included since the level-batched FiLM runs up front);
+        every other parameter can still be in flight until that level starts.
+        None when the model is too shallow for a useful split."""
+        L = self.num_resolutions
+        if L < 3:
+            return None
+        level = 2
+        early = []
+        early += list(self.conditioningprocessor.parameters())
+        early += list(self.conv.parameters())
+        for i in range(level):
+            early += list(self.xunetblocks[i].parameters())
+        groups = self._film_groups()
+        for i in range(level):
+            for b in groups[i]:
+                early += [b.film.dense.weight, b.film.dense.bias]
+        seen, out = set(), []
+        for p_ in early:
+            if id(p_) not in seen:
+                seen.add(id(p_))
+                out.append(p_)
+        return out, level
+
     def _cond_stream(self, ref: Optional[torch.Tensor]):
         """The conditioning side stream (HIP path, level-batched FiLM): the
         camera-ray / logSNR conditioning and the FiLM projections of every
@@ -480,9 +514,12 @@ class XUNet(nn.Module):
                 if isinstance(t, torch.Tensor) and t.is_cuda:
                     t.record_stream(cs)
             sembs, events = [], []
+            fence = PARAM_FENCE[0]
             with torch.cuda.stream(cs):
                 for i, (semb, blocks) in enumerate(zip(self.conditioningprocessor.levels(cbatch, cond_mask, dt),
                                                        self._film_groups())):
+                    if fence is not None and i == fence[0]:
+                        cs.wait_event(fence[1])
                     outs = ops.film_batch(semb, [b.film.dense.weight for b in blocks],
                                           [b.film.dense.bias for b in blocks])
                     for o in outs:
@@ -497,7 +534,10 @@ class XUNet(nn.Module):
             # every FiLM projection of a level reads the same embedding: run
             # them as one GEMM per level (ops.film_batch) and hand each
             # ResnetBlock its modulation slice
+            fence = PARAM_FENCE[0]
             for i, blocks in enumerate(self._film_groups()):
+                if fence is not None and i == fence[0]:
+                    torch.cuda.current_stream().wait_event(fence[1])
                 outs = ops.film_batch(sembs[i], [b.film.dense.weight for b in blocks],
                                       [b.film.dense.bias for b in blocks])
                 for b, o in zip(blocks, outs):
@@ -513,9 +553,12 @@ class XUNet(nn.Module):
 
         L = self.num_resolutions
         hs = [h]
+        fence = PARAM_FENCE[0]
         for i in range(L):
             if events is not None:
                 torch.cuda.current_stream().wait_event(events[i])
+            if fence is not None and i == fence[0]:
+                torch.cuda.current_stream().wait_event(fence[1])
             for j in range(self.num_res_blocks):
                 h = self.xunetblocks[i][j](h, sembs[i])
                 hs.append(h)

@@ -1522,9 +1522,13 @@ def adam_flat(p, g, m, v, ema, lr, b1, b2, eps, wd, step_size, bc2_sqrt, grad_sc
 _FUSED = {}
 
 
-def _fused_tables(flat):
+def _fused_tables(flat, only=None, key=None, take_unowned=True):
+    """``only``: restrict the update to these parameter indices (one part of
+    a split update, :func:`prepare_update_parts`); ``key``: its cache key;
+    ``take_unowned``: this part also repacks cached operands of tensors that
+    are not flat parameters."""
     import numpy as np
-    key = id(flat)
+    key = id(flat) if key is None else key
     ent = _FUSED.get(key)
     if ent is not None and ent["rev"] == _REV[0] and ent["flat"] is flat:
         return ent
@@ -1534,6 +1538,9 @@ def _fused_tables(flat):
     for ckey, (tok, t, (p, desc)) in _WCACHE.items():
         i = pidx.get(id(p))
         if i is None or desc is None or len(desc) > 6 or desc[5] not in (0, 1):
+            continue
+        if only is not None and i not in only:
+            absorbed.add(ckey)                 # another part's weight: neither tiled nor repacked here
             continue
         OC, IC, OCp, ICp, taps, mode = desc[:6]
         if p.shape[0] != OC or p.numel() != OC * IC * taps or taps > 9:
@@ -1554,14 +1561,28 @@ def _fused_tables(flat):
         trows.append((flat.offsets[i], t0[0].data_ptr() if t0 else 0, t1[0].data_ptr() if t1 else 0, OC, IC, taps,
                       t0[1][3] if t0 else 0, t1[1][2] if t1 else 0, tblk))
         tblk += ((OC + 31) // 32) * ((IC + 15) // 16)
-    # range table: the complement of the tile weights' spans
-    tiled = sorted((flat.offsets[i], flat.span(i)[1]) for i in per)
-    rrows, rblk, pos = [], 0, 0
-    for a, b in tiled + [(flat.numel, flat.numel)]:
-        if a > pos:
-            rrows.append((pos, a - pos, rblk, 0))
-            rblk += (a - pos + 4095) // 4096
-        pos = max(pos, b)
+    # range table: the complement of the tile weights' spans (of this part's
+    # parameters when split)
+    rrows, rblk = [], 0
+    if only is None:
+        tiled = sorted((flat.offsets[i], flat.span(i)[1]) for i in per)
+        pos = 0
+        for a, b in tiled + [(flat.numel, flat.numel)]:
+            if a > pos:
+                rrows.append((pos, a - pos, rblk, 0))
+                rblk += (a - pos + 4095) // 4096
+            pos = max(pos, b)
+    else:
+        spans = sorted(flat.span(i) for i in only if i not in per)
+        merged = []
+        for a, b in spans:
+            if merged and a <= merged[-1][1]:
+                merged[-1][1] = max(merged[-1][1], b)
+            else:
+                merged.append([a, b])
+        for a, b in merged:
+            rrows.append((a, b - a, rblk, 0))
+            rblk += (b - a + 4095) // 4096
     dev = flat.data.device
     tdt = np.dtype([("off", np.int64), ("dst0", np.uint64), ("dst1", np.uint64), ("OC", np.int32),
                     ("IC", np.int32), ("taps", np.int32), ("ICp0", np.int32), ("OCp1", np.int32), ("blk0", np.int32)])
@@ -1580,6 +1601,10 @@ def _fused_tables(flat):
     for ckey, (tok, t, (p, desc)) in _WCACHE.items():
         if desc is None or ckey in absorbed:
             continue
+        if only is not None:
+            owner = pidx.get(id(p))
+            if (owner is None and not take_unowned) or (owner is not None and owner not in only):
+                continue
         OC, IC, OCp, ICp, taps, mode = desc[:6]
         src_off = desc[6] if len(desc) > 6 else 0
         ics = desc[7] if len(desc) > 7 else 0
@@ -1595,6 +1620,32 @@ def _fused_tables(flat):
 def prepare_fused_update(flat) -> None:
     """Build the fused-update tables now (host work; call before a capture)."""
     _fused_tables(flat)
+
+
+def prepare_update_parts(flat, parts) -> None:
+    """Build the fused-update tables of a split update: ``parts`` is a list of
+    parameter-index sets covering ``flat.params`` (host work; before a
+    capture).  :func:`adam_update_part` then updates one part."""
+    for k, only in enumerate(parts):
+        _fused_tables(flat, set(only), key=(id(flat), "part", k), take_unowned=k == 0)
+
+
+def adam_update_part(flat, m, v, ema, hp, k) -> None:
+    """The fused Adam + operand repack of part ``k`` (:func:`prepare_update_parts`)."""
+    ent = _FUSED.get((id(flat), "part", k))
+    if ent is None or ent["rev"] != _REV[0] or ent["flat"] is not flat:
+        raise RuntimeError("update-part tables missing or stale (prepare_update_parts before the capture)")
+    _adam_fused_launch(flat, m, v, ema, hp, ent)
+
+
+def _adam_fused_launch(flat, m, v, ema, hp, ent) -> None:
+    (tt, tb, tblk), (rt, rb, rblk), (rd, rm, rest_blk) = ent["tiles"], ent["ranges"], ent["rest"]
+    if tblk or rblk:
+        _chk(_lib.d3d_adam_fused(flat.data.data_ptr(), flat.grad.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(ema),
+                                 hp.data_ptr(), _ptr(rt), _ptr(rb), int(rblk), _ptr(tt), _ptr(tb), int(tblk), _st()),
+             "adam_fused")
+    if rest_blk:
+        _chk(_lib.d3d_pack_all(rd.data_ptr(), rm.data_ptr(), rest_blk, _st()), "pack_all")
 
 
 def adam_update_all(flat, m, v, ema, hp) -> None:

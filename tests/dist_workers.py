@@ -151,6 +151,7 @@ def gpu_graph_vs_eager(out_dir):
         torch.manual_seed(0)
         tr = make(graph)
         losses = [float(tr.train_step(*b)) for b in batches]
+        tr.sync()
         p = tr.flat.data.clone()
         other = p.clone()
         torch.distributed.broadcast(other, 0)

@@ -497,10 +497,14 @@ def test_film_batch_with_gn_film(H, chans, N, Hh, blas):
         assert rel(a, b) < 3e-2, rel(a, b)
 
 
-def test_graph_train_step_matches_eager():
+@pytest.mark.parametrize("micro", [2, 0])
+def test_graph_train_step_matches_eager(micro):
     """HIP-graph replayed training step == eager step (dropout ON: the graph
     adds the same per-step device words the eager step uses as host seeds;
-    counter-based input draw): losses and parameters after 3 steps."""
+    counter-based input draw): losses and parameters after 3 steps.  With one
+    micro-batch (micro=0) the graph step defers each update into the next
+    replay, overlapped with its forward (engine/graphs.py): Trainer.sync()
+    applies the last one before the comparison."""
     from distributed_3d_diffusion_pytorch_amd.config import make_config
     from distributed_3d_diffusion_pytorch_amd.engine import Trainer
     from distributed_3d_diffusion_pytorch_amd.parallel import DistContext
@@ -509,7 +513,7 @@ def test_graph_train_step_matches_eager():
 
     def make(graph):
         cfg = make_config(None, {"model.H": 32, "model.W": 32, "model.dropout": 0.1, "data.imgsize": 32,
-                                 "global_batch": 4, "micro_batch": 2, "data.synthetic": True, "log_every": 0,
+                                 "global_batch": 4, "micro_batch": micro, "data.synthetic": True, "log_every": 0,
                                  "ckpt_every": 0, "graph": graph, "optim.warmup_examples": 8})
         return Trainer(cfg, ctx)
 
@@ -519,10 +523,15 @@ def test_graph_train_step_matches_eager():
     assert torch.equal(te.flat.data, tg.flat.data)
     le = [te.train_step(*b).item() for b in batches]
     lg = [tg.train_step(*b).item() for b in batches]
+    assert tg._graphed is not None and tg._graphed.defer == (micro == 0)
+    tg.sync()
     for a, b in zip(le, lg):
         assert abs(a - b) <= 2e-3 * abs(a) + 1e-4, (le, lg)
     d = (te.flat.data - tg.flat.data).abs().max().item()
     assert d < 5e-4, d
+    dm = (te.optim.exp_avg_sq - tg.optim.exp_avg_sq).abs().max().item()
+    assert dm <= 1e-3 * te.optim.exp_avg_sq.abs().max().item() + 1e-12, dm
+    assert tg.flat.grad.abs().max().item() == 0.0        # the flush zeroed the gradients like the eager step
     from distributed_3d_diffusion_pytorch_amd.ops import hip_impl
     hip_impl.set_device_seed(None)
 
@@ -819,6 +828,7 @@ def _graph_comm_worker(out_dir):
         tr = make(graph)
         losses = [float(tr.train_step(*b)) for b in batches]
         mode = tr._graphed.comm_mode if tr._graphed is not None else "eager"
+        tr.sync()
         p = tr.flat.data.clone()
         other = p.clone()
         dist.broadcast(other, 0)
@@ -1052,6 +1062,7 @@ def test_fused_update_matches_separate(graph, monkeypatch):
         tr = Trainer(cfg, ctx)
         for b in batches:
             tr.train_step(*b)
+        tr.sync()
         img, R, t, K = batches[0]
         batch = {"x": img[:, 0], "z": img[:, 1], "logsnr": torch.full((4, 2), 1.5, device=DEV), "R": R, "t": t,
                  "K": K}
