@@ -119,6 +119,9 @@ class ResnetBlock(nn.Module):
         # that reads their output (GN1 here; the next block's GN0 below)
         h = ops.conv3x3(h, self.conv1.weight, self.conv1.bias, gn_groups=self.groupnorm1.gn.num_groups)
         ss = self.__dict__.pop("_ss", None)     # precomputed by the level-batched FiLM
+        ev = self.__dict__.pop("_ss_event", None)
+        if ev is not None:                      # ... on the conditioning stream: first read here
+            torch.cuda.current_stream().wait_event(ev)
         if ss is None:
             ss = self.film(semb)
         # shared conditioning: ss holds one modulation per conditioning class,
@@ -276,9 +279,8 @@ class ConditioningProcessor(nn.Module):
         # only the 51 direction channels go through the spatial conv, the
         # origin half enters as per-image tap biases (ops.cond_conv).
         mask = cond_mask.to(batch["R"].device).bool()
-        rays_dir = ops.ray_posenc_dir(batch["R"], batch["t"], batch["K"], self.H, self.W, mask,
-                                      rescale_from=128 if self.rescale_intrinsics else 0, out_dtype=dtype)
-        orig_pe = ops.ray_origin_pe(batch["t"], mask)
+        rays_dir, orig_pe = ops.ray_conditioning(batch["R"], batch["t"], batch["K"], self.H, self.W, mask,
+                                                 rescale_from=128 if self.rescale_intrinsics else 0, out_dtype=dtype)
         # Convolution is linear, so conv(rays + emb) = conv(rays) + conv(emb):
         # the learned term is convolved once per FRAME (2 images) and added as
         # a batch-broadcast residual.  Its input gradient (for pos_emb /
@@ -472,7 +474,8 @@ class XUNet(nn.Module):
         idx = ref.device.index if ref.device.index is not None else torch.cuda.current_device()
         st = _COND_STREAMS.get(idx)
         if st is None:
-            st = _COND_STREAMS[idx] = torch.cuda.Stream(device=idx)
+            st = _COND_STREAMS[idx] = torch.cuda.Stream(device=idx,
+                                                        priority=int(os.environ.get("D3D_COND_STREAM_PRIO", "0")))
             from ..ops.gradsink import SINK
             SINK.add_compute_stream(st)
         return st
@@ -524,10 +527,11 @@ class XUNet(nn.Module):
                                           [b.film.dense.bias for b in blocks])
                     for o in outs:
                         o.record_stream(main)       # read by the trunk's GN-FiLM kernels
-                    for b, o in zip(blocks, outs):
-                        b.__dict__["_ss"] = o
                     ev = torch.cuda.Event()
                     ev.record(cs)
+                    for b, o in zip(blocks, outs):
+                        b.__dict__["_ss"] = o
+                        b.__dict__["_ss_event"] = ev     # the block waits right before its GN-FiLM
                     events.append(ev)
                     sembs.append(semb)
         elif ss_map is not None or self.batch_film:
@@ -555,8 +559,6 @@ class XUNet(nn.Module):
         hs = [h]
         fence = PARAM_FENCE[0]
         for i in range(L):
-            if events is not None:
-                torch.cuda.current_stream().wait_event(events[i])
             if fence is not None and i == fence[0]:
                 torch.cuda.current_stream().wait_event(fence[1])
             for j in range(self.num_res_blocks):

@@ -88,6 +88,15 @@ def ray_posenc_dir(R, t, K, H: int, W: int, cond_mask, rescale_from: int = 0, ou
     return y.to(out_dtype) if out_dtype is not None else y
 
 
+def ray_conditioning(R, t, K, H: int, W: int, cond_mask, rescale_from: int = 0, out_dtype=None):
+    """(masked ray-direction image [2B,H,W,>=51], masked origin posenc [2B,93]
+    fp32) -- :func:`ray_posenc_dir` and :func:`ray_origin_pe` together; two
+    HIP launches for bf16 GPU runs."""
+    if out_dtype == torch.bfloat16 and R.is_cuda and use_hip(R, any_dtype=True):
+        return _h().ray_conditioning(R, t, K, H, W, cond_mask, rescale_from)
+    return ray_posenc_dir(R, t, K, H, W, cond_mask, rescale_from, out_dtype), ray_origin_pe(t, cond_mask)
+
+
 def ray_origin_pe(t, cond_mask):
     return _t.ray_origin_pe(t, cond_mask)
 
@@ -166,7 +175,7 @@ camera_rays = _t.camera_rays
 posenc_nerf = _t.posenc_nerf
 
 __all__ = ["diffusion_inputs", "diff_loss_nhwc", "group_norm", "gn_film", "conv3x3", "linear", "film_batch", "cat_gn_silu_dense", "cond_conv", "ray_posenc_dir",
-           "ray_origin_pe", "attention", "avgpool2", "upsample2",
+           "ray_origin_pe", "ray_conditioning", "attention", "avgpool2", "upsample2",
            "silu", "logsnr_mlp", "ray_posenc", "posenc_ddpm", "camera_rays", "posenc_nerf", "set_backend",
            "use_hip", "load_library", "library_error", "lib_path"]
 

@@ -67,6 +67,7 @@ SIGNATURES = {
     "d3d_conv_wgrad3": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, P],
     # rays.hip
     "d3d_ray_posenc": [P, P, P, P, P, P, P, P, I, I, I, P],
+    "d3d_cond_prep": [P, P, P, I, C.c_double, C.c_double, P, P, P, P],
     # attention.hip
     "d3d_attn_fwd": [P, P, P, I, I, I, I, I, F, P],
     "d3d_adam_fused": [P, P, P, P, P, P, P, P, I, P, P, I, P],

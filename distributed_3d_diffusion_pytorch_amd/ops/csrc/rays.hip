@@ -151,3 +151,57 @@ D3D_API int d3d_ray_posenc(const float* Rm, const float* tv, const float* Kinv, 
                      other_emb, (bf16*)out, B, H, W);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------- conditioning prep ----
+// Everything the conditioning convs need besides the direction image, in one
+// launch (it used to be ~40 small torch ops at the head of the conditioning
+// stream, `xunet.py:311-336`):
+//   Kinv [B,9] fp32   -- inverse intrinsics, fp64 adjugate (rows 0/1 of K
+//                        scaled by sx / sy first: rescale_intrinsics);
+//   mask [B]  uint8   -- conditioning mask;
+//   ope  [2B,93] fp32 -- NeRF posenc (degrees 0..15) of the camera position
+//                        t[b,f,:], [x, sin(x 2^k), sin(x 2^k + pi/2)], scale-
+//                        major / xyz-minor, zeroed where mask[b] == 0.
+// K is fp32 [B,3,3]; t fp32 [B,2,3]; cmask: any nonzero byte = on.
+__global__ void cond_prep_k(const float* __restrict__ K, const float* __restrict__ t,
+                            const uint8_t* __restrict__ cmask, int B, double sx, double sy,
+                            float* __restrict__ Kinv, uint8_t* __restrict__ mask, float* __restrict__ ope) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;     // image (example b = r / 2, frame r % 2)
+  if (r >= 2 * B) return;
+  const int b = r >> 1;
+  const bool on = cmask[b] != 0;
+  if ((r & 1) == 0) {
+    mask[b] = on ? 1 : 0;
+    const float* k = K + (long)b * 9;
+    const double a = k[0] * sx, bb = k[1] * sx, c = k[2] * sx;
+    const double d = k[3] * sy, e = k[4] * sy, f = k[5] * sy;
+    const double g = k[6], h = k[7], i = k[8];
+    const double A = e * i - f * h, Bc = -(d * i - f * g), C = d * h - e * g;
+    const double det = a * A + bb * Bc + c * C;
+    const double adj[9] = {A, -(bb * i - c * h), bb * f - c * e,
+                           Bc, a * i - c * g, -(a * f - c * d),
+                           C, -(a * h - bb * g), a * e - bb * d};
+    for (int j = 0; j < 9; ++j) Kinv[(long)b * 9 + j] = (float)(adj[j] / det);
+  }
+  const float* x = t + (long)r * 3;
+  float* o = ope + (long)r * 93;
+  const float m = on ? 1.f : 0.f;
+  for (int j = 0; j < 3; ++j) o[j] = x[j] * m;
+  const float hp = 1.5707963267948966f;
+  for (int kdeg = 0; kdeg < 15; ++kdeg) {
+    const float s = (float)(1 << kdeg);
+    for (int j = 0; j < 3; ++j) {
+      const float xb = x[j] * s;
+      o[3 + kdeg * 3 + j] = sinf(xb) * m;
+      o[48 + kdeg * 3 + j] = sinf(xb + hp) * m;
+    }
+  }
+}
+
+D3D_API int d3d_cond_prep(const float* K, const float* t, const void* cmask, int B, double sx, double sy, float* Kinv,
+                          void* mask, float* ope, hipStream_t st) {
+  if (B <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(cond_prep_k, dim3((2 * B + 63) / 64), dim3(64), 0, st, K, t, (const uint8_t*)cmask, B, sx, sy,
+                     Kinv, (uint8_t*)mask, ope);
+  return (int)hipGetLastError();
+}

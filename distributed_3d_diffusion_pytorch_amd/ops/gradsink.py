@@ -47,6 +47,9 @@ from typing import Callable, Dict, Optional
 import torch
 
 
+_PRIO = int(os.environ.get("D3D_WGRAD_STREAM_PRIO", "0"))
+
+
 class GradSink:
     def __init__(self) -> None:
         self.enabled = False
@@ -114,7 +117,10 @@ class GradSink:
     def _side(self, idx: int):
         st = self._streams.get(idx)
         if st is None:
-            st = self._streams[idx] = torch.cuda.Stream(device=idx)
+            # D3D_WGRAD_STREAM_PRIO < 0: a higher-priority HIP queue, so the
+            # weight-gradient work keeps pace with the input-gradient chain
+            # instead of piling up into an exposed tail at the end of backward
+            st = self._streams[idx] = torch.cuda.Stream(device=idx, priority=_PRIO)
         return st
 
     @contextlib.contextmanager

@@ -901,6 +901,29 @@ def ray_posenc_dir(R, t, K, H, W, cond_mask, rescale_from=0, ld=64):
     return out
 
 
+def ray_conditioning(R, t, K, H, W, cond_mask, rescale_from=0, ld=64):
+    """(direction image [2B,H,W,ld] bf16, origin posenc [2B,93] fp32): the
+    inverse intrinsics, mask and origin posenc come from one prep launch
+    (rays.hip cond_prep_k), the direction image from ray_dir_k."""
+    B = R.shape[0]
+    dev = R.device
+    Kf = K.float().reshape(B, 9).contiguous()
+    tf = t.float().reshape(B * 2, 3).contiguous()
+    cm = cond_mask.to(torch.bool).contiguous()
+    sx = W / rescale_from if rescale_from else 1.0
+    sy = H / rescale_from if rescale_from else 1.0
+    Kinv = torch.empty(B, 9, dtype=F32, device=dev)
+    mask = torch.empty(B, dtype=torch.uint8, device=dev)
+    ope = torch.empty(B * 2, 93, dtype=F32, device=dev)
+    _chk(_lib.d3d_cond_prep(Kf.data_ptr(), tf.data_ptr(), cm.data_ptr(), B, float(sx), float(sy), Kinv.data_ptr(),
+                            mask.data_ptr(), ope.data_ptr(), _st()), "cond_prep")
+    Rf = R.float().reshape(B * 2, 9).contiguous()
+    out = torch.empty(B * 2, H, W, ld, dtype=BF16, device=dev)
+    _chk(_lib.d3d_ray_dir(Rf.data_ptr(), Kinv.data_ptr(), mask.data_ptr(), out.data_ptr(), B, H, W, ld, _st()),
+         "ray_dir")
+    return out, ope
+
+
 # --------------------------------------------------------------- linear ----
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     try:

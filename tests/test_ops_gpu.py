@@ -1104,3 +1104,26 @@ def test_logsnr_mlp(H, R):
     assert rel(yh, yr) < 1e-2
     for a, b in zip(ph, pr):
         assert rel(a.grad, b.grad) < 1e-2
+
+
+@pytest.mark.parametrize("rescale", [0, 128])
+def test_ray_conditioning_prep(H, rescale):
+    """One-launch conditioning prep (inverse intrinsics, mask, origin posenc;
+    rays.hip cond_prep_k) + direction image == the torch composition."""
+    from distributed_3d_diffusion_pytorch_amd import ops
+    torch.manual_seed(3)
+    B, Hh, W = 5, 32, 32
+    A = torch.randn(B, 2, 3, 3, device=DEV)
+    R = torch.linalg.qr(A)[0].contiguous()
+    t = torch.randn(B, 2, 3, device=DEV) * 2
+    K = torch.tensor([[60.0, 0.0, 16.0], [0.0, 58.0, 15.5], [0.0, 0.0, 1.0]], device=DEV).repeat(B, 1, 1)
+    K[:, 0, 0] += torch.rand(B, device=DEV) * 5
+    mask = torch.tensor([True, False, True, True, False], device=DEV)
+    dh, oh = H.ray_conditioning(R, t, K, Hh, W, mask, rescale)
+    dr = T.ray_posenc_dir(R, t, K, Hh, W, mask, rescale)
+    orr = T.ray_origin_pe(t, mask)
+    assert oh.shape == orr.shape == (2 * B, 93)
+    assert (oh - orr).abs().max().item() < 1e-5
+    assert dh.shape == dr.shape == (2 * B, Hh, W, 64)
+    assert rel(dh, dr) < 1e-2
+    assert dh[..., 51:].abs().max().item() == 0.0
