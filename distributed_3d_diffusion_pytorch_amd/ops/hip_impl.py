@@ -586,12 +586,13 @@ class _GNFiLM(torch.autograd.Function):
         x, w, b, ss, stats = ctx.saved_tensors
         G, p, seed, ld = ctx.cfg
         dss = None
-        if ctx.slot is not None and ctx.needs_input_grad[3]:
+        if ctx.slot is not None and ctx.needs_input_grad[3] and ctx.slot[0].width == ld:
             # write d(scale|shift) straight into the level's shared dY buffer
-            # so the batched FiLM backward runs one GEMM with no gather
+            # so the batched FiLM backward runs one GEMM with no gather (the
+            # kernel reads ss and writes dss with ONE row stride: only when
+            # the forward modulation has the buffer's width)
             holder, off = ctx.slot
             dss = holder.grad_slice(off, x.shape[-1])
-            ld = holder.width
         dx, dss, dg, db = _gn_bwd(2, x, dy.contiguous(), ss, stats, w, b, G, p, seed, dss=dss, ssld=ld)
         return dx, dg, db, dss, None, None, None, None, None
 
