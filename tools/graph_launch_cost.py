@@ -55,3 +55,60 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def segments(B=16, n=8):
+    """Host time of each part of GraphedTrainStep.step over back-to-back steps."""
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.parallel import DistContext
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    from distributed_3d_diffusion_pytorch_amd.engine.trainer import dropout_word
+    ctx = DistContext(device=torch.device("cuda", 0))
+    cfg = make_config(None, {"model.H": 64, "model.W": 64, "data.imgsize": 64, "global_batch": B,
+                             "micro_batch": 0, "data.synthetic": True, "log_every": 0, "ckpt_every": 0,
+                             "graph": True})
+    tr = Trainer(cfg, ctx)
+    img, R, T, K = next(SyntheticBatches(B, 64, "cuda", seed=3))
+    for _ in range(4):
+        tr.train_step(img, R, T, K)
+    torch.cuda.synchronize()
+    g = tr._graphed
+    o = tr.optim
+    acc = {}
+
+    def tick(k, t):
+        now = time.perf_counter()
+        acc[k] = acc.get(k, 0.0) + now - t
+        return now
+
+    t_all = time.perf_counter()
+    for i in range(n):
+        t = time.perf_counter()
+        word = (tr.step + i) * tr.ctx.world + tr.ctx.rank
+        g.frac.fill_(1.0)
+        for j, v in enumerate((dropout_word(word, 0), word, 0)):
+            g.seed[j].fill_(v)
+        t = tick("fills", t)
+        g.img.copy_(img)
+        g.R.copy_(R)
+        g.T.copy_(T)
+        g.K.copy_(K)
+        t = tick("copies", t)
+        g.gA.replay()
+        t = tick("gA.replay", t)
+        loss = g.loss_acc.clone()
+        t = tick("clone", t)
+        o.hparams_to(g.hp, 1.0)
+        t = tick("set_words", t)
+        g.gB.replay()
+        t = tick("gB.replay", t)
+    t_host = time.perf_counter() - t_all
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t_all
+    print("host ms/step by segment: " + ", ".join(f"{k} {1e3 * v / n:.3f}" for k, v in acc.items())
+          + f" | host total {1e3 * t_host / n:.3f}, wall {1e3 * wall / n:.3f}", flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("GLC_SEGMENTS"):
+    segments()
