@@ -471,6 +471,12 @@ class XUNet(nn.Module):
         if not (self.batch_film and _COND_STREAM and ref is not None and ref.is_cuda
                 and (self.compute_dtype or ref.dtype) == torch.bfloat16 and ops.use_hip(ref, any_dtype=True)):
             return None
+        # measured gain at 64x64 (bs16 / bs128); at 128x128 (two micro-batches
+        # of 64, multi-GB conditioning tensors) the second stream made the
+        # eager step 4.5x slower (profiles/ab_cond_stream_r2.txt): only the
+        # measured regime uses it unless D3D_COND_STREAM=2
+        if self.H * self.W > 64 * 64 and os.environ.get("D3D_COND_STREAM", "1") != "2":
+            return None
         idx = ref.device.index if ref.device.index is not None else torch.cuda.current_device()
         st = _COND_STREAMS.get(idx)
         if st is None:
