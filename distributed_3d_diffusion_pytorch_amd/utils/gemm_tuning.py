@@ -25,9 +25,11 @@ TABLE = os.path.join(ROOT, "tuning", "tunableop_mi355x.csv")
 _DONE = [False]
 
 
-def enable_tuned_gemms(path: str = TABLE) -> bool:
-    """Load the tuned-solution table (once per process).  Returns True when
-    TunableOp is active with it."""
+def enable_tuned_gemms(path: str = None) -> bool:
+    """Load the tuned-solution table (once per process; ``D3D_TUNED_GEMMS_TABLE``
+    overrides the repository table).  Returns True when TunableOp is active
+    with it."""
+    path = path or os.environ.get("D3D_TUNED_GEMMS_TABLE") or TABLE
     if _DONE[0]:
         return torch.cuda.tunable.is_enabled()
     _DONE[0] = True

@@ -28,7 +28,7 @@ def child(batch: int, out: str) -> None:
     from distributed_3d_diffusion_pytorch_amd.engine import Trainer
     from distributed_3d_diffusion_pytorch_amd.parallel import DistContext
     from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
-    mb = 64 if batch > 64 else 0
+    mb = 64 if batch > 128 else 0          # bench.py: one micro-batch up to 128 examples at 64x64
     cfg = make_config(None, {"global_batch": batch, "micro_batch": mb, "data.synthetic": True, "log_every": 0,
                              "ckpt_every": 0, "graph": False})
     tr = Trainer(cfg, DistContext(device=torch.device("cuda", 0)))
