@@ -1127,6 +1127,30 @@ class _Linear(torch.autograd.Function):
         return dx, dW, db, dres, None, None, None, None
 
 
+# Explicit split-K of the hipBLASLt FiLM weight-gradient product: the pixel
+# reduction (K up to 1M rows at bs128) as a batch of ``nsl`` GEMMs whose fp32
+# partial products the scatter kernel sums while it writes the parameter
+# gradients (no separate sum pass).  hipBLASLt's own choice for the single
+# mixed-precision GEMM runs 640-950 TF/s on these shapes; 8 (4 for the
+# smallest level) slabs run 910-1160 TF/s (profiles/film_wgrad_split_r2.txt).
+# D3D_FILM_WGRAD_SPLIT: 0 = auto by row count, 1 = off, else the slab count.
+_FILM_WGRAD_SPLIT = int(os.environ.get("D3D_FILM_WGRAD_SPLIT", "0"))
+
+
+def _film_wgrad_product(dy: torch.Tensor, x2: torch.Tensor):
+    """``dy^T @ x2`` in fp32 as ``nsl`` stacked partial products."""
+    rows, S = dy.shape
+    K = x2.shape[1]
+    nsl = _FILM_WGRAD_SPLIT or (8 if rows >= 32768 else 4 if rows >= 8192 else 1)
+    if nsl > 1 and rows % nsl == 0:
+        try:
+            a = dy.view(nsl, rows // nsl, S).transpose(1, 2)
+            return torch.bmm(a, x2.view(nsl, rows // nsl, K), out_dtype=F32), nsl
+        except (RuntimeError, TypeError):
+            pass
+    return _mm_f32(dy.t(), x2), 1
+
+
 class _FiLMSlot:
     """Shared gradient buffer of one level-batched FiLM projection: each
     GN-FiLM backward deposits its d(scale|shift) into its column slice."""
@@ -1222,10 +1246,10 @@ class _FiLMBatch(torch.autograd.Function):
                     # profiles/kbench_lin_v2.jsonl) than on the split-K MFMA
                     # kernel; its fp32 [S, K] product and the bias column sums are
                     # then scattered into the parameters' gradients in one launch
-                    prod = _mm_f32(dy.t(), x2)
+                    prod, nsl = _film_wgrad_product(dy, x2)
                     nimg = 64 if rows % 64 == 0 else 1
                     _, bsum = _chansum(dy.view(nimg, rows // nimg, 1, S), False)
-                    _chk(_lib.d3d_wgrad_scatter(prod.data_ptr(), S, K, 1, 1, bsum.data_ptr(), 1, n, row0, wd, bd,
+                    _chk(_lib.d3d_wgrad_scatter(prod.data_ptr(), S, K, nsl, 1, bsum.data_ptr(), 1, n, row0, wd, bd,
                                                 _st()), "film_wgrad_scatter")
                 else:
                     sp, pps = ctypes.c_int(), ctypes.c_int()

@@ -456,7 +456,8 @@ def test_sampler_step_matches_posterior(H):
 
 @pytest.mark.parametrize("blas", [True, False])
 @pytest.mark.parametrize("chans,N,Hh", [([128, 128, 256], 4, 8), ([512, 512], 4, 8),
-                                        ([128, 256, 384], 32, 32)])   # 32768 rows: 8-wave 1x1 wgrad
+                                        ([128, 256, 384], 32, 32),    # 32768 rows: 8-wave 1x1 wgrad
+                                        ([256, 512], 8, 32)])         # 8192 rows: 4 blas slabs
 def test_film_batch_with_gn_film(H, chans, N, Hh, blas):
     """Level-batched FiLM projection feeding strided GN-FiLM: forward, the
     shared d(scale|shift) buffer and the segmented weight-gradient scatter
