@@ -23,6 +23,8 @@ def main():
     dev = torch.device("cuda", 0)
     # (rows, S, K): level 0..3 of the bs128 step (256 images of 64^2 .. 8^2)
     shapes = [(1048576, 2048, 1024), (262144, 4608, 1024), (65536, 4608, 1024), (16384, 9216, 1024)]
+    if len(sys.argv) > 1 and sys.argv[1] == "bs32":   # the 4-GPU per-GPU share
+        shapes = [(262144, 2048, 1024), (65536, 4608, 1024), (16384, 4608, 1024), (4096, 9216, 1024)]
     for rows, S, K in shapes:
         dy = torch.randn(rows, S, device=dev, dtype=torch.bfloat16)
         x = torch.randn(rows, K, device=dev, dtype=torch.bfloat16)
@@ -30,7 +32,7 @@ def main():
         flop = 2.0 * rows * S * K
         t = timeit(lambda: torch.mm(dy.t(), x, out_dtype=torch.float32))
         print(f"rows={rows} S={S} K={K} mm_f32 {1e3 * t:.3f} ms {flop / t / 1e12:.0f} TF/s", flush=True)
-        for sp in (2, 4, 8):
+        for sp in (2, 4, 8, 16):
             if rows % sp:
                 continue
             a = dy.view(sp, rows // sp, S).transpose(1, 2)
