@@ -443,6 +443,7 @@ class _GroupNorm(torch.autograd.Function):
 
 import os as _os
 _CAT_FUSE = _os.environ.get("D3D_CAT_FUSE", "1")
+_CAT_PP = _os.environ.get("D3D_CAT_PP", "0") != "0"      # forward NIN skip of the virtual concat on gemm.hip only
 
 
 class _CatGNDense(torch.autograd.Function):
@@ -463,7 +464,7 @@ class _CatGNDense(torch.autograd.Function):
         OC = wb.shape[0]
         a2, b2 = a.reshape(-1, C1), b.reshape(-1, C2)
         C = C1 + C2
-        if _LIN_PP and _pp_ok(OC, a2.shape[0], C1, C, C1) and _pp_ok(OC, b2.shape[0], C2, C, C2):
+        if (_LIN_PP or _CAT_PP) and _pp_ok(OC, a2.shape[0], C1, C, C1) and _pp_ok(OC, b2.shape[0], C2, C, C2):
             skip = torch.empty(a2.shape[0], OC, dtype=BF16, device=a.device)
             gemm_nt(wb, a2, skip, OC, a2.shape[0], C1, C, C1, OC, bias=db.detach() if db is not None else None)
             gemm_nt(wb[:, C1:], b2, skip, OC, b2.shape[0], C2, C, C2, OC, res=skip)

@@ -576,12 +576,17 @@ def test_ray_dir_matches_torch(H):
     assert torch.allclose(T.ray_origin_pe(t, mask)[:, None, None, :].expand(-1, Hh, Hh, -1), full[..., :93])
 
 
+@pytest.mark.parametrize("pp", [False, True])
 @pytest.mark.parametrize("C1,C2,OC", [(256, 128, 128), (128, 128, 128), (512, 512, 512), (512, 256, 256)])
-def test_cat_gn_silu_dense(H, C1, C2, OC):
+def test_cat_gn_silu_dense(H, C1, C2, OC, pp, monkeypatch):
     """Decoder block entry on the virtual concat == GN+SiLU and dense on the
-    materialised concat (forward and every gradient)."""
+    materialised concat (forward and every gradient); ``pp``: the skip
+    forward on the hand-written ping-pong GEMM (D3D_CAT_PP)."""
     torch.manual_seed(11)
-    N, Hh = 4, 8
+    N, Hh = (4, 32) if pp else (4, 8)
+    monkeypatch.setattr(H, "_CAT_PP", pp)
+    if pp:
+        monkeypatch.setattr(H, "_PP_MIN_TILES", 1)
     a = (torch.randn(N, Hh, Hh, C1, device=DEV) + 0.3).to(BF)
     b = (torch.randn(N, Hh, Hh, C2, device=DEV) * 2).to(BF)
     gw = torch.rand(C1 + C2, device=DEV) + 0.5
