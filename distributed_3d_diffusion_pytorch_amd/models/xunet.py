@@ -14,8 +14,8 @@ re-designed:
 * camera rays are generated on device (the reference round-trips through numpy
   on the host every forward, `xunet.py:311-318`);
 * ``silu(logsnr_emb + pose_emb_i)`` is computed once per resolution level and
-  shared by all FiLM layers of that level (the reference recomputes the SiLU in
-  every FiLM, `xunet.py:84`);
+  shared by all FiLM layers of that level, whose projections run as one GEMM
+  (the reference recomputes the SiLU in every FiLM, `xunet.py:84`);
 * the output head runs on frame 1 only (the reference computes both frames and
   discards frame 0, `xunet.py:535-536`).
 """
@@ -58,17 +58,18 @@ class GroupNorm(nn.Module):
 
 class FiLM(nn.Module):
     """FiLM projection ``dense(silu(emb)) -> [scale | shift]`` (`xunet.py:74-87`).
-    ``forward`` takes the already-activated per-level embedding and returns the
+    ``forward`` takes the per-level (pre-activation) embedding and returns the
     packed ``[N, H, W, 2C]`` modulation; the modulation itself is fused into the
-    GroupNorm kernel (:func:`ops.gn_film`)."""
+    GroupNorm kernel (:func:`ops.gn_film`).  The level-batched path
+    (:func:`ops.film_batch`) runs every FiLM of a level as one GEMM."""
 
     def __init__(self, features: int, emb_ch: int = 1024):
         super().__init__()
         self.features = features
         self.dense = nn.Linear(emb_ch, 2 * features)
 
-    def forward(self, semb: torch.Tensor) -> torch.Tensor:
-        return ops.linear(semb, self.dense.weight, self.dense.bias)
+    def forward(self, emb: torch.Tensor) -> torch.Tensor:
+        return ops.linear(ops.silu(emb), self.dense.weight, self.dense.bias)
 
 
 class ResnetBlock(nn.Module):
@@ -218,8 +219,9 @@ class XUNetBlock(nn.Module):
 class ConditioningProcessor(nn.Module):
     """logSNR embedding MLP + camera-ray conditioning (`xunet.py:259-352`).
 
-    Returns the per-level activated embeddings ``silu(logsnr_emb + pose_emb_i)``
-    as ``[2B, H_i, W_i, emb_ch]`` tensors (the only form FiLM consumes)."""
+    Returns the per-level embeddings ``logsnr_emb + pose_emb_i`` as
+    ``[2B, H_i, W_i, emb_ch]`` tensors; FiLM applies the SiLU (`xunet.py:84`),
+    fused into its projection's GEMM."""
 
     D = 144
 
@@ -292,7 +294,7 @@ class ConditioningProcessor(nn.Module):
             e_emb = ops.conv3x3(emb_img, conv.weight, None, stride=s) if emb_img is not None else None
             e = ops.cond_conv(rays_dir, orig_pe, conv.weight, conv.bias, s, row_bias=logsnr_emb, residual=e_emb,
                               res_period=2 if e_emb is not None else 0)
-            yield ops.silu(e)
+            yield e
 
 
 class XUNet(nn.Module):

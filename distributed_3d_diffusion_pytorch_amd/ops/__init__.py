@@ -107,10 +107,11 @@ def cat_gn_silu_dense(a, b, gw, gb, dw, db, groups: int = 32, eps: float = 1e-5)
     return _t.cat_gn_silu_dense(a, b, gw, gb, dw, db, groups, eps)
 
 
-def film_batch(semb, weights, biases):
-    if use_hip(semb):
-        return _h().film_batch(semb, weights, biases)
-    return _t.film_batch(semb, weights, biases)
+def film_batch(emb, weights, biases):
+    """``dense_i(silu(emb))`` for every FiLM projection of one level."""
+    if use_hip(emb):
+        return _h().film_batch(emb, weights, biases)
+    return _t.film_batch(emb, weights, biases)
 
 
 def attention(qkv, heads: int, cross: bool):

@@ -2534,7 +2534,11 @@ struct PackDesc {
   int OC, IC, OCp, ICp, taps, mode;     // mode 0: pack, 1: transposed pack, 2: cast (OC elements)
   int blk0;                             // first block of this descriptor in the flattened grid
   int ICs;                              // source IC stride (0: IC) -- channel slices of a weight
+  int ldd;                              // mode 1: destination row stride (0: OCp) -- column block of a
+                                        // concatenated transposed operand
+  int pad_;                             // (host table rows are packed: keep the size a multiple of 8)
 };
+static_assert(sizeof(PackDesc) == 56, "PackDesc must match hip_impl._desc_tensors");
 
 // One launch repacks every cached bf16 operand.  The grid is flattened over
 // descriptors (host-built block -> descriptor map, sizes in hip_impl
@@ -2600,7 +2604,7 @@ __global__ void __launch_bounds__(256) pack_all_k(const PackDesc* __restrict__ d
     bf16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (bf16)tile[(c8 + e) * 16 * T + ci * T + tap];
-    *reinterpret_cast<bf16x8*>(d.dst + ((long)(ci0 + ci) * T + tap) * d.OCp + co0 + c8) = o;
+    *reinterpret_cast<bf16x8*>(d.dst + ((long)(ci0 + ci) * T + tap) * (d.ldd ? d.ldd : d.OCp) + co0 + c8) = o;
   }
 }
 

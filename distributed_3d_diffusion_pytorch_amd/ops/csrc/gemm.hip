@@ -1,404 +1,202 @@
 // Dense per-pixel GEMM on the gfx950 matrix cores: the 1x1 layers of the
 // X-UNet (FiLM projections `xunet.py:74-87`, attention in/out projections
-// `xunet.py:154-177`, NIN skips `xunet.py:128-129`) as
+// `xunet.py:154-177`, NIN skips `xunet.py:128-129`) and their input gradients,
 //
-//     O[n][m] = (alpha * sum_k A[m][k] * B[n][k] + bias[m] + R[n][m]) * scale
+//     O[n][m] = epi(sum_k A[m][k] * B[n][k])
 //
 // with A the bf16 weight ([M][lda], K contiguous), B the NHWC activations
-// ([N][ldb], K contiguous), O / R NHWC bf16 rows of stride ldo / ldr.
+// ([N][ldb], K contiguous) and O / R NHWC bf16 rows (strides ldo / ldr).
+// Epilogues: EPI 0  (alpha * acc + bias[m] + R[n][m]) * scale, optionally
+//                   with the GroupNorm partial statistics of O;
+//            EPI 1  alpha * acc * dsilu(R[n][m]) -- the FiLM input gradient
+//                   through the SiLU of the conditioning embedding.
 //
-// Schedule ("ping-pong", one 256 x 256 output tile per 512-thread block):
-//   * 8 waves as 2 (M) x 4 (N), 128 x 64 outputs each (8 x 4 MFMA 16x16x32
-//     tiles, 128 fp32 accumulators), two waves per SIMD -- one of each M half;
-//   * the M-half-1 waves run one barrier behind the M-half-0 waves, so on every
-//     SIMD one wave issues its 16 MFMAs while its partner issues the next
-//     phase's ds_reads and LDS-DMA: the matrix core never waits for a
-//     fragment read or a DMA issue;
-//   * a 64-deep K-tile is four phases (quadrants of the wave tile: 64 x 32 x 64
-//     = 16 MFMAs), and its LDS image is four 16-KiB pieces (A rows of M-quarter
-//     0 / 2, B rows of N-eighth 0 / 2 of each wave, ...) restaged one piece per
-//     phase into the other of two stages -- each piece is read 1-3 phases
-//     after the wave's counted `vmcnt(4)` retires it (never `vmcnt(0)` in the
-//     loop), and rewritten >= 4 phases after its last read;
-//   * LDS-DMA (`buffer_load ... lds`, 16 B per lane) with the XOR chunk swizzle
-//     applied to the source address, conflict-free `ds_read_b128` fragments;
-//   * per-block buffer descriptors (row base m0 / n0), so 32-bit offsets cover
-//     operands of any size and rows past M / N read as zeros;
-//   * bijective XCD remap: the blocks of one N tile (sharing the activation
-//     panel) run on one XCD.
+// Schedule ("fat waves"): a 256-thread block = 2 x 2 waves, one per SIMD, each
+// owning WI x WJ MFMA 16x16x32 tiles (8 x 8 = 128 x 128 outputs and 256 fp32
+// accumulators for the big layers, 4 x 4 / 2 x 2 for small problems):
+//   * BK = 32, FOUR LDS stages (A rows, then B rows; 64-byte rows with the
+//     chunk swizzle c ^ 3*((row >> 3) & 1): conflict-free ds_read_b128);
+//   * K-tile s: `vmcnt` retires this wave's LDS-DMA of K-tile s + 1, ONE
+//     barrier publishes it, then WI*WJ slots, each one MFMA of K-tile s plus
+//     at most one other instruction: the fragment reads of K-tile s + 1 (into
+//     the other register set), the LDS-DMA pieces of K-tile s + 3 (into the
+//     stage K-tile s - 1 used), the loader's cursor update.  The DMA runs two
+//     K-tiles ahead of its reader and the matrix pipe never waits on a read;
+//   * the MFMAs are inline asm with "a"-constrained accumulators (the
+//     compiler's own lowering splits 256 accumulators between the register
+//     files and shuffles them every K-tile);
+//   * persistent: each block walks tiles rb, rb + G, ... as ONE stream of
+//     K-tiles, so the next tile's DMA is in flight during the epilogue; the
+//     bias rides on a DMA into one of 4 LDS slots;
+//   * epilogue: fragment pairs become 16-byte rows by v_permlane16_swap and
+//     leave as exactly WI*WJ/2 buffer stores per wave (masked lanes get an
+//     out-of-range offset), so the next tile's counted waits step over them;
+//   * per-tile buffer descriptors (rows m0 / n0 based): 32-bit offsets for
+//     any operand size, rows past M / N read as zeros;
+//   * bijective XCD remap + grouped tile order: the tiles an XCD runs at once
+//     share their activation panels.
 #include "common.h"
 
 #include <algorithm>
 #include <cstdlib>
+#include <utility>
 
 namespace {
-constexpr int PP_BK = 64;
-constexpr int PP_PIECE = 128 * PP_BK;       // bf16 elements per LDS piece (16 KiB)
-constexpr int PP_STAGE = 4 * PP_PIECE;      // one K-tile (64 KiB)
-// behind the two stages: two 1-KiB bias slots (tile parity) and a 1-KiB sink
-// for the aux DMA of K-tiles that carry no bias (see pp_issue)
-constexpr int PP_BIAS = 2 * PP_STAGE;       // bf16 offset of the bias slots
-constexpr int PP_SINK = PP_BIAS + 1024;
-constexpr int PP_LDS = PP_SINK + 512;
+constexpr int G_BK = 32;
+constexpr int G_NST = 4;
 
-__device__ __forceinline__ int pp_swz(int row, int chunk) { return row * PP_BK + ((chunk ^ (row & 7)) << 3); }
-
-// Issue piece `p` (0: A mi0, 1: B ni0, 2: B ni1, 3: A mi1 -> LDS slots 0, 1, 3, 2)
-// of K-tile `t` into stage `s & 1`: two 1-KiB DMA instructions per wave.
-// Piece 0 carries a third, "aux" instruction in EVERY K-tile, so the counted
-// waits stay uniform: on the first K-tile of a tile wave 0 DMAs the tile's 256
-// fp32 biases into the bias slot (the epilogue then reads them from LDS -- no
-// global load, hence no vmcnt drain of the in-flight pieces, in the epilogue);
-// otherwise it is an out-of-range (no memory access) DMA into the sink.
-__device__ __forceinline__ void pp_issue(bf16* smem, const bf16* A, const bf16* B, int a_rec, int b_rec, int t, int p,
-                                         int wave, const int (&aoff)[2][2], const int (&boff)[2][2], int s,
-                                         const float* aux = nullptr, int aux_rec = 0, int aux_dst = PP_SINK) {
-  typedef __attribute__((address_space(3))) void lds_void;
-  const int slot = p == 0 ? 0 : p == 1 ? 1 : p == 2 ? 3 : 2;
-  bf16* dst = smem + (s & 1) * PP_STAGE + slot * PP_PIECE + wave * 16 * PP_BK;
-  const int kb = t * PP_BK * 2;
-  if (p == 0 || p == 3) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_rec, 0x00020000);
-    const int h = p == 3;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, aoff[h][0], kb, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(dst + 8 * PP_BK), 16, aoff[h][1], kb, 0, 0);
-    if (p == 0) {
-      const __amdgpu_buffer_rsrc_t ra =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(aux ? (const void*)aux : (const void*)A), (short)0, aux_rec,
-                                            0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(smem + aux_dst), 16,
-                                               (int)(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))) * 16,
-                                               0, 0, 0);
-    }
-  } else {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_rec, 0x00020000);
-    const int h = p == 2;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, boff[h][0], kb, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(dst + 8 * PP_BK), 16, boff[h][1], kb, 0, 0);
-  }
+__device__ __forceinline__ int g_swz(int row, int chunk) {
+  return row * G_BK + ((chunk ^ (((row >> 3) & 1) * 3)) << 3);
 }
 
-#define PP_BAR()                          \
-  do {                                    \
-    __builtin_amdgcn_sched_barrier(0);    \
-    __builtin_amdgcn_s_barrier();         \
-    __builtin_amdgcn_sched_barrier(0);    \
-  } while (0)
-}  // namespace
-
-// Tile id -> (m tile, n tile): m fastest inside groups of `gm` m tiles, so the
-// 32 consecutive ids an XCD runs at once share ~gm A panels and ~32/gm B panels.
-__device__ __forceinline__ void pp_tile(int tile, int mt, int nt, int gm, int& mb, int& nb) {
-  const int full = mt / gm, span = gm * nt;
-  if (tile < full * span) {
-    const int g = tile / span, r = tile - g * span;
-    mb = g * gm + r % gm;
-    nb = r / gm;
-  } else {
-    const int rem = mt - full * gm, r = tile - full * span;
-    mb = full * gm + r % rem;
-    nb = r / rem;
-  }
-}
-
-struct PPTile {
-  const bf16* A;
-  const bf16* B;
-  int a_rec, b_rec;
-  long m0;
+template <int WI, int WJ>
+struct GCfg {
+  static constexpr int BM = 32 * WI, BN = 32 * WJ;       // 2 x 2 waves of 16*WI x 16*WJ
+  static constexpr int STAGE = (BM + BN) * G_BK;         // bf16 per stage
+  static constexpr int BIAS = G_NST * STAGE;             // 4 slots of 256 fp32
+  static constexpr int LDS = BIAS + 4 * 512;
+  static constexpr int DA = BM / 64, DB = BN / 64;       // DMA pieces (16 rows) per wave and K-tile
+  static constexpr int ND = DA + DB;
+  static constexpr int NM = WI * WJ;                     // MFMAs per wave and K-tile
+  static constexpr int NR = WI + WJ;                     // fragment reads
+  static constexpr int NS = WI * WJ / 2;                 // epilogue stores per wave
 };
 
-__device__ __forceinline__ PPTile pp_tile_ops(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
-                                              int mb, int nb) {
-  const long m0 = (long)mb * 256, n0 = (long)nb * 256;
-  const long arows = M - m0 < 256 ? M - m0 : 256, brows = N - n0 < 256 ? N - n0 : 256;
-  PPTile o;
-  o.A = A + m0 * lda;
-  o.B = B + n0 * ldb;
-  o.a_rec = (int)((arows - 1) * lda + K) * 2;      // descriptor range: this tile's rows only
-  o.b_rec = (int)((brows - 1) * ldb + K) * 2;
-  o.m0 = m0;
-  return o;
+#define G_BAR()                        \
+  do {                                 \
+    __builtin_amdgcn_sched_barrier(0); \
+    __builtin_amdgcn_s_barrier();      \
+    __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+
+__device__ __forceinline__ void g_mma(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void g_mma0(f32x4& c, const bf16x8& a, const bf16x8& b) {   // first K-tile: C = 0
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
 }
 
-// Epilogue of one 256 x 256 tile: acc[ii][jj] holds rows m0 + wr*128 + ii*16 +
-// fq*4 + e of pixel n0 + wn*64 + jj*16 + fr; the tile's biases are in LDS.
-__device__ __forceinline__ void pp_epi(const f32x4 (&acc)[8][4], const float* __restrict__ sbias, bf16* __restrict__ O,
-                                       const bf16* __restrict__ R, int M, int N, int ldo, int ldr, float alpha,
-                                       float scale, long m0, long n0, int wr, int wn, int lane,
-                                       float* __restrict__ gnp, int gn_groups, int gn_hw) {
-  const int fr = lane & 15, fq = lane >> 4;
-  const bool vec = (ldo & 3) == 0 && (!R || (ldr & 3) == 0);
-  // fused GroupNorm partials of the output (host guarantees vec, M % 4 == 0,
-  // gn_hw % 64 == 0): this wave's 64 pixels are one 64-pixel part
-  float gs[8][1], gq[8][1];
-#pragma unroll
-  for (int ii = 0; ii < 8; ++ii) gs[ii][0] = gq[ii][0] = 0.f;
-#pragma unroll
-  for (int ii = 0; ii < 8; ++ii) {
-    const long co = m0 + wr * 128 + ii * 16 + fq * 4;
-    if (co >= M) continue;
-    const f32x4 cb = sbias ? *reinterpret_cast<const f32x4*>(sbias + wr * 128 + ii * 16 + fq * 4)
-                           : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const long pix = n0 + wn * 64 + jj * 16 + fr;
-      if (pix >= N) continue;
-      bf16* dst = O + pix * ldo + co;
-      if (vec && co + 3 < M) {
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[ii][jj][e] * alpha + cb[e];
-        if (R) {
-          const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(R + pix * ldr + co);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
-        }
-        bf16x4 o4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o4[e] = (bf16)(v[e] * scale);
-          const float yv = (float)o4[e];
-          gs[ii][0] += yv;
-          gq[ii][0] += yv * yv;
-        }
-        *reinterpret_cast<bf16x4*>(dst) = o4;
-      } else {
-        for (int e = 0; e < 4 && co + e < M; ++e) {
-          float v = acc[ii][jj][e] * alpha + cb[e];
-          if (R) v += (float)R[pix * ldr + co + e];
-          dst[e] = (bf16)(v * scale);
-        }
-      }
-    }
-  }
-  if (gnp) gn_part_store<8, 1>(gs, gq, lane, (int)(m0 + wr * 128), n0 + wn * 64, M, gn_groups, gn_hw, N, gnp);
-}
-
-// Persistent: each block walks tiles rb, rb + G, ... (rb = XCD-contiguous
-// rank of the block, G = grid) as ONE stream of K-tiles -- the next tile's
-// first pieces are in flight while this tile's last phases and its epilogue
-// run, so neither the prologue latency nor the epilogue stores idle the CU.
-__global__ void __launch_bounds__(512, 1)
-gemm_pp_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ O, const float* __restrict__ bias,
-          const bf16* __restrict__ R, int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha,
-          float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[PP_LDS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wn = wave & 3;
-  const int G = gridDim.x;
-  int rb = blockIdx.x;
-  {
-    const int q = G / 8, r = G % 8, xcd = rb % 8;
-    rb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + rb / 8;
-  }
-  const int ntiles = mt * nt;
-  if (rb >= ntiles) return;
-
-  const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
-  int aoff[2][2], boff[2][2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int prow = wave * 16 + q * 8 + lrow;                         // row of the 128-row piece
-      const int ar = (prow >> 6) * 128 + h * 64 + (prow & 63);
-      const int br = (prow >> 5) * 64 + h * 32 + (prow & 31);
-      aoff[h][q] = (ar * lda + lchunk * 8) * 2;
-      boff[h][q] = (br * ldb + lchunk * 8) * 2;
-    }
-
-  f32x4 acc[8][4];
-  bf16x8 af[4][2], bq[2][2][2];
-  const int fr = lane & 15, fq = lane >> 4;
-  const int nk = K / PP_BK;
-
-  auto readA = [&](int st, int h) {
-    const bf16* base = smem + st * PP_STAGE + (h ? 2 : 0) * PP_PIECE;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i][kk] = *reinterpret_cast<const bf16x8*>(base + pp_swz(wr * 64 + i * 16 + fr, kk * 4 + fq));
-  };
-  auto readB = [&](int st, int h) {
-    const bf16* base = smem + st * PP_STAGE + (h ? 3 : 1) * PP_PIECE;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bq[h][j][kk] = *reinterpret_cast<const bf16x8*>(base + pp_swz(wn * 32 + j * 16 + fr, kk * 4 + fq));
-  };
-  auto quad = [&](int mi, int ni) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[mi * 4 + i][ni * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bq[ni][j][kk], acc[mi * 4 + i][ni * 2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  int tile = rb, mb, nb;
-  pp_tile(tile, mt, nt, gm, mb, nb);
-  PPTile cur = pp_tile_ops(A, B, M, N, K, lda, ldb, mb, nb);
-  // aux DMA of a tile's first K-tile: its bias (wave 0), else the sink
-  auto aux_of = [&](const PPTile& o, int parity, const float*& src, int& rec, int& dst) {
-    src = nullptr;
-    rec = 0;
-    dst = PP_SINK;
-    if (bias && wave == 0) {
-      src = bias + o.m0;
-      rec = (int)((M - o.m0 < 256 ? M - o.m0 : 256) * 4);
-      dst = PP_BIAS + parity * 512;
-    }
-  };
-  {
-    const float* as;
-    int ar, ad;
-    aux_of(cur, 0, as, ar, ad);
-    pp_issue(smem, cur.A, cur.B, cur.a_rec, cur.b_rec, 0, 0, wave, aoff, boff, 0, as, ar, ad);
-  }
-#pragma unroll
-  for (int p = 1; p < 4; ++p) pp_issue(smem, cur.A, cur.B, cur.a_rec, cur.b_rec, 0, p, wave, aoff, boff, 0);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  PP_BAR();
-  if (wr == 1) PP_BAR();                 // the M-half-1 waves trail by one barrier
-
-  int s = 0;                             // K-tile stream position (LDS stage = s & 1)
-  int ti = 0;                            // tiles done by this block (bias slot = ti & 1)
-  while (true) {
-    const int ntile = tile + G;
-    const bool more = ntile < ntiles;
-    int nmb = 0, nnb = 0;
-    if (more) pp_tile(ntile, mt, nt, gm, nmb, nnb);
-    const PPTile nxtop = more ? pp_tile_ops(A, B, M, N, K, lda, ldb, nmb, nnb) : cur;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < nk; ++t, ++s) {
-      const int st = s & 1;
-      const bool in_tile = t + 1 < nk;
-      const bool nxt = in_tile || more;
-      // the K-tile after this one in the stream: (this tile, t + 1) or (next tile, 0)
-      const PPTile& lo = in_tile ? cur : nxtop;
-      const int lt = in_tile ? t + 1 : 0;
-      const int ls = s + 1;
-      // phase 0: quadrant (0, 0)
-      readA(st, 0);
-      readB(st, 0);
-      if (nxt) {
-        const float* as = nullptr;
-        int ar = 0, ad = PP_SINK;
-        if (!in_tile) aux_of(lo, (ti + 1) & 1, as, ar, ad);
-        pp_issue(smem, lo.A, lo.B, lo.a_rec, lo.b_rec, lt, 0, wave, aoff, boff, ls, as, ar, ad);
-        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      }
-      PP_BAR();
-      quad(0, 0);
-      PP_BAR();
-      // phase 1: quadrant (0, 1)
-      readB(st, 1);
-      if (nxt) {
-        pp_issue(smem, lo.A, lo.B, lo.a_rec, lo.b_rec, lt, 1, wave, aoff, boff, ls);
-        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      PP_BAR();
-      quad(0, 1);
-      PP_BAR();
-      // phase 2: quadrant (1, 1)
-      readA(st, 1);
-      if (nxt) pp_issue(smem, lo.A, lo.B, lo.a_rec, lo.b_rec, lt, 2, wave, aoff, boff, ls);
-      PP_BAR();
-      quad(1, 1);
-      PP_BAR();
-      // phase 3: quadrant (1, 0) from registers
-      if (nxt) {
-        pp_issue(smem, lo.A, lo.B, lo.a_rec, lo.b_rec, lt, 3, wave, aoff, boff, ls);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      }
-      PP_BAR();
-      quad(1, 0);
-      PP_BAR();
-    }
-
-    pp_epi(acc, bias ? reinterpret_cast<const float*>(smem + PP_BIAS) + (ti & 1) * 256 : nullptr, O, R, M, N, ldo, ldr,
-           alpha, scale, (long)mb * 256, (long)nb * 256, wr, wn, lane, gnp, gn_groups, gn_hw);
-    if (!more) break;
-    ++ti;
-    tile = ntile;
-    mb = nmb;
-    nb = nnb;
-    cur = nxtop;
-  }
-  if (wr == 0) PP_BAR();                 // balance the trailing group's extra barrier
-}
-
-// ---------------------------------------------------------------- v2 ----
-// BK = 32, FOUR LDS stages (32 KiB each: A then B, 256 rows x 64 B), ONE
-// ping-pong phase per K-tile: 32 MFMAs per wave between the barriers (512
-// cycles of matrix-core work per SIMD and wave, twice the v1 phase, so the
-// barrier hand-over costs half as much), the stage of K-tile s + 3 issued in
-// phase s (3 K-tiles ~ 3000 cycles of DMA latency budget), a uniform
-// `vmcnt(10)` (5 DMA instructions per wave per K-tile: 2 A, 2 B, 1 aux; past
-// the end of the stream they are out-of-range no-ops into the sink) and
-// `lgkmcnt(0)` before each barrier, so the stage rewritten in phase s (last
-// read in phase s - 1) has no reader left.
-// 64-byte rows: chunk c of row r sits at 16-byte slot c ^ (((r >> 3) & 1) * 3),
-// which makes every ds_read_b128 lane group hit 16 distinct bank slots.
-namespace {
-constexpr int Q_BK = 32;
-constexpr int Q_STAGE = 2 * 256 * Q_BK;     // bf16 elements per stage (A rows 0..255, then B rows)
-constexpr int Q_NST = 4;
-constexpr int Q_BIAS = Q_NST * Q_STAGE;     // 4 bias slots (tile & 3) of 256 fp32
-constexpr int Q_SINK = Q_BIAS + 4 * 512;
-constexpr int Q_LDS = Q_SINK + 512;
-
-__device__ __forceinline__ int q_swz(int row, int chunk) {
-  return row * Q_BK + ((chunk ^ (((row >> 3) & 1) * 3)) << 3);
-}
-
-__device__ __forceinline__ void q_issue(bf16* smem, const PPTile& o, bool valid, int t, int s, const int (&aoff)[2],
-                                        const int (&boff)[2], int wave, const float* aux, int aux_rec, int aux_dst) {
+// LDS-DMA of 16 bytes per lane from buffer (base, nrec bytes) at voff + soff
+// into lds (wave-uniform base + lane * 16).  Plain (non-template) helpers:
+// the address-space cast and the descriptor are device-only constructs that
+// the host pass of a kernel template must never instantiate.
+__device__ __forceinline__ void g_dma(const void* base, int nrec, void* lds, int voff, int soff) {
   typedef __attribute__((address_space(3))) void lds_void;
-  const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const __amdgpu_buffer_rsrc_t rA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)o.A, (short)0, valid ? o.a_rec : 0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rB =
-      __builtin_amdgcn_make_buffer_rsrc((void*)o.B, (short)0, valid ? o.b_rec : 0, 0x00020000);
-  bf16* st = smem + (s & (Q_NST - 1)) * Q_STAGE;
-  bf16* dA = valid ? st + wave * 32 * Q_BK : smem + Q_SINK;
-  bf16* dB = valid ? st + (256 + wave * 32) * Q_BK : smem + Q_SINK;
-  const int step = valid ? 16 * Q_BK : 0;
-  const int kb = t * Q_BK * 2;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)dA, 16, aoff[0], kb, 0, 0);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dA + step), 16, aoff[1], kb, 0, 0);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)dB, 16, boff[0], kb, 0, 0);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dB + step), 16, boff[1], kb, 0, 0);
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(aux ? (const void*)aux : (const void*)o.A), (short)0, aux_rec,
-                                        0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(smem + aux_dst), 16, lane * 16, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000),
+                                           (lds_void*)lds, 16, voff, soff, 0, 0);
 }
+typedef unsigned g_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void g_store16(const void* base, int nrec, g_u4 v, int off) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000),
+                                         off, 0, 0);
+}
+
+template <int... I, typename F>
+__device__ __forceinline__ void g_for(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+
+// Epilogue parameters of one tile.
+struct GEpi {
+  const float* sbias;
+  const bf16* sbias16;           // bf16 bias (one of the two, or neither)
+  const bf16* R;
+  bf16* obase;                   // output rows n0.. of this tile (buffer descriptor base / size:
+  int orec;                      // descriptors stay out of structs and lambda signatures, which the
+                                 // host pass must also type-check)
+  int M, ldo, ldr;
+  float as, bs, rs;              // acc, bias and residual factors
+  long m0, n0, Npix;
+  int wm, wn, lane;
+};
 }  // namespace
 
-__global__ void __launch_bounds__(512, 1)
-gemm_pp2_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ O, const float* __restrict__ bias,
-           const bf16* __restrict__ R, int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha,
-           float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[Q_LDS];
+// Fragment pair (ii, 2jp), (ii, 2jp + 1) -> one 16-byte store per lane.  Before
+// the swap lane (fq, fr) holds channels fq*4..+3 of pixels P(2jp, fr) /
+// P(2jp+1, fr); v_permlane16_swap (odd rows of X <-> even rows of Y) leaves it
+// 8 consecutive channels ((fq >> 1) * 8..) of pixel P(2jp + (fq & 1), fr).
+template <int EPI, int WI, int WJ, int II, int JP>
+__device__ __forceinline__ void g_epi_pair(const f32x4 (&acc)[WI][WJ], const GEpi& e, float (&gs)[WI][2],
+                                           float (&gq)[WI][2], bool gn) {
+  const int fr = e.lane & 15, fq = e.lane >> 4;
+  const f32x4 x = acc[II][2 * JP], y = acc[II][2 * JP + 1];
+  const int cl = e.wm * 16 * WI + II * 16 + fq * 4;              // tile-local channel (pre-swap)
+  const long co = e.m0 + cl;
+  const long px = e.n0 + e.wn * 16 * WJ + 2 * JP * 16 + fr, py = px + 16;
+  float vx[4], vy[4];
+  if constexpr (EPI == 1) {
+    // d pre-activation = alpha * acc * dsilu(pre-activation)
+    bf16x4 rx = {}, ry = {};
+    if (co < e.M) {
+      if (px < e.Npix) rx = *reinterpret_cast<const bf16x4*>(e.R + px * e.ldr + co);
+      if (py < e.Npix) ry = *reinterpret_cast<const bf16x4*>(e.R + py * e.ldr + co);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      vx[k] = x[k] * e.as * dsiluf_((float)rx[k]);
+      vy[k] = y[k] * e.as * dsiluf_((float)ry[k]);
+    }
+  } else {
+    f32x4 cb = e.sbias ? *reinterpret_cast<const f32x4*>(e.sbias + cl) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (e.sbias16) {
+      const bf16x4 c4 = *reinterpret_cast<const bf16x4*>(e.sbias16 + cl);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cb[k] = (float)c4[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      vx[k] = x[k] * e.as + cb[k] * e.bs;
+      vy[k] = y[k] * e.as + cb[k] * e.bs;
+    }
+    if (e.R && co < e.M) {
+      if (px < e.Npix) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(e.R + px * e.ldr + co);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vx[k] += (float)r[k] * e.rs;
+      }
+      if (py < e.Npix) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(e.R + py * e.ldr + co);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vy[k] += (float)r[k] * e.rs;
+      }
+    }
+  }
+  bf16x4 ox, oy;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    ox[k] = (bf16)vx[k];
+    oy[k] = (bf16)vy[k];
+  }
+  if (gn) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float fx = (float)ox[k], fy = (float)oy[k];
+      gs[II][(2 * JP * 16) / 64] += fx + fy;
+      gq[II][(2 * JP * 16) / 64] += fx * fx + fy * fy;
+    }
+  }
+  typedef unsigned u2 __attribute__((ext_vector_type(2)));
+  const u2 ux = __builtin_bit_cast(u2, ox), uy = __builtin_bit_cast(u2, oy);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(ux[0], uy[0], false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(ux[1], uy[1], false, false);
+  const g_u4 v = {s0[0], s1[0], s0[1], s1[1]};
+  const int pl = e.wn * 16 * WJ + (2 * JP + (fq & 1)) * 16 + fr;    // tile-local pixel (post-swap)
+  const long cs = e.m0 + e.wm * 16 * WI + II * 16 + (fq >> 1) * 8;
+  const int off = cs < e.M ? (int)((long)pl * e.ldo + cs) * 2 : (int)0x80000000;
+  g_store16(e.obase, e.orec, v, off);
+  __builtin_amdgcn_sched_barrier(0);       // one pair at a time: bounded live registers
+}
+
+template <int WI, int WJ, int EPI>
+__global__ void __launch_bounds__(256, 1)
+gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ O, const float* __restrict__ bias,
+          const bf16* __restrict__ R, int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha,
+          float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw, int bbf) {
+  using C = GCfg<WI, WJ>;
+  __shared__ __attribute__((aligned(16))) bf16 smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wn = wave & 3;
+  const int wm = wave >> 1, wn = wave & 1;
   const int G = gridDim.x;
   int rb = blockIdx.x;
   {
@@ -407,159 +205,308 @@ gemm_pp2_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restr
   }
   const int ntiles = mt * nt;
   if (rb >= ntiles) return;
-  const int nk = K / Q_BK;
+  const int nk = K / G_BK;                   // even (K % 64 == 0), >= 4
 
-  // loader: 16-row DMA pieces, lane -> (row lane >> 2, slot lane & 3) holding chunk slot ^ f(row)
-  int aoff[2], boff[2];
+  // tile id -> (m tile, n tile): m fastest inside groups of gm m tiles
+  auto tile_mn = [&](int tl, int& mb_, int& nb_) {
+    const int full = mt / gm, span = gm * nt;
+    if (tl < full * span) {
+      const int g = tl / span, r = tl - g * span;
+      mb_ = g * gm + r % gm;
+      nb_ = r / gm;
+    } else {
+      const int rem = mt - full * gm, r = tl - full * span;
+      mb_ = full * gm + r % rem;
+      nb_ = r / rem;
+    }
+  };
+
+  // loader: per operand DA / DB pieces of 16 rows (64-byte rows, 4 lanes a
+  // row), lane -> (row lane >> 2, LDS slot lane & 3 holding chunk slot ^ f(row))
+  int aoff[C::DA], boff[C::DB];
   {
     const int chunk = (lane & 3) ^ (((lane >> 5) & 1) * 3);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int row = wave * 32 + q * 16 + (lane >> 2);
-      aoff[q] = (row * lda + chunk * 8) * 2;
-      boff[q] = (row * ldb + chunk * 8) * 2;
-    }
+    for (int q = 0; q < C::DA; ++q) aoff[q] = ((wave * (C::BM / 4) + q * 16 + (lane >> 2)) * lda + chunk * 8) * 2;
+#pragma unroll
+    for (int q = 0; q < C::DB; ++q) boff[q] = ((wave * (C::BN / 4) + q * 16 + (lane >> 2)) * ldb + chunk * 8) * 2;
   }
-  // loader cursor (runs 3 K-tiles ahead of the compute cursor)
-  int ltile = rb, lt = 0, lti = 0;
-  PPTile lops;
-  {
-    int mb, nb;
-    pp_tile(ltile, mt, nt, gm, mb, nb);
-    lops = pp_tile_ops(A, B, M, N, K, lda, ldb, mb, nb);
-  }
-  auto load_next = [&](int s) {
-    const bool valid = ltile < ntiles;
-    const float* as = nullptr;
-    int ar = 0, ad = Q_SINK;
-    if (valid && lt == 0 && bias && wave == 0) {
-      as = bias + lops.m0;
-      ar = (int)((M - lops.m0 < 256 ? M - lops.m0 : 256) * 4);
-      ad = Q_BIAS + (lti & 3) * 512;
-    }
-    q_issue(smem, lops, valid, lt, s, aoff, boff, wave, as, ar, ad);
-    if (valid && ++lt == nk) {
-      lt = 0;
-      ++lti;
-      ltile += G;
-      if (ltile < ntiles) {
-        int mb, nb;
-        pp_tile(ltile, mt, nt, gm, mb, nb);
-        lops = pp_tile_ops(A, B, M, N, K, lda, ldb, mb, nb);
-      }
+  const int fr = lane & 15, fq = lane >> 4;
+  // fragment read offsets (bf16 elements within a stage): fragment i is 16 rows further
+  const int fa0 = g_swz(wm * 16 * WI + fr, fq), fb0 = g_swz(C::BM + wn * 16 * WJ + fr, fq);
+
+  // loader cursor: tile ltile (descriptors lA / lB), byte offset lkb of its
+  // next K-tile; the following tile's descriptors are prepared when the
+  // cursor enters a tile
+  int ltile = rb, lkb = 0;
+  struct Ops {                               // one tile's operand panels: descriptor bases / sizes
+    const bf16* a;
+    const bf16* b;
+    int ra, rb;
+    long m0;
+  };
+  Ops lo, no;
+  auto ops_of = [&](int tl) -> Ops {
+    const bool v = tl < ntiles;
+    int mb_ = 0, nb_ = 0;
+    if (v) tile_mn(tl, mb_, nb_);
+    const long m0 = (long)mb_ * C::BM, n0 = (long)nb_ * C::BN;
+    const long arows = M - m0 < C::BM ? M - m0 : C::BM, brows = N - n0 < C::BN ? N - n0 : C::BN;
+    Ops o;
+    o.a = A + m0 * lda;
+    o.b = B + n0 * ldb;
+    o.ra = v ? (int)((arows - 1) * lda + K) * 2 : 0;
+    o.rb = v ? (int)((brows - 1) * ldb + K) * 2 : 0;
+    o.m0 = v ? m0 : -1;
+    return o;
+  };
+  lo = ops_of(ltile);
+  no = ops_of(ltile + G);
+  int lbslot = 0;                            // bias slot of the loader's tile (tile count & 3)
+  // bias of the loader's tile: wave 0 DMAs it (one instruction) with the tile's first K-tile
+  auto bias_dma = [&]() {
+    if (EPI == 0 && bias && wave == 0 && lo.m0 >= 0) {
+      const long m0 = lo.m0;
+      g_dma(bbf ? (const void*)(reinterpret_cast<const bf16*>(bias) + m0) : (const void*)(bias + m0),
+            (int)((M - m0 < C::BM ? M - m0 : C::BM) * (bbf ? 2 : 4)), smem + C::BIAS + lbslot * 512, lane * 16, 0);
     }
   };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int fr = lane & 15, fq = lane >> 4;
-
-  load_next(0);
-  load_next(1);
-  load_next(2);
-  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-  PP_BAR();
-  if (wr == 1) PP_BAR();                 // the M-half-1 waves trail by one barrier
-
-  int tile = rb, t = 0, ti = 0, mb, nb;
-  pp_tile(tile, mt, nt, gm, mb, nb);
-  for (int s = 0;; ++s) {
-    const bf16* st = smem + (s & (Q_NST - 1)) * Q_STAGE;
-    bf16x8 af[8], bq[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bq[j] = *reinterpret_cast<const bf16x8*>(st + q_swz(256 + wn * 64 + j * 16 + fr, fq));
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const bf16x8*>(st + q_swz(wr * 128 + i * 16 + fr, fq));
-    load_next(s + 3);
-    asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
-    PP_BAR();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bq[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    PP_BAR();
-    if (++t == nk) {
-      pp_epi(acc, bias ? reinterpret_cast<const float*>(smem + Q_BIAS + (ti & 3) * 512) : nullptr, O, R, M, N, ldo,
-             ldr, alpha, scale, (long)mb * 256, (long)nb * 256, wr, wn, lane, gnp, gn_groups, gn_hw);
-      tile += G;
-      if (tile >= ntiles) break;
-      ++ti;
-      t = 0;
-      pp_tile(tile, mt, nt, gm, mb, nb);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto advance = [&]() {                     // after the pieces of one K-tile
+    lkb += G_BK * 2;
+    if (lkb == K * 2) {
+      lkb = 0;
+      lo = no;
+      lbslot = (lbslot + 1) & 3;
+      ltile += G;
+      no = ops_of(ltile + G);
     }
+  };
+  auto dma = [&](int st, int d) {            // piece d (< DA: A, else B) into stage st
+    if (d < C::DA)
+      g_dma(lo.a, lo.ra, smem + st * C::STAGE + (wave * (C::BM / 4) + d * 16) * G_BK, aoff[d], lkb);
+    else
+      g_dma(lo.b, lo.rb, smem + st * C::STAGE + (C::BM + wave * (C::BN / 4) + (d - C::DA) * 16) * G_BK,
+            boff[d - C::DA], lkb);
+  };
+
+  bf16x8 a0[WI], b0[WJ], a1[WI], b1[WJ];
+  f32x4 acc[WI][WJ];
+  int tile = rb, ti = 0, mb, nb;
+  tile_mn(tile, mb, nb);
+  bias_dma();
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+#pragma unroll
+    for (int d = 0; d < C::ND; ++d) dma(k, d);
+    advance();
   }
-  if (wr == 0) PP_BAR();                 // balance the trailing group's extra barrier
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C::ND) : "memory");
+  G_BAR();
+#pragma unroll
+  for (int j = 0; j < WJ; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + fb0 + j * 512);
+#pragma unroll
+  for (int i = 0; i < WI; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(smem + fa0 + i * 512);
+
+  int s = 0;
+  // One K-tile at stream position s: wait (the tile's first two K-tiles also
+  // step over the previous epilogue's NS stores), barrier, then NM slots.
+  auto body = [&](auto first, bf16x8(&ca)[WI], bf16x8(&cb)[WJ], bf16x8(&na)[WI], bf16x8(&nbf)[WJ],
+                  bool after_epi) {
+    if (after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::ND + C::NS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::ND) : "memory");
+    G_BAR();
+    const bf16* sn = smem + ((s + 1) & 3) * C::STAGE;
+    const int ls = (s + 3) & 3;
+    g_for(std::make_integer_sequence<int, C::NM>{}, [&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr (decltype(first)::value) g_mma0(acc[k / WJ][k % WJ], ca[k / WJ], cb[k % WJ]);
+      else g_mma(acc[k / WJ][k % WJ], ca[k / WJ], cb[k % WJ]);
+      // fragment reads of s + 1 at slots r * NM / NR (B fragments first)
+      g_for(std::make_integer_sequence<int, C::NR>{}, [&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        if constexpr (r * C::NM / C::NR == k) {
+          if constexpr (r < WJ) nbf[r] = *reinterpret_cast<const bf16x8*>(sn + fb0 + r * 512);
+          else na[r - WJ] = *reinterpret_cast<const bf16x8*>(sn + fa0 + (r - WJ) * 512);
+        }
+      });
+      // DMA pieces of s + 3 at slots (2d + 1) * NM / (2 ND); the cursor moves after the last
+      g_for(std::make_integer_sequence<int, C::ND>{}, [&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        if constexpr ((2 * d + 1) * C::NM / (2 * C::ND) == k) {
+          dma(ls, d);
+          if constexpr (d == C::ND - 1) {
+            advance();
+            if (lkb == 0) bias_dma();
+          }
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    ++s;
+  };
+
+  while (true) {
+    body(std::integral_constant<bool, true>{}, a0, b0, a1, b1, ti > 0);
+    body(std::integral_constant<bool, false>{}, a1, b1, a0, b0, ti > 0);
+    for (int t = 2; t < nk; t += 2) {
+      body(std::integral_constant<bool, false>{}, a0, b0, a1, b1, false);
+      body(std::integral_constant<bool, false>{}, a1, b1, a0, b0, false);
+    }
+    // ---- epilogue of tile (mb, nb)
+    {
+      GEpi e;
+      const long m0 = (long)mb * C::BM, n0 = (long)nb * C::BN;
+      e.sbias = (EPI == 0 && bias && !bbf) ? reinterpret_cast<const float*>(smem + C::BIAS + (ti & 3) * 512) : nullptr;
+      e.sbias16 = (EPI == 0 && bias && bbf) ? smem + C::BIAS + (ti & 3) * 512 : nullptr;
+      e.R = R;
+      const long rows = N - n0 < C::BN ? N - n0 : C::BN;
+      e.obase = O + n0 * ldo;
+      e.orec = (int)(rows * ldo * 2);
+      e.M = M;
+      e.ldo = ldo;
+      e.ldr = ldr;
+      e.as = EPI == 1 ? alpha : alpha * scale;
+      e.bs = scale;
+      e.rs = scale;
+      e.m0 = m0;
+      e.n0 = n0;
+      e.Npix = N;
+      e.wm = wm;
+      e.wn = wn;
+      // an opaque copy of the lane id: the per-lane addressing below cannot be
+      // hoisted out of the tile loop (where it would occupy registers across
+      // the K loop)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      e.lane = ln;
+      float gs[WI][2], gq[WI][2];
+#pragma unroll
+      for (int i = 0; i < WI; ++i) gs[i][0] = gq[i][0] = gs[i][1] = gq[i][1] = 0.f;
+      const bool gn = EPI == 0 && gnp != nullptr;
+      g_for(std::make_integer_sequence<int, WI * WJ / 2>{}, [&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        g_epi_pair<EPI, WI, WJ, p / (WJ / 2), p % (WJ / 2)>(acc, e, gs, gq, gn);
+      });
+      if constexpr (EPI == 0 && WJ >= 4) {
+        if (gn) {
+          float s2[WI][WJ / 4], q2[WI][WJ / 4];
+#pragma unroll
+          for (int i = 0; i < WI; ++i)
+#pragma unroll
+            for (int h = 0; h < WJ / 4; ++h) {
+              s2[i][h] = gs[i][h];
+              q2[i][h] = gq[i][h];
+            }
+          gn_part_store<WI, WJ / 4>(s2, q2, ln, (int)(m0 + wm * 16 * WI), n0 + wn * 16 * WJ, M, gn_groups, gn_hw, N,
+                                    gnp);
+        }
+      }
+    }
+    tile += G;
+    if (tile >= ntiles) break;
+    ++ti;
+    tile_mn(tile, mb, nb);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the block ends
 }
 
-static int g_pp_ver = getenv("D3D_GEMM_V") ? atoi(getenv("D3D_GEMM_V")) : 1;
-static int g_pp_grid = getenv("D3D_GEMM_GRID") ? atoi(getenv("D3D_GEMM_GRID")) : 0;   // 0: one block per CU
-static int g_pp_gm = getenv("D3D_GEMM_GM") ? atoi(getenv("D3D_GEMM_GM")) : 4;
-static int pp_cus() {
+// ------------------------------------------------------------------ host ----
+static int g_cfg_force = 0;     // 0: by problem size; 8 / 4 / 2: force the WI = WJ tile
+static int g_gm = 8;
+static int g_grid = 0;          // 0: resident blocks on every CU
+static int g_cus() {
   static int n = 0;
   if (!n) {
     int dev = 0;
-    hipGetDevice(&dev);
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
   }
   return n;
 }
 
-// Tuning switches for in-process A/B (kernel version, tile-group width, grid);
-// a value <= 0 leaves the setting unchanged.
-D3D_API void d3d_gemm_tune(int ver, int gm, int grid) {
-  if (ver > 0) g_pp_ver = ver;
-  if (gm > 0) g_pp_gm = gm;
-  if (grid > 0) g_pp_grid = grid;
+// Tuning switches for in-process A/B (forced tile config, tile-group width,
+// grid); a value <= 0 leaves the setting unchanged (cfg 1 restores the size rule).
+D3D_API void d3d_gemm_tune(int cfg, int gm, int grid) {
+  if (cfg == 1) g_cfg_force = 0;
+  else if (cfg > 0) g_cfg_force = cfg;
+  if (gm > 0) g_gm = gm;
+  if (grid > 0) g_grid = grid;
 }
 
-// Shapes the kernel takes: K a multiple of 64, 16-byte aligned operand rows,
-// one block's operand rows addressable by 32-bit offsets.
+// Tile configuration for a problem: the 256 x 256 tile when it gives the chip
+// most of a wave of tiles, smaller tiles (more blocks per CU) otherwise.
+static int g_cfg(int M, int N) {
+  if (g_cfg_force) return g_cfg_force;
+  const long cus = g_cus();
+  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256);
+  if (t256 >= cus * 3 / 4) return 8;
+  const long t128 = (long)cdiv(M, 128) * cdiv(N, 128);
+  if (t128 >= cus) return 4;
+  return 2;
+}
+
+// Shapes the kernel takes: K a multiple of 64 and >= 128, M a multiple of 8,
+// 16-byte aligned operand rows, one tile's operand rows addressable by
+// 32-bit offsets.
 D3D_API int d3d_gemm_nt_ok(int M, int N, int K, int lda, int ldb) {
-  if (M <= 0 || N <= 0 || K <= 0 || K % PP_BK) return 0;
+  if (M <= 0 || N <= 0 || K < 128 || K % 64 || M % 8) return 0;
   if (lda % 8 || ldb % 8 || lda < K || ldb < K) return 0;
   if (256L * lda * 2 >= (1L << 31) || 256L * ldb * 2 >= (1L << 31)) return 0;
   return 1;
 }
 
-// gnp: optional fused GroupNorm partials of the output ([N / gn_hw][G][gn_hw /
-// 64] x (sum, sumsq), gn_part_store layout); needs M % 4 == 0, ldo % 4 == 0,
-// gn_hw % 64 == 0 and M / G in {4, 8, 16, 32}.
+template <int W, int EPI>
+static void g_launch(int G_, hipStream_t st, const void* A, const void* B, void* O, const float* bias, const void* R,
+                     int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, int mt, int nt,
+                     int gm, float* gnp, int G, int hw, int bbf) {
+  hipLaunchKernelGGL((gemm_fw_k<W, W, EPI>), dim3(G_), dim3(256), 0, st, (const bf16*)A, (const bf16*)B, (bf16*)O,
+                     bias, (const bf16*)R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, hw, bbf);
+}
+
+// epi 0: O = (alpha * A.B^T + bias + R) * scale (+ GroupNorm partials gnp:
+// [N / hw][G][hw / 64] x (sum, sumsq), gn_part_store layout; needs hw % 64 ==
+// 0 and M / G in {4, 8, 16, 32}); epi 1: O = alpha * A.B^T * dsilu(R).
+// bias_bf16: the bias vector is bf16 (else fp32).
+D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, int bias_bf16, const void* R, int M,
+                     int N, int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, float* gnp, int G,
+                     int hw, int epi, hipStream_t st) {
+  const float* bias = (const float*)bias_;
+  if (!d3d_gemm_nt_ok(M, N, K, lda, ldb)) return -1;
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)O) & 15) return -1;
+  if (ldo % 8 || ldo < M || (R && (ldr % 4 || ldr < M || ((uintptr_t)R & 7)))) return -1;
+  if (epi == 1 && (!R || bias || gnp)) return -1;
+  int W = g_cfg(M, N);
+  if (gnp) {
+    const int cg = G > 0 ? M / G : 0;
+    if (G <= 0 || M % G || hw <= 0 || hw % 64 || N % hw || !(cg == 4 || cg == 8 || cg == 16 || cg == 32)) return -1;
+    if (W == 2) W = 4;                         // the partials need whole 64-pixel parts per wave
+  }
+  const int BT = 32 * W;
+  if (256L * ldo * 2 >= (1L << 31)) return -1;
+  const int mt = cdiv(M, BT), nt = cdiv(N, BT);
+  const long tiles = (long)mt * nt;
+  if (tiles >= (1L << 31)) return -1;
+  const int per_cu = W == 8 ? 1 : W == 4 ? 2 : 4;
+  const int G_ = (int)std::min<long>(tiles, g_grid > 0 ? g_grid : (long)g_cus() * per_cu);
+  const int gm = std::max(1, std::min(mt, g_gm));
+#define G_CASE(W_, E_)                                                                                         \
+  if (W == W_ && epi == E_) {                                                                                  \
+    g_launch<W_, E_>(G_, st, A, B, O, bias, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, \
+                     hw, bias_bf16);                                                                           \
+    return (int)hipGetLastError();                                                                             \
+  }
+  G_CASE(8, 0) G_CASE(8, 1) G_CASE(4, 0) G_CASE(4, 1) G_CASE(2, 0) G_CASE(2, 1)
+#undef G_CASE
+  return -1;
+}
+
 D3D_API int d3d_gemm_nt_gn(const void* A, const void* B, void* O, const float* bias, const void* R, int M, int N,
                            int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, float* gnp, int G,
                            int hw, hipStream_t st) {
-  if (!d3d_gemm_nt_ok(M, N, K, lda, ldb)) return -1;
-  if (((uintptr_t)A | (uintptr_t)B) & 15) return -1;
-  if (gnp) {
-    const int cg = G > 0 ? M / G : 0;
-    if (G <= 0 || M % G || M % 4 || ldo % 4 || (R && ldr % 4) || hw <= 0 || hw % 64 || N % hw ||
-        !(cg == 4 || cg == 8 || cg == 16 || cg == 32))
-      return -1;
-  }
-  const int mt = cdiv(M, 256), nt = cdiv(N, 256);
-  const long tiles = (long)mt * nt;
-  if (tiles >= (1L << 31)) return -1;
-  const int G_ = (int)std::min<long>(tiles, g_pp_grid > 0 ? g_pp_grid : pp_cus());
-  const int gm = std::max(1, std::min(mt, g_pp_gm));
-  if (g_pp_ver == 2)
-    hipLaunchKernelGGL(gemm_pp2_k, dim3(G_), dim3(512), 0, st, (const bf16*)A, (const bf16*)B, (bf16*)O, bias,
-                       (const bf16*)R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, hw);
-  else
-    hipLaunchKernelGGL(gemm_pp_k, dim3(G_), dim3(512), 0, st, (const bf16*)A, (const bf16*)B, (bf16*)O, bias,
-                       (const bf16*)R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, hw);
-  return (int)hipGetLastError();
+  return d3d_gemm(A, B, O, bias, 0, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, gnp, G, hw, 0, st);
 }
 
 D3D_API int d3d_gemm_nt(const void* A, const void* B, void* O, const float* bias, const void* R, int M, int N, int K,
                         int lda, int ldb, int ldo, int ldr, float alpha, float scale, hipStream_t st) {
-  return d3d_gemm_nt_gn(A, B, O, bias, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, nullptr, 0, 0, st);
+  return d3d_gemm(A, B, O, bias, 0, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, nullptr, 0, 0, 0, st);
 }

@@ -183,7 +183,7 @@ def _desc_tensors(rows, blk):
     import numpy as np
     dt = np.dtype([("src", np.uint64), ("dst", np.uint64), ("OC", np.int32), ("IC", np.int32),
                    ("OCp", np.int32), ("ICp", np.int32), ("taps", np.int32), ("mode", np.int32),
-                   ("blk0", np.int32), ("ICs", np.int32)])
+                   ("blk0", np.int32), ("ICs", np.int32), ("ldd", np.int32), ("pad", np.int32)])
     arr = np.array(rows, dtype=dt)
     host = torch.from_numpy(arr.view(np.uint8).copy())
     counts = np.diff(np.append(arr["blk0"], blk))
@@ -206,7 +206,8 @@ def refresh_weights() -> None:
             OC, IC, OCp, ICp, taps, mode = desc[:6]
             src_off = desc[6] if len(desc) > 6 else 0        # byte offset (channel slice)
             ics = desc[7] if len(desc) > 7 else 0            # source IC stride
-            rows.append((p.data_ptr() + src_off, t.data_ptr(), OC, IC, OCp, ICp, taps, mode, blk, ics))
+            ldd = desc[8] if len(desc) > 8 else 0            # destination row stride (transposed cat)
+            rows.append((p.data_ptr() + src_off, t.data_ptr(), OC, IC, OCp, ICp, taps, mode, blk, ics, ldd, 0))
             blk += _pack_blocks(OC, OCp, ICp, mode)
         _DESC_TABLE[0], _DESC_TABLE[1] = _desc_tensors(rows, blk)
         _DESC_TABLE[2] = _REV[0]
@@ -285,6 +286,32 @@ def bf16_cat(params, kind: str) -> torch.Tensor:
         _cached(p, f"{kind}@{buf.data_ptr()}", build, (p.numel(), 1, 1, 1, 1, 2))
         off += r
     return buf if cols > 1 else buf.reshape(-1)
+
+
+def bf16_catT(params, kind: str) -> torch.Tensor:
+    """bf16 ``cat([p for p in params]).t()`` ([K, sum rows], the input-gradient
+    operand of a level-batched projection) kept as ONE persistent buffer:
+    every parameter's column block is a cache entry of the transposed pack
+    (mode 1, destination row stride = the total width), refreshed in the
+    batched repack after each optimizer step."""
+    key = (kind,) + tuple((p.data_ptr(), tuple(p.shape)) for p in params)
+    rows = [p.shape[0] for p in params]
+    K = params[0].shape[1]
+    S = sum(rows)
+    buf = _CATBUF.get(key)
+    if buf is None:
+        buf = torch.empty(K, S, dtype=BF16, device=params[0].device)
+        _CATBUF[key] = buf
+    off = 0
+    for p, r in zip(params, rows):
+        view = buf[:, off: off + r]
+
+        def build(p=p, view=view):
+            view.copy_(p.detach().t())
+            return view
+        _cached(p, f"{kind}@{buf.data_ptr()}", build, (r, K, r, K, 1, 1, 0, 0, S))
+        off += r
+    return buf
 
 
 def bf16_weight(w: torch.Tensor) -> torch.Tensor:
@@ -441,9 +468,6 @@ class _GroupNorm(torch.autograd.Function):
         return dx, dg, db, None, None, None, None
 
 
-import os as _os
-_CAT_FUSE = _os.environ.get("D3D_CAT_FUSE", "1")
-_CAT_PP = _os.environ.get("D3D_CAT_PP", "0") != "0"      # forward NIN skip of the virtual concat on gemm.hip only
 
 
 class _CatGNDense(torch.autograd.Function):
@@ -464,11 +488,13 @@ class _CatGNDense(torch.autograd.Function):
         OC = wb.shape[0]
         a2, b2 = a.reshape(-1, C1), b.reshape(-1, C2)
         C = C1 + C2
-        if (_LIN_PP or _CAT_PP) and _pp_ok(OC, a2.shape[0], C1, C, C1) and _pp_ok(OC, b2.shape[0], C2, C, C2):
+        if _gemm_ok(OC, a2.shape[0], C1, C, C1) and _gemm_ok(OC, b2.shape[0], C2, C, C2):
+            # two GEMMs over the halves; the second accumulates through its residual epilogue
             skip = torch.empty(a2.shape[0], OC, dtype=BF16, device=a.device)
             gemm_nt(wb, a2, skip, OC, a2.shape[0], C1, C, C1, OC, bias=db.detach() if db is not None else None)
             gemm_nt(wb[:, C1:], b2, skip, OC, b2.shape[0], C2, C, C2, OC, res=skip)
         else:
+            _fallback("cat_gn_silu_dense", f"C1={C1} C2={C2} OC={OC} (library GEMM)")
             skip = torch.addmm(bf16_weight(db), a2, wb[:, :C1].t()) if db is not None else \
                 torch.mm(a2, wb[:, :C1].t())
             skip.addmm_(b2, wb[:, C1:].t())
@@ -493,7 +519,7 @@ class _CatGNDense(torch.autograd.Function):
         g2 = g.reshape(-1, OC)
         OCp = _up(OC, 64)
         rows_ = g2.shape[0]
-        if _LIN_PP and g2.is_contiguous() and _pp_ok(C1, rows_, OC, OCp, OC) and _pp_ok(C2, rows_, OC, OCp, OC):
+        if g2.is_contiguous() and _gemm_ok(C1, rows_, OC, OCp, OC) and _gemm_ok(C2, rows_, OC, OCp, OC):
             pk = packed_weight(dw, True, 1)                      # [ICp][OCp]: rows = input channels
             d2a, d2b = da.view(-1, C1), db_in.view(-1, C2)
             gemm_nt(pk, g2, d2a, C1, rows_, OC, OCp, OC, C1, res=d2a)
@@ -542,7 +568,7 @@ class _CatGNDense(torch.autograd.Function):
 def cat_gn_silu_dense(a, b, gw, gb, dw, db, groups=32, eps=1e-5):
     _need_bf16(a, b)
     C1, C2 = a.shape[-1], b.shape[-1]
-    if C1 % 8 or C2 % 8 or (C1 + C2) // groups > 1024 or _CAT_FUSE == "0":
+    if C1 % 8 or C2 % 8 or (C1 + C2) // groups > 1024:
         x = torch.cat([a, b], -1)
         return group_norm(x, gw, gb, groups, eps, True), linear(x, dw, db)
     return _CatGNDense.apply(a, b, gw, gb, dw, db, groups, eps)
@@ -934,68 +960,36 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         return torch.mm(a, b).float()
 
 
-# Dense-layer dispatch.  In isolation the MFMA implicit-GEMM kernels (taps =
-# 1) beat hipBLASLt on the small per-pixel GEMMs of the small-batch step (the
-# attention projections / 1x1 convs at 16 examples per GPU: 1-4 GFLOP, 16 vs
-# 24 us, profiles/kbench_linear_r2.txt) and fuse the residual / scale
-# epilogue -- but inside the replayed training step they measured SLOWER
-# (bs16 31.4 -> 32.2 ms for the input-gradient GEMMs, 32.2 -> 33.1 ms for the
-# forward ones, profiles/ab_linear_dispatch_r2.txt): off by default (0),
-# enabled per GEMM size by D3D_LIN_HIP_FWD_FLOP / D3D_LIN_HIP_DGRAD_FLOP.
-_LIN_HIP_FWD_FLOP = float(os.environ.get("D3D_LIN_HIP_FWD_FLOP", "0"))
-_LIN_HIP_DGRAD_FLOP = float(os.environ.get("D3D_LIN_HIP_DGRAD_FLOP", "0"))
-
-
-# Hand-written ping-pong MFMA GEMM (ops/csrc/gemm.hip) for the dense layers:
-# "1" (default) routes the attention projections / NIN skips through it (fused
-# bias / residual / scale epilogue); the level-batched FiLM projections stay on
-# hipBLASLt unless D3D_FILM_PP=1 (kbench: 78-89 % of hipBLASLt on those,
-# profiles/kbench_gemm_pp_r2.txt).
-_LIN_PP = os.environ.get("D3D_LIN_PP", "0") != "0"
-_FILM_PP = os.environ.get("D3D_FILM_PP", "0") != "0"
-
-
-_PP_MIN_TILES = int(os.environ.get("D3D_LIN_PP_MIN_TILES", "128"))
-
-
-def _pp_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
-    # 256 x 256 output tiles: a GEMM of fewer tiles than ~half the CUs leaves
-    # the chip idle (the small per-GPU-batch layers stay on hipBLASLt's
-    # smaller tiles)
-    tiles = -(-M // 256) * -(-N // 256)
-    return tiles >= _PP_MIN_TILES and bool(_lib.d3d_gemm_nt_ok(M, N, K, lda, ldb))
+def _gemm_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
+    """Shapes csrc/gemm.hip takes (K % 64 == 0 and >= 128, M % 8 == 0, 16-byte rows)."""
+    return bool(_lib.d3d_gemm_nt_ok(M, N, K, lda, ldb))
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, M: int, N: int, K: int, lda: int, ldb: int, ldo: int,
             bias: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None, ldr: int = 0,
             alpha: float = 1.0, scale: float = 1.0, gnp: Optional[torch.Tensor] = None, gn_groups: int = 0,
-            gn_hw: int = 0) -> torch.Tensor:
-    """out[n][m] = (alpha * sum_k a[m][k] b[n][k] + bias[m] + res[n][m]) * scale
-    on the ping-pong MFMA kernel (bf16 operands / output, fp32 bias); ``gnp``:
-    the output's GroupNorm partial statistics (groups ``gn_groups`` over images
-    of ``gn_hw`` rows) from the same epilogue."""
+            gn_hw: int = 0, dsilu_of: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[n][m] = (alpha * sum_k a[m][k] b[n][k] + bias[m] + res[n][m]) * scale on
+    the gfx950 GEMM (csrc/gemm.hip; bf16 operands / output, fp32 or bf16 bias).
+    ``gnp``: the output's GroupNorm partial statistics (groups ``gn_groups``
+    over images of ``gn_hw`` rows) from the same epilogue.  ``dsilu_of``
+    (row stride ``ldr``): instead out = alpha * acc * dsilu(dsilu_of[n][m]) --
+    an input gradient through a SiLU whose pre-activation is dsilu_of."""
     if bias is not None:
-        assert bias.dtype == F32 and bias.is_contiguous()
-    _chk(_lib.d3d_gemm_nt_gn(a.data_ptr(), b.data_ptr(), out.data_ptr(), _ptr(bias), _ptr(res), M, N, K, lda, ldb,
-                             ldo, ldr or ldo, float(alpha), float(scale), _ptr(gnp), int(gn_groups), int(gn_hw),
-                             _st()), "gemm_nt")
+        assert bias.dtype in (F32, BF16) and bias.is_contiguous()
+    epi = 0 if dsilu_of is None else 1
+    r = res if dsilu_of is None else dsilu_of
+    _chk(_lib.d3d_gemm(a.data_ptr(), b.data_ptr(), out.data_ptr(), _ptr(bias),
+                       int(bias is not None and bias.dtype == BF16), _ptr(r), M, N, K, lda, ldb, ldo, ldr or ldo,
+                       float(alpha), float(scale), _ptr(gnp), int(gn_groups), int(gn_hw), epi, _st()), "gemm")
     return out
 
 
-def _lin_hip_fwd(P: int, IC: int, OC: int) -> bool:
-    return _LIN_HIP_FWD_FLOP > 0 and IC % 8 == 0 and OC % 8 == 0 and OC >= 64 and 2.0 * P * IC * OC <= _LIN_HIP_FWD_FLOP
-
-
-def _lin_hip_dgrad(P: int, IC: int, OC: int) -> bool:
-    # the input-gradient GEMM reduces over OC: short reductions (OC < IC)
-    # leave the tiled kernel prologue-bound
-    return _LIN_HIP_DGRAD_FLOP > 0 and IC % 8 == 0 and OC % 8 == 0 and IC >= 64 and OC >= IC and 2.0 * P * IC * OC <= _LIN_HIP_DGRAD_FLOP
-
-
 class _Linear(torch.autograd.Function):
-    """Per-pixel dense layer: hand-written MFMA GEMM (conv kernels, taps=1)
-    with the bias / residual / scale epilogue fused for small problems, the
-    hipBLASLt library GEMM + a fused HIP epilogue kernel for large ones."""
+    """Per-pixel dense layer on the gfx950 GEMM: forward with the bias /
+    residual / scale (+ GroupNorm statistics) epilogue, input gradient against
+    the cached transposed weight, weight gradient on the split-K MFMA kernel
+    (the reduction runs over every pixel of the batch)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, residual, out_scale, res_slot=None, in_slot=None, gn=None):
@@ -1004,48 +998,25 @@ class _Linear(torch.autograd.Function):
         P, IC = x2.shape
         OC = weight.shape[0]
         L = shp[1] if len(shp) == 3 else 0
-        gnp = None
-        if gn is not None and L % 64 == 0 and L and OC % 4 == 0 and OC % gn["groups"] == 0 and \
-                OC // gn["groups"] in (4, 8, 16, 32):
-            gnp = torch.empty((P // L) * gn["groups"] * (L // 64) * 2, dtype=F32, device=x.device)
-        if _LIN_PP and (gn is None or gnp is not None) and x2.is_contiguous() and _pp_ok(OC, P, IC, IC, IC):
-            wb = bf16_weight(weight)
+        r = residual.reshape(P, OC).contiguous() if residual is not None else None
+        if x2.is_contiguous() and _gemm_ok(OC, P, IC, IC, IC):
+            gnp = None
+            if gn is not None and L and L % 64 == 0 and OC % gn["groups"] == 0 and \
+                    OC // gn["groups"] in (4, 8, 16, 32):
+                gnp = torch.empty((P // L) * gn["groups"] * (L // 64) * 2, dtype=F32, device=x.device)
             y = torch.empty(P, OC, dtype=BF16, device=x.device)
-            r = residual.reshape(P, OC).contiguous() if residual is not None else None
-            gemm_nt(wb, x2, y, OC, P, IC, IC, IC, OC, bias=bias.detach() if bias is not None else None, res=r,
-                    scale=float(out_scale), gnp=gnp, gn_groups=gn["groups"] if gnp is not None else 0, gn_hw=L)
+            gemm_nt(bf16_weight(weight), x2, y, OC, P, IC, IC, IC, OC,
+                    bias=bias.detach() if bias is not None else None, res=r, scale=float(out_scale), gnp=gnp,
+                    gn_groups=gn["groups"] if gnp is not None else 0, gn_hw=L)
             if gnp is not None:
                 gn["part"] = (gnp, L // 64)
-        elif _lin_hip_fwd(P, IC, OC):
-            x2 = x2.contiguous()
-            y = torch.empty(P, OC, dtype=BF16, device=x.device)
-            r = residual.reshape(P, OC).contiguous() if residual is not None else None
-            _conv_fwd(x2, packed_weight(weight, False, 1), bias, None, r, y, P, 1, 1, IC, _up(IC, 64), 1, 1, OC, OC,
-                      1, False, float(out_scale), 0, 1)
-            wb = None
         else:
+            _fallback("linear", f"P={P} IC={IC} OC={OC} (library GEMM)")
             wb = bf16_weight(weight)
-            if bias is not None:
-                y = torch.addmm(bf16_weight(bias), x2, wb.t())
-            else:
-                y = torch.mm(x2, wb.t())
+            y = torch.addmm(bf16_weight(bias), x2, wb.t()) if bias is not None else torch.mm(x2, wb.t())
             if residual is not None or out_scale != 1.0:
-                r = residual.reshape(y.shape).contiguous() if residual is not None else None
-                done = False
-                if gn is not None and len(shp) == 3:
-                    # the epilogue also emits the consuming GroupNorm's partials
-                    L, G = shp[1], gn["groups"]
-                    gnp = torch.empty((P // L) * G * (L // 64) * 2 if L % 64 == 0 else 0, dtype=F32,
-                                      device=x.device)
-                    rc = _lib.d3d_add_scale_gn(y.data_ptr(), _ptr(r), y.data_ptr(), float(out_scale), P, OC, L, G,
-                                               gnp.data_ptr(), _st()) if gnp.numel() else -1
-                    if rc >= 0:
-                        _chk(rc, "add_scale_gn")
-                        gn["part"] = (gnp, L // 64)
-                        done = True
-                if not done:
-                    _chk(_lib.d3d_add_scale(y.data_ptr(), _ptr(r), y.data_ptr(), float(out_scale), y.numel(),
-                                            _st()), "add_scale")
+                _chk(_lib.d3d_add_scale(y.data_ptr(), _ptr(r), y.data_ptr(), float(out_scale), y.numel(), _st()),
+                     "add_scale")
         ctx.save_for_backward(x2, weight)
         ctx.cfg = (shp, out_scale, residual is not None, bias is not None)
         ctx.bias_param = bias
@@ -1081,20 +1052,14 @@ class _Linear(torch.autograd.Function):
         elif lazy:
             ks = scale
         if ctx.needs_input_grad[0]:
-            pk = packed_weight(weight, True, 1) if (_LIN_PP and g.is_contiguous()) else None
-            if pk is not None and _pp_ok(IC, rows, OC, _up(OC, 64), OC):
+            OCp = _up(OC, 64)
+            if g.is_contiguous() and _gemm_ok(IC, rows, OC, OCp, OC):
                 dx = torch.empty(rows, IC, dtype=g.dtype, device=g.device)
-                gemm_nt(pk, g, dx, IC, rows, OC, _up(OC, 64), OC, IC, alpha=float(ks))
-            elif _lin_hip_dgrad(rows, IC, OC):
-                gc = g.contiguous()
-                dx = torch.empty(rows, IC, dtype=g.dtype, device=g.device)
-                _conv_fwd(gc, packed_weight(weight, True, 1), None, None, None, dx, rows, 1, 1, OC, _up(OC, 64), 1, 1,
-                          IC, IC, 1, True, float(ks), 0, 1)
-            elif ks != 1.0:
+                gemm_nt(packed_weight(weight, True, 1), g, dx, IC, rows, OC, OCp, OC, IC, alpha=float(ks))
+            else:
+                _fallback("linear dgrad", f"P={rows} IC={IC} OC={OC} (library GEMM)")
                 dx = torch.empty(rows, IC, dtype=g.dtype, device=g.device).addmm_(g, bf16_weight(weight), beta=0.0,
                                                                                    alpha=ks)
-            else:
-                dx = torch.mm(g, bf16_weight(weight))
             dx = dx.reshape(shp)
         else:
             dx = None
@@ -1134,15 +1099,11 @@ class _Linear(torch.autograd.Function):
 # gradients (no separate sum pass).  hipBLASLt's own choice for the single
 # mixed-precision GEMM runs 640-950 TF/s on these shapes; 8 (4 for the
 # smallest level) slabs run 910-1160 TF/s (profiles/film_wgrad_split_r2.txt).
-# D3D_FILM_WGRAD_SPLIT: 0 = auto by row count, 1 = off, else the slab count.
-_FILM_WGRAD_SPLIT = int(os.environ.get("D3D_FILM_WGRAD_SPLIT", "0"))
-
-
 def _film_wgrad_product(dy: torch.Tensor, x2: torch.Tensor):
     """``dy^T @ x2`` in fp32 as ``nsl`` stacked partial products."""
     rows, S = dy.shape
     K = x2.shape[1]
-    nsl = _FILM_WGRAD_SPLIT or (8 if rows >= 32768 else 4 if rows >= 8192 else 1)
+    nsl = 8 if rows >= 32768 else 4 if rows >= 8192 else 1
     if nsl > 1 and rows % nsl == 0:
         try:
             a = dy.view(nsl, rows // nsl, S).transpose(1, 2)
@@ -1168,30 +1129,40 @@ class _FiLMSlot:
 
 class _FiLMBatch(torch.autograd.Function):
     """All FiLM projections that read one level's conditioning embedding
-    (`xunet.py:74-87`, one ``nn.Linear(emb_ch, 2C)`` per ResnetBlock) as ONE
-    GEMM ``[P, emb_ch] x [emb_ch, sum 2C_i]``: the 1024-channel embedding is
-    read once instead of once per block, and in backward the input gradient is
-    one GEMM over the concatenated d(scale|shift) -- no per-block [P, 1024]
-    partial products and no autograd accumulation adds.  The weight gradient
-    is one split-K MFMA launch whose reduction scatters rows into each block's
-    parameter gradient."""
+    (`xunet.py:74-87`, ``dense(silu(emb))`` per ResnetBlock) as ONE GEMM
+    ``silu(e)[P, emb_ch] x [emb_ch, sum 2C_i]``: the 1024-channel embedding is
+    read once instead of once per block.  Backward: the input gradient is one
+    GEMM over the concatenated d(scale|shift) whose epilogue applies the SiLU
+    derivative of the pre-activation ``e`` (no separate dsilu pass, no
+    d(silu(e)) tensor); the weight gradient is one split-K launch whose
+    reduction scatters rows into each block's parameter gradient."""
 
     @staticmethod
-    def forward(ctx, semb, slot, n, *wb):
+    def forward(ctx, e, slot, n, *wb):
         Ws, Bs = wb[:n], wb[n:]
-        shp = semb.shape
+        shp = e.shape
         K = shp[-1]
-        x2 = semb.reshape(-1, K)
+        e2 = e.reshape(-1, K)
+        P = e2.shape[0]
+        x2 = torch.empty_like(e2)                           # silu(e): the GEMM operand, kept for the wgrad
+        _chk(_lib.d3d_silu(e2.data_ptr(), x2.data_ptr(), e2.numel(), _st()), "silu")
         wcat = bf16_cat(Ws, "filmW")
         bcat = bf16_cat(list(Bs), "filmB")
-        y = torch.addmm(bcat, x2, wcat.t()).view(*shp[:-1], wcat.shape[0])
-        ctx.save_for_backward(x2, wcat)
+        S = wcat.shape[0]
+        y = torch.empty(P, S, dtype=BF16, device=e.device)
+        if _gemm_ok(S, P, K, K, K):
+            gemm_nt(wcat, x2, y, S, P, K, K, K, S, bias=bcat)
+        else:
+            _fallback("film_batch", f"P={P} K={K} S={S} (library GEMM)")
+            torch.addmm(bcat, x2, wcat.t(), out=y)
+        ctx.save_for_backward(x2, e2)
         ctx.n, ctx.slot, ctx.shp = n, slot, shp
         ctx.params = (Ws, Bs)
         ctx.widths = [w.shape[0] for w in Ws]
         for i, (w, b) in enumerate(zip(Ws, Bs)):
             SINK.use(w, ctx.needs_input_grad[3 + i])
             SINK.use(b, ctx.needs_input_grad[3 + n + i])
+        y = y.view(*shp[:-1], S)
         outs, off = [], 0
         for wd in ctx.widths:
             outs.append(y[..., off: off + wd])
@@ -1200,9 +1171,10 @@ class _FiLMBatch(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *gs):
-        x2, wcat = ctx.saved_tensors
+        x2, e2 = ctx.saved_tensors
         n, slot, shp = ctx.n, ctx.slot, ctx.shp
-        S = wcat.shape[0]
+        Ws, Bs = ctx.params
+        S = sum(ctx.widths)
         buf = slot.buf
         offs = [0]
         for wd in ctx.widths:
@@ -1224,9 +1196,18 @@ class _FiLMBatch(torch.autograd.Function):
                 if g is not None:
                     dy[:, o: o + wd].copy_(g.reshape(-1, wd))
         slot.buf = None
-        dx = torch.mm(dy, wcat).view(shp) if ctx.needs_input_grad[0] else None
-        Ws, Bs = ctx.params
         rows, K = x2.shape
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(rows, K, dtype=BF16, device=x2.device)
+            if _gemm_ok(K, rows, S, S, S):
+                # d e = (dy @ Wcat) * dsilu(e), the SiLU derivative in the epilogue
+                gemm_nt(bf16_catT(Ws, "filmWT"), dy, dx, K, rows, S, S, S, K, dsilu_of=e2, ldr=K)
+            else:
+                _fallback("film_batch dgrad", f"P={rows} K={K} S={S} (library GEMM)")
+                ds = torch.mm(dy, bf16_cat(Ws, "filmW"))
+                _chk(_lib.d3d_dsilu(e2.data_ptr(), ds.data_ptr(), dx.data_ptr(), dx.numel(), _st()), "dsilu")
+            dx = dx.view(shp)
         grads_w, grads_b = [None] * n, [None] * n
         need_w = any(ctx.needs_input_grad[3: 3 + n])
         if need_w:
@@ -1243,10 +1224,9 @@ class _FiLMBatch(torch.autograd.Function):
                 bd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tb])
                 if _FILM_WGRAD == "blas" or (_FILM_WGRAD == "auto" and shp[0] > 32):
                     # wide FiLM weight gradients ([S, 1024] over every pixel of the
-                    # level) run 1.4-1.6x faster on hipBLASLt (850-880 TF/s,
-                    # profiles/kbench_lin_v2.jsonl) than on the split-K MFMA
-                    # kernel; its fp32 [S, K] product and the bias column sums are
-                    # then scattered into the parameters' gradients in one launch
+                    # level): the fp32 [S, K] product (stacked split-K slabs) and
+                    # the bias column sums are scattered into the parameters'
+                    # gradients in one launch
                     prod, nsl = _film_wgrad_product(dy, x2)
                     nimg = 64 if rows % 64 == 0 else 1
                     _, bsum = _chansum(dy.view(nimg, rows // nimg, 1, S), False)
@@ -1267,17 +1247,19 @@ class _FiLMBatch(torch.autograd.Function):
         return (dx, None, None, *grads_w, *grads_b)
 
 
-def film_batch(semb, weights, biases):
-    """Level-batched FiLM projections -> tuple of ``[N,H,W,2C_i]`` modulations
-    (column slices of one GEMM output; GN-FiLM reads them strided)."""
-    _need_bf16(semb)
-    K = semb.shape[-1]
+def film_batch(emb, weights, biases):
+    """Level-batched FiLM projections ``dense_i(silu(emb))`` of the per-level
+    pre-activation embedding -> tuple of ``[N,H,W,2C_i]`` modulations (column
+    slices of one GEMM output; GN-FiLM reads them strided)."""
+    _need_bf16(emb)
+    K = emb.shape[-1]
     widths = [w.shape[0] for w in weights]
     if K % 8 or any(wd % 8 for wd in widths) or len(weights) > 16:
         _fallback("film_batch", f"K={K} widths={widths}")
-        return tuple(linear(semb, w, b) for w, b in zip(weights, biases))
-    slot = _FiLMSlot(semb.shape[:-1], sum(widths), semb.device)
-    outs = _FiLMBatch.apply(semb.contiguous(), slot, len(weights), *weights, *biases)
+        se = silu(emb)
+        return tuple(linear(se, w, b) for w, b in zip(weights, biases))
+    slot = _FiLMSlot(emb.shape[:-1], sum(widths), emb.device)
+    outs = _FiLMBatch.apply(emb.contiguous(), slot, len(weights), *weights, *biases)
     off = 0
     for o, wd in zip(outs, widths):
         o._d3d_slot = (slot, off)
@@ -1289,13 +1271,11 @@ _EPI_GN_STATS = os.environ.get("D3D_EPI_GN_STATS", "1") != "0"     # A/B switch 
 
 
 def linear(x, weight, bias, residual=None, out_scale=1.0, res_slot=None, in_slot=None, gn_groups=0):
-    """Per-pixel dense layer.  Forward and input-gradient are plain GEMMs on
-    hipBLASLt (≈1 PF/s on these shapes); the weight gradient -- a GEMM whose
-    reduction runs over every pixel of the batch (K up to 5e5), where
-    hipBLASLt drops to 45-240 TF/s -- uses the split-K MFMA kernel, and the
-    bias / residual epilogues are fused HIP kernels.  ``gn_groups`` (x of
-    shape [N, L, C] with a residual / scale epilogue): the epilogue also emits
-    the partial statistics of the GroupNorm that reads the output (attached as
+    """Per-pixel dense layer on the gfx950 GEMM (fused bias / residual / scale
+    epilogue; input gradient on the same kernel, weight gradient -- a
+    reduction over every pixel of the batch -- on the split-K MFMA kernel).
+    ``gn_groups`` (x of shape [N, L, C]): the epilogue also emits the partial
+    statistics of the GroupNorm that reads the output (attached as
     ``_d3d_gnpart``; see :func:`carry_gn_stats` across reshapes)."""
     _need_bf16(x, residual)
     gn = {"groups": int(gn_groups)} if (gn_groups and _EPI_GN_STATS) else None
@@ -1657,7 +1637,8 @@ def _fused_tables(flat, only=None, key=None, take_unowned=True):
         OC, IC, OCp, ICp, taps, mode = desc[:6]
         src_off = desc[6] if len(desc) > 6 else 0
         ics = desc[7] if len(desc) > 7 else 0
-        rest_rows.append((p.data_ptr() + src_off, t.data_ptr(), OC, IC, OCp, ICp, taps, mode, rest_blk, ics))
+        ldd = desc[8] if len(desc) > 8 else 0
+        rest_rows.append((p.data_ptr() + src_off, t.data_ptr(), OC, IC, OCp, ICp, taps, mode, rest_blk, ics, ldd, 0))
         rest_blk += _pack_blocks(OC, OCp, ICp, mode)
     rd, rm = _desc_tensors(rest_rows, rest_blk) if rest_rows else (None, None)
     ent = {"rev": _REV[0], "flat": flat, "tiles": (tt, tb, tblk), "ranges": (rt, rb, rblk),

@@ -210,9 +210,11 @@ def ray_posenc(R: torch.Tensor, t: torch.Tensor, K: torch.Tensor, H: int, W: int
     return emb.reshape(B * 2, H, W, emb.shape[-1])
 
 
-def film_batch(semb, weights, biases):
-    """Level-batched FiLM projections (oracle): one linear over the
-    concatenated weights, split into per-block ``[.., 2C_i]`` modulations."""
+def film_batch(emb, weights, biases):
+    """Level-batched FiLM projections (oracle): ``silu(emb)`` through one linear
+    over the concatenated weights, split into per-block ``[.., 2C_i]``
+    modulations (`xunet.py:84-87`)."""
+    semb = F.silu(emb)
     y = F.linear(semb, torch.cat([w.to(semb.dtype) for w in weights], 0),
                  torch.cat([b.to(semb.dtype) for b in biases], 0))
     return tuple(torch.split(y, [w.shape[0] for w in weights], dim=-1))

@@ -242,54 +242,108 @@ def test_conv3x3_wgrad_w8(H, N, Hh, W, Ci, Co, s, res, rb, scale):
         H.set_wgrad_impl(os.environ.get("D3D_WGRAD_IMPL", "w8"))
 
 
+@pytest.mark.parametrize("cfg", [8, 4, 2])
 @pytest.mark.parametrize("M,N,K,lda,ldb,ldo,bias,res,alpha,scale", [
-    (256, 256, 64, 64, 64, 256, False, False, 1.0, 1.0),
+    (256, 256, 128, 128, 128, 256, False, False, 1.0, 1.0),
     (768, 8192, 256, 256, 256, 768, True, False, 1.0, 1.0),
     (200, 1000, 192, 200, 256, 208, True, True, 0.5, 0.7),        # M / N tails, padded rows
     (1024, 4096, 4608, 4608, 4608, 1024, False, False, 1.0, 1.0),  # long reduction
     (128, 70000, 256, 256, 256, 128, True, True, 1.0, 0.25),       # M < tile, many tiles per block
     (4608, 2048, 1024, 1024, 1024, 4608, True, False, 1.0, 1.0),
 ])
-def test_gemm_nt(H, M, N, K, lda, ldb, ldo, bias, res, alpha, scale):
-    """Ping-pong MFMA GEMM against the fp32 product (bias / residual / alpha /
-    scale epilogue, tails in M and N, row strides wider than K)."""
-    torch.manual_seed(11)
-    a = torch.randn(M, lda, device=DEV).to(BF)
-    b = torch.randn(N, ldb, device=DEV).to(BF)
-    bb = torch.randn(M, device=DEV) if bias else None
-    r = torch.randn(N, ldo, device=DEV).to(BF) if res else None
-    out = torch.full((N, ldo), 7.0, device=DEV).to(BF)
-    H.gemm_nt(a, b, out, M, N, K, lda, ldb, ldo, bias=bb, res=r, alpha=alpha, scale=scale)
-    ref = a[:, :K].float() @ b[:, :K].float().t() * alpha
-    ref = ref.t()
-    if bias:
-        ref = ref + bb
-    if res:
-        ref = ref + r[:, :M].float()
-    ref = ref * scale
-    assert rel(out[:, :M], ref) < 1e-2
-    if ldo > M:
-        assert (out[:, M:] == 7.0).all()          # columns past M untouched
+def test_gemm_nt(H, cfg, M, N, K, lda, ldb, ldo, bias, res, alpha, scale):
+    """gfx950 GEMM (every tile configuration) against the fp32 product: bias /
+    residual / alpha / scale epilogue, tails in M and N, row strides wider
+    than K, output rows wider than M left untouched."""
+    H._lib.d3d_gemm_tune(cfg, 0, 0)
+    try:
+        torch.manual_seed(11)
+        a = torch.randn(M, lda, device=DEV).to(BF)
+        b = torch.randn(N, ldb, device=DEV).to(BF)
+        bb = torch.randn(M, device=DEV) if bias else None
+        r = torch.randn(N, ldo, device=DEV).to(BF) if res else None
+        out = torch.full((N, ldo), 7.0, device=DEV).to(BF)
+        H.gemm_nt(a, b, out, M, N, K, lda, ldb, ldo, bias=bb, res=r, alpha=alpha, scale=scale)
+        ref = a[:, :K].float() @ b[:, :K].float().t() * alpha
+        ref = ref.t()
+        if bias:
+            ref = ref + bb
+        if res:
+            ref = ref + r[:, :M].float()
+        ref = ref * scale
+        assert rel(out[:, :M], ref) < 1e-2
+        if ldo > M:
+            assert (out[:, M:] == 7.0).all()          # columns past M untouched
+    finally:
+        H._lib.d3d_gemm_tune(1, 0, 0)
 
 
-@pytest.mark.parametrize("impl", ["pp", "mfma", "blas"])
+@pytest.mark.parametrize("cfg", [8, 4, 2])
+def test_gemm_bf16_bias_and_dsilu_epilogue(H, cfg):
+    """bf16 bias, the in-place residual (out == res) of the virtual-concat
+    skip, and the dsilu epilogue (FiLM input gradient) against fp32."""
+    H._lib.d3d_gemm_tune(cfg, 0, 0)
+    try:
+        torch.manual_seed(3)
+        M, N, K = 1024, 3000, 2048
+        a = torch.randn(M, K, device=DEV).to(BF)
+        b = torch.randn(N, K, device=DEV).to(BF)
+        bb = torch.randn(M, device=DEV).to(BF)
+        out = torch.empty(N, M, device=DEV, dtype=BF)
+        H.gemm_nt(a, b, out, M, N, K, K, K, M, bias=bb)
+        ref = (b.float() @ a.float().t()) + bb.float()
+        assert rel(out, ref) < 1e-2
+        keep = out.clone()
+        H.gemm_nt(a, b, out, M, N, K, K, K, M, res=out)            # accumulate in place
+        assert rel(out, keep.float() + b.float() @ a.float().t()) < 1e-2
+        e = torch.randn(N, M, device=DEV).to(BF) * 3
+        H.gemm_nt(a, b, out, M, N, K, K, K, M, dsilu_of=e, ldr=M, alpha=0.5)
+        s = torch.sigmoid(e.float())
+        ref = 0.5 * (b.float() @ a.float().t()) * s * (1 + e.float() * (1 - s))
+        assert rel(out, ref) < 1e-2
+    finally:
+        H._lib.d3d_gemm_tune(1, 0, 0)
+
+
+@pytest.mark.parametrize("N,L,C", [(4, 256, 256), (8, 64, 512), (32, 64, 512)])
+def test_gemm_gn_partials(H, N, L, C):
+    """GroupNorm partial statistics from the GEMM epilogue (every tile config
+    that carries them) equal the statistics pass over the written output."""
+    torch.manual_seed(5)
+    for cfg in (8, 4):
+        H._lib.d3d_gemm_tune(cfg, 0, 0)
+        try:
+            P = N * L
+            a = torch.randn(C, C, device=DEV).to(BF)
+            b = torch.randn(P, C, device=DEV).to(BF)
+            out = torch.empty(P, C, device=DEV, dtype=BF)
+            gnp = torch.empty(N * 32 * (L // 64) * 2, device=DEV)
+            H.gemm_nt(a, b, out, C, P, C, C, C, C, gnp=gnp, gn_groups=32, gn_hw=L)
+            y = out.float().view(N, L // 64, 64, 32, C // 32)
+            s = y.sum((2, 4)).permute(0, 2, 1)
+            q = (y * y).sum((2, 4)).permute(0, 2, 1)
+            got = gnp.view(N, 32, L // 64, 2)
+            assert rel(got[..., 0], s) < 1e-4 and rel(got[..., 1], q) < 1e-4
+        finally:
+            H._lib.d3d_gemm_tune(1, 0, 0)
+
+
 @pytest.mark.parametrize("P,IC,OC", [(128, 256, 768), (8192, 256, 768), (2048, 512, 512), (2048, 512, 1536),
                                      (4096, 384, 128), (32768, 1024, 512)])
-def test_linear(H, P, IC, OC, impl, monkeypatch):
-    """Every dispatch regime: the ping-pong GEMM with the fused bias /
-    residual / scale epilogue, the conv MFMA kernel (taps = 1) and hipBLASLt +
-    the epilogue kernel."""
-    monkeypatch.setattr(H, "_LIN_PP", impl == "pp")
-    monkeypatch.setattr(H, "_LIN_HIP_FWD_FLOP", 1e12 if impl == "mfma" else 0.0)
-    monkeypatch.setattr(H, "_LIN_HIP_DGRAD_FLOP", 1e12 if impl == "mfma" else 0.0)
+def test_linear(H, P, IC, OC):
+    """Per-pixel dense layer (GEMM with the fused bias / residual / scale
+    epilogue, input gradient on the same kernel, split-K weight gradient)
+    against the torch composition."""
     torch.manual_seed(4)
     x = torch.randn(2, P // 2, IC, device=DEV).to(BF)
     w = torch.randn(OC, IC, device=DEV) / math.sqrt(IC)
     b = torch.randn(OC, device=DEV) * 0.1
     r = torch.randn(2, P // 2, OC, device=DEV).to(BF)
     go = torch.randn(2, P // 2, OC, device=DEV)
+    nfb = len(H.FALLBACKS)
     yh, yr, gh, gr = run_both(lambda x, w, b, r: H.linear(x, w, b, r, 0.7),
                               lambda x, w, b, r: T.linear(x, w, b, r, 0.7), [x, w, b, r], go)
+    assert len(H.FALLBACKS) == nfb, H.FALLBACKS          # the native GEMM ran
     assert rel(yh, yr) < 2e-2
     for a, c in zip(gh, gr):
         assert rel(a, c) < 3e-2
@@ -459,12 +513,13 @@ def test_sampler_step_matches_posterior(H):
                                         ([128, 256, 384], 32, 32),    # 32768 rows: 8-wave 1x1 wgrad
                                         ([256, 512], 8, 32)])         # 8192 rows: 4 blas slabs
 def test_film_batch_with_gn_film(H, chans, N, Hh, blas):
-    """Level-batched FiLM projection feeding strided GN-FiLM: forward, the
-    shared d(scale|shift) buffer and the segmented weight-gradient scatter
+    """Level-batched FiLM projection ``dense_i(silu(emb))`` feeding strided
+    GN-FiLM: forward, the shared d(scale|shift) buffer, the input gradient
+    through the SiLU (GEMM epilogue) and the segmented weight-gradient scatter
     against per-block fp32 linears."""
     torch.manual_seed(0)
     K = 1024
-    semb = (torch.randn(N, Hh, Hh, K, device=DEV)).to(BF)
+    semb = (torch.randn(N, Hh, Hh, K, device=DEV) * 2).to(BF)
     Ws = [torch.randn(2 * c, K, device=DEV) / 32 for c in chans]
     Bs = [torch.randn(2 * c, device=DEV) * 0.1 for c in chans]
     xs = [torch.randn(N, Hh, Hh, c, device=DEV).to(BF) for c in chans]
@@ -479,7 +534,7 @@ def test_film_batch_with_gn_film(H, chans, N, Hh, blas):
         if hip:
             sss = H.film_batch(s, ws, bs)
         else:
-            sss = [T.linear(s, w, b) for w, b in zip(ws, bs)]
+            sss = [T.linear(torch.nn.functional.silu(s), w, b) for w, b in zip(ws, bs)]
         loss = 0
         for x, g, b, ss, go in zip(xs, gam, bet, sss, gos):
             xx = x if hip else x.float()
@@ -576,17 +631,14 @@ def test_ray_dir_matches_torch(H):
     assert torch.allclose(T.ray_origin_pe(t, mask)[:, None, None, :].expand(-1, Hh, Hh, -1), full[..., :93])
 
 
-@pytest.mark.parametrize("pp", [False, True])
 @pytest.mark.parametrize("C1,C2,OC", [(256, 128, 128), (128, 128, 128), (512, 512, 512), (512, 256, 256)])
-def test_cat_gn_silu_dense(H, C1, C2, OC, pp, monkeypatch):
+@pytest.mark.parametrize("Hh", [8, 32])
+def test_cat_gn_silu_dense(H, C1, C2, OC, Hh):
     """Decoder block entry on the virtual concat == GN+SiLU and dense on the
-    materialised concat (forward and every gradient); ``pp``: the skip
-    forward on the hand-written ping-pong GEMM (D3D_CAT_PP)."""
+    materialised concat (forward and every gradient); the skip runs as two
+    GEMMs, the second accumulating through its residual epilogue."""
     torch.manual_seed(11)
-    N, Hh = (4, 32) if pp else (4, 8)
-    monkeypatch.setattr(H, "_CAT_PP", pp)
-    if pp:
-        monkeypatch.setattr(H, "_PP_MIN_TILES", 1)
+    N = 4
     a = (torch.randn(N, Hh, Hh, C1, device=DEV) + 0.3).to(BF)
     b = (torch.randn(N, Hh, Hh, C2, device=DEV) * 2).to(BF)
     gw = torch.rand(C1 + C2, device=DEV) + 0.5

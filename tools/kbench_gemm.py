@@ -47,7 +47,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
-    ap.add_argument("--vers", default="2", help="comma list of kernel versions timed interleaved")
+    ap.add_argument("--vers", default="1", help="comma list of tile configs timed interleaved (1 = by size, 8 / 4 / 2 forced)")
+    ap.add_argument("--gm", type=int, default=0, help="tile-group width (d3d_gemm_tune gm; 0 = default)")
+    ap.add_argument("--nobias", action="store_true")
     args = ap.parse_args()
     H._ensure_impl()
     lib = H._lib
@@ -57,23 +59,23 @@ def main():
             continue
         w = (torch.rand(M, K, device="cuda") * 2 - 1).to(BF)
         x = (torch.rand(N, K, device="cuda") * 2 - 1).to(BF)
-        bias = torch.randn(M, device="cuda")
+        bias = None if args.nobias else torch.randn(M, device="cuda")
         y = torch.empty(N, M, dtype=BF, device="cuda")
         st = H._st()
 
         def ours(v=None):
             if v is not None:
-                lib.d3d_gemm_tune(v, 0, 0)
-            rc = lib.d3d_gemm_nt(w.data_ptr(), x.data_ptr(), y.data_ptr(), bias.data_ptr(), None, M, N, K, K, K, M,
+                lib.d3d_gemm_tune(v, args.gm, 0)
+            rc = lib.d3d_gemm_nt(w.data_ptr(), x.data_ptr(), y.data_ptr(), H._ptr(bias), None, M, N, K, K, K, M,
                                  M, 1.0, 1.0, st)
             assert rc == 0, rc
 
         def blas():
-            return torch.addmm(bias.to(BF), x, w.t())
+            return torch.addmm(bias.to(BF), x, w.t()) if bias is not None else torch.mm(x, w.t())
 
         vers = [int(v) for v in args.vers.split(",")]
         rows = torch.randint(0, N, (256,), device="cuda")
-        ref = x[rows].float() @ w.float().t() + bias
+        ref = x[rows].float() @ w.float().t() + (bias if bias is not None else 0)
         errs = {}
         for v in vers:
             y.zero_()
@@ -87,7 +89,7 @@ def main():
         t_o, t_b = {v: [] for v in vers}, []
         for _ in range(args.rounds):
             for v in vers:
-                lib.d3d_gemm_tune(v, 0, 0)
+                lib.d3d_gemm_tune(v, args.gm, 0)
                 t_o[v].append(timeit(ours, args.iters))
             t_b.append(timeit(blas, args.iters))
         fl = 2.0 * M * N * K
