@@ -64,17 +64,31 @@ class CachedBatchLoader:
         P = poses[rows[:, None], views]                                         # [B,2,4,4]
         return img, P[:, :, :3, :3].copy(), P[:, :, :3, 3].copy(), Ks[rows].copy()
 
-    def _producer(self, batches: List[List], q: "queue.Queue") -> None:
+    @staticmethod
+    def _put(q: "queue.Queue", item, stop: threading.Event) -> bool:
+        """Blocking put that gives up once the consumer has stopped."""
+        while not stop.is_set():
+            try:
+                q.put(item, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def _producer(self, batches: List[List], q: "queue.Queue", stop: threading.Event) -> None:
         try:
             for keys in batches:
+                if stop.is_set():
+                    return
                 img, R, T, K = self.gather(keys)
                 t = torch.from_numpy(np.ascontiguousarray(img))
                 if self.device.type == "cuda":
                     t = t.pin_memory()
-                q.put((t, torch.from_numpy(R), torch.from_numpy(T), torch.from_numpy(K)))
+                if not self._put(q, (t, torch.from_numpy(R), torch.from_numpy(T), torch.from_numpy(K)), stop):
+                    return
         except BaseException as e:          # surface loader errors in the consumer
-            q.put(e)
-        q.put(None)
+            self._put(q, e, stop)
+        self._put(q, None, stop)
 
     # -------------------------------------------------------------- device
     def __iter__(self) -> Iterator[tuple]:
@@ -82,7 +96,8 @@ class CachedBatchLoader:
         nb = len(self)
         batches = [keys[i * self.B:(i + 1) * self.B] for i in range(nb)]
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
-        th = threading.Thread(target=self._producer, args=(batches, q), daemon=True)
+        stop = threading.Event()
+        th = threading.Thread(target=self._producer, args=(batches, q, stop), daemon=True)
         th.start()
         cuda = self.device.type == "cuda"
         side = torch.cuda.Stream(device=self.device) if cuda else None
@@ -108,16 +123,26 @@ class CachedBatchLoader:
             return img, R, T, K
 
         pending = None
-        while True:
-            item = q.get()
-            if isinstance(item, BaseException):
-                raise item
-            if item is None:
-                break
-            nxt = upload(item)              # H2D of batch k+1 is queued before batch k is consumed
+        try:
+            while True:
+                item = q.get()
+                if isinstance(item, BaseException):
+                    raise item
+                if item is None:
+                    break
+                nxt = upload(item)          # H2D of batch k+1 is queued before batch k is consumed
+                if pending is not None:
+                    yield finish(*pending)
+                pending = nxt
             if pending is not None:
                 yield finish(*pending)
-            pending = nxt
-        if pending is not None:
-            yield finish(*pending)
-        th.join()
+        finally:
+            # also on an early stop (steps_per_epoch, max_steps, an exception in
+            # the step): release the producer and its pinned batches
+            stop.set()
+            while True:
+                try:
+                    q.get_nowait()
+                except queue.Empty:
+                    break
+            th.join()

@@ -235,12 +235,23 @@ class DiffusionSampler:
         torch.cuda.synchronize(dev)
         g["z"].copy_(z_keep)
         g["graph"] = graph
+        g["weights"] = self._weight_signature()
         self._g = g
         return g
+
+    def _weight_signature(self):
+        """The captured graph reads the cached bf16 weight operands by address:
+        any out-of-place change (``load_state_dict`` / ``copy_`` bump the
+        parameters' versions and the cache rebuilds the operand in a new
+        buffer) must force a recapture."""
+        from ..ops import hip_impl
+        return (hip_impl._REV[0], tuple(p._version for p in self.model.parameters()))
 
     def _graph_ok(self, b, H, W, K, w, target_R, target_T) -> bool:
         g = self._g
         if g is None or g["b"] != b or g["H"] != H or g["W"] != W or g["shared"] != self.share_cond:
+            return False
+        if g["weights"] != self._weight_signature():
             return False
         tR, tT, tK, tw = g["target"]
         return bool(torch.equal(tK.to(K.device), K) and torch.equal(tw.to(w.device), w))

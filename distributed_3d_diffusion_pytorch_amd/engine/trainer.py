@@ -122,9 +122,17 @@ class Trainer:
             self.optim.load_state_dict(ck["optim"])
         self.optim.load_ema_state_dict(self.model, ck.get("ema"))
         self.step = int(ck.get("step", 0))
-        if "sampler_epoch" in ck:           # mid-epoch checkpoint (after_warmup.pt)
+        if "sampler_epoch" in ck:           # mid-epoch checkpoint (after_warmup.pt, or latest.pt of a max_steps stop)
             self.epoch = int(ck["sampler_epoch"])
-            self.epoch_pos = int(ck.get("epoch_pos", 0))
+            # position = examples of the epoch consumed by ALL ranks (the shard
+            # sampler deals the epoch's permutation round-robin, so any world size
+            # resumes at the same global position); older files: batches
+            if "epoch_examples" in ck:
+                self.epoch_pos = int(ck["epoch_examples"]) // max(self.cfg.global_batch, 1)
+            elif int(ck.get("world_size", 1)) == self.ctx.world:
+                self.epoch_pos = int(ck.get("epoch_pos", 0))
+            else:
+                self.epoch_pos = 0
         else:                               # end-of-epoch checkpoint (latest.pt) or reference file
             self.epoch = int(ck.get("epoch", -1)) + 1 if "epoch" in ck else 0
             self.epoch_pos = 0
@@ -164,6 +172,7 @@ class Trainer:
         if epoch_pos is not None:
             extra["sampler_epoch"] = int(self.epoch)
             extra["epoch_pos"] = int(epoch_pos)
+            extra["epoch_examples"] = int(epoch_pos) * int(self.cfg.global_batch)
         ema = self.optim.ema_state_dict(self.model)
         if ema is not None:
             extra["ema"] = {k: v.cpu() for k, v in ema.items()}
@@ -325,7 +334,7 @@ class Trainer:
         done = False
         for epoch in range(self.epoch, cfg.num_epochs):
             self.epoch = epoch
-            n = self.epoch_pos if epoch == self.epoch else 0
+            n = self.epoch_pos                # > 0 only for the epoch a mid-epoch checkpoint resumes
             if sampler is not None:
                 sampler.set_epoch(epoch, start=n * self.local_batch)
                 ds.set_epoch(epoch)
@@ -368,9 +377,12 @@ class Trainer:
                 if cfg.max_steps and self.step >= cfg.max_steps:
                     done = True
                     break
-            self.save("latest.pt", epoch=epoch)
             if done:
+                # stopped inside the epoch: latest.pt records the position, so a
+                # resume continues this epoch instead of skipping its remainder
+                self.save("latest.pt", epoch_pos=n)
                 break
+            self.save("latest.pt", epoch=epoch)
         self.sync()
         self._profile_hook(None)
         self.logger.close()

@@ -126,3 +126,23 @@ def test_cached_batch_loader_matches_dataset_and_feeds_fast(tmp_path):
     rate = len(big) / (time.perf_counter() - t0)
     print(f"cached batch gather: {rate:.0f} pairs/s")
     assert rate > 4000, rate
+
+
+def test_cached_batch_loader_early_stop_releases_producer(tmp_path):
+    """A consumer that stops after one batch (steps_per_epoch, max_steps, an
+    exception in the step) must not leave the producer thread blocked on the
+    full prefetch queue holding pinned batches."""
+    import threading
+    from distributed_3d_diffusion_pytorch_amd.data import build_cache, CachedSRNDataset, CachedBatchLoader
+    root = str(tmp_path / "srn")
+    write_synthetic_srn(root, num_instances=40, num_views=6, size=16, seed=3)
+    cache = build_cache(root, str(tmp_path / "cache"), 16)
+    ds = CachedSRNDataset("train", cache, seed=1)
+    sampler = ShardSampler(len(ds), 0, 1, shuffle=True, seed=2, with_epoch=True)
+    dl = CachedBatchLoader(ds, 2, sampler, "cpu")
+    base = threading.active_count()
+    for _ in range(3):
+        it = iter(dl)
+        next(it)
+        it.close()                      # the generator's finally stops and joins the producer
+    assert threading.active_count() == base
