@@ -23,7 +23,7 @@ Layout of one step (MI355X, one process per GPU):
       joining RCCL's stream (work.wait() captured as an edge).
   [world > 1, comm_mode "post"] fallback when a probe capture of an RCCL
       collective fails (or D3D_GRAPH_COMM=0, or gloo): eager all-reduce of the
-      flat gradient after graph A in D3D_AR_CHUNKS (default 4) async chunks,
+      flat gradient after graph A in 4 async chunks,
       each chunk's Adam launched as soon as its collective lands.
   graph B: fused Adam reading its per-step hyper-parameters from a device
       block (lr warmup / bias correction change every step; the 1/world
@@ -79,7 +79,7 @@ def probe_graph_collective(device: torch.device) -> bool:
     return bool(flag.item() > 0.5)
 
 
-_FUSED_UPDATE = os.environ.get("D3D_FUSED_UPDATE", "1") != "0"
+_FUSED_UPDATE = True
 # Deferred optimizer step: the Adam update of step t runs inside the replay of
 # step t+1's graph A, the bulk of it on a side stream overlapped with the
 # forward (bs16: the ~1 ms bandwidth-bound update hides behind the first
@@ -274,7 +274,7 @@ class GraphedTrainStep:
         o = self.tr.optim
         p, g, m, v, ema = o.flat.data, o.flat.grad, o.exp_avg, o.exp_avg_sq, o.ema
         n = g.numel()
-        k = max(1, int(os.environ.get("D3D_AR_CHUNKS", "4")))
+        k = 4
         cuts = [0] + [min(n, (n * i // k + 255) // 256 * 256) for i in range(1, k)] + [n]
         spans = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
         works = [dist.all_reduce(g[a:b], async_op=True) for a, b in spans]

@@ -24,7 +24,7 @@ import torch
 
 from ..parallel.flat import FlatParams
 
-FUSED_UPDATE = os.environ.get("D3D_FUSED_UPDATE", "1") != "0"
+FUSED_UPDATE = True      # Adam + operand repack in one pass (hip_impl.adam_update_all)
 
 
 class FusedAdam(torch.optim.Optimizer):

@@ -380,7 +380,7 @@ class Trainer:
             if done:
                 # stopped inside the epoch: latest.pt records the position, so a
                 # resume continues this epoch instead of skipping its remainder
-                self.save("latest.pt", epoch_pos=n)
+                self.save("latest.pt", epoch=epoch - 1, epoch_pos=n)     # epoch: the last completed one
                 break
             self.save("latest.pt", epoch=epoch)
         self.sync()

@@ -483,7 +483,7 @@ class XUNet(nn.Module):
         st = _COND_STREAMS.get(idx)
         if st is None:
             st = _COND_STREAMS[idx] = torch.cuda.Stream(device=idx,
-                                                        priority=int(os.environ.get("D3D_COND_STREAM_PRIO", "0")))
+                                                        priority=0)
             from ..ops.gradsink import SINK
             SINK.add_compute_stream(st)
         return st

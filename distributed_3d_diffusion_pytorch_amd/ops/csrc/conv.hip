@@ -2621,28 +2621,22 @@ D3D_API int d3d_pack_all(const void* descs, const int* blk_desc, int total_block
 // I: [N, IH, IW, IC] bf16 (IC % 8 == 0), Wp: packed [OCp][taps][ICp] bf16 with
 // OCp % 128 == 0 and ICp % 64 == 0.  O: [N, OH, OW, ldo] bf16.  taps = 9 (3x3)
 // or 1 (1x1 / per-pixel linear).
-// 32-wide images on the halo kernel too (measured 2-7 % slower than conv_w8_k
-// there, profiles/kbench_conv_halo.jsonl; kept selectable for the sweep)
-static int g_halo32 = getenv("D3D_HALO32") ? atoi(getenv("D3D_HALO32")) : 0;
-// 256-pixel halo tiles for grids the 512-pixel ones cannot fill: measured
-// 10-15 % slower than the 4-wave 128x128 kernel on the 32x32 level at 16
-// examples per GPU (profiles/kbench_conv_halo256.jsonl); selectable only
-static int g_halo256 = getenv("D3D_HALO256") ? atoi(getenv("D3D_HALO256")) : 0;
-// fragment double-buffering in the halo conv (PF): measured 4-15 % slower
-// (249 VGPRs, the extra copies outweigh the overlap; profiles/ab_halo_prefetch.txt)
-static int g_halo_pf = getenv("D3D_HALO_PF") ? atoi(getenv("D3D_HALO_PF")) : 0;
+// Halo variants measured and dropped: 32-wide images (2-7 % slower than
+// conv_w8_k, profiles/kbench_conv_halo.jsonl), 256-pixel tiles (10-15 %
+// slower than the 4-wave 128x128 kernel, kbench_conv_halo256.jsonl),
+// fragment double-buffering (4-15 % slower, ab_halo_prefetch.txt).
 // 64 x 64 no-split tiles (conv_small.hip) where the 128 x 128 kernels would
 // split K over a small grid (the low-resolution levels at small per-GPU batch)
-static int g_s64 = getenv("D3D_CONV_S64") ? atoi(getenv("D3D_CONV_S64")) : 1;
+static int g_s64 = 1;
 extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias, const float* row_bias,
                                 const void* res, void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW,
                                 int OC, int ldo, int stride, int trans, float scale, int res_nmod, int taps,
                                 float* gnp, int gn_groups, int* gn_done, hipStream_t st);
-// 64x64 no-split tiles (conv_small.hip) on grids of at most D3D_S64_MAXB
+// 64x64 no-split tiles (conv_small.hip) on grids of at most g_s64_maxb
 // 128x128 blocks (default 160): the 16x16 / 8x8 levels at 16 examples per GPU
 // and the 8x8 level at 32 (in-graph A/B: +1.1 % at bs16; the 16x16 level at
 // bs32, 256 such blocks, stays on split-K bufl, which is faster there)
-static const long g_s64_maxb = getenv("D3D_S64_MAXB") ? atol(getenv("D3D_S64_MAXB")) : 160;
+static const long g_s64_maxb = 160;
 static bool s64_wanted(long Mpix, int OC, int ICp, int taps) {
   const long blocks128 = ((Mpix + 127) / 128) * ((OC + 127) / 128);
   const long blocks64 = ((Mpix + 63) / 64) * (OC / 64);
@@ -2678,7 +2672,7 @@ D3D_API int d3d_conv_plan(int N, int OH, int OW, int OC, int ICp, int taps) {
   long Mpix = (long)N * OH * OW;
   long blocks = ((Mpix + BN - 1) / BN) * ((OC + BM - 1) / BM);
   int nk = taps * ICp / 64;
-  static const int target = getenv("D3D_CONV_SPLIT_TARGET") ? atoi(getenv("D3D_CONV_SPLIT_TARGET")) : 512;
+  static const int target = 512;
   if (blocks >= 384 || (OC & 3) || g_conv_impl < 1) return 1;
   if (g_conv_impl >= 2 && s64_wanted(Mpix, OC, ICp, taps)) return 1;     // no-split small tiles instead
   long want = target / blocks;      // rounded down: no nearly empty extra round of blocks
@@ -2715,40 +2709,18 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
   const long in_bytes = (long)N * IH * IW * IC * 2, w_bytes = (long)((OC + 127) / 128 * 128) * taps * ICp * 2;
   if (g_conv_impl == 8 && taps == 9 && stride == 1 && IW == OW && IH == OH && ldo == OC && IC % HALO_CH == 0 &&
       OC % 128 == 0 && (OW == 32 || OW == 64 || OW == 128) && in_bytes < (1L << 31) && w_bytes < (1L << 31)) {
-    // 512-pixel tiles where they fill the chip (64/128-wide images; 32-wide
-    // only on request: conv_w8_k is faster there at large batch), else
-    // 256-pixel tiles when those do (the 32x32 level at 16 examples per GPU)
+    // 512-pixel tiles where they fill the chip (64/128-wide images)
     auto nblk = [&](int bn) { return OH % (bn / OW) ? 0L : (long)N * (OH / (bn / OW)) * (OC / 128); };
-    int bn = 0;
-    if ((OW != 32 || g_halo32) && nblk(512) >= 256) bn = 512;
-    else if (g_halo256 && nblk(512) < 256 && nblk(256) >= 256) bn = 256;
-    if (bn) {
-      dim3 gh((unsigned)(N * (OH / (bn / OW))), (unsigned)(OC / 128), 1);
-#define HALO(OWv, TR, BNv)                                                                                         \
-  if (g_halo_pf && BNv == 512 && OWv == 64)                                                                         \
-    hipLaunchKernelGGL((conv_halo_k<OWv, TR, BNv, true>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp,   \
-                       bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, \
-                       scale, res_nmod, gnp, gn_groups);                                                            \
-  else                                                                                                              \
-    hipLaunchKernelGGL((conv_halo_k<OWv, TR, BNv>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias,   \
-                       row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale, \
-                       res_nmod, gnp, gn_groups)
-      if (bn == 512) {
-        if (OW == 32) {
-          if (trans) HALO(32, true, 512); else HALO(32, false, 512);
-        } else if (OW == 64) {
-          if (trans) HALO(64, true, 512); else HALO(64, false, 512);
-        } else {
-          if (trans) HALO(128, true, 512); else HALO(128, false, 512);
-        }
+    if (OW != 32 && nblk(512) >= 256) {
+      dim3 gh((unsigned)(N * (OH / (512 / OW))), (unsigned)(OC / 128), 1);
+#define HALO(OWv, TR)                                                                                              \
+  hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias,     \
+                     row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale,   \
+                     res_nmod, gnp, gn_groups)
+      if (OW == 64) {
+        if (trans) HALO(64, true); else HALO(64, false);
       } else {
-        if (OW == 32) {
-          if (trans) HALO(32, true, 256); else HALO(32, false, 256);
-        } else if (OW == 64) {
-          if (trans) HALO(64, true, 256); else HALO(64, false, 256);
-        } else {
-          if (trans) HALO(128, true, 256); else HALO(128, false, 256);
-        }
+        if (trans) HALO(128, true); else HALO(128, false);
       }
 #undef HALO
       if (gn_done && gnp) *gn_done = 1;
@@ -2986,9 +2958,9 @@ D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps
   // so ~1024 blocks fill the chip in one round; rounded down (no straggler
   // round).  Sweep on the X-UNet shapes (profiles/kbench_wgrad_plan.txt):
   // 1024 beats 512 by 10-35 %.  Every extra split costs a full fp32 OCxK slab
-  // of write + reduce traffic.  D3D_WGRAD_TARGET / D3D_WGRAD_CEIL: tuning knobs
-  static const long target = getenv("D3D_WGRAD_TARGET") ? atol(getenv("D3D_WGRAD_TARGET")) : 1024;
-  static const bool ceil_ = getenv("D3D_WGRAD_CEIL") && atoi(getenv("D3D_WGRAD_CEIL"));
+  // of write + reduce traffic.
+  static const long target = 1024;
+  static const bool ceil_ = false;
   long want = ceil_ ? (target + tiles - 1) / tiles : target / tiles;
   long maxs = (P + 255) / 256;       // small reductions (8x8 level at small batch): fill the chip first
   if (want > maxs) want = maxs;
@@ -3003,11 +2975,11 @@ D3D_API int d3d_conv_wgrad_plan2(int N, int OH, int OW, int OC, int IC, int taps
 // conv_wgrad_w8_k takes a 3x3 stride-1 same-size power-of-two shape when
 // at least one of its channel counts fills a 256-wide tile side (the 128x128
 // level-0 convs stay on the 4-wave kernel); impl 6 enables it.
-// taps == 1 (per-pixel GEMMs, D3D_WGRAD_W8_1X1, default on): any geometry,
+// taps == 1 (per-pixel GEMMs): any geometry,
 // long reductions (the FiLM projections over every pixel of a level) are
 // where the 4-wave kernel's 16-MFMA stages stall most.
 static bool wgrad_w8_1x1() {
-  static const int v = getenv("D3D_WGRAD_W8_1X1") ? atoi(getenv("D3D_WGRAD_W8_1X1")) : 1;
+  static const int v = 1;
   return v != 0;
 }
 

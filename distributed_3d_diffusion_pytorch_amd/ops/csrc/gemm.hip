@@ -42,20 +42,20 @@
 #include <utility>
 
 namespace {
-constexpr int G_BK = 32;
-constexpr int G_NST = 4;
+constexpr int G_BK = 32;         // K per MFMA step
+constexpr int G_PK = 64;         // K per LDS stage (two steps): 128-byte rows, whole cache lines per DMA row
 
-__device__ __forceinline__ int g_swz(int row, int chunk) {
-  return row * G_BK + ((chunk ^ (((row >> 3) & 1) * 3)) << 3);
-}
+// 16-byte chunk c (0..7) of row r of a stage: XOR swizzle by r & 7 (the
+// ds_read_b128 lane groups read 16 rows at one chunk: conflict-free)
+__device__ __forceinline__ int g_swz(int row, int chunk) { return row * G_PK + ((chunk ^ (row & 7)) << 3); }
 
 template <int WI, int WJ>
 struct GCfg {
   static constexpr int BM = 32 * WI, BN = 32 * WJ;       // 2 x 2 waves of 16*WI x 16*WJ
-  static constexpr int STAGE = (BM + BN) * G_BK;         // bf16 per stage
-  static constexpr int BIAS = G_NST * STAGE;             // 4 slots of 256 fp32
+  static constexpr int STAGE = (BM + BN) * G_PK;         // bf16 per stage (two K-steps)
+  static constexpr int BIAS = 2 * STAGE;                 // 4 slots of 256 fp32
   static constexpr int LDS = BIAS + 4 * 512;
-  static constexpr int DA = BM / 64, DB = BN / 64;       // DMA pieces (16 rows) per wave and K-tile
+  static constexpr int DA = BM / 32, DB = BN / 32;       // DMA pieces (8 rows x 128 B) per wave and stage
   static constexpr int ND = DA + DB;
   static constexpr int NM = WI * WJ;                     // MFMAs per wave and K-tile
   static constexpr int NR = WI + WJ;                     // fragment reads
@@ -205,7 +205,7 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   }
   const int ntiles = mt * nt;
   if (rb >= ntiles) return;
-  const int nk = K / G_BK;                   // even (K % 64 == 0), >= 4
+  const int nk = K / G_BK;                   // K-steps: even (K % 64 == 0), >= 4
 
   // tile id -> (m tile, n tile): m fastest inside groups of gm m tiles
   auto tile_mn = [&](int tl, int& mb_, int& nb_) {
@@ -221,19 +221,22 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
     }
   };
 
-  // loader: per operand DA / DB pieces of 16 rows (64-byte rows, 4 lanes a
-  // row), lane -> (row lane >> 2, LDS slot lane & 3 holding chunk slot ^ f(row))
+  // loader: per operand DA / DB pieces of 8 rows (128-byte rows, 8 lanes a
+  // row), lane -> (row lane >> 3, LDS slot lane & 7 holding chunk slot ^ (row & 7))
   int aoff[C::DA], boff[C::DB];
   {
-    const int chunk = (lane & 3) ^ (((lane >> 5) & 1) * 3);
+    const int chunk = (lane & 7) ^ (lane >> 3);
 #pragma unroll
-    for (int q = 0; q < C::DA; ++q) aoff[q] = ((wave * (C::BM / 4) + q * 16 + (lane >> 2)) * lda + chunk * 8) * 2;
+    for (int q = 0; q < C::DA; ++q) aoff[q] = ((wave * (C::BM / 4) + q * 8 + (lane >> 3)) * lda + chunk * 8) * 2;
 #pragma unroll
-    for (int q = 0; q < C::DB; ++q) boff[q] = ((wave * (C::BN / 4) + q * 16 + (lane >> 2)) * ldb + chunk * 8) * 2;
+    for (int q = 0; q < C::DB; ++q) boff[q] = ((wave * (C::BN / 4) + q * 8 + (lane >> 3)) * ldb + chunk * 8) * 2;
   }
   const int fr = lane & 15, fq = lane >> 4;
-  // fragment read offsets (bf16 elements within a stage): fragment i is 16 rows further
+  // fragment read offsets (bf16 elements within a stage) of the stage's
+  // first K-step; the second K-step is chunk + 4 (offset fh); fragment i is
+  // 16 rows further (16 * G_PK elements: the swizzle depends on row & 7 only)
   const int fa0 = g_swz(wm * 16 * WI + fr, fq), fb0 = g_swz(C::BM + wn * 16 * WJ + fr, fq);
+  const int fa1 = g_swz(wm * 16 * WI + fr, fq + 4), fb1 = g_swz(C::BM + wn * 16 * WJ + fr, fq + 4);
 
   // loader cursor: tile ltile (descriptors lA / lB), byte offset lkb of its
   // next K-tile; the following tile's descriptors are prepared when the
@@ -271,8 +274,8 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
             (int)((M - m0 < C::BM ? M - m0 : C::BM) * (bbf ? 2 : 4)), smem + C::BIAS + lbslot * 512, lane * 16, 0);
     }
   };
-  auto advance = [&]() {                     // after the pieces of one K-tile
-    lkb += G_BK * 2;
+  auto advance = [&]() {                     // after the pieces of one stage (two K-steps)
+    lkb += G_PK * 2;
     if (lkb == K * 2) {
       lkb = 0;
       lo = no;
@@ -283,9 +286,9 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   };
   auto dma = [&](int st, int d) {            // piece d (< DA: A, else B) into stage st
     if (d < C::DA)
-      g_dma(lo.a, lo.ra, smem + st * C::STAGE + (wave * (C::BM / 4) + d * 16) * G_BK, aoff[d], lkb);
+      g_dma(lo.a, lo.ra, smem + st * C::STAGE + (wave * (C::BM / 4) + d * 8) * G_PK, aoff[d], lkb);
     else
-      g_dma(lo.b, lo.rb, smem + st * C::STAGE + (C::BM + wave * (C::BN / 4) + (d - C::DA) * 16) * G_BK,
+      g_dma(lo.b, lo.rb, smem + st * C::STAGE + (C::BM + wave * (C::BN / 4) + (d - C::DA) * 8) * G_PK,
             boff[d - C::DA], lkb);
   };
 
@@ -295,62 +298,76 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   tile_mn(tile, mb, nb);
   bias_dma();
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < 2; ++k) {              // stages 0 and 1: K-steps 0..3
 #pragma unroll
     for (int d = 0; d < C::ND; ++d) dma(k, d);
     advance();
   }
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C::ND) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::ND) : "memory");
   G_BAR();
 #pragma unroll
-  for (int j = 0; j < WJ; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + fb0 + j * 512);
+  for (int j = 0; j < WJ; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + fb0 + j * 16 * G_PK);
 #pragma unroll
-  for (int i = 0; i < WI; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(smem + fa0 + i * 512);
+  for (int i = 0; i < WI; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(smem + fa0 + i * 16 * G_PK);
 
+  // K-step s = 2p + h uses stage p & 1.  Body s: NM slots, each one MFMA of
+  // K-step s plus at most one other instruction -- the fragment reads of
+  // s + 1 (B fragments first: the next step's first row needs all of them)
+  // and, in odd bodies, the DMA of stage p + 2 into stage p & 1 (free: its
+  // last fragments were read in body 2p) and the cursor update.  Odd bodies
+  // open with the wait for stage p + 1 (issued one stage earlier; after an
+  // epilogue its NS stores may stay in flight) and the only barrier of the
+  // stage: it publishes stage p + 1 and frees stage p & 1.
   int s = 0;
-  // One K-tile at stream position s: wait (the tile's first two K-tiles also
-  // step over the previous epilogue's NS stores), barrier, then NM slots.
-  auto body = [&](auto first, bf16x8(&ca)[WI], bf16x8(&cb)[WJ], bf16x8(&na)[WI], bf16x8(&nbf)[WJ],
+  auto body = [&](auto first, auto odd, bf16x8(&ca)[WI], bf16x8(&cb)[WJ], bf16x8(&na)[WI], bf16x8(&nbf)[WJ],
                   bool after_epi) {
-    if (after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::ND + C::NS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::ND) : "memory");
-    G_BAR();
-    const bf16* sn = smem + ((s + 1) & 3) * C::STAGE;
-    const int ls = (s + 3) & 3;
+    constexpr bool ODD = decltype(odd)::value;
+    if constexpr (ODD) {
+      if (after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      G_BAR();
+    }
+    // next K-step's fragments: second half of this stage, or first half of the next
+    const bf16* sn = smem + (ODD ? (((s >> 1) + 1) & 1) : ((s >> 1) & 1)) * C::STAGE;
+    const int ra = ODD ? fa0 : fa1, rbo = ODD ? fb0 : fb1;
+    const int ls = (s >> 1) & 1;
     g_for(std::make_integer_sequence<int, C::NM>{}, [&](auto kc) {
       constexpr int k = decltype(kc)::value;
       if constexpr (decltype(first)::value) g_mma0(acc[k / WJ][k % WJ], ca[k / WJ], cb[k % WJ]);
       else g_mma(acc[k / WJ][k % WJ], ca[k / WJ], cb[k % WJ]);
-      // fragment reads of s + 1 at slots r * NM / NR (B fragments first)
       g_for(std::make_integer_sequence<int, C::NR>{}, [&](auto rc) {
         constexpr int r = decltype(rc)::value;
         if constexpr (r * C::NM / C::NR == k) {
-          if constexpr (r < WJ) nbf[r] = *reinterpret_cast<const bf16x8*>(sn + fb0 + r * 512);
-          else na[r - WJ] = *reinterpret_cast<const bf16x8*>(sn + fa0 + (r - WJ) * 512);
+          if constexpr (r < WJ) nbf[r] = *reinterpret_cast<const bf16x8*>(sn + rbo + r * 16 * G_PK);
+          else na[r - WJ] = *reinterpret_cast<const bf16x8*>(sn + ra + (r - WJ) * 16 * G_PK);
         }
       });
-      // DMA pieces of s + 3 at slots (2d + 1) * NM / (2 ND); the cursor moves after the last
-      g_for(std::make_integer_sequence<int, C::ND>{}, [&](auto dc) {
-        constexpr int d = decltype(dc)::value;
-        if constexpr ((2 * d + 1) * C::NM / (2 * C::ND) == k) {
-          dma(ls, d);
-          if constexpr (d == C::ND - 1) {
-            advance();
-            if (lkb == 0) bias_dma();
+      if constexpr (ODD) {
+        // DMA pieces at slots (2d + 1) * NM / (2 ND); the cursor moves after the last
+        g_for(std::make_integer_sequence<int, C::ND>{}, [&](auto dc) {
+          constexpr int d = decltype(dc)::value;
+          if constexpr ((2 * d + 1) * C::NM / (2 * C::ND) == k) {
+            dma(ls, d);
+            if constexpr (d == C::ND - 1) {
+              advance();
+              if (lkb == 0) bias_dma();
+            }
           }
-        }
-      });
+        });
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
     ++s;
   };
+  using T_ = std::integral_constant<bool, true>;
+  using F_ = std::integral_constant<bool, false>;
 
   while (true) {
-    body(std::integral_constant<bool, true>{}, a0, b0, a1, b1, ti > 0);
-    body(std::integral_constant<bool, false>{}, a1, b1, a0, b0, ti > 0);
+    body(T_{}, F_{}, a0, b0, a1, b1, false);
+    body(F_{}, T_{}, a1, b1, a0, b0, ti > 0);
     for (int t = 2; t < nk; t += 2) {
-      body(std::integral_constant<bool, false>{}, a0, b0, a1, b1, false);
-      body(std::integral_constant<bool, false>{}, a1, b1, a0, b0, false);
+      body(F_{}, F_{}, a0, b0, a1, b1, false);
+      body(F_{}, T_{}, a1, b1, a0, b0, false);
     }
     // ---- epilogue of tile (mb, nb)
     {

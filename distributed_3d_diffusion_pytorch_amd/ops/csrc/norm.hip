@@ -28,18 +28,10 @@ struct Plan {
   int rows;     // rows per chunk (multiple of rpi)
 };
 
-// blocks per GroupNorm launch (D3D_GN_TARGET overrides; read once).  1024
-// beat 2048 and 512 by 0.5-1 % on both headline configs (the per-block
-// merge / LDS epilogue amortises over more rows; profiles/ab_gn_target.txt)
-static int gn_target_blocks() {
-  static int t = -1;
-  if (t < 0) {
-    const char* e = getenv("D3D_GN_TARGET");
-    t = e ? atoi(e) : 1024;
-    if (t < 64) t = 1024;
-  }
-  return t;
-}
+// blocks per GroupNorm launch: 1024 beat 2048 and 512 by 0.5-1 % on both
+// headline configs (the per-block merge / LDS epilogue amortises over more
+// rows; profiles/ab_gn_target.txt)
+static int gn_target_blocks() { return 1024; }
 
 Plan make_plan(int N, int P, int C) {
   Plan p;

@@ -27,11 +27,11 @@ Per-parameter accumulation order is unchanged (one side stream, launch
 order), so results stay bitwise reproducible.  ``D3D_WGRAD_STREAM=0`` runs
 everything on the compute stream.
 
-Inside HIP-graph capture (:meth:`submit`, ``D3D_GRAPH_WGRAD_STREAM``): a fork
+Inside HIP-graph capture (:meth:`submit`): a fork
 per weight gradient cost ~7 us of graph dependency latency per edge -- ~1,600
 edges ate the concurrency (busy 88.7 %, profiles/busy_bs16_side_stream.txt).
 There the weight-gradient jobs are DEFERRED instead: queued as closures and
-flushed onto the side stream ``D3D_WGRAD_DEFER_BATCH`` (default 8; 4 measured 1.5 % slower at bs16) at a time
+flushed onto the side stream 8 at a time (4 measured 1.5 % slower at bs16)
 behind ONE fork each, and joined once at the end of backward, so the graph
 holds a few dozen cross-stream edges while the weight-gradient branch runs
 concurrently with the input-gradient chain.  Deferred operands stay alive in
@@ -47,7 +47,7 @@ from typing import Callable, Dict, Optional
 import torch
 
 
-_PRIO = int(os.environ.get("D3D_WGRAD_STREAM_PRIO", "0"))
+_PRIO = 0          # HIP stream priority of the weight-gradient stream (higher measured slower)
 
 
 class GradSink:
@@ -60,8 +60,8 @@ class GradSink:
         self.seen = set()
         self.notify: Optional[Callable[[int], None]] = None
         self.stream_enabled = os.environ.get("D3D_WGRAD_STREAM", "1") != "0"
-        self.graph_defer = os.environ.get("D3D_GRAPH_WGRAD_STREAM", "1") != "0"
-        self.defer_batch = max(1, int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "8")))
+        self.graph_defer = True      # weight gradients on the side stream inside graph capture too
+        self.defer_batch = 8         # jobs per fork (4 measured 1.5 % slower at bs16)
         self._queue = []
         self._compute = []
         self._streams: Dict[int, "torch.cuda.Stream"] = {}
@@ -117,9 +117,8 @@ class GradSink:
     def _side(self, idx: int):
         st = self._streams.get(idx)
         if st is None:
-            # D3D_WGRAD_STREAM_PRIO < 0: a higher-priority HIP queue, so the
-            # weight-gradient work keeps pace with the input-gradient chain
-            # instead of piling up into an exposed tail at the end of backward
+            # (a higher-priority queue, to keep the weight-gradient work in
+            # pace with the input-gradient chain, measured slower)
             st = self._streams[idx] = torch.cuda.Stream(device=idx, priority=_PRIO)
         return st
 

@@ -32,7 +32,7 @@ _ZERO_PAGE: Dict[int, torch.Tensor] = {}
 # per micro-batch (16 examples: the 8-GPU headline's per-GPU share, 33.7 ->
 # 33.2 ms/step), hipBLASLt above (bs128 on one GPU: 792 -> 804 examples/s);
 # profiles/ab_film_wgrad.txt
-_FILM_WGRAD = os.environ.get("D3D_FILM_WGRAD", "auto")
+_FILM_WGRAD = "auto"
 
 
 def set_conv_impl(impl: str) -> None:
@@ -66,8 +66,8 @@ _IMPL_SET = [False]
 def _ensure_impl():
     if not _IMPL_SET[0]:
         import os
-        set_conv_impl(os.environ.get("D3D_CONV_IMPL", "halo"))
-        set_wgrad_impl(os.environ.get("D3D_WGRAD_IMPL", "w8"))
+        set_conv_impl("halo")
+        set_wgrad_impl("w8")
         _IMPL_SET[0] = True
 
 
@@ -1267,7 +1267,7 @@ def film_batch(emb, weights, biases):
     return outs
 
 
-_EPI_GN_STATS = os.environ.get("D3D_EPI_GN_STATS", "1") != "0"     # A/B switch of the fused statistics
+_EPI_GN_STATS = True     # GroupNorm statistics from the producing epilogue
 
 
 def linear(x, weight, bias, residual=None, out_scale=1.0, res_slot=None, in_slot=None, gn_groups=0):

@@ -26,10 +26,9 @@ _DONE = [False]
 
 
 def enable_tuned_gemms(path: str = None) -> bool:
-    """Load the tuned-solution table (once per process; ``D3D_TUNED_GEMMS_TABLE``
-    overrides the repository table).  Returns True when TunableOp is active
-    with it."""
-    path = path or os.environ.get("D3D_TUNED_GEMMS_TABLE") or TABLE
+    """Load the tuned-solution table (once per process; ``path`` overrides
+    the repository table).  Returns True when TunableOp is active with it."""
+    path = path or TABLE
     if _DONE[0]:
         return torch.cuda.tunable.is_enabled()
     _DONE[0] = True

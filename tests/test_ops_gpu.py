@@ -176,7 +176,7 @@ W8_SHAPES = [
     (16, 32, 32, 512, 512, 1, False, True, 0.5),                  # w8n: 2 x 128 tiles of 256 x 128
     (32, 64, 64, 384, 128, 1, True, True, 1 / math.sqrt(2)),      # halo: 8-row tiles, 12 channel chunks
     (8, 128, 128, 128, 256, 1, False, False, 1.0),                # halo: 4-row tiles of 128-wide images
-    (64, 32, 32, 128, 256, 1, False, False, 1.0),                 # 32-wide: halo only with D3D_HALO32=1
+    (64, 32, 32, 128, 256, 1, False, False, 1.0),                 # 32-wide: conv_w8_k
 ]
 
 
@@ -187,7 +187,7 @@ def test_conv3x3_w8(H, impl, N, Hh, W, Ci, Co, s, res, rb, scale):
     try:
         test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale)
     finally:
-        H.set_conv_impl(os.environ.get("D3D_CONV_IMPL", "halo"))
+        H.set_conv_impl("halo")
 
 
 S64_SHAPES = [
@@ -207,23 +207,6 @@ def test_conv3x3_small_tiles(H, N, Hh, W, Ci, Co, s, res, rb, scale):
     test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale)
 
 
-@pytest.mark.parametrize("N,Hh,Ci,Co", [(32, 32, 256, 256), (64, 32, 128, 256), (16, 64, 128, 128)])
-def test_conv3x3_halo_variants(N, Hh, Ci, Co):
-    """The opt-in halo tile variants (32-wide 512-pixel tiles, 256-pixel
-    tiles) against the torch composition, in a child process (the switches
-    are read once at library load)."""
-    import subprocess
-    import sys
-    code = ("import math, torch\n"
-            "from tests.test_ops_gpu import test_conv3x3\n"
-            "from distributed_3d_diffusion_pytorch_amd.ops import hip_impl as H\n"
-            f"H.set_conv_impl('halo'); test_conv3x3(H, {N}, {Hh}, {Hh}, {Ci}, {Co}, 1, True, False, 0.5)\n")
-    env = dict(os.environ, D3D_HALO32="1", D3D_HALO256="1")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
-                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-
-
 WGRAD_W8_SHAPES = [
     # 3x3 stride-1 weight gradients on the 8-wave kernel (impl "w8")
     (8, 32, 32, 256, 256, 1, False, False, 1.0),                  # 256 x 256 tiles
@@ -239,7 +222,7 @@ def test_conv3x3_wgrad_w8(H, N, Hh, W, Ci, Co, s, res, rb, scale):
     try:
         test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale)
     finally:
-        H.set_wgrad_impl(os.environ.get("D3D_WGRAD_IMPL", "w8"))
+        H.set_wgrad_impl("w8")
 
 
 @pytest.mark.parametrize("cfg", [8, 4, 2])

@@ -105,7 +105,7 @@ def test_mid_epoch_resume_continues_where_it_stopped(tmp_path):
     assert ck["sampler_epoch"] == 0 and ck["epoch_pos"] == 2 and len(ck["rng"]) == 1
     # the max_steps stop wrote latest.pt at the same mid-epoch position
     ck = torch.load(str(tmp_path / "r" / "latest.pt"), weights_only=True)
-    assert ck["sampler_epoch"] == 0 and ck["epoch_pos"] == 2 and ck["epoch_examples"] == 4 and "epoch" not in ck
+    assert ck["sampler_epoch"] == 0 and ck["epoch_pos"] == 2 and ck["epoch_examples"] == 4 and ck["epoch"] == -1
     # resume (find_resume picks latest.pt): epoch 0 continues at batch 2
     cfg2 = make_config(None, dict(ov, out_dir=str(tmp_path / "r"), transfer=str(tmp_path / "r")))
     tr2 = Trainer(cfg2, DistContext())
