@@ -6,10 +6,11 @@
 //
 // with A the bf16 weight ([M][lda], K contiguous), B the NHWC activations
 // ([N][ldb], K contiguous) and O / R NHWC bf16 rows (strides ldo / ldr).
-// Epilogues: EPI 0  (alpha * acc + bias[m] + R[n][m]) * scale, optionally
-//                   with the GroupNorm partial statistics of O;
-//            EPI 1  alpha * acc * dsilu(R[n][m]) -- the FiLM input gradient
-//                   through the SiLU of the conditioning embedding.
+// Epilogue (compile-time flags F): (alpha * acc + bias[m] + R[n][m]) * scale
+// with an fp32 (F_B32) or bf16 (F_B16) bias, a residual (F_RES) and the
+// GroupNorm partial statistics of O (F_GN); or F_DSILU: alpha * acc *
+// dsilu(R[n][m]) -- the FiLM input gradient through the SiLU of the
+// conditioning embedding.
 //
 // Schedule ("fat waves"): a 256-thread block = 2 x 2 waves, one per SIMD, each
 // owning WI x WJ MFMA 16x16x32 tiles (8 x 8 = 128 x 128 outputs and 256 fp32
@@ -86,6 +87,11 @@ __device__ __forceinline__ void g_dma(const void* base, int nrec, void* lds, int
                                            (lds_void*)lds, 16, voff, soff, 0, 0);
 }
 typedef unsigned g_u4 __attribute__((ext_vector_type(4)));
+typedef unsigned g_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ g_u2 g_load8(const void* base, int nrec, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b64(__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000),
+                                              off, 0, 0);
+}
 __device__ __forceinline__ void g_store16(const void* base, int nrec, g_u4 v, int off) {
   __builtin_amdgcn_raw_buffer_store_b128(v, __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000),
                                          off, 0, 0);
@@ -96,17 +102,16 @@ __device__ __forceinline__ void g_for(std::integer_sequence<int, I...>, F&& f) {
   (f(std::integral_constant<int, I>{}), ...);
 }
 
-// Epilogue parameters of one tile.
+enum : int { F_B32 = 1, F_B16 = 2, F_RES = 4, F_GN = 8, F_DSILU = 16 };
+
+// Epilogue parameters of one tile (32-bit offsets from the tile's row base).
 struct GEpi {
-  const float* sbias;
-  const bf16* sbias16;           // bf16 bias (one of the two, or neither)
-  const bf16* R;
-  bf16* obase;                   // output rows n0.. of this tile (buffer descriptor base / size:
-  int orec;                      // descriptors stay out of structs and lambda signatures, which the
-                                 // host pass must also type-check)
+  const bf16* R;                 // residual / pre-activation rows n0.. of this tile
+  bf16* obase;                   // output rows n0.. (buffer descriptor base / size: descriptors stay out of
+  int orec, rrec;                // structs and lambda signatures, which the host pass also type-checks)
   int M, ldo, ldr;
   float as, bs, rs;              // acc, bias and residual factors
-  long m0, n0, Npix;
+  int m0;
   int wm, wn, lane;
 };
 }  // namespace
@@ -115,50 +120,50 @@ struct GEpi {
 // the swap lane (fq, fr) holds channels fq*4..+3 of pixels P(2jp, fr) /
 // P(2jp+1, fr); v_permlane16_swap (odd rows of X <-> even rows of Y) leaves it
 // 8 consecutive channels ((fq >> 1) * 8..) of pixel P(2jp + (fq & 1), fr).
-template <int EPI, int WI, int WJ, int II, int JP>
-__device__ __forceinline__ void g_epi_pair(const f32x4 (&acc)[WI][WJ], const GEpi& e, float (&gs)[WI][2],
-                                           float (&gq)[WI][2], bool gn) {
+// cb: this lane's 4 bias values (already times scale).
+template <int F, int WI, int WJ, int II, int JP>
+__device__ __forceinline__ void g_epi_pair(const f32x4 (&acc)[WI][WJ], const GEpi& e, const f32x4& cb,
+                                           float (&gs)[WI][2], float (&gq)[WI][2]) {
+#pragma clang fp contract(off)      // explicit fmas: every instantiation rounds alike
   const int fr = e.lane & 15, fq = e.lane >> 4;
-  const f32x4 x = acc[II][2 * JP], y = acc[II][2 * JP + 1];
-  const int cl = e.wm * 16 * WI + II * 16 + fq * 4;              // tile-local channel (pre-swap)
-  const long co = e.m0 + cl;
-  const long px = e.n0 + e.wn * 16 * WJ + 2 * JP * 16 + fr, py = px + 16;
-  float vx[4], vy[4];
-  if constexpr (EPI == 1) {
-    // d pre-activation = alpha * acc * dsilu(pre-activation)
-    bf16x4 rx = {}, ry = {};
-    if (co < e.M) {
-      if (px < e.Npix) rx = *reinterpret_cast<const bf16x4*>(e.R + px * e.ldr + co);
-      if (py < e.Npix) ry = *reinterpret_cast<const bf16x4*>(e.R + py * e.ldr + co);
-    }
+  // accumulators leave the AGPRs here, one pair at a time (plain reads were
+  // hoisted as one 256-register block ahead of the epilogue, spilling)
+  f32x4 x, y;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      vx[k] = x[k] * e.as * dsiluf_((float)rx[k]);
-      vy[k] = y[k] * e.as * dsiluf_((float)ry[k]);
+  for (int k = 0; k < 4; ++k) {
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(x[k]) : "a"(acc[II][2 * JP][k]));
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(y[k]) : "a"(acc[II][2 * JP + 1][k]));
+  }
+  const int cl = e.m0 + e.wm * 16 * WI + II * 16 + fq * 4;        // channel (pre-swap)
+  const int px = e.wn * 16 * WJ + 2 * JP * 16 + fr;               // tile-local pixel (pre-swap)
+  float vx[4], vy[4];
+  if constexpr ((F & F_RES) || (F & F_DSILU)) {
+    // 8-byte reads through a range-checked descriptor: rows past the tile end and
+    // channels past M read as zero without a branch
+    typedef unsigned u2l __attribute__((ext_vector_type(2)));
+    const bool cok = cl < e.M;
+    const int ox = cok ? (px * e.ldr + cl) * 2 : (int)0x80000000;
+    const int oy = cok ? ((px + 16) * e.ldr + cl) * 2 : (int)0x80000000;
+    const u2l rx2 = g_load8(e.R, e.rrec, ox), ry2 = g_load8(e.R, e.rrec, oy);
+    const bf16x4 rx = __builtin_bit_cast(bf16x4, rx2), ry = __builtin_bit_cast(bf16x4, ry2);
+    if constexpr (F & F_DSILU) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        vx[k] = x[k] * e.as * dsiluf_((float)rx[k]);
+        vy[k] = y[k] * e.as * dsiluf_((float)ry[k]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        vx[k] = __builtin_fmaf((float)rx[k], e.rs, __builtin_fmaf(x[k], e.as, cb[k]));
+        vy[k] = __builtin_fmaf((float)ry[k], e.rs, __builtin_fmaf(y[k], e.as, cb[k]));
+      }
     }
   } else {
-    f32x4 cb = e.sbias ? *reinterpret_cast<const f32x4*>(e.sbias + cl) : f32x4{0.f, 0.f, 0.f, 0.f};
-    if (e.sbias16) {
-      const bf16x4 c4 = *reinterpret_cast<const bf16x4*>(e.sbias16 + cl);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) cb[k] = (float)c4[k];
-    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      vx[k] = x[k] * e.as + cb[k] * e.bs;
-      vy[k] = y[k] * e.as + cb[k] * e.bs;
-    }
-    if (e.R && co < e.M) {
-      if (px < e.Npix) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(e.R + px * e.ldr + co);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) vx[k] += (float)r[k] * e.rs;
-      }
-      if (py < e.Npix) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(e.R + py * e.ldr + co);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) vy[k] += (float)r[k] * e.rs;
-      }
+      vx[k] = __builtin_fmaf(x[k], e.as, cb[k]);
+      vy[k] = __builtin_fmaf(y[k], e.as, cb[k]);
     }
   }
   bf16x4 ox, oy;
@@ -167,7 +172,7 @@ __device__ __forceinline__ void g_epi_pair(const f32x4 (&acc)[WI][WJ], const GEp
     ox[k] = (bf16)vx[k];
     oy[k] = (bf16)vy[k];
   }
-  if (gn) {
+  if constexpr (F & F_GN) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float fx = (float)ox[k], fy = (float)oy[k];
@@ -181,17 +186,17 @@ __device__ __forceinline__ void g_epi_pair(const f32x4 (&acc)[WI][WJ], const GEp
   const auto s1 = __builtin_amdgcn_permlane16_swap(ux[1], uy[1], false, false);
   const g_u4 v = {s0[0], s1[0], s0[1], s1[1]};
   const int pl = e.wn * 16 * WJ + (2 * JP + (fq & 1)) * 16 + fr;    // tile-local pixel (post-swap)
-  const long cs = e.m0 + e.wm * 16 * WI + II * 16 + (fq >> 1) * 8;
-  const int off = cs < e.M ? (int)((long)pl * e.ldo + cs) * 2 : (int)0x80000000;
-  g_store16(e.obase, e.orec, v, off);
+  const int cs = e.m0 + e.wm * 16 * WI + II * 16 + (fq >> 1) * 8;
+  g_store16(e.obase, e.orec, v, cs < e.M ? (pl * e.ldo + cs) * 2 : (int)0x80000000);
   __builtin_amdgcn_sched_barrier(0);       // one pair at a time: bounded live registers
 }
 
-template <int WI, int WJ, int EPI>
+template <int WI, int WJ, int F>
 __global__ void __launch_bounds__(256, 1)
 gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ O, const float* __restrict__ bias,
           const bf16* __restrict__ R, int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha,
-          float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw, int bbf) {
+          float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw) {
+  constexpr bool BIAS = (F & (F_B32 | F_B16)) != 0, BBF = (F & F_B16) != 0;
   using C = GCfg<WI, WJ>;
   __shared__ __attribute__((aligned(16))) bf16 smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -223,14 +228,20 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
 
   // loader: per operand DA / DB pieces of 8 rows (128-byte rows, 8 lanes a
   // row), lane -> (row lane >> 3, LDS slot lane & 7 holding chunk slot ^ (row & 7))
-  int aoff[C::DA], boff[C::DB];
+  // One VGPR per operand: piece q adds q * 8 rows, an opaque (never hoisted)
+  // v_add at the DMA -- sixteen live offsets spilled the 8x8 variants.
+  int aoff, boff;
   {
     const int chunk = (lane & 7) ^ (lane >> 3);
-#pragma unroll
-    for (int q = 0; q < C::DA; ++q) aoff[q] = ((wave * (C::BM / 4) + q * 8 + (lane >> 3)) * lda + chunk * 8) * 2;
-#pragma unroll
-    for (int q = 0; q < C::DB; ++q) boff[q] = ((wave * (C::BN / 4) + q * 8 + (lane >> 3)) * ldb + chunk * 8) * 2;
+    aoff = ((wave * (C::BM / 4) + (lane >> 3)) * lda + chunk * 8) * 2;
+    boff = ((wave * (C::BN / 4) + (lane >> 3)) * ldb + chunk * 8) * 2;
   }
+  const int astep = 8 * lda * 2, bstep = 8 * ldb * 2;
+  auto piece_off = [](int base, int step) {
+    int r;
+    asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "s"(step), "v"(base));
+    return r;
+  };
   const int fr = lane & 15, fq = lane >> 4;
   // fragment read offsets (bf16 elements within a stage) of the stage's
   // first K-step; the second K-step is chunk + 4 (offset fh); fragment i is
@@ -268,10 +279,10 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   int lbslot = 0;                            // bias slot of the loader's tile (tile count & 3)
   // bias of the loader's tile: wave 0 DMAs it (one instruction) with the tile's first K-tile
   auto bias_dma = [&]() {
-    if (EPI == 0 && bias && wave == 0 && lo.m0 >= 0) {
+    if (BIAS && wave == 0 && lo.m0 >= 0) {
       const long m0 = lo.m0;
-      g_dma(bbf ? (const void*)(reinterpret_cast<const bf16*>(bias) + m0) : (const void*)(bias + m0),
-            (int)((M - m0 < C::BM ? M - m0 : C::BM) * (bbf ? 2 : 4)), smem + C::BIAS + lbslot * 512, lane * 16, 0);
+      g_dma(BBF ? (const void*)(reinterpret_cast<const bf16*>(bias) + m0) : (const void*)(bias + m0),
+            (int)((M - m0 < C::BM ? M - m0 : C::BM) * (BBF ? 2 : 4)), smem + C::BIAS + lbslot * 512, lane * 16, 0);
     }
   };
   auto advance = [&]() {                     // after the pieces of one stage (two K-steps)
@@ -286,10 +297,11 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   };
   auto dma = [&](int st, int d) {            // piece d (< DA: A, else B) into stage st
     if (d < C::DA)
-      g_dma(lo.a, lo.ra, smem + st * C::STAGE + (wave * (C::BM / 4) + d * 8) * G_PK, aoff[d], lkb);
+      g_dma(lo.a, lo.ra, smem + st * C::STAGE + (wave * (C::BM / 4) + d * 8) * G_PK,
+            d ? piece_off(aoff, d * astep) : aoff, lkb);
     else
       g_dma(lo.b, lo.rb, smem + st * C::STAGE + (C::BM + wave * (C::BN / 4) + (d - C::DA) * 8) * G_PK,
-            boff[d - C::DA], lkb);
+            d > C::DA ? piece_off(boff, (d - C::DA) * bstep) : boff, lkb);
   };
 
   bf16x8 a0[WI], b0[WJ], a1[WI], b1[WJ];
@@ -319,9 +331,9 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   // epilogue its NS stores may stay in flight) and the only barrier of the
   // stage: it publishes stage p + 1 and frees stage p & 1.
   int s = 0;
-  auto body = [&](auto first, auto odd, bf16x8(&ca)[WI], bf16x8(&cb)[WJ], bf16x8(&na)[WI], bf16x8(&nbf)[WJ],
-                  bool after_epi) {
-    constexpr bool ODD = decltype(odd)::value;
+  auto body = [&](auto first, auto odd, auto last, bf16x8(&ca)[WI], bf16x8(&cb)[WJ], bf16x8(&na)[WI],
+                  bf16x8(&nbf)[WJ], bool after_epi) {
+    constexpr bool ODD = decltype(odd)::value, LAST = decltype(last)::value;
     if constexpr (ODD) {
       if (after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -337,7 +349,7 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
       else g_mma(acc[k / WJ][k % WJ], ca[k / WJ], cb[k % WJ]);
       g_for(std::make_integer_sequence<int, C::NR>{}, [&](auto rc) {
         constexpr int r = decltype(rc)::value;
-        if constexpr (r * C::NM / C::NR == k) {
+        if constexpr (!LAST && r * C::NM / C::NR == k) {
           if constexpr (r < WJ) nbf[r] = *reinterpret_cast<const bf16x8*>(sn + rbo + r * 16 * G_PK);
           else na[r - WJ] = *reinterpret_cast<const bf16x8*>(sn + ra + (r - WJ) * 16 * G_PK);
         }
@@ -362,32 +374,33 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   using T_ = std::integral_constant<bool, true>;
   using F_ = std::integral_constant<bool, false>;
 
+  // (the tile's last K-step reads no fragments: the next tile's first ones
+  // are read after the epilogue, so they do not occupy registers across it)
   while (true) {
-    body(T_{}, F_{}, a0, b0, a1, b1, false);
-    body(F_{}, T_{}, a1, b1, a0, b0, ti > 0);
-    for (int t = 2; t < nk; t += 2) {
-      body(F_{}, F_{}, a0, b0, a1, b1, false);
-      body(F_{}, T_{}, a1, b1, a0, b0, false);
+    body(T_{}, F_{}, F_{}, a0, b0, a1, b1, false);
+    body(F_{}, T_{}, F_{}, a1, b1, a0, b0, ti > 0);
+    for (int t = 2; t < nk - 2; t += 2) {
+      body(F_{}, F_{}, F_{}, a0, b0, a1, b1, false);
+      body(F_{}, T_{}, F_{}, a1, b1, a0, b0, false);
     }
+    body(F_{}, F_{}, F_{}, a0, b0, a1, b1, false);
+    body(F_{}, T_{}, T_{}, a1, b1, a0, b0, false);
     // ---- epilogue of tile (mb, nb)
     {
       GEpi e;
       const long m0 = (long)mb * C::BM, n0 = (long)nb * C::BN;
-      e.sbias = (EPI == 0 && bias && !bbf) ? reinterpret_cast<const float*>(smem + C::BIAS + (ti & 3) * 512) : nullptr;
-      e.sbias16 = (EPI == 0 && bias && bbf) ? smem + C::BIAS + (ti & 3) * 512 : nullptr;
-      e.R = R;
       const long rows = N - n0 < C::BN ? N - n0 : C::BN;
       e.obase = O + n0 * ldo;
       e.orec = (int)(rows * ldo * 2);
+      e.R = (F & (F_RES | F_DSILU)) ? R + n0 * ldr : nullptr;
+      e.rrec = (F & (F_RES | F_DSILU)) ? (int)(rows * ldr * 2) : 0;
       e.M = M;
       e.ldo = ldo;
       e.ldr = ldr;
-      e.as = EPI == 1 ? alpha : alpha * scale;
+      e.as = (F & F_DSILU) ? alpha : alpha * scale;
       e.bs = scale;
       e.rs = scale;
-      e.m0 = m0;
-      e.n0 = n0;
-      e.Npix = N;
+      e.m0 = (int)m0;
       e.wm = wm;
       e.wn = wn;
       // an opaque copy of the lane id: the per-lane addressing below cannot be
@@ -399,30 +412,48 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
       float gs[WI][2], gq[WI][2];
 #pragma unroll
       for (int i = 0; i < WI; ++i) gs[i][0] = gq[i][0] = gs[i][1] = gq[i][1] = 0.f;
-      const bool gn = EPI == 0 && gnp != nullptr;
-      g_for(std::make_integer_sequence<int, WI * WJ / 2>{}, [&](auto pc) {
-        constexpr int p = decltype(pc)::value;
-        g_epi_pair<EPI, WI, WJ, p / (WJ / 2), p % (WJ / 2)>(acc, e, gs, gq, gn);
-      });
-      if constexpr (EPI == 0 && WJ >= 4) {
-        if (gn) {
-          float s2[WI][WJ / 4], q2[WI][WJ / 4];
+      const bf16* sb = smem + C::BIAS + (ti & 3) * 512;
+      g_for(std::make_integer_sequence<int, WI>{}, [&](auto ic) {
+        constexpr int ii = decltype(ic)::value;
+        f32x4 cb = {0.f, 0.f, 0.f, 0.f};
+        const int cl = wm * 16 * WI + ii * 16 + (ln >> 4) * 4;       // tile-local channel of the lane
+        if constexpr (F & F_B32) {
+          cb = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(sb) + cl);
+        } else if constexpr (F & F_B16) {
+          const bf16x4 c4 = *reinterpret_cast<const bf16x4*>(sb + cl);
 #pragma unroll
-          for (int i = 0; i < WI; ++i)
-#pragma unroll
-            for (int h = 0; h < WJ / 4; ++h) {
-              s2[i][h] = gs[i][h];
-              q2[i][h] = gq[i][h];
-            }
-          gn_part_store<WI, WJ / 4>(s2, q2, ln, (int)(m0 + wm * 16 * WI), n0 + wn * 16 * WJ, M, gn_groups, gn_hw, N,
-                                    gnp);
+          for (int k = 0; k < 4; ++k) cb[k] = (float)c4[k];
         }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cb[k] *= scale;
+        g_for(std::make_integer_sequence<int, WJ / 2>{}, [&](auto jc) {
+          g_epi_pair<F, WI, WJ, ii, decltype(jc)::value>(acc, e, cb, gs, gq);
+        });
+      });
+      if constexpr ((F & F_GN) && WJ >= 4) {
+        float s2[WI][WJ / 4], q2[WI][WJ / 4];
+#pragma unroll
+        for (int i = 0; i < WI; ++i)
+#pragma unroll
+          for (int h = 0; h < WJ / 4; ++h) {
+            s2[i][h] = gs[i][h];
+            q2[i][h] = gq[i][h];
+          }
+        gn_part_store<WI, WJ / 4>(s2, q2, ln, (int)(m0 + wm * 16 * WI), n0 + wn * 16 * WJ, M, gn_groups, gn_hw, N,
+                                  gnp);
       }
     }
     tile += G;
     if (tile >= ntiles) break;
     ++ti;
     tile_mn(tile, mb, nb);
+    {   // first fragments of the next tile: stage (s / 2) & 1, published by the last body's barrier
+      const bf16* sn = smem + ((s >> 1) & 1) * C::STAGE;
+#pragma unroll
+      for (int j = 0; j < WJ; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(sn + fb0 + j * 16 * G_PK);
+#pragma unroll
+      for (int i = 0; i < WI; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(sn + fa0 + i * 16 * G_PK);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the block ends
 }
@@ -472,12 +503,13 @@ D3D_API int d3d_gemm_nt_ok(int M, int N, int K, int lda, int ldb) {
   return 1;
 }
 
-template <int W, int EPI>
-static void g_launch(int G_, hipStream_t st, const void* A, const void* B, void* O, const float* bias, const void* R,
+template <int W, int F>
+static void g_launch(int G_, hipStream_t st, const void* A, const void* B, void* O, const void* bias, const void* R,
                      int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, int mt, int nt,
-                     int gm, float* gnp, int G, int hw, int bbf) {
-  hipLaunchKernelGGL((gemm_fw_k<W, W, EPI>), dim3(G_), dim3(256), 0, st, (const bf16*)A, (const bf16*)B, (bf16*)O,
-                     bias, (const bf16*)R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, hw, bbf);
+                     int gm, float* gnp, int G, int hw) {
+  hipLaunchKernelGGL((gemm_fw_k<W, W, F>), dim3(G_), dim3(256), 0, st, (const bf16*)A, (const bf16*)B, (bf16*)O,
+                     (const float*)bias, (const bf16*)R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G,
+                     hw);
 }
 
 // epi 0: O = (alpha * A.B^T + bias + R) * scale (+ GroupNorm partials gnp:
@@ -487,11 +519,11 @@ static void g_launch(int G_, hipStream_t st, const void* A, const void* B, void*
 D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, int bias_bf16, const void* R, int M,
                      int N, int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, float* gnp, int G,
                      int hw, int epi, hipStream_t st) {
-  const float* bias = (const float*)bias_;
   if (!d3d_gemm_nt_ok(M, N, K, lda, ldb)) return -1;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)O) & 15) return -1;
   if (ldo % 8 || ldo < M || (R && (ldr % 4 || ldr < M || ((uintptr_t)R & 7)))) return -1;
-  if (epi == 1 && (!R || bias || gnp)) return -1;
+  if (epi == 1 && (!R || bias_ || gnp)) return -1;
+  if (gnp && bias_ && bias_bf16) return -1;
   int W = g_cfg(M, N);
   if (gnp) {
     const int cg = G > 0 ? M / G : 0;
@@ -499,20 +531,27 @@ D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, i
     if (W == 2) W = 4;                         // the partials need whole 64-pixel parts per wave
   }
   const int BT = 32 * W;
-  if (256L * ldo * 2 >= (1L << 31)) return -1;
+  if (256L * ldo * 2 >= (1L << 31) || (R && 256L * ldr * 2 >= (1L << 31)) || (long)M * 2 >= (1L << 31)) return -1;
   const int mt = cdiv(M, BT), nt = cdiv(N, BT);
   const long tiles = (long)mt * nt;
   if (tiles >= (1L << 31)) return -1;
   const int per_cu = W == 8 ? 1 : W == 4 ? 2 : 4;
   const int G_ = (int)std::min<long>(tiles, g_grid > 0 ? g_grid : (long)g_cus() * per_cu);
   const int gm = std::max(1, std::min(mt, g_gm));
-#define G_CASE(W_, E_)                                                                                         \
-  if (W == W_ && epi == E_) {                                                                                  \
-    g_launch<W_, E_>(G_, st, A, B, O, bias, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, \
-                     hw, bias_bf16);                                                                           \
-    return (int)hipGetLastError();                                                                             \
+  const int F = epi == 1 ? F_DSILU
+                          : (bias_ ? (bias_bf16 ? F_B16 : F_B32) : 0) | (R ? F_RES : 0) | (gnp ? F_GN : 0);
+#define G_CASE(W_, F_)                                                                                          \
+  if (W == W_ && F == (F_)) {                                                                                   \
+    g_launch<W_, F_>(G_, st, A, B, O, bias_, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, hw); \
+    return (int)hipGetLastError();                                                                              \
   }
-  G_CASE(8, 0) G_CASE(8, 1) G_CASE(4, 0) G_CASE(4, 1) G_CASE(2, 0) G_CASE(2, 1)
+#define G_CASES(W_)                                                                                             \
+  G_CASE(W_, 0) G_CASE(W_, F_B32) G_CASE(W_, F_B16) G_CASE(W_, F_RES) G_CASE(W_, F_B32 | F_RES)                 \
+  G_CASE(W_, F_B16 | F_RES) G_CASE(W_, F_DSILU)
+  G_CASES(8) G_CASES(4) G_CASES(2)
+  G_CASE(8, F_GN) G_CASE(8, F_B32 | F_GN) G_CASE(8, F_RES | F_GN) G_CASE(8, F_B32 | F_RES | F_GN)
+  G_CASE(4, F_GN) G_CASE(4, F_B32 | F_GN) G_CASE(4, F_RES | F_GN) G_CASE(4, F_B32 | F_RES | F_GN)
+#undef G_CASES
 #undef G_CASE
   return -1;
 }
