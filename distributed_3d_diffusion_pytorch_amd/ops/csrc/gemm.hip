@@ -15,28 +15,34 @@
 // Schedule ("fat waves"): a 256-thread block = 2 x 2 waves, one per SIMD, each
 // owning WI x WJ MFMA 16x16x32 tiles (8 x 8 = 128 x 128 outputs and 256 fp32
 // accumulators for the big layers, 4 x 4 / 2 x 2 for small problems):
-//   * BK = 32, FOUR LDS stages (A rows, then B rows; 64-byte rows with the
-//     chunk swizzle c ^ 3*((row >> 3) & 1): conflict-free ds_read_b128);
-//   * K-tile s: `vmcnt` retires this wave's LDS-DMA of K-tile s + 1, ONE
-//     barrier publishes it, then WI*WJ slots, each one MFMA of K-tile s plus
-//     at most one other instruction: the fragment reads of K-tile s + 1 (into
-//     the other register set), the LDS-DMA pieces of K-tile s + 3 (into the
-//     stage K-tile s - 1 used), the loader's cursor update.  The DMA runs two
-//     K-tiles ahead of its reader and the matrix pipe never waits on a read;
+//   * LDS stages of K = 64 (two MFMA K-steps), two of them: 128-byte rows
+//     (whole cache lines per DMA row) with the chunk swizzle c ^ (row & 7):
+//     conflict-free ds_read_b128;
+//   * K-step s: WI*WJ slots, each one MFMA plus at most one other
+//     instruction -- a fragment read of step s + 1 (into the other register
+//     set) or, in odd steps, an LDS-DMA piece of the stage after next and the
+//     loader's cursor update.  Odd steps open with the wait for the next
+//     stage and the ONLY barrier of the stage;
 //   * the MFMAs are inline asm with "a"-constrained accumulators (the
 //     compiler's own lowering splits 256 accumulators between the register
-//     files and shuffles them every K-tile);
+//     files and shuffles them every K-tile); the epilogue reads them out one
+//     fragment pair at a time (a bulk read ahead of it spilled);
 //   * persistent: each block walks tiles rb, rb + G, ... as ONE stream of
-//     K-tiles, so the next tile's DMA is in flight during the epilogue; the
-//     bias rides on a DMA into one of 4 LDS slots;
-//   * epilogue: fragment pairs become 16-byte rows by v_permlane16_swap and
-//     leave as exactly WI*WJ/2 buffer stores per wave (masked lanes get an
-//     out-of-range offset), so the next tile's counted waits step over them;
+//     stages, so the next tile's DMA is in flight during the epilogue; the
+//     bias rides on a DMA into one of 4 LDS slots; the next tile's first
+//     fragments are read after the epilogue (not held across it);
+//   * epilogue specialised at compile time (flags F): fragment pairs become
+//     16-byte rows by v_permlane16_swap and leave as exactly WI*WJ/2 buffer
+//     stores per wave (masked lanes get an out-of-range offset), so the next
+//     tile's counted waits step over them; explicit fmas, so every variant
+//     rounds alike;
 //   * per-tile buffer descriptors (rows m0 / n0 based): 32-bit offsets for
-//     any operand size, rows past M / N read as zeros;
+//     any operand size, rows past M / N read as zeros; one VGPR per operand
+//     for the DMA offsets (piece rows added by an opaque v_add at the DMA);
 //   * bijective XCD remap + grouped tile order: the tiles an XCD runs at once
 //     share their activation panels.
 #include "common.h"
+#include "mfma_gemm.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -62,45 +68,6 @@ struct GCfg {
   static constexpr int NR = WI + WJ;                     // fragment reads
   static constexpr int NS = WI * WJ / 2;                 // epilogue stores per wave
 };
-
-#define G_BAR()                        \
-  do {                                 \
-    __builtin_amdgcn_sched_barrier(0); \
-    __builtin_amdgcn_s_barrier();      \
-    __builtin_amdgcn_sched_barrier(0); \
-  } while (0)
-
-__device__ __forceinline__ void g_mma(f32x4& c, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void g_mma0(f32x4& c, const bf16x8& a, const bf16x8& b) {   // first K-tile: C = 0
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
-}
-
-// LDS-DMA of 16 bytes per lane from buffer (base, nrec bytes) at voff + soff
-// into lds (wave-uniform base + lane * 16).  Plain (non-template) helpers:
-// the address-space cast and the descriptor are device-only constructs that
-// the host pass of a kernel template must never instantiate.
-__device__ __forceinline__ void g_dma(const void* base, int nrec, void* lds, int voff, int soff) {
-  typedef __attribute__((address_space(3))) void lds_void;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000),
-                                           (lds_void*)lds, 16, voff, soff, 0, 0);
-}
-typedef unsigned g_u4 __attribute__((ext_vector_type(4)));
-typedef unsigned g_u2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ g_u2 g_load8(const void* base, int nrec, int off) {
-  return __builtin_amdgcn_raw_buffer_load_b64(__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000),
-                                              off, 0, 0);
-}
-__device__ __forceinline__ void g_store16(const void* base, int nrec, g_u4 v, int off) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000),
-                                         off, 0, 0);
-}
-
-template <int... I, typename F>
-__device__ __forceinline__ void g_for(std::integer_sequence<int, I...>, F&& f) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
 
 enum : int { F_B32 = 1, F_B16 = 2, F_RES = 4, F_GN = 8, F_DSILU = 16 };
 
@@ -237,11 +204,7 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
     boff = ((wave * (C::BN / 4) + (lane >> 3)) * ldb + chunk * 8) * 2;
   }
   const int astep = 8 * lda * 2, bstep = 8 * ldb * 2;
-  auto piece_off = [](int base, int step) {
-    int r;
-    asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "s"(step), "v"(base));
-    return r;
-  };
+  auto piece_off = [](int base, int step) { return g_vadd(base, step); };
   const int fr = lane & 15, fq = lane >> 4;
   // fragment read offsets (bf16 elements within a stage) of the stage's
   // first K-step; the second K-step is chunk + 4 (offset fh); fragment i is

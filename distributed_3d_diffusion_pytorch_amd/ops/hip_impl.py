@@ -27,12 +27,11 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 
 _ZERO_PAGE: Dict[int, torch.Tensor] = {}
-# FiLM weight gradients: "blas" (hipBLASLt product + segment scatter), "mfma"
-# (split-K MFMA kernel with fused bias sums) or "auto": mfma up to 32 frames
-# per micro-batch (16 examples: the 8-GPU headline's per-GPU share, 33.7 ->
-# 33.2 ms/step), hipBLASLt above (bs128 on one GPU: 792 -> 804 examples/s);
-# profiles/ab_film_wgrad.txt
-_FILM_WGRAD = "auto"
+# FiLM weight gradients: "tn" (the transposed-read split-K MFMA GEMM of
+# wgrad_gemm.hip with the bias sums folded in), "blas" (hipBLASLt product +
+# separate bias sums + segment scatter; profiles/ab_film_wgrad.txt) or "seg"
+# (the 1x1 conv weight-gradient kernel)
+_FILM_WGRAD = "tn"
 
 
 def set_conv_impl(impl: str) -> None:
@@ -1099,6 +1098,31 @@ class _Linear(torch.autograd.Function):
 # gradients (no separate sum pass).  hipBLASLt's own choice for the single
 # mixed-precision GEMM runs 640-950 TF/s on these shapes; 8 (4 for the
 # smallest level) slabs run 910-1160 TF/s (profiles/film_wgrad_split_r2.txt).
+def wgrad_tn(dy: torch.Tensor, x: torch.Tensor, splits: int = 0):
+    """Split-K weight-gradient GEMM (wgrad_gemm.hip): ``dy [P, M]`` (row
+    stride ``dy.stride(0)``) and ``x [P, N]`` bf16 -> ``(ws [used, M, N],
+    bws [used, M], used)`` fp32 partials whose sums over the first axis are
+    ``dy^T @ x`` and the column sums of ``dy`` (bws: ``2 cdiv(N, 256)`` partial
+    rows per split)."""
+    P, M = dy.shape
+    N = x.shape[1]
+    ldy, ldx = dy.stride(0), x.stride(0)
+    if dy.stride(1) != 1 or x.stride(1) != 1 or x.shape[0] != P:
+        raise ValueError("wgrad_tn: row-major [P, C] operands")
+    if not splits:
+        splits = _lib.d3d_wgrad_tn_plan(M, N, P, ldy, ldx)
+    if splits <= 0:
+        raise ValueError(f"wgrad_tn: unsupported shape P={P} M={M} N={N}")
+    bpr = 2 * ((N + 255) // 256)                 # bias partial rows per split
+    buf = torch.empty(splits * M * N + splits * bpr * M, dtype=F32, device=dy.device)
+    ws, bws = buf[: splits * M * N], buf[splits * M * N:]
+    used = _lib.d3d_wgrad_tn(dy.data_ptr(), x.data_ptr(), ws.data_ptr(), bws.data_ptr(), M, N, P, ldy, ldx, splits,
+                             _st())
+    if used <= 0:
+        raise RuntimeError(f"d3d_wgrad_tn failed ({used})")
+    return ws.view(splits, M, N)[:used], bws.view(splits * bpr, M)[: used * bpr], used
+
+
 def _film_wgrad_product(dy: torch.Tensor, x2: torch.Tensor):
     """``dy^T @ x2`` in fp32 as ``nsl`` stacked partial products."""
     rows, S = dy.shape
@@ -1218,11 +1242,19 @@ class _FiLMBatch(torch.autograd.Function):
                 tw = [torch.zeros(w.shape, dtype=F32, device=x2.device) for w in Ws]
                 tb = [torch.zeros(b.shape, dtype=F32, device=x2.device) for b in Bs]
             _ensure_impl()
+            sp_tn = _lib.d3d_wgrad_tn_plan(S, K, rows, S, K) if _FILM_WGRAD == "tn" else 0
+
             def job():
                 row0 = (ctypes.c_int * n)(*offs[:n])
                 wd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tw])
                 bd = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tb])
-                if _FILM_WGRAD == "blas" or (_FILM_WGRAD == "auto" and shp[0] > 32):
+                if sp_tn:
+                    # fp32 split slabs + bias partials from one MFMA launch, then the
+                    # reduction scatters rows into each block's parameter gradients
+                    ws, bws, used = wgrad_tn(dy, x2, sp_tn)
+                    _chk(_lib.d3d_wgrad_scatter(ws.data_ptr(), S, K, used, 1, bws.data_ptr(), bws.shape[0], n, row0,
+                                                wd, bd, _st()), "film_wgrad_scatter")
+                elif _FILM_WGRAD == "blas":
                     # wide FiLM weight gradients ([S, 1024] over every pixel of the
                     # level): the fp32 [S, K] product (stacked split-K slabs) and
                     # the bias column sums are scattered into the parameters'

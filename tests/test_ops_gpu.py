@@ -491,11 +491,11 @@ def test_sampler_step_matches_posterior(H):
     assert abs(nz.mean().item()) < 0.05 and abs(nz.std().item() - 1) < 0.05
 
 
-@pytest.mark.parametrize("blas", [True, False])
+@pytest.mark.parametrize("mode", ["tn", "blas", "seg"])
 @pytest.mark.parametrize("chans,N,Hh", [([128, 128, 256], 4, 8), ([512, 512], 4, 8),
                                         ([128, 256, 384], 32, 32),    # 32768 rows: 8-wave 1x1 wgrad
                                         ([256, 512], 8, 32)])         # 8192 rows: 4 blas slabs
-def test_film_batch_with_gn_film(H, chans, N, Hh, blas):
+def test_film_batch_with_gn_film(H, chans, N, Hh, mode):
     """Level-batched FiLM projection ``dense_i(silu(emb))`` feeding strided
     GN-FiLM: forward, the shared d(scale|shift) buffer, the input gradient
     through the SiLU (GEMM epilogue) and the segmented weight-gradient scatter
@@ -527,13 +527,34 @@ def test_film_batch_with_gn_film(H, chans, N, Hh, blas):
         return [s.grad] + [w.grad for w in ws] + [b.grad for b in bs]
 
     prev = H._FILM_WGRAD
-    H._FILM_WGRAD = "blas" if blas else "mfma"   # hipBLASLt product + scatter, or the split-K MFMA kernel
+    H._FILM_WGRAD = mode       # transposed-read TN GEMM, hipBLASLt product + scatter, or the 1x1 conv wgrad
     try:
         gh, gr = run(True), run(False)
     finally:
         H._FILM_WGRAD = prev
     for a, b in zip(gh, gr):
         assert rel(a, b) < 3e-2, rel(a, b)
+
+
+@pytest.mark.parametrize("P,M,N,ldy,splits", [(16384, 2048, 1024, 2048, 0), (8192, 4608, 1024, 4608, 0),
+                                               (256, 200, 136, 200, 1), (1024, 264, 520, 384, 2),
+                                               (4096, 512, 256, 512, 3), (128, 256, 256, 256, 1)])
+def test_wgrad_tn_matches_fp32(H, P, M, N, ldy, splits):
+    """Transposed-read split-K weight-gradient GEMM (wgrad_gemm.hip): the
+    slabs sum to dy^T x and the bias partials to the column sums of dy, for
+    full 256 x 256 tiles, ragged M / N (past-the-end columns), a column
+    slice of a wider dy (ldy > M) and uneven splits."""
+    torch.manual_seed(3)
+    dyw = torch.randn(P, ldy, device=DEV).to(BF)
+    dy = dyw[:, :M]
+    x = torch.randn(P, N, device=DEV).to(BF)
+    ws, bws, used = H.wgrad_tn(dy, x, splits)
+    assert used >= 1 and ws.shape == (used, M, N)
+    ref = dy.float().t() @ x.float()
+    got = ws.sum(0)
+    assert rel(got, ref) < 1e-4, rel(got, ref)
+    rb = dy.float().sum(0)
+    assert (bws.sum(0) - rb).abs().max().item() <= 1e-3 * rb.abs().max().item() + 1e-3
 
 
 @pytest.mark.parametrize("micro", [2, 0])
