@@ -143,9 +143,35 @@ class Diff3D(nn.Module):
         return mean + var.sqrt() * torch.randn_like(z)
 
     @torch.no_grad()
-    def sample(self, x, R, T, K, w, timesteps: int = 256):
-        """Fixed-conditioning sampler (`train.py:62-78`): x [b,3,H,W] is the
-        conditioning view, R/T [b,2,...] the (condition, target) poses."""
-        smp = DiffusionSampler(self.xunet_denoiser, timesteps, device=self.device)
-        rec = [RecordEntry(x.to(self.device), R[0, 0], T[0, 0])]
-        return smp.sample(rec, R[0, 1], T[0, 1], K if K.dim() == 2 else K[0], w)
+    def sample(self, model=None, img=None, R=None, T=None, K=None, w=None, timesteps: int = 256, *,
+               return_all: bool = True):
+        """Fixed-conditioning CFG sampler with the reference's signature
+        (`lightning/diff3d.py:151-166`): ``sample(model, img, R, T, K, w,
+        timesteps)``.  ``img`` [b, 2, 3, H, W] (frame 0 is the conditioning
+        view, as the reference reads ``img[:, 0]``) or [b, 3, H, W]; ``R`` /
+        ``T`` PER EXAMPLE [b, 2, ...] (condition, target) poses; ``K`` [3, 3]
+        or [b, 3, 3]; ``w`` a scalar or one guidance weight per example;
+        ``model`` None -> this module's denoiser.  Returns the per-step images
+        (numpy [b, 3, H, W] each, like the reference) or, with
+        ``return_all=False``, the final image tensor.  The call without the
+        model argument, ``sample(img, R, T, K, w, ...)``, is accepted too."""
+        if isinstance(model, torch.Tensor):
+            model, img, R, T, K, w = None, model, img, R, T, K
+        net = model if model is not None else self.xunet_denoiser
+        dev = next(net.parameters()).device
+        x = (img[:, 0] if img.dim() == 5 else img).to(dev).float()
+        b = x.shape[0]
+        R = R.to(dev).float()
+        T = T.to(dev).float()
+        K = K.to(dev).float()
+        Kb = K if K.dim() == 3 else K[None].expand(b, 3, 3).contiguous()
+        wt = torch.as_tensor(w, dtype=torch.float32, device=dev).reshape(-1)
+        wt = wt.expand(b).contiguous() if wt.numel() == 1 else wt
+        smp = DiffusionSampler(net, timesteps, device=dev)
+        z = torch.randn_like(x)
+        imgs = []
+        for k in range(timesteps):
+            z = smp.step(z, x, R, T, Kb, wt, k)
+            if return_all:
+                imgs.append(z.float().cpu().numpy())
+        return imgs if return_all else z.float()

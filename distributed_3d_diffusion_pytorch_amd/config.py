@@ -82,6 +82,8 @@ class DistConfig:
     grad_dtype: str = "fp32"         # fp32 | bf16 all-reduce payload
     timeout_s: float = 600.0
     checksum_every: int = 0          # cross-rank parameter checksum cadence
+    force_comm: bool = False         # test switch: bucketed reducer + its collectives even at world 1
+                                     # (a 1-rank RCCL group exercises the multi-GPU step topology)
 
 
 @dataclass

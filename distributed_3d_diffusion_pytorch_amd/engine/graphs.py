@@ -20,7 +20,10 @@ Layout of one step (MI355X, one process per GPU):
       reduction of bucket k runs concurrently with the backward kernels of
       the layers below it, exactly like the eager overlapped step, and only
       the last (small, first-layer) buckets are exposed.  Graph A ends by
-      joining RCCL's stream (work.wait() captured as an edge).
+      joining RCCL's stream (work.wait() captured as an edge).  A bf16
+      payload (dist.grad_dtype) narrows each bucket into a persistent bf16
+      mirror on the collective's stream and widens it back inside the graph.
+      ``dist.force_comm`` runs this topology on a 1-rank RCCL group (tests).
   [world > 1, comm_mode "post"] fallback when a probe capture of an RCCL
       collective fails (or D3D_GRAPH_COMM=0, or gloo): eager all-reduce of the
       flat gradient after graph A in 4 async chunks,
@@ -119,10 +122,12 @@ class GraphedTrainStep:
         self.gA: Optional[torch.cuda.CUDAGraph] = None      # fwd+bwd (+ captured all-reduce)
         self.gA0: Optional[torch.cuda.CUDAGraph] = None     # fwd+bwd without comm (leading micro-batches)
         self.gB: Optional[torch.cuda.CUDAGraph] = None
-        world = trainer.ctx.world
         self.comm_mode = None
-        if world > 1:
-            want = os.environ.get("D3D_GRAPH_COMM", "1") != "0" and trainer.cfg.dist.grad_dtype != "bf16"
+        red = trainer.reducer
+        if red is not None and red.active:
+            # fp32 and bf16 payloads alike (the bf16 mirror is persistent, see
+            # parallel/ddp.py): the collectives are captured inside graph A
+            want = os.environ.get("D3D_GRAPH_COMM", "1") != "0"
             self.comm_mode = "graph" if (want and probe_graph_collective(dev)) else "post"
         # Deferred, overlapped optimizer step (see step()): needs the fused
         # update, the in-graph (or no) reduction and one micro-batch per step.
@@ -313,7 +318,7 @@ class GraphedTrainStep:
         o = tr.optim
         clip = tr.cfg.optim.grad_clip
         o.hparams_to(self.hp, 1.0 / world)        # kernel-argument write: no host wait
-        post = world > 1 and self.comm_mode != "graph"
+        post = self.comm_mode == "post"
         if post and (clip > 0 or want_norm or tr.cfg.dist.grad_dtype == "bf16"):
             g = tr.flat.grad
             if tr.cfg.dist.grad_dtype == "bf16":

@@ -69,8 +69,9 @@ class Trainer:
             raise ValueError(f"global_batch {cfg.global_batch} not divisible by world size {W}")
         self.local_batch = cfg.global_batch // W
         self.reducer = None
-        if W > 1:
-            self.reducer = GradReducer(self.flat, cfg.dist.bucket_mb, cfg.dist.first_bucket_mb, cfg.dist.grad_dtype)
+        if W > 1 or cfg.dist.force_comm:
+            self.reducer = GradReducer(self.flat, cfg.dist.bucket_mb, cfg.dist.first_bucket_mb, cfg.dist.grad_dtype,
+                                       force=cfg.dist.force_comm)
         # Direct gradient sink: HIP weight-gradient kernels deposit straight
         # into the flat gradient buffer (no AccumulateGrad adds) and report
         # completion to the bucketed reducer themselves.

@@ -834,6 +834,16 @@ def _tap_coef(IH, IW, OH, OW, stride, device):
     return m
 
 
+def _sgemm(A, B, C, M, N, K, batch, sa, sb, sc, alpha: float = 1.0, beta: float = 0.0) -> None:
+    """C_b = alpha A_b B_b + beta C_b over fp32 element-strided views
+    (small_gemm.hip); s* = (batch, row, column) strides of each operand."""
+    for t in (A, B, C):
+        if t.dtype != F32 or not t.is_cuda:
+            raise ValueError("_sgemm: fp32 device tensors")
+    _chk(_lib.d3d_sgemm_strided(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, batch, *sa, *sb, *sc, alpha, beta,
+                                _st()), "sgemm_strided")
+
+
 class _CondConv(torch.autograd.Function):
     """Conditioning conv (`xunet.py:292-299,340-350`) on the split ray input:
     MFMA conv over the 51 direction channels (padded to 64) + the constant
@@ -848,8 +858,9 @@ class _CondConv(torch.autograd.Function):
         nd = IC - no
         OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
         wp = packed_weight_slice(weight, no, nd, ICd)
-        W_o = weight.detach()[:, :no].reshape(OC, no, 9)
-        U = torch.einsum("nk,okt->nto", orig_pe, W_o).contiguous()          # [N, 9, OC] fp32
+        # U[n, t, o] = sum_k pe[n, k] W[o, k, t] (origin channels k < no)     [N, 9, OC] fp32
+        U = torch.empty(N, 9, OC, dtype=F32, device=rays_dir.device)
+        _sgemm(orig_pe, weight.detach(), U, N, OC, no, 9, (0, no, 1), (1, 9, IC * 9), (OC, 9 * OC, 1))
         rb = U.sum(1)
         if row_bias is not None:
             rb = rb + row_bias.float()
@@ -883,15 +894,20 @@ class _CondConv(torch.autograd.Function):
             S = torch.empty(N, 8, OC, dtype=F32, device=g.device)
             _chk(_lib.d3d_border_sums(g.data_ptr(), S.data_ptr(), N, OH, OW, OC, _st()), "border_sums")
             stats = torch.cat([per[:, None], S], 1)                         # [N, 9, OC]
-            dU = torch.einsum("tk,nko->nto", _tap_coef(H, W, OH, OW, stride, g.device), stats)
-            dWo = torch.einsum("nto,nk->okt", dU, orig_pe)                  # [OC, no, 9]
+            # dU[n, t, o] = sum_k M[t, k] stats[n, k, o]
+            dU = torch.empty(N, 9, OC, dtype=F32, device=g.device)
+            _sgemm(_tap_coef(H, W, OH, OW, stride, g.device), stats, dU, 9, OC, 9, N, (0, 9, 1), (9 * OC, OC, 1),
+                   (9 * OC, OC, 1))
+            # dW[o, k, t] (+)= sum_n dU[n, t, o] pe[n, k]: straight into the gradient
             tw = SINK.target(weight)
             if tw is not None:
                 tv = tw.view(OC, IC, 9)
-                tv[:, :no].add_(dWo)
+                _sgemm(dU, orig_pe, tv, OC, no, N, 9, (OC, 1, 9 * OC), (0, no, 1), (1, IC * 9, 9), beta=1.0)
                 tv[:, no:].add_(dWd[:, :nd])
                 SINK.done(weight)
             else:
+                dWo = torch.empty(OC, no, 9, dtype=F32, device=g.device)
+                _sgemm(dU, orig_pe, dWo, OC, no, N, 9, (OC, 1, 9 * OC), (0, no, 1), (1, no * 9, 9))
                 dW = torch.cat([dWo, dWd[:, :nd]], 1).reshape(weight.shape)
         if need_b:
             tb = SINK.target(bias)

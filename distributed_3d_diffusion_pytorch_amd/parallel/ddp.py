@@ -19,7 +19,11 @@ Design here (MI355X, 8 GPUs on xGMI, 7 point-to-point links per GPU):
   gradient lands, on RCCL's own stream (``async_op``), so reduction overlaps the
   rest of backward; ``finish()`` makes the compute stream wait on the handles;
 * averaging is folded into the optimizer (``grad_scale = 1/world``) -- no
-  separate divide pass; optional bf16 payload halves link traffic.
+  separate divide pass;
+* optional bf16 payload halves link traffic: each bucket is narrowed into a
+  persistent bf16 mirror on the collective's stream, reduced there, and
+  widened back by ``finish()`` -- no allocation per step, so the same code
+  runs eagerly and captured in the graph step (engine/graphs.py).
 """
 from __future__ import annotations
 
@@ -34,11 +38,16 @@ from .flat import FlatParams
 
 class GradReducer:
     def __init__(self, flat: FlatParams, bucket_mb: float = 64.0, first_bucket_mb: float = 4.0,
-                 grad_dtype: str = "fp32", group=None):
+                 grad_dtype: str = "fp32", group=None, force: bool = False):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # collectives run at world > 1, or when forced (tests: a 1-rank RCCL
+        # group runs the full multi-GPU step topology on one GPU)
+        self.active = self.world > 1 or (force and dist.is_initialized())
         self.grad_dtype = torch.bfloat16 if grad_dtype == "bf16" else torch.float32
+        self.mirror = (torch.empty(flat.grad.numel(), dtype=torch.bfloat16, device=flat.grad.device)
+                       if self.grad_dtype != torch.float32 and self.active else None)
         self.enabled = True
         # buckets over the backward-ordered layout
         self.buckets: List[dict] = []
@@ -89,7 +98,7 @@ class GradReducer:
     def mark_ready(self, i: int) -> None:
         """Parameter i's gradient is complete in the flat buffer (called by the
         autograd hook, or by the HIP gradient sink for kernel-deposited grads)."""
-        if not self.enabled or self.world == 1:
+        if not self.enabled or not self.active:
             return
         b = self.param_bucket[i]
         self._pending[b] -= 1
@@ -104,10 +113,11 @@ class GradReducer:
         view = self.flat.grad[bk["start"]: bk["end"]]
         ctx = self.sink.collective() if self.sink is not None else contextlib.nullcontext()
         with ctx:       # behind the sink's weight-gradient stream (ops/gradsink.py)
-            if self.grad_dtype == torch.float32:
+            if self.mirror is None:
                 self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
             else:
-                tmp = view.to(self.grad_dtype)
+                tmp = self.mirror[bk["start"]: bk["end"]]
+                tmp.copy_(view)                                     # narrow on the collective's stream
                 self._works.append((dist.all_reduce(tmp, group=self.group, async_op=True), tmp, view))
 
     def finish(self) -> None:
@@ -115,7 +125,7 @@ class GradReducer:
         make the current stream wait for every reduction."""
         if self.sink is not None:
             self.sink.join()
-        if self.world == 1 or not self.enabled:
+        if not self.active or not self.enabled:
             self.reset()
             return
         for b in range(len(self.buckets)):
@@ -124,11 +134,7 @@ class GradReducer:
         for w, tmp, view in self._works:
             w.wait()
             if tmp is not None:
-                if tmp.is_cuda:
-                    # tmp was allocated on the sink's side stream; without this
-                    # the allocator may recycle it before the copy below runs
-                    tmp.record_stream(torch.cuda.current_stream(tmp.device))
-                view.copy_(tmp)
+                view.copy_(tmp)                                     # widen (persistent mirror: no recycling)
         self.reset()
 
     @contextlib.contextmanager
@@ -142,7 +148,7 @@ class GradReducer:
             self.enabled = prev
 
     def broadcast_params(self, src: int = 0) -> None:
-        if self.world > 1:
+        if self.active:
             dist.broadcast(self.flat.data, src, group=self.group)
 
     def remove_hooks(self) -> None:

@@ -18,13 +18,14 @@ TINY_OV = {"model.ch": 32, "model.emb_ch": 64, "model.H": 16, "model.W": 16, "da
            "dist.timeout_s": 20.0}
 
 
-def reducer_matches_manual_average(out_dir, bucket_mb):
+def reducer_matches_manual_average(out_dir, bucket_mb, grad_dtype="fp32"):
     from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup, FlatParams, GradReducer
     from helpers import tiny_model, tiny_batch
     ctx = init_distributed("gloo", 60, use_gpu=False)
     m = tiny_model(seed=0).eval()      # no dropout: both passes must be identical
     flat = FlatParams(list(m.parameters()))
-    red = GradReducer(flat, bucket_mb=bucket_mb, first_bucket_mb=bucket_mb / 4)
+    red = GradReducer(flat, bucket_mb=bucket_mb, first_bucket_mb=bucket_mb / 4, grad_dtype=grad_dtype)
+    assert (red.mirror is not None) == (grad_dtype == "bf16")
     assert len(red.buckets) >= 1
     b = tiny_batch(2, seed=10 + ctx.rank)       # different data per rank
     cm = torch.tensor([True, ctx.rank == 0])
@@ -39,8 +40,13 @@ def reducer_matches_manual_average(out_dir, bucket_mb):
     red.finish()
     summed = flat.grad.clone()
     ref = local.clone()
-    dist.all_reduce(ref)
-    ok = torch.allclose(summed, ref, atol=1e-6, rtol=1e-5)
+    if grad_dtype == "bf16":            # the payload is rounded to bf16 before the sum
+        ref = local.to(torch.bfloat16)
+        dist.all_reduce(ref)
+        ok = torch.allclose(summed, ref.float(), atol=1e-6, rtol=1e-5)
+    else:
+        dist.all_reduce(ref)
+        ok = torch.allclose(summed, ref, atol=1e-6, rtol=1e-5)
     with open(os.path.join(out_dir, f"r{ctx.rank}.txt"), "w") as f:
         f.write(f"{int(ok)} {len(red.buckets)}")
     cleanup()

@@ -49,7 +49,16 @@ def test_diff3d_api(srn):
     assert abs(m.optimizers().param_groups[0]["lr"] - 0.0) < 1e-12
     m.training_step(batch)
     assert abs(m.optimizers().param_groups[0]["lr"] - 0.25e-4) < 1e-12
-    x = batch[0][:, 0]
-    out = m.sample(x, batch[1].float(), batch[2].float(), batch[3][0].float(), torch.tensor([0.0, 2.0]),
-                   timesteps=2)
-    assert out.shape == (2, 3, 16, 16) and torch.isfinite(out).all()
+    # reference signature: sample(model, img, R, T, K, w, timesteps) -> per-step list
+    imgs = m.sample(m.xunet_denoiser, batch[0], batch[1].float(), batch[2].float(), batch[3][0].float(),
+                    torch.tensor([0.0, 2.0]), timesteps=2)
+    assert len(imgs) == 2 and imgs[-1].shape == (2, 3, 16, 16) and np.isfinite(imgs[-1]).all()
+    # per-example poses are honoured: swapping example 1's target pose changes only example 1
+    R2 = batch[1].float().clone()
+    R2[1, 1] = torch.linalg.qr(torch.randn(3, 3))[0]
+    torch.manual_seed(1)
+    a = m.sample(batch[0][:, 0], batch[1].float(), batch[2].float(), batch[3][0].float(), 2.0, timesteps=2,
+                 return_all=False)
+    torch.manual_seed(1)
+    c = m.sample(None, batch[0], R2, batch[2].float(), batch[3][0].float(), 2.0, timesteps=2, return_all=False)
+    assert torch.allclose(a[0], c[0]) and not torch.allclose(a[1], c[1])

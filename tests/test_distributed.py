@@ -9,9 +9,11 @@ from distributed_3d_diffusion_pytorch_amd.parallel import spawn
 import dist_workers as W
 
 
-@pytest.mark.parametrize("bucket_mb", [64.0, 0.05])
-def test_bucketed_allreduce_equals_sum(tmp_path, bucket_mb):
-    spawn(W.reducer_matches_manual_average, 2, (str(tmp_path), bucket_mb))
+@pytest.mark.parametrize("bucket_mb,grad_dtype", [(64.0, "fp32"), (0.05, "fp32"), (0.05, "bf16")])
+def test_bucketed_allreduce_equals_sum(tmp_path, bucket_mb, grad_dtype):
+    """Bucketed hooks == one all-reduce of the local gradient; the bf16
+    payload (persistent mirror, narrowed per bucket) == a bf16 all-reduce."""
+    spawn(W.reducer_matches_manual_average, 2, (str(tmp_path), bucket_mb, grad_dtype))
     res = [open(tmp_path / f"r{r}.txt").read().split() for r in range(2)]
     assert all(r[0] == "1" for r in res), res
     if bucket_mb < 1:

@@ -621,6 +621,29 @@ def test_cond_conv_split_matches_full_conv(H, s):
         assert rel(a, c) < 3e-2, (name, rel(a, c))
 
 
+def test_sgemm_strided_matches_einsum(H):
+    """Strided batched fp32 GEMM (small_gemm.hip) on the conditioning conv's
+    three permuted products == the fp32 einsums, incl. beta accumulation."""
+    torch.manual_seed(5)
+    N, OC, IC, no = 6, 200, 144, 93
+    pe = torch.randn(N, no, device=DEV)
+    w = torch.randn(OC, IC, 3, 3, device=DEV)
+    U = torch.empty(N, 9, OC, device=DEV)
+    H._sgemm(pe, w, U, N, OC, no, 9, (0, no, 1), (1, 9, IC * 9), (OC, 9 * OC, 1))
+    ref = torch.einsum("nk,okt->nto", pe, w[:, :no].reshape(OC, no, 9))
+    assert rel(U, ref) < 1e-5
+    M9 = torch.randn(9, 9, device=DEV)
+    st = torch.randn(N, 9, OC, device=DEV)
+    dU = torch.empty(N, 9, OC, device=DEV)
+    H._sgemm(M9, st, dU, 9, OC, 9, N, (0, 9, 1), (9 * OC, OC, 1), (9 * OC, OC, 1))
+    assert rel(dU, torch.einsum("tk,nko->nto", M9, st)) < 1e-5
+    tgt = torch.randn(OC, IC, 3, 3, device=DEV)
+    want = tgt.clone()
+    want.view(OC, IC, 9)[:, :no] += torch.einsum("nto,nk->okt", dU, pe)
+    H._sgemm(dU, pe, tgt.view(OC, IC, 9), OC, no, N, 9, (OC, 1, 9 * OC), (0, no, 1), (1, IC * 9, 9), beta=1.0)
+    assert rel(tgt, want) < 1e-5
+
+
 def test_ray_dir_matches_torch(H):
     torch.manual_seed(2)
     B, Hh = 3, 16
@@ -900,6 +923,66 @@ def _graph_comm_worker(out_dir):
     with open(os.path.join(out_dir, f"gc{ctx.rank}.txt"), "w") as f:
         f.write(f"{(pe - pg).abs().max().item()} {de} {dg} {max(abs(a - b) for a, b in zip(le, lg))} {mode}")
     cleanup()
+
+
+def _graph_comm_1rank_worker(out_dir):
+    """The multi-GPU step topology on ONE GPU: a 1-rank RCCL group with the
+    bucketed reducer forced on (dist.force_comm), so graph A is captured with
+    the real bucket all-reduces, the sink's collective flushes, the
+    conditioning stream and the deferred update -- against the eager bucketed
+    step, for fp32 and bf16 gradient payloads."""
+    import datetime
+    import torch.distributed as dist
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.parallel import DistContext, cleanup
+    from distributed_3d_diffusion_pytorch_amd.parallel.dist import rccl_env_defaults
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    rccl_env_defaults()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, timeout=datetime.timedelta(seconds=120))
+    ctx = DistContext(device=dev)
+    data = SyntheticBatches(4, 32, "cuda", seed=21)
+    batches = [next(data) for _ in range(3)]
+    lines = []
+    for gd in ("fp32", "bf16"):
+        res = []
+        for graph in (False, True):
+            cfg = make_config(None, {"model.H": 32, "model.W": 32, "data.imgsize": 32, "global_batch": 4,
+                                     "micro_batch": 0, "data.synthetic": True, "log_every": 0, "ckpt_every": 0,
+                                     "graph": graph, "optim.warmup_examples": 8, "dist.bucket_mb": 16.0,
+                                     "dist.grad_dtype": gd, "dist.force_comm": True})
+            tr = Trainer(cfg, ctx)
+            assert tr.reducer is not None and tr.reducer.active
+            losses = [float(tr.train_step(*b)) for b in batches]
+            g = tr._graphed
+            mode = f"{g.comm_mode}/{int(g.defer)}" if g is not None else "eager"
+            tr.sync()
+            res.append((losses, tr.flat.data.clone(), mode))
+            del tr
+        (le, pe, _), (lg, pg, mode) = res
+        lines.append(f"{gd} {(pe - pg).abs().max().item()} {max(abs(a - b) for a, b in zip(le, lg))} {mode}")
+    with open(os.path.join(out_dir, "gc1.txt"), "w") as f:
+        f.write("\n".join(lines))
+    cleanup()
+
+
+def test_graph_step_captured_collectives_one_rank(tmp_path):
+    """Graph A captured with the real bucketed RCCL all-reduces (1-rank
+    group), deferred update on, fp32 and bf16 payloads: comm_mode "graph",
+    parameters equal to the eager bucketed step within 5e-4."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from distributed_3d_diffusion_pytorch_amd.parallel import spawn
+    import test_ops_gpu as me
+    spawn(me._graph_comm_1rank_worker, 1, (str(tmp_path),))
+    rows = open(tmp_path / "gc1.txt").read().split("\n")
+    assert [r.split()[0] for r in rows] == ["fp32", "bf16"]
+    for r in rows:
+        gd, d, dl, mode = r.split()
+        assert mode == "graph/1", r
+        assert float(d) < 5e-4 and float(dl) < 2e-3, r
 
 
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs 2 GPUs (RCCL: one rank per device)")

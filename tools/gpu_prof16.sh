@@ -1,19 +1,21 @@
-# rocprofv3 kernel trace of the steady-state graph step at per-GPU batch 16 and 32
-# (the 8- and 4-GPU shares of the global batch 128): per-kernel ms/step over the
-# last STEPS steps only (tools/rpstats.py --window), plus per-grid rows.
+# bs16 (the 8-GPU per-GPU share) steady-state trace: rocprofv3 kernel trace of
+# 20 replayed steps; rpstats over the last 5 steps: per-kernel stats with the
+# kernel count, device busy share and idle gaps.  Summaries under gpurun_out/p16.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
-O=/root/repo/gpurun_out/${TAG:-prof}
+O=/root/repo/gpurun_out/p16
 mkdir -p $O
-for B in ${BS:-16 32}; do
-  timeout -k 10 300 rocprofv3 --kernel-trace -d $O/rp$B -o run -- python3 /root/repo/bench.py --steps 20 --warmup 3 --global_batch $B > $O/b$B.json 2> $O/b$B.err || exit $?
-  db=$(find $O/rp$B -name '*.db' | head -n1)
-  ms=$(python3 -c "import json;print(json.load(open('$O/b$B.json'))['ms_per_step'])")
-  W=$(python3 -c "print(10*$ms)")
-  python3 /root/repo/tools/rpstats.py "$db" --window $W --steps 10 --top 90 > $O/bs${B}_stats.txt
-  python3 /root/repo/tools/rpstats.py "$db" --window $W --steps 10 --top 160 --grid > $O/bs${B}_grid.txt
-  python3 /root/repo/tools/rpstats.py "$db" --busy $W >> $O/bs${B}_stats.txt
-  python3 /root/repo/tools/rpstats.py "$db" --solo $W --steps 10 --top 60 > $O/bs${B}_solo.txt
-  python3 /root/repo/tools/rpstats.py "$db" --gaps $W --steps 10 --top 40 > $O/bs${B}_gaps.txt
-  find $O/rp$B -name '*.db' -delete
-done
+timeout -k 10 600 rocprofv3 --kernel-trace -d $O/db -o run -- python3 /root/repo/bench.py --steps 20 --warmup 3 --global_batch 16 > $O/bench.log 2>&1
+rc=$?
+tail -n1 $O/bench.log | cut -c1-200
+db=$(find $O/db -name '*.db' | head -n1)
+if [ -n "$db" ]; then
+  W=${WIN:-140}
+  python3 /root/repo/tools/rpstats.py "$db" --window $W --steps 5 --top 70 > $O/stats.txt
+  python3 /root/repo/tools/rpstats.py "$db" --busy $W > $O/busy.txt
+  python3 /root/repo/tools/rpstats.py "$db" --gaps $W --top 25 > $O/gaps.txt
+  python3 /root/repo/tools/rpstats.py "$db" --solo $W --top 40 > $O/solo.txt
+  find $O/db -name '*.db' -delete
+fi
+head -3 $O/stats.txt; cat $O/busy.txt | head -5; head -8 $O/gaps.txt
+exit $rc
