@@ -128,6 +128,11 @@ class GradSink:
         module doc).  ``keep``: tensors the work reads that autograd may free
         right after the enclosing backward returns."""
         if not (self.stream_enabled and dev.type == "cuda") or torch.cuda.is_current_stream_capturing():
+            if self._compute and dev.type == "cuda":
+                # no side stream, but deposits may come from a registered
+                # compute stream (the conditioning stream): the end-of-backward
+                # join must still make the optimizer's stream wait for it
+                self._queue_end_callback()
             yield
             return
         idx = dev.index if dev.index is not None else torch.cuda.current_device()
@@ -179,7 +184,12 @@ class GradSink:
         deferral on: queued and flushed in batches behind one fork each."""
         if (self.stream_enabled and self.graph_defer and dev.type == "cuda"
                 and torch.cuda.is_current_stream_capturing()):
-            self._queue.append((fn, tuple(t for t in keep if t is not None), tuple(p for p in done if p is not None)))
+            # the submitting stream travels with the job: its inputs were
+            # produced there, and it need not be the stream that flushes
+            # (conditioning-stream jobs are often flushed from the compute
+            # stream -- see flush())
+            self._queue.append((fn, tuple(t for t in keep if t is not None), tuple(p for p in done if p is not None),
+                                torch.cuda.current_stream(dev.index if dev.index is not None else None)))
             self._queue_end_callback()
             if len(self._queue) >= self.defer_batch:
                 self.flush()
@@ -198,15 +208,27 @@ class GradSink:
         q, self._queue = self._queue, []
         idx = torch.cuda.current_device()
         side = self._side(idx)
-        side.wait_stream(torch.cuda.current_stream(idx))
+        # wait for every stream a queued job was submitted from, not only the
+        # flushing one: a job queued from the conditioning stream's backward
+        # (logSNR MLP, conditioning convs, level-batched FiLM) reads inputs
+        # that stream produced, and the batch is usually flushed from the
+        # compute stream.  Waiting on the flushing stream alone let those
+        # jobs read their inputs before they were written (run-to-run
+        # differences of the conditioning gradients in the replayed step,
+        # tests/test_ops_gpu.py::test_graph_step_bitwise_deterministic).
+        waited = []
+        for st in [torch.cuda.current_stream(idx)] + [j[3] for j in q]:
+            if all(st.cuda_stream != w.cuda_stream for w in waited):
+                side.wait_stream(st)
+                waited.append(st)
         with torch.cuda.stream(side):
-            for fn, _, _ in q:
+            for fn, _, _, _ in q:
                 fn()
-        for _, keep, _ in q:
+        for _, keep, _, _ in q:
             for t in keep:
                 t.record_stream(side)
         self._forked.add(idx)
-        for _, _, done in q:
+        for _, _, done, _ in q:
             for p in done:
                 self.done(p)
 

@@ -782,6 +782,52 @@ def test_training_step_bitwise_deterministic():
         assert torch.equal(runs[0][1], r[1]), (runs[0][1] - r[1]).abs().max().item()
 
 
+def test_graph_step_bitwise_deterministic():
+    """Race screen of the REPLAYED step (the 8-GPU per-GPU share):
+    64x64, batch 16, one micro-batch, graph=True -- so the captured step runs
+    the deferred overlapped update (update stream + parameter fence), the
+    conditioning stream and the in-graph weight-gradient side stream (jobs
+    flushed 8 per fork).  Two identical 4-step runs must agree bit for bit in
+    losses, parameters, Adam moments and the EMA-free flat gradient; a third
+    run with the weight-gradient side stream off must too (every reduction has
+    a fixed order, so stream placement may not change a bit)."""
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.parallel import DistContext
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    from distributed_3d_diffusion_pytorch_amd.ops.gradsink import SINK
+    from distributed_3d_diffusion_pytorch_amd.ops import hip_impl
+    ctx = DistContext(device=torch.device("cuda", 0))
+    data = SyntheticBatches(16, 64, "cuda", seed=33)
+    batches = [next(data) for _ in range(4)]
+    runs = []
+    prev = SINK.stream_enabled
+    try:
+        for side in (True, True, False):
+            SINK.stream_enabled = side
+            torch.manual_seed(0)
+            cfg = make_config(None, {"model.H": 64, "model.W": 64, "data.imgsize": 64, "global_batch": 16,
+                                     "micro_batch": 0, "data.synthetic": True, "log_every": 0, "ckpt_every": 0,
+                                     "graph": True, "optim.warmup_examples": 32})
+            tr = Trainer(cfg, ctx)
+            losses = [tr.train_step(*b).item() for b in batches]
+            g = tr._graphed
+            assert g is not None and g.defer, "graph step with the deferred update expected"
+            tr.sync()
+            torch.cuda.synchronize()
+            runs.append((losses, tr.flat.data.clone(), tr.optim.exp_avg.clone(), tr.optim.exp_avg_sq.clone()))
+            del tr, g
+    finally:
+        SINK.stream_enabled = prev
+        hip_impl.set_device_seed(None)
+    ref = runs[0]
+    assert all(math.isfinite(v) for v in ref[0]), ref[0]
+    for r in runs[1:]:
+        assert ref[0] == r[0], (ref[0], r[0])
+        for a, b in zip(ref[1:], r[1:]):
+            assert torch.equal(a, b), (a - b).abs().max().item()
+
+
 @pytest.mark.parametrize("kind", ["conv_res", "linear_res", "nin_input"])
 def test_residual_grad_slot(H, kind):
     """ResGradSlot: the residual branch's gradient of x handed to the
