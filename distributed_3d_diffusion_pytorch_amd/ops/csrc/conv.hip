@@ -1078,10 +1078,12 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     for (int c = 0; c < NCH; ++c) {
 #pragma unroll 1
       for (int t = 0; t < 9; ++t, ++s) {
+        // (lgkmcnt(0): the prefetched fragments of this slot must be read
+        // before the barrier frees it for the DMA below)
         if (t >= 1 && t <= 3) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + Gm::HPW) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 + Gm::HPW) : "memory");
         } else {
-          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
         }
         __builtin_amdgcn_s_barrier();
         halo_issue_a(sAr + ((s + 4) & 3) * Gm::ABUF, Wp, w_bytes, aoff, a_soff(s + 4), wave);

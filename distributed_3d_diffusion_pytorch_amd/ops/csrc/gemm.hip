@@ -298,8 +298,15 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
                   bf16x8(&nbf)[WJ], bool after_epi) {
     constexpr bool ODD = decltype(odd)::value, LAST = decltype(last)::value;
     if constexpr (ODD) {
-      if (after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // lgkmcnt(0): this wave's fragment reads of the stage the DMAs below
+      // refill (issued in the previous body) must have completed before the
+      // barrier frees that stage.  Without it another wave's DMA could land
+      // on top of a read still queued in the LDS pipeline -- which happened
+      // whenever an LDS-heavy kernel shared the CU (the per-pixel weight
+      // gradients on the side stream): wrong GEMM outputs under co-residency
+      // (tools/stress_concurrent.py, profiles/race_graph_wgrad_flush_r3.txt).
+      if (after_epi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(C::NS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       G_BAR();
     }
     // next K-step's fragments: second half of this stage, or first half of the next

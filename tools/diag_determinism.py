@@ -171,7 +171,13 @@ def main():
         for s, (ga, gb) in enumerate(zip(ref["grads"], r["grads"])):
             d = (ga - gb).abs()
             rows, n = where(d, spans, ref["names"])
-            print(f"   step {s} grad: {n} params differ; top {rows}", flush=True)
+            # relative size: |difference| against the gradient's own magnitude
+            rel = []
+            for name, cnt, mx in rows[:4]:
+                i = ref["names"].index(name)
+                off, numel = spans[i]
+                rel.append(f"{name}: |g|max {ga[off:off + numel].abs().max().item():.1e}")
+            print(f"   step {s} grad: {n} params differ; top {rows}; {rel}", flush=True)
 
 
 if __name__ == "__main__":
