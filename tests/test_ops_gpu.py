@@ -1318,3 +1318,34 @@ def test_ray_conditioning_prep(H, rescale):
     assert dh.shape == dr.shape == (2 * B, Hh, W, 64)
     assert rel(dh, dr) < 1e-2
     assert dh[..., 51:].abs().max().item() == 0.0
+
+
+def test_kernels_bitwise_under_coresidency():
+    """Race screen: the dense-layer GEMM, convs, weight
+    gradients, attention and GroupNorm kernels give bit-identical results
+    alone and while another HIP stream keeps LDS-heavy kernels (the per-pixel
+    weight gradients of the side stream) resident on the same CUs
+    (tools/stress_concurrent.py; a missing LDS-read retirement in the GEMM
+    produced wrong outputs only in this situation)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import stress_concurrent as S
+    side = torch.cuda.Stream()
+    noise = S.noise_setup("wgrad1x1")
+    bad = []
+    for name, f in S.cases():
+        ref = f().clone()
+        torch.cuda.synchronize()
+        for i in range(6):
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                noise()
+            for _ in range(i % 3):
+                torch.empty(1, device=DEV).zero_()
+            o = f()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            if not torch.equal(o, ref):
+                bad.append(name)
+                break
+    assert not bad, bad
