@@ -198,6 +198,10 @@ def main() -> None:
                        "backend": "hip" if (ctx.device.type == "cuda" and use_hip(probe)) else "torch"},
             "final_loss": lv,
             "hbm_peak_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if ctx.device.type == "cuda" else None,
+            # caching-allocator retries (a full cache flush + device sync each): non-zero means the step
+            # ran at the HBM limit and paid for it
+            "alloc_retries": torch.cuda.memory_stats().get("num_alloc_retries", 0) if ctx.device.type == "cuda"
+            else None,
         }
         print(json.dumps(out), flush=True)
     cleanup()

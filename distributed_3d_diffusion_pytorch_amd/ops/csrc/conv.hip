@@ -33,6 +33,8 @@
 #include "common.h"
 #include <stdlib.h>
 
+#include <algorithm>
+
 D3D_API int d3d_colsum(const float* in, long R, int Cc, float* part, float* out, float* out_odd, int accumulate,
                        hipStream_t st);
 
@@ -2694,6 +2696,41 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
                       int gn_groups, int* gn_done, hipStream_t st) {
   long Mpix = (long)N * OH * OW;
   if (gn_done) *gn_done = 0;
+  // Operands beyond the kernels' 32-bit buffer offsets (2 GiB: e.g. the
+  // 256-channel decoder concat of 128x128 images at one micro-batch of 128):
+  // run the conv over image chunks that fit, each at full speed, instead of
+  // dropping to the register-staged fallback.  Chunk boundaries are multiples
+  // of res_nmod (the broadcast residual's period); per-image operands
+  // (output, per-image bias rows, GroupNorm partial slots) are offset, the
+  // split-K workspace is reused chunk after chunk on the stream.
+  {
+    const long img_in = (long)IH * IW * IC * 2, img_out = (long)OH * OW * ldo * 2;
+    const long lim = (1L << 31) - (1L << 20);
+    if (N > 1 && ((long)N * img_in >= lim || (long)N * img_out >= lim)) {
+      long per = lim / std::max(img_in, img_out);
+      const int q = res_nmod > 0 ? res_nmod : 1;
+      per = per / q * q;
+      if (per >= 1) {
+        const int parts_per_img = (OH * OW) % 64 == 0 ? OH * OW / 64 : 0;
+        int all_gn = 1;
+        for (int n0 = 0; n0 < N; n0 += (int)per) {
+          const int nc = (int)std::min<long>(per, N - n0);
+          int d = 0;
+          const int rc = d3d_conv2((const char*)I + n0 * img_in, Wp, bias,
+                                   row_bias ? row_bias + (long)n0 * OC : nullptr,
+                                   res ? (res_nmod > 0 ? res : (const char*)res + n0 * img_out) : nullptr,
+                                   (char*)O + n0 * img_out, nc, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans, scale,
+                                   res_nmod, taps, ws, nsplit,
+                                   gnp ? gnp + (long)n0 * gn_groups * parts_per_img * 2 : nullptr, gn_groups,
+                                   gn_done ? &d : nullptr, st);
+          if (rc) return rc;
+          all_gn &= d;
+        }
+        if (gn_done) *gn_done = gnp ? all_gn : 0;
+        return 0;
+      }
+    }
+  }
   if (gnp) {
     const int Cg = gn_groups > 0 && OC % gn_groups == 0 ? OC / gn_groups : 0;
     const bool ok = (Cg == 4 || Cg == 8 || Cg == 16 || Cg == 32) && (OH * OW) % 64 == 0 && Mpix % 64 == 0 &&
@@ -2907,11 +2944,13 @@ static void launch_wgrad(const void* dY, const void* I, float* ws, int N, int IH
   const bool wide_long = taps == 1 && (long)OC * IC >= (4L << 20) && pps > 16384;
   // the dY descriptor is re-based per stage (its records span one split), so
   // only the input tensor's size is limited by the 32-bit offsets
-  if (g_wgrad_impl >= 5 && !wide_long && in_elems * 2 < (1L << 30) && (long)pps * OC * 2 < (1L << 31)) {
+  // (the FAST path measured slower on the 144-channel conditioning conv:
+  // keep it to full 128-channel tiles).  FAST re-bases the input descriptor
+  // per stage, so only the general path is bounded by 32-bit input offsets.
+  const bool fast = stride == 1 && lw >= 0 && IH == OH && IW == OW && IC % 128 == 0;
+  if (g_wgrad_impl >= 5 && !wide_long && (fast || in_elems * 2 < (1L << 31) - (1L << 20)) &&
+      (long)pps * OC * 2 < (1L << 31)) {
     constexpr int PK = 32;
-    // (the FAST path measured slower on the 144-channel conditioning conv:
-    // keep it to full 128-channel tiles)
-    const bool fast = stride == 1 && lw >= 0 && IH == OH && IW == OW && IC % 128 == 0;
 #define WB(TP, F)                                                                                                \
   hipLaunchKernelGGL((conv_wgrad_bufl_k<TP, PK, F>), grid, dim3(256), 0, st, (const bf16*)dY, (const bf16*)I, ws,   \
                      (long)N * IH * IW, N, IH, IW, IC, OH, OW, OC, stride, pps, ncb, bws, lw, lh, (const bf16*)I2, C1)
@@ -2988,7 +3027,8 @@ static bool wgrad_w8_1x1() {
 static bool wgrad_w8_ok(int taps, int IH, int IW, int OH, int OW, int IC, int OC, int stride, long in_elems, int* bm,
                         int* bn) {
   auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
-  if (g_wgrad_impl != 6 || IC % 128 || OC % 8 || in_elems * 2 >= (1L << 30)) return false;
+  // (the input descriptor is re-based per stage: no bound on the input size)
+  if (g_wgrad_impl != 6 || IC % 128 || OC % 8) return false;
   if (taps == 1) {
     if (!wgrad_w8_1x1() || stride != 1 || IH != OH || IW != OW) return false;
   } else if (taps != 9 || stride != 1 || IH != OH || IW != OW || !pow2(OH) || !pow2(OW)) {

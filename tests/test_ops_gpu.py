@@ -1349,3 +1349,33 @@ def test_kernels_bitwise_under_coresidency():
                 bad.append(name)
                 break
     assert not bad, bad
+
+
+def test_conv_operands_beyond_2gib(H):
+    """Large-operand path (128x128 images at one micro-batch of 128): a 3x3
+    conv whose input exceeds the kernels' 32-bit buffer offsets runs as
+    image chunks at full speed (d3d_conv2), and the weight gradient over a
+    > 1 GiB input stays on the descriptor-rebased fast kernels; both against
+    the fp32 torch composition."""
+    torch.manual_seed(0)
+    N, Hh, IC, OC = 132, 128, 512, 64                  # input 2.2 GB bf16
+    x = (torch.randn(N, Hh, Hh, IC, device=DEV) * 0.5).to(BF)
+    w = torch.randn(OC, IC, 3, 3, device=DEV) * 0.02
+    b = torch.randn(OC, device=DEV) * 0.1
+    y = H.conv3x3(x, w, b)
+    for sl in (slice(0, 3), slice(125, 132)):          # both chunks
+        ref = F.conv2d(x[sl].permute(0, 3, 1, 2).float(), w, b, padding=1).permute(0, 2, 3, 1)
+        assert rel(y[sl], ref) < 1e-2, rel(y[sl], ref)
+    del y
+    # weight gradient over a 1.07 GB input (128 channels, 256 frames of 128x128)
+    N2, C2 = 256, 128
+    x2 = (torch.randn(N2, Hh, Hh, C2, device=DEV) * 0.5).to(BF)
+    g2 = (torch.randn(N2, Hh, Hh, C2, device=DEV) * 0.5).to(BF)
+    dW, db = H._wgrad(g2, x2, C2, C2, N2, Hh, Hh, Hh, Hh, 1, 9, want_bias=True)
+    ref = torch.zeros(C2, C2, 3, 3, device=DEV)
+    for s in range(0, N2, 32):
+        ref += torch.nn.grad.conv2d_weight(x2[s:s + 32].permute(0, 3, 1, 2).float(), (C2, C2, 3, 3),
+                                           g2[s:s + 32].permute(0, 3, 1, 2).float(), padding=1)
+    assert rel(dW.reshape(C2, C2, 3, 3), ref) < 1e-3, rel(dW.reshape(C2, C2, 3, 3), ref)
+    rb = g2.float().sum((0, 1, 2))
+    assert (db - rb).abs().max().item() <= 1e-3 * rb.abs().max().item() + 1e-2

@@ -1,5 +1,4 @@
-# bs16 (8-GPU per-GPU share) graph step under HIP runtime settings that govern
-# how far the host can enqueue ahead of the device (interleaved, 2 rounds)
+# bs16 graph step under HIP runtime settings: host wait policy / queues (interleaved, 2 rounds)
 set -o pipefail
 O=gpurun_out/envab
 mkdir -p $O
@@ -10,8 +9,9 @@ run() {  # name, env...
 }
 for r in 1 2; do
   run base$r X=1
-  run aql64k$r ROC_AQL_QUEUE_SIZE=65536
-  run pktcap1_$r DEBUG_CLR_GRAPH_PACKET_CAPTURE=1
-  run pktcap0_$r DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run wait1s$r ROC_ACTIVE_WAIT_TIMEOUT=1000000
+  run wait0$r ROC_ACTIVE_WAIT_TIMEOUT=0
   run hwq8_$r GPU_MAX_HW_QUEUES=8
+  run hwq8w$r GPU_MAX_HW_QUEUES=8 ROC_ACTIVE_WAIT_TIMEOUT=1000000
+  run hwq16_$r GPU_MAX_HW_QUEUES=16
 done
