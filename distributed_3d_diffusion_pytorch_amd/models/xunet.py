@@ -36,6 +36,8 @@ INV_SQRT2 = 1.0 / math.sqrt(2.0)
 
 
 _COND_STREAM = os.environ.get("D3D_COND_STREAM", "1") != "0"
+# conditioning stream: one FiLM GEMM + ready event per block instead of one per level
+FILM_BLOCK_EVENTS = True
 _COND_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
 # (level, event): parameters outside the early update part become valid at
 # `event` -- the trunk waits on it before encoder level `level` and the
@@ -532,14 +534,16 @@ class XUNet(nn.Module):
                     if fence is not None and i == fence[0]:
                         cs.wait_event(fence[1])
                     outs = ops.film_batch(semb, [b.film.dense.weight for b in blocks],
-                                          [b.film.dense.bias for b in blocks])
+                                          [b.film.dense.bias for b in blocks], block_events=FILM_BLOCK_EVENTS)
                     for o in outs:
                         o.record_stream(main)       # read by the trunk's GN-FiLM kernels
                     ev = torch.cuda.Event()
                     ev.record(cs)
                     for b, o in zip(blocks, outs):
                         b.__dict__["_ss"] = o
-                        b.__dict__["_ss_event"] = ev     # the block waits right before its GN-FiLM
+                        # the block waits right before its GN-FiLM, for its own slice when the
+                        # projection ran per block
+                        b.__dict__["_ss_event"] = getattr(o, "_d3d_ready", ev)
                     events.append(ev)
                     sembs.append(semb)
         elif ss_map is not None or self.batch_film:

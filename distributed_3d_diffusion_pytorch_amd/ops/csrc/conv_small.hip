@@ -45,22 +45,32 @@ __device__ __forceinline__ void lds_wait(bf16x8 (&a)[2], bf16x8 (&b)[2]) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]) :: "memory");
 }
 
-constexpr int S64_BM = 64, S64_BN = 64, S64_BK = 64, S64_NS = 4;
+constexpr int S64_BM = 64, S64_BN = 64, S64_BK = 64;
 
-template <int TAPS, bool TRANS>
-__global__ void __launch_bounds__(256, 2)
+// G wave groups (4 waves each) split the K-steps of one 64 x 64 tile
+// round-robin (group g takes k-steps g, g + G, ...), each through its own
+// NS-stage LDS ring; at the end groups 1.. hand their accumulators to group 0
+// through LDS and group 0 sums them in a fixed order (deterministic) and runs
+// the epilogue.  G > 1 puts 2-4x the waves on a CU for the small grids (the
+// 8x8 / 16x16 levels at batch 16 give only 256-512 tiles): more loads and
+// MFMAs in flight per CU where one 4-wave block per tile was latency-bound.
+template <int TAPS, bool TRANS, int G = 1, int NS = 4>
+__global__ void __launch_bounds__(256 * G, G == 1 ? 2 : 1)
 conv_s64_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
            const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
            int w_bytes, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
            float scale, int res_nmod, float* __restrict__ gnp, int gn_groups) {
-  constexpr int BM = S64_BM, BN = S64_BN, BK = S64_BK, NS = S64_NS;
+  constexpr int BM = S64_BM, BN = S64_BN, BK = S64_BK;
   constexpr int STAGE = (BM + BN) * BK;                 // elements
-  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
+  static_assert(G * NS * STAGE * 2 <= 160 * 1024 - 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16 smem_all[G * NS * STAGE];
   __shared__ float gn_x[2][2][2][4];                    // [wm][i][s|q][fq] pixel-half-1 partials
   typedef __attribute__((address_space(3))) void lds_void;
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_g = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave_g >> 2, wave = wave_g & 3;        // wave group, wave within the group
+  bf16* const smem = smem_all + grp * NS * STAGE;
   const int wm = wave >> 1, wn = wave & 1;
   const long Mpix = (long)Nimg * OH * OW;
   // XCD-aware order over the (pixel tile, channel tile) grid, pixel-major
@@ -138,21 +148,26 @@ conv_s64_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float*
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = Kp / BK;
+  // this group's k-steps: grp, grp + G, ...; every group runs J iterations
+  // (one barrier each) so the block-wide barriers stay matched
+  const int nkg = nk > grp ? (nk - grp + G - 1) / G : 0;
+  const int J = (nk + G - 1) / G;
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) issue(s, s);
-  for (int ks = 0; ks < nk; ++ks) {
-    // stages ks .. ks + NS - 2 are in flight (4 DMA pieces each): retire ks
-    const int after = nk - 1 - ks < NS - 2 ? nk - 1 - ks : NS - 2;
+    if (s < nkg) issue(grp + s * G, s);
+  for (int j = 0; j < J; ++j) {
+    // stages j .. j + NS - 2 of this group are in flight (4 DMA pieces each): retire j
+    const int after = nkg - 1 - j < NS - 2 ? nkg - 1 - j : NS - 2;
     if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // stage ks landed for every wave, and every wave is done reading the
-    // buffer the next issue overwrites (it held stage ks - 1)
+    // stage j landed for every wave, and every wave is done reading the
+    // buffer the next issue overwrites (it held stage j - 1)
     __builtin_amdgcn_s_barrier();
-    if (ks + NS - 1 < nk) issue(ks + NS - 1, (ks + NS - 1) % NS);
-    const bf16* a = smem + (ks % NS) * STAGE;
+    if (j + NS - 1 < nkg) issue(grp + (j + NS - 1) * G, (j + NS - 1) % NS);
+    if (j >= nkg) continue;
+    const bf16* a = smem + (j % NS) * STAGE;
     const bf16* b = a + BM * BK;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -173,11 +188,33 @@ conv_s64_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float*
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 
+  if constexpr (G > 1) {
+    // groups 1.. hand their accumulators to group 0 through the (drained) ring
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(smem_all);      // [G - 1][4 waves][2][2][64 lanes]
+    if (grp > 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) red[((((grp - 1) * 4 + wave) * 2 + i) * 2 + jj) * 64 + lane] = acc[i][jj];
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int g = 1; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) acc[i][jj] += red[((((g - 1) * 4 + wave) * 2 + i) * 2 + jj) * 64 + lane];
+    }
+  }
+  const bool lead = grp == 0;                            // group 0 runs the epilogue
   // ---- epilogue: bias / per-image bias / residual / scale, GN partials
   const int OHW = OH * OW;
   float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < 2 && lead; ++j) {
     const long pix = n0 + wn * 32 + j * 16 + fr;
     if (pix >= Mpix) continue;
     const int img = (int)(pix / OHW);
@@ -244,7 +281,7 @@ conv_s64_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float*
       gq[i] += __shfl_xor(gq[i], 32, 64);
     }
   }
-  if (wn == 1 && fr == 0) {
+  if (lead && wn == 1 && fr == 0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       gn_x[wm][i][0][fq] = gs[i];
@@ -252,7 +289,7 @@ conv_s64_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float*
     }
   }
   __syncthreads();
-  if (wn != 0 || fr != 0) return;
+  if (!lead || wn != 0 || fr != 0) return;
   const long p = n0;                                   // the slot: pixels n0 .. n0 + 63 (64 | OHW)
   if (p >= Mpix) return;
   const long n = p / OHW;
@@ -278,6 +315,11 @@ conv_s64_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float*
 
 }  // namespace
 
+// 0: wave groups by grid size; 1: one group (the 4-wave form); 2 / 4: 2 / 4
+// groups with 2-stage rings; 3: 2 groups with 4-stage rings (A/B, kbench)
+static int g_s64_cfg = 0;
+D3D_API void d3d_conv_s64_cfg(int cfg) { g_s64_cfg = cfg; }
+
 // Launch the small-tile kernel when it applies; returns 1 if launched (and
 // *gn_done = 1 when the GroupNorm partials were written), 0 if not applicable.
 extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias, const float* row_bias,
@@ -294,15 +336,29 @@ extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias
     if (!((Cg == 4 || Cg == 8 || Cg == 16 || Cg == 32) && (OH * OW) % 64 == 0 && ldo == OC)) gnp = nullptr;
   }
   dim3 grid((unsigned)((Mpix + 63) / 64), (unsigned)(OC / 64), 1);
-#define S64(TP, TR)                                                                                             \
-  hipLaunchKernelGGL((conv_s64_k<TP, TR>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias, row_bias, \
-                     (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, OC, ldo, \
-                     stride, scale, res_nmod, gnp, gn_groups)
+  const long blocks = (long)grid.x * grid.y;
+  const int nk = taps * ICp / 64;
+  // wave groups per tile: the grid alone gives ~one 4-wave block per CU
+  // (256 tiles) or two (512): split each tile's K over 4 / 2 groups
+  int cfg = g_s64_cfg;
+  if (cfg == 0) cfg = nk < 8 ? 1 : blocks <= 320 ? 4 : blocks <= 640 ? 2 : 1;
+#define S64(TP, TR, GV, NSV)                                                                                    \
+  hipLaunchKernelGGL((conv_s64_k<TP, TR, GV, NSV>), grid, dim3(256 * GV), 0, st, (const bf16*)I, (const bf16*)Wp, \
+                     bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, \
+                     OW, OC, ldo, stride, scale, res_nmod, gnp, gn_groups)
+#define S64G(TP, TR)                                                                                            \
+  do {                                                                                                          \
+    if (cfg == 4) S64(TP, TR, 4, 2);                                                                            \
+    else if (cfg == 2) S64(TP, TR, 2, 2);                                                                       \
+    else if (cfg == 3) S64(TP, TR, 2, 4);                                                                       \
+    else S64(TP, TR, 1, 4);                                                                                     \
+  } while (0)
   if (taps == 9) {
-    if (trans) S64(9, true); else S64(9, false);
+    if (trans) S64G(9, true); else S64G(9, false);
   } else {
-    if (trans) S64(1, true); else S64(1, false);
+    if (trans) S64G(1, true); else S64G(1, false);
   }
+#undef S64G
 #undef S64
   if (gn_done) *gn_done = gnp ? 1 : 0;
   const int e = (int)hipGetLastError();

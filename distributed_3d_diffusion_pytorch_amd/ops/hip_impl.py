@@ -1157,9 +1157,11 @@ class _FiLMSlot:
     """Shared gradient buffer of one level-batched FiLM projection: each
     GN-FiLM backward deposits its d(scale|shift) into its column slice."""
 
-    def __init__(self, shape, width, device):
+    def __init__(self, shape, width, device, want_events=False):
         self.shape, self.width, self.device = tuple(shape), width, device
         self.buf = None
+        self.want_events = want_events      # forward: one GEMM + ready event per block (film_batch)
+        self.events = []
 
     def grad_slice(self, off: int, C: int) -> torch.Tensor:
         if self.buf is None:
@@ -1190,7 +1192,20 @@ class _FiLMBatch(torch.autograd.Function):
         bcat = bf16_cat(list(Bs), "filmB")
         S = wcat.shape[0]
         y = torch.empty(P, S, dtype=BF16, device=e.device)
-        if _gemm_ok(S, P, K, K, K):
+        if _gemm_ok(S, P, K, K, K) and slot.want_events:
+            # one GEMM per block's column slice, each followed by an event:
+            # the trunk's block i waits for its own modulation only, so the
+            # conditioning stream computes slice i + 1 while block i runs
+            # (the whole-level GEMM made level 0 wait ~4 ms at bs128)
+            off = 0
+            slot.events = []
+            for wd in [w.shape[0] for w in Ws]:
+                gemm_nt(wcat[off:off + wd], x2, y[:, off:], wd, P, K, K, K, S, bias=bcat[off:off + wd])
+                ev = torch.cuda.Event()
+                ev.record()
+                slot.events.append(ev)
+                off += wd
+        elif _gemm_ok(S, P, K, K, K):
             gemm_nt(wcat, x2, y, S, P, K, K, K, S, bias=bcat)
         else:
             _fallback("film_batch", f"P={P} K={K} S={S} (library GEMM)")
@@ -1295,10 +1310,12 @@ class _FiLMBatch(torch.autograd.Function):
         return (dx, None, None, *grads_w, *grads_b)
 
 
-def film_batch(emb, weights, biases):
+def film_batch(emb, weights, biases, block_events=False):
     """Level-batched FiLM projections ``dense_i(silu(emb))`` of the per-level
     pre-activation embedding -> tuple of ``[N,H,W,2C_i]`` modulations (column
-    slices of one GEMM output; GN-FiLM reads them strided)."""
+    slices of one GEMM output; GN-FiLM reads them strided).  ``block_events``:
+    one GEMM per block with a ready event attached to each output as
+    ``_d3d_ready`` (consumers on another stream wait per block)."""
     _need_bf16(emb)
     K = emb.shape[-1]
     widths = [w.shape[0] for w in weights]
@@ -1306,12 +1323,15 @@ def film_batch(emb, weights, biases):
         _fallback("film_batch", f"K={K} widths={widths}")
         se = silu(emb)
         return tuple(linear(se, w, b) for w, b in zip(weights, biases))
-    slot = _FiLMSlot(emb.shape[:-1], sum(widths), emb.device)
+    slot = _FiLMSlot(emb.shape[:-1], sum(widths), emb.device, want_events=bool(block_events))
     outs = _FiLMBatch.apply(emb.contiguous(), slot, len(weights), *weights, *biases)
     off = 0
-    for o, wd in zip(outs, widths):
+    for i, (o, wd) in enumerate(zip(outs, widths)):
         o._d3d_slot = (slot, off)
+        if slot.events:
+            o._d3d_ready = slot.events[i]
         off += wd
+    slot.events = []
     return outs
 
 

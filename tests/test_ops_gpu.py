@@ -207,6 +207,21 @@ def test_conv3x3_small_tiles(H, N, Hh, W, Ci, Co, s, res, rb, scale):
     test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale)
 
 
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,Hh,W,Ci,Co,s,res,rb,scale", [S64_SHAPES[0], S64_SHAPES[1], S64_SHAPES[4],
+                                                         S64_SHAPES[5]])
+def test_conv3x3_small_tiles_wave_groups(H, cfg, N, Hh, W, Ci, Co, s, res, rb, scale):
+    """Every wave-group split of the small-grid conv (one 4-wave group; 2 / 4
+    groups with 2-stage rings; 2 groups with 4-stage rings) against fp32,
+    forward and input gradient (the fused GN statistics are covered by
+    test_conv_fused_gn_stats at the automatic choice)."""
+    H._lib.d3d_conv_s64_cfg(cfg)
+    try:
+        test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale)
+    finally:
+        H._lib.d3d_conv_s64_cfg(0)
+
+
 WGRAD_W8_SHAPES = [
     # 3x3 stride-1 weight gradients on the 8-wave kernel (impl "w8")
     (8, 32, 32, 256, 256, 1, False, False, 1.0),                  # 256 x 256 tiles
