@@ -37,7 +37,7 @@ INV_SQRT2 = 1.0 / math.sqrt(2.0)
 
 _COND_STREAM = os.environ.get("D3D_COND_STREAM", "1") != "0"
 # conditioning stream: one FiLM GEMM + ready event per block instead of one per level
-FILM_BLOCK_EVENTS = True
+FILM_BLOCK_EVENTS = False        # measured -1.2 % at bs16 and bs128 (profiles/r3/ab_film_events_s64.txt)
 _COND_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
 # (level, event): parameters outside the early update part become valid at
 # `event` -- the trunk waits on it before encoder level `level` and the
