@@ -74,10 +74,12 @@ __global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, 
   const int g = lane >> 4, fr = lane & 15;
   const long C3 = 3L * C;
   const int q = qblk * 64 + w * 16 + fr;
-  const bf16* qrow = qkv + ((long)n * L + q) * C3 + h * D;
+  const bool qok = q < L;                    // ragged last query block (L % 64 != 0)
+  const bf16* qrow = qkv + ((long)n * L + (qok ? q : 0)) * C3 + h * D;
   bf16x8 qf[KC];
 #pragma unroll
-  for (int kc = 0; kc < KC; ++kc) qf[kc] = *reinterpret_cast<const bf16x8*>(qrow + 32 * kc + 8 * g);
+  for (int kc = 0; kc < KC; ++kc)
+    qf[kc] = qok ? *reinterpret_cast<const bf16x8*>(qrow + 32 * kc + 8 * g) : bf16x8{};
 
   f32x4 o[DT];
 #pragma unroll
@@ -93,9 +95,10 @@ __global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, 
     for (int i = 0; i < 64 * CH / 256; ++i) {
       int idx = tid + i * 256;
       int r = idx / CH, c = idx % CH;
-      const bf16* src = qkv + ((long)nkv * L + kb + r) * C3 + h * D + c * 8;
-      bf16x8 kv = *reinterpret_cast<const bf16x8*>(src + C);
-      bf16x8 vv = *reinterpret_cast<const bf16x8*>(src + 2 * C);
+      const bool kok = kb + r < L;
+      const bf16* src = qkv + ((long)nkv * L + (kok ? kb + r : 0)) * C3 + h * D + c * 8;
+      bf16x8 kv = kok ? *reinterpret_cast<const bf16x8*>(src + C) : bf16x8{};
+      bf16x8 vv = kok ? *reinterpret_cast<const bf16x8*>(src + 2 * C) : bf16x8{};
       *reinterpret_cast<bf16x8*>(Ks + swz<D>(r, c)) = kv;
       *reinterpret_cast<bf16x8*>(Vs + r * VS + c * 8) = vv;
     }
@@ -116,7 +119,7 @@ __global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, 
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        s[kt][i] *= sl2;
+        s[kt][i] = kb + 16 * kt + 4 * g + i < L ? s[kt][i] * sl2 : -INFINITY;   // keys past L
         mb = fmaxf(mb, s[kt][i]);
       }
     mb = fmaxf(mb, __shfl_xor(mb, 16, 64));
@@ -150,6 +153,7 @@ __global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, 
     }
     __syncthreads();
   }
+  if (!qok) return;
   const float inv = 1.f / l;
   bf16* orow = out + ((long)n * L + q) * C + h * D;
 #pragma unroll
@@ -191,15 +195,17 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
     int idx = tid + i * 256;
     int r = idx / CH, c = idx % CH;
     *reinterpret_cast<bf16x8*>(Kt + r * TS + c * 8) =
-        *reinterpret_cast<const bf16x8*>(qkv + ((long)nkv * L + k0 + r) * C3 + C + h * D + c * 8);
+        k0 + r < L ? *reinterpret_cast<const bf16x8*>(qkv + ((long)nkv * L + k0 + r) * C3 + C + h * D + c * 8)
+                   : bf16x8{};
   }
   const int key = k0 + 16 * w + fr;
-  const bf16* krow = qkv + ((long)nkv * L + key) * C3 + h * D;
+  const bool kok = key < L;                       // ragged last key block (L % 64 != 0)
+  const bf16* krow = qkv + ((long)nkv * L + (kok ? key : 0)) * C3 + h * D;
   bf16x8 kf[KC], vf[KC];
 #pragma unroll
   for (int kc = 0; kc < KC; ++kc) {
-    kf[kc] = *reinterpret_cast<const bf16x8*>(krow + C + 32 * kc + 8 * g);
-    vf[kc] = *reinterpret_cast<const bf16x8*>(krow + 2 * C + 32 * kc + 8 * g);
+    kf[kc] = kok ? *reinterpret_cast<const bf16x8*>(krow + C + 32 * kc + 8 * g) : bf16x8{};
+    vf[kc] = kok ? *reinterpret_cast<const bf16x8*>(krow + 2 * C + 32 * kc + 8 * g) : bf16x8{};
   }
   f32x4 dk[DT], dv[DT];
 #pragma unroll
@@ -208,7 +214,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
     dv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const float* lse_nh = lse + ((long)n * heads + h) * L;
-  const bool direct_dq = L == 64;                 // one key block: dQ is complete here
+  const bool direct_dq = L <= 64;                 // one key block: dQ is complete here
 
   for (int q0 = 0; q0 < L; q0 += 32) {
     __syncthreads();
@@ -217,24 +223,27 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
       int idx = tid + i * 256;
       if (idx < 32 * CH) {
         int r = idx / CH, c = idx % CH;
-        long row = (long)n * L + q0 + r;
+        const bool ok = q0 + r < L;
+        long row = (long)n * L + (ok ? q0 + r : 0);
         *reinterpret_cast<bf16x8*>(Qs + r * TS + c * 8) =
-            *reinterpret_cast<const bf16x8*>(qkv + row * C3 + h * D + c * 8);
+            ok ? *reinterpret_cast<const bf16x8*>(qkv + row * C3 + h * D + c * 8) : bf16x8{};
         *reinterpret_cast<bf16x8*>(dOs + r * TS + c * 8) =
-            *reinterpret_cast<const bf16x8*>(dout + row * C + h * D + c * 8);
+            ok ? *reinterpret_cast<const bf16x8*>(dout + row * C + h * D + c * 8) : bf16x8{};
       }
     }
-    if (tid < 32) lse_s[tid] = lse_nh[q0 + tid] * LOG2E;
+    // query rows past L: lse = +inf makes their probabilities exactly 0
+    if (tid < 32) lse_s[tid] = q0 + tid < L ? lse_nh[q0 + tid] * LOG2E : INFINITY;
     {
       // D[q] = sum_d dO[q, d] O[q, d]: 8 adjacent lanes per query row
       constexpr int PER = D / 8;                  // elements per lane (8 or 16)
       const int r = tid >> 3, part = tid & 7;
-      const long row = (long)n * L + q0 + r;
+      const bool ok = q0 + r < L;
+      const long row = (long)n * L + (ok ? q0 + r : 0);
       const bf16* o = out + row * C + h * D + part * PER;
       const bf16* d = dout + row * C + h * D + part * PER;
       float acc = 0.f;
 #pragma unroll
-      for (int k = 0; k < PER; k += 8) {
+      for (int k = 0; k < PER && ok; k += 8) {
         const f32x8 a = ld8(o + k), b = ld8(d + k);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc += a[j] * b[j];
@@ -260,7 +269,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         int qi = 16 * qt + 4 * g + i;
-        float pv = exp2f(s[i] * sl2 - lse_s[qi]);
+        float pv = kok ? exp2f(s[i] * sl2 - lse_s[qi]) : 0.f;
         p[qt][i] = pv;
         ds[qt][i] = pv * (dp[i] - D_s[qi]);
       }
@@ -305,6 +314,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
       if (direct_dq) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+          if (q0 + 16 * qt + 4 * g + i >= L) continue;
           long row = (long)n * L + q0 + 16 * qt + 4 * g + i;
           dqkv[row * C3 + h * D + 16 * t + fr] = (bf16)(acc[i] * scale);
         }
@@ -312,6 +322,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
         float* slab = dq_acc + (long)kblk * gridDim.z * L * C;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+          if (q0 + 16 * qt + 4 * g + i >= L) continue;
           long row = (long)n * L + q0 + 16 * qt + 4 * g + i;
           slab[row * C + h * D + 16 * t + fr] = acc[i] * scale;
         }
@@ -323,6 +334,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
   for (int t = 0; t < DT; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      if (k0 + 16 * w + 4 * g + i >= L) continue;
       long row = (long)nkv * L + k0 + 16 * w + 4 * g + i;
       dqkv[row * C3 + C + h * D + 16 * t + fr] = (bf16)(dk[t][i] * scale);
       dqkv[row * C3 + 2 * C + h * D + 16 * t + fr] = (bf16)dv[t][i];
@@ -344,11 +356,12 @@ __global__ void dq_convert_k(const float* __restrict__ dq, bf16* __restrict__ dq
 }  // namespace
 
 // qkv: [N, L, 3C] bf16; out: [N, L, C] bf16; lse: [N, heads, L] fp32.
-// Requires L % 64 == 0, D = C/heads in {64, 128}.
+// D = C/heads in {64, 128}; any L >= 1 (a ragged last 64-block is masked).
 D3D_API int d3d_attn_fwd(const void* qkv, void* out, float* lse, int N, int L, int C, int heads, int cross,
                          float scale, hipStream_t st) {
   int D = C / heads;
-  dim3 grid(L / 64, heads, N);
+  if (L < 1) return (int)hipErrorInvalidValue;
+  dim3 grid((L + 63) / 64, heads, N);
   if (D == 64)
     hipLaunchKernelGGL(attn_fwd_k<64>, grid, dim3(256), 0, st, (const bf16*)qkv, (bf16*)out, lse, L, C, heads, cross,
                        scale);
@@ -360,14 +373,15 @@ D3D_API int d3d_attn_fwd(const void* qkv, void* out, float* lse, int N, int L, i
   return (int)hipGetLastError();
 }
 
-// dq_acc: [L/64, N, L, C] fp32 workspace (one slab per key block, fully
+// dq_acc: [ceil(L/64), N, L, C] fp32 workspace (one slab per key block, fully
 // written; unused and may be null when L == 64); dqkv: [N, L, 3C] bf16
 // output (every element written).
 D3D_API int d3d_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* dq_acc,
                          void* dqkv, int N, int L, int C, int heads, int cross, float scale, hipStream_t st) {
   int D = C / heads;
-  if (L % 64 || (L > 64 && dq_acc == nullptr)) return (int)hipErrorInvalidValue;
-  dim3 grid(L / 64, heads, N);
+  if (L < 1 || (L > 64 && dq_acc == nullptr)) return (int)hipErrorInvalidValue;
+  const int kblocks = (L + 63) / 64;
+  dim3 grid(kblocks, heads, N);
   if (D == 64)
     hipLaunchKernelGGL(attn_bwd_k<64>, grid, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse,
                        (const bf16*)out, dq_acc, (bf16*)dqkv, L, C, heads, cross, scale);
@@ -376,10 +390,10 @@ D3D_API int d3d_attn_bwd(const void* qkv, const void* out, const void* dout, con
                        (const bf16*)out, dq_acc, (bf16*)dqkv, L, C, heads, cross, scale);
   else
     return (int)hipErrorInvalidValue;
-  if (L == 64) return (int)hipGetLastError();
+  if (L <= 64) return (int)hipGetLastError();
   long rows = (long)N * L;
   long g = (rows * C / 8 + 255) / 256;
   if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(dq_convert_k, dim3((int)g), dim3(256), 0, st, dq_acc, (bf16*)dqkv, rows, C, L / 64);
+  hipLaunchKernelGGL(dq_convert_k, dim3((int)g), dim3(256), 0, st, dq_acc, (bf16*)dqkv, rows, C, kblocks);
   return (int)hipGetLastError();
 }

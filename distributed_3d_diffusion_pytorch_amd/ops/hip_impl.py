@@ -1385,8 +1385,9 @@ class _Attention(torch.autograd.Function):
         C = C3 // 3
         dout = dout.contiguous()
         # one fp32 dQ slab per 64-key block, summed in fixed order
-        # (deterministic); a single key block (L = 64) writes dQ directly
-        dq = torch.empty(L // 64, N, L, C, dtype=F32, device=qkv.device) if L > 64 else None
+        # (deterministic); a single key block (L <= 64) writes dQ directly;
+        # a ragged last block (L % 64 != 0) is masked in the kernels
+        dq = torch.empty((L + 63) // 64, N, L, C, dtype=F32, device=qkv.device) if L > 64 else None
         dqkv = torch.empty_like(qkv)
         _chk(_lib.d3d_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), _ptr(dq),
                                dqkv.data_ptr(), N, L, C, heads, int(cross), scale, _st()), "attn_bwd")
@@ -1397,7 +1398,7 @@ def attention(qkv, heads, cross):
     _need_bf16(qkv)
     N, L, C3 = qkv.shape
     D = C3 // 3 // heads
-    if L % 64 != 0 or D not in (64, 128) or (cross and N % 2):
+    if D not in (64, 128) or (cross and N % 2):
         _fallback("attention", f"L={L} head_dim={D} N={N} cross={cross}")
         return _t.attention(qkv, heads, cross)
     return _Attention.apply(qkv, heads, cross)

@@ -348,7 +348,11 @@ def test_linear(H, P, IC, OC):
 
 
 @pytest.mark.parametrize("N,L,C,cross", [(4, 256, 256, False), (4, 256, 256, True), (4, 64, 512, False),
-                                         (4, 64, 512, True), (2, 1024, 256, True)])
+                                         (4, 64, 512, True), (2, 1024, 256, True),
+                                         # ragged sequences (masked last block): the 4x4 level of the 32x32
+                                         # chairs config, 7x7 / 14x14 levels of 56x56 images, 10x10
+                                         (4, 16, 512, True), (4, 49, 512, False), (2, 196, 256, True),
+                                         (2, 100, 256, False)])
 def test_attention(H, N, L, C, cross):
     torch.manual_seed(5)
     qkv = torch.randn(N, L, 3 * C, device=DEV).to(BF)
