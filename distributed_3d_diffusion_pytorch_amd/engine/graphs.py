@@ -40,6 +40,7 @@ added to every mask kernel's baked seed) and the Adam block ``hp``.
 from __future__ import annotations
 
 import os
+import time
 from typing import Optional
 
 import torch
@@ -62,6 +63,7 @@ def probe_graph_collective(device: torch.device) -> bool:
             dist.all_reduce(x)
         torch.cuda.current_stream(device).wait_stream(s)
         torch.cuda.synchronize(device)
+        time.sleep(0.3)                      # the watchdog retires the eager warm-up first (see _capture)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             w = dist.all_reduce(x, async_op=True)
@@ -243,6 +245,12 @@ class GraphedTrainStep:
                 self._body(comm)
         torch.cuda.current_stream().wait_stream(s)
         self.H.refresh_weights()                 # descriptor table final before capture
+        if comm:
+            # let RCCL's watchdog retire the warm-up's eager collectives before
+            # the capture starts: it polls their events from its own thread,
+            # and nothing it still tracks may be touched by the capture
+            torch.cuda.synchronize()
+            time.sleep(0.3)
         if _FUSED_UPDATE:
             self.H.prepare_fused_update(tr.flat)
         if self.defer:

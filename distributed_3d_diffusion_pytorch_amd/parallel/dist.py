@@ -64,12 +64,18 @@ def rccl_env_defaults() -> None:
       other ranks blocked inside RCCL kernels;
     * ``TORCH_NCCL_ENABLE_MONITORING=1`` with a heartbeat timeout above the
       collective timeout: a rank whose watchdog itself hangs is killed;
-    * ``TORCH_NCCL_DUMP_ON_TIMEOUT=0``: no flight-recorder files in the repo.
+    * ``TORCH_NCCL_DUMP_ON_TIMEOUT=0``: no flight-recorder files in the repo;
+    * ``TORCH_NCCL_CUDA_EVENT_CACHE=0``: every collective gets fresh events.
+      With the cache, an event recorded by a collective CAPTURED into the graph
+      step could be one the watchdog thread still queries for an eager work
+      (warm-up / probe), and the query fails ("operation not permitted on an
+      event last recorded in a capturing stream"), aborting the rank.
     """
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     os.environ.setdefault("TORCH_NCCL_ENABLE_MONITORING", "1")
     os.environ.setdefault("TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC", "1200")
     os.environ.setdefault("TORCH_NCCL_DUMP_ON_TIMEOUT", "0")
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (the only mode the host driver has)
 
 

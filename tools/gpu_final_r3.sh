@@ -15,5 +15,5 @@ timeout -k 10 300 python bench.py --steps 30 --warmup 5 --global_batch 32 > $O/b
 cat $O/bench32.json
 timeout -k 10 300 python bench.py --mode sample > $O/sample.json 2> $O/sample.err || exit $?
 cat $O/sample.json
-bash tools/gpu_prof_r3.sh > $O/prof.log 2>&1 || exit $?
-tail -12 $O/prof.log
+[ -n "$PROF" ] && { bash tools/gpu_prof_r3.sh > $O/prof.log 2>&1 || exit $?; }
+[ -n "$PROF" ] && tail -12 $O/prof.log; true
