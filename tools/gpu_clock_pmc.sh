@@ -1,0 +1,11 @@
+# GRBM_GUI_ACTIVE cycles per ns of the heaviest kernels: sustained training step vs short isolated bench
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+O=/root/repo/gpurun_out/clk
+mkdir -p $O
+timeout -s KILL 300 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace -f csv -d $O/step -o run -- python3 /root/repo/bench.py --steps 3 --warmup 2 > $O/step.log 2>&1 || exit $?
+timeout -s KILL 200 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace -f csv -d $O/iso -o run -- python3 /root/repo/tools/kbench_conv_epi_r3.py 256 > $O/iso.log 2>&1 || exit $?
+python3 /root/repo/tools/pmc_clock.py $O/step > $O/clock_step.txt 2>&1
+python3 /root/repo/tools/pmc_clock.py $O/iso > $O/clock_iso.txt 2>&1
+find $O -name '*.csv' -size +20M -delete
+cat $O/clock_step.txt; echo ---; cat $O/clock_iso.txt
