@@ -927,8 +927,13 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
 //     piece per wave) stream through a 4-deep LDS ring, the halo through two
 //     buffers filled one whole chunk (nine steps) ahead; total L2 traffic is
 //     ~12 B/clk/CU at the MFMA rate;
-//   * XOR swizzle of the 16-byte channel quarter by ((row >> 2) & 3) keeps
-//     every 16-row fragment read conflict-free for any tap shift;
+//   * XOR swizzle of the 16-byte channel quarter by ((row >> 1) & 2) keeps
+//     every 16-row fragment read conflict-free for any tap shift under the
+//     ds_read_b128 lane groups ({0-3,12-15,20-27}, ...: lanes fr and fr+4 of
+//     neighbouring quarters share a group).  The earlier ((row >> 2) & 3)
+//     swizzle was conflict-free only for contiguous 16-lane groups and ran
+//     2-way conflicted: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 47 %
+//     (profiles/r3/pmc_step/);
 //   * one barrier per step; the counted vmcnt waits only for the step's own
 //     weights (issue order: weights then halo, so in-order completion lets the
 //     halo land up to four steps later).
@@ -996,7 +1001,7 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
 
   // weights: row = wave*16 + (lane>>2), source quarter = slot ^ ((row>>2)&3)
   const int arow = wave * 16 + (lane >> 2);
-  const int aoff = ((m0 + arow) * Kp + (((lane & 3) ^ ((arow >> 2) & 3)) << 3)) * 2;
+  const int aoff = ((m0 + arow) * Kp + (((lane & 3) ^ ((arow >> 1) & 2)) << 3)) * 2;
   // halo pieces: flat halo pixel fi = (wave + 8k)*16 + (lane>>2)
   unsigned hoff[Gm::HPW];
 #pragma unroll
@@ -1005,7 +1010,7 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     const int hr = fi / Gm::HW2, hc = fi - hr * Gm::HW2;
     const int ih = r0 - 1 + hr, iw = hc - 1;
     const bool ok = fi < Gm::HP && ih >= 0 && ih < IH && iw >= 0 && iw < IW;
-    const int q = (lane & 3) ^ ((fi >> 2) & 3);
+    const int q = (lane & 3) ^ ((fi >> 1) & 2);
     const unsigned o = (unsigned)((((img * IH + (ok ? ih : 0)) * IW + (ok ? iw : 0)) * IC + q * 8) * 2);
     hoff[k] = ok ? o : 0x80000000u;            // past every operand: the range check returns zeros
   }
@@ -1057,12 +1062,12 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int hp = hp0[j] + dsh;
-      bfr[j] = *reinterpret_cast<const bf16x8*>(hb + hp * HALO_CH + ((fq ^ ((hp >> 2) & 3)) << 3));
+      bfr[j] = *reinterpret_cast<const bf16x8*>(hb + hp * HALO_CH + ((fq ^ ((hp >> 1) & 2)) << 3));
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = wm * WM + i * 16 + fr;
-      af[i] = *reinterpret_cast<const bf16x8*>(a + row * HALO_CH + ((fq ^ ((row >> 2) & 3)) << 3));
+      af[i] = *reinterpret_cast<const bf16x8*>(a + row * HALO_CH + ((fq ^ ((row >> 1) & 2)) << 3));
     }
   };
   if constexpr (PF) {
@@ -1150,12 +1155,12 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int hp = hp0[j] + dsh;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(hb + hp * HALO_CH + ((fq ^ ((hp >> 2) & 3)) << 3));
+        bfr[j] = *reinterpret_cast<const bf16x8*>(hb + hp * HALO_CH + ((fq ^ ((hp >> 1) & 2)) << 3));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(a + row * HALO_CH + ((fq ^ ((row >> 2) & 3)) << 3));
+        af[i] = *reinterpret_cast<const bf16x8*>(a + row * HALO_CH + ((fq ^ ((row >> 1) & 2)) << 3));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
