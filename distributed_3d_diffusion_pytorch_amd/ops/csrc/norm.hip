@@ -490,7 +490,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
                                                       int ssld, const uint64_t* __restrict__ seed_dev, Cat cat) {
   constexpr int U = 1;      // rows in flight per thread (more: VGPR-bound occupancy, measured slower)
   if (seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][C][4]
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][rpi][C]
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int tpr = C / 8, rpi = NT / tpr;
   const int tid = threadIdx.x;
@@ -554,37 +554,57 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
         }
       }
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float* o = lds + ((roff * C) + c0 + j) * 4;
-      o[0] = dg[j];
-      o[1] = db[j];
-      o[2] = gs[j];
-      o[3] = gs2[j];
-    }
+    // structure-of-arrays [4][rpi][C]: each thread's 8 channels are two
+    // 16-byte stores.  (The interleaved [rpi][C][4] layout put every lane of
+    // a wave on one bank: 86 % of the kernel's LDS cycles were conflicts,
+    // profiles/r3/pmc_step/table_bs16.txt, a fixed cost per block that
+    // dominated the small-batch calls.)
+    const int SL = rpi * C;
+    float* o = lds + roff * C + c0;
+    *reinterpret_cast<f32x4*>(o) = f32x4{dg[0], dg[1], dg[2], dg[3]};
+    *reinterpret_cast<f32x4*>(o + 4) = f32x4{dg[4], dg[5], dg[6], dg[7]};
+    *reinterpret_cast<f32x4*>(o + SL) = f32x4{db[0], db[1], db[2], db[3]};
+    *reinterpret_cast<f32x4*>(o + SL + 4) = f32x4{db[4], db[5], db[6], db[7]};
+    *reinterpret_cast<f32x4*>(o + 2 * SL) = f32x4{gs[0], gs[1], gs[2], gs[3]};
+    *reinterpret_cast<f32x4*>(o + 2 * SL + 4) = f32x4{gs[4], gs[5], gs[6], gs[7]};
+    *reinterpret_cast<f32x4*>(o + 3 * SL) = f32x4{gs2[0], gs2[1], gs2[2], gs2[3]};
+    *reinterpret_cast<f32x4*>(o + 3 * SL + 4) = f32x4{gs2[4], gs2[5], gs2[6], gs2[7]};
   }
   __syncthreads();
+  const int SL = rpi * C;
   const long prow = (long)n * nchunks + chunk, R = (long)gridDim.y * nchunks;
   for (int c = tid; c < C; c += NT) {
     float a = 0.f, b = 0.f;
     for (int rr = 0; rr < rpi; ++rr) {
-      const float* o = lds + ((rr * C) + c) * 4;
-      a += o[0];
-      b += o[1];
+      a += lds[rr * C + c];
+      b += lds[SL + rr * C + c];
     }
     chan_part[(2L * c) * R + prow] = a;         // [2C][R]: one contiguous row per dgamma / dbeta entry
     chan_part[(2L * c + 1) * R + prow] = b;
   }
-  for (int g = tid; g < G; g += NT) {
+  // group sums: TPG consecutive lanes per group (a power of two <= 64, so a
+  // group never straddles a wave), each summing a strided share of the
+  // group's rpi x Cg entries, then a fixed-order butterfly (deterministic)
+  int TPG = 1;
+  while (TPG < 64 && TPG * 2 * G <= NT) TPG <<= 1;
+  const int E = rpi * Cg;
+  for (int g0 = 0; g0 < G; g0 += NT / TPG) {
+    const int g = g0 + tid / TPG, sub = tid % TPG;
     float a = 0.f, b = 0.f;
-    for (int rr = 0; rr < rpi; ++rr)
-      for (int cc = 0; cc < Cg; ++cc) {
-        const float* o = lds + ((rr * C) + g * Cg + cc) * 4;
-        a += o[2];
-        b += o[3];
+    if (g < G)
+      for (int e = sub; e < E; e += TPG) {
+        const int rr = e / Cg, cc = e - rr * Cg;
+        a += lds[2 * SL + rr * C + g * Cg + cc];
+        b += lds[3 * SL + rr * C + g * Cg + cc];
       }
-    grp_part[(prow * G + g) * 2 + 0] = a;
-    grp_part[(prow * G + g) * 2 + 1] = b;
+    for (int w = 1; w < TPG; w <<= 1) {
+      a += __shfl_xor(a, w);
+      b += __shfl_xor(b, w);
+    }
+    if (g < G && sub == 0) {
+      grp_part[(prow * G + g) * 2 + 0] = a;
+      grp_part[(prow * G + g) * 2 + 1] = b;
+    }
   }
 }
 

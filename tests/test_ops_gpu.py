@@ -60,6 +60,24 @@ def test_group_norm(H, N, Hh, W, C, silu):
     assert rel(gh[2], gr[2]) < 1e-2
 
 
+@pytest.mark.parametrize("G,C", [(1, 128), (4, 128), (8, 256), (16, 384), (64, 256)])
+def test_group_norm_group_counts(H, G, C):
+    """Group counts other than 32: the backward's per-block group reduction
+    splits each group over a power-of-two lane team (64 lanes at G <= 4, one
+    lane at G >= 256) -- every team width of the rule is exercised."""
+    torch.manual_seed(5)
+    x = (torch.randn(2, 16, 16, C, device=DEV) * 2 + 0.5).to(BF)
+    w = torch.randn(C, device=DEV) * 0.5 + 1
+    b = torch.randn(C, device=DEV) * 0.1
+    go = torch.randn(2, 16, 16, C, device=DEV)
+    yh, yr, gh, gr = run_both(lambda x, w, b: H.group_norm(x, w, b, G, 1e-5, True),
+                              lambda x, w, b: T.group_norm(x, w, b, G, 1e-5, True), [x, w, b], go)
+    assert rel(yh, yr) < 2e-2
+    assert rel(gh[0], gr[0]) < 3e-2
+    assert rel(gh[1], gr[1]) < 1e-2
+    assert rel(gh[2], gr[2]) < 1e-2
+
+
 @pytest.mark.parametrize("N,Hh,W,C", [(4, 16, 16, 128), (2, 8, 8, 512)])
 def test_gn_film(H, N, Hh, W, C):
     torch.manual_seed(1)
