@@ -163,6 +163,7 @@ def main() -> None:
     sync()
     dt = time.perf_counter() - t0
     trainer.sync()          # (a deferred update of the last timed step; outside the timed region)
+    comm = comm_diagnostics(trainer, pool, ctx) if (trainer.reducer is not None and trainer.reducer.active) else None
     if prof is not None:
         prof.__exit__(None, None, None)
         if ctx.rank == 0:
@@ -197,6 +198,8 @@ def main() -> None:
                        "tuned_gemms": bool(getattr(trainer, "tuned_gemms", False)),
                        "backend": "hip" if (ctx.device.type == "cuda" and use_hip(probe)) else "torch"},
             "final_loss": lv,
+            # N > 1: what the gradient communication did (measured after the timed steps)
+            "comm": comm,
             "hbm_peak_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if ctx.device.type == "cuda" else None,
             # caching-allocator retries (a full cache flush + device sync each): non-zero means the step
             # ran at the HBM limit and paid for it
@@ -205,6 +208,45 @@ def main() -> None:
         }
         print(json.dumps(out), flush=True)
     cleanup()
+
+
+def comm_diagnostics(trainer, pool, ctx) -> dict:
+    """Gradient-communication record of a multi-rank run (untimed, after the
+    benchmark): bucket layout and payload, the process group's own world size,
+    the step path (eager / graph with the all-reduces captured / post-graph
+    chunked) with the capture probe's verdict, and the exposed all-reduce time
+    per step (max over ranks):
+      * eager step: device events around the reducer's join (host wall-clock
+        on gloo);
+      * graph step: graph A replayed against a capture of itself without the
+        collectives (GraphedTrainStep.measure_comm)."""
+    import torch.distributed as dist
+    from distributed_3d_diffusion_pytorch_amd.parallel import all_reduce_max
+    red = trainer.reducer
+    info = red.describe()
+    info["world_pg"] = dist.get_world_size() if dist.is_initialized() else 1
+    info["backend_pg"] = dist.get_backend() if dist.is_initialized() else None
+    g = trainer._graphed
+    ms = -1.0
+    try:            # (every rank reaches the all_reduce_max below, whatever happens here)
+        if trainer.cfg.graph and g is not None:
+            info["step"] = "graph"
+            info["comm_mode"] = g.comm_mode
+            info["probe_ok"] = g.comm_mode == "graph"
+            ms = g.measure_comm(3)
+        else:
+            info["step"] = "eager"
+            info["comm_mode"] = "eager"
+            info["probe_ok"] = None
+            vals = []
+            for i in range(3):
+                trainer.train_step(*pool[i % len(pool)], want_stats=True)
+                vals.append(trainer.last_allreduce_ms)
+            ms = sum(vals) / len(vals)
+    except Exception as e:      # noqa: BLE001 -- a diagnostic must not lose the benchmark line
+        info["error"] = f"{type(e).__name__}: {e}"[:200]
+    info["exposed_allreduce_ms"] = round(all_reduce_max(float(ms if ms is not None else 0.0), ctx.device), 3)
+    return info
 
 
 def bench_sample(args) -> None:

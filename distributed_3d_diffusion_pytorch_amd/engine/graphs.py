@@ -40,7 +40,6 @@ added to every mask kernel's baked seed) and the Adam block ``hp``.
 from __future__ import annotations
 
 import os
-import time
 from typing import Optional
 
 import torch
@@ -62,8 +61,7 @@ def probe_graph_collective(device: torch.device) -> bool:
         with torch.cuda.stream(s):          # warm the collective outside the capture
             dist.all_reduce(x)
         torch.cuda.current_stream(device).wait_stream(s)
-        torch.cuda.synchronize(device)
-        time.sleep(0.3)                      # the watchdog retires the eager warm-up first (see _capture)
+        torch.cuda.synchronize(device)      # the warm-up has completed (see _capture on the watchdog)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             w = dist.all_reduce(x, async_op=True)
@@ -245,12 +243,15 @@ class GraphedTrainStep:
                 self._body(comm)
         torch.cuda.current_stream().wait_stream(s)
         self.H.refresh_weights()                 # descriptor table final before capture
-        if comm:
-            # let RCCL's watchdog retire the warm-up's eager collectives before
-            # the capture starts: it polls their events from its own thread,
-            # and nothing it still tracks may be touched by the capture
-            torch.cuda.synchronize()
-            time.sleep(0.3)
+        # RCCL's watchdog thread keeps polling the events of the warm-up's eager
+        # collectives while the capture runs.  That is safe by construction, no
+        # timing involved: (1) every capture below is thread_local when
+        # collectives are in play, so the watchdog's event queries from its own
+        # thread are legal during it; (2) TORCH_NCCL_CUDA_EVENT_CACHE=0
+        # (parallel/dist.py) gives every collective fresh events, so no event
+        # the watchdog still tracks is re-recorded inside the capture; (3)
+        # collectives issued during capture are not handed to the watchdog.
+        # The synchronize below only makes the warm-up complete first.
         if _FUSED_UPDATE:
             self.H.prepare_fused_update(tr.flat)
         if self.defer:
@@ -262,14 +263,14 @@ class GraphedTrainStep:
         if comm and nchunks > 1:
             self.gA0 = torch.cuda.CUDAGraph()
             self.gA0.register_generator_state(tr.gen)
-            with torch.cuda.graph(self.gA0, pool=self.pool):
+            with torch.cuda.graph(self.gA0, pool=self.pool, capture_error_mode=mode):
                 self._body(False)
         self.gA = torch.cuda.CUDAGraph()
         self.gA.register_generator_state(tr.gen)
         with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
             self._body(comm, defer=self.defer)
         self.gB = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.gB, pool=self.pool):
+        with torch.cuda.graph(self.gB, pool=self.pool, capture_error_mode=mode):
             self._update()
         torch.cuda.synchronize()
         tr.gen.set_state(gstate)
@@ -352,6 +353,48 @@ class GraphedTrainStep:
         for cb in o.on_step:
             cb()
         return loss
+
+    def measure_comm(self, reps: int = 3) -> Optional[float]:
+        """Exposed gradient-communication time per step of the captured step
+        (diagnostics after a benchmark; changes the training state): graph A
+        is captured once more WITHOUT its collectives (own pool) and the two
+        are replayed alternately; the difference of their device times is the
+        part of the bucketed all-reduce that the backward did not hide.
+        ``post`` mode: the device time of the chunked all-reduce + Adam after
+        the graph minus the fused update alone.  None when there is no comm."""
+        if self.comm_mode is None or self.gA is None:
+            return None
+        tr = self.tr
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+        def dev_ms(fn):
+            torch.cuda.synchronize()
+            ev[0].record()
+            for _ in range(reps):
+                fn()
+            ev[1].record()
+            ev[1].synchronize()
+            return ev[0].elapsed_time(ev[1]) / reps
+
+        if self.comm_mode == "post":
+            with_comm = dev_ms(lambda: (self.gA.replay(), self._reduce_update_chunked()))
+            without = dev_ms(lambda: (self.gA.replay(), self._update()))
+            return max(0.0, with_comm - without)
+        g0 = torch.cuda.CUDAGraph()
+        g0.register_generator_state(tr.gen)
+        self.H.set_device_seed(self.seed)
+        try:
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g0, pool=torch.cuda.graph_pool_handle(), capture_error_mode="thread_local"):
+                self._body(False, defer=self.defer)
+        finally:
+            self.H.set_device_seed(None)
+        t_comm = dev_ms(self.gA.replay)
+        t_none = dev_ms(g0.replay)
+        t_comm = min(t_comm, dev_ms(self.gA.replay))
+        del g0
+        tr.flat.zero_grad()
+        return max(0.0, t_comm - t_none)
 
     def flush(self) -> None:
         """Apply a deferred update now (checkpoint, evaluation, end of

@@ -252,9 +252,12 @@ class Trainer:
         if timing:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
+        t_host = time.perf_counter()
         if self.reducer is not None:
             with range_push("allreduce_wait"):
                 self.reducer.finish()
+        if want_stats and self.device.type != "cuda":
+            self.last_allreduce_ms = 1e3 * (time.perf_counter() - t_host)     # gloo: host-blocking wait
         if timing:
             ev1.record()
         scale = 1.0 / self.ctx.world

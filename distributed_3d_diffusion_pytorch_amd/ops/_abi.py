@@ -89,6 +89,11 @@ SIGNATURES = {
     "d3d_gemm_nt": [P, P, P, P, P, I, I, I, I, I, I, I, F, F, P],
     "d3d_gemm_nt_gn": [P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, I, I, P],
     "d3d_attn_bwd": [P, P, P, P, P, P, I, I, I, I, I, F, P],
+    # wgrad_group.hip (job tables: arrays of hip_impl._WgJob)
+    "d3d_wgrad_group_cfg": [I, I, I],
+    "d3d_wgrad_group_ok": [P],
+    "d3d_wgrad_group": [P, I, P, L, P],
+    "d3d_wgrad_group_plan": [P, I, IP, IP, C.POINTER(C.c_long)],
 }
 
 
@@ -101,4 +106,4 @@ def declare(lib: C.CDLL) -> None:
         fn.restype = C.c_long if name in RET_LONG else C.c_int
 
 
-RET_LONG = {"d3d_mlp_ws"}
+RET_LONG = {"d3d_mlp_ws", "d3d_wgrad_group"}

@@ -1,0 +1,543 @@
+// Grouped weight gradients: every deferred weight-gradient job of one flush
+// (ops/gradsink.py: the 3x3 ResnetBlock convs `xunet.py:114-126`, the 1x1 NIN
+// skips `:129`, the attention projections and 1x1 `:175,190`) in ONE launch,
+// plus ONE launch that reduces the split-K slabs of the jobs that need them.
+//
+// Per job:  dW[co][ci][tap] = scale * sum_p dY[p][co] * X[p + shift(tap)][ci]
+//           db[co]          = scale * sum_p dY[p][co]
+// (X may be a virtual channel concat [X | X2] split at C1: the decoder's
+// skip concat `xunet.py:525`.)
+//
+// Why grouped: at 16 examples per GPU (the 8-GPU share of the headline batch)
+// most weight gradients are far too small to fill 256 CUs alone -- a 1x1
+// projection of the 8x8 level is 1 GFLOP -- so each job used to be split-K'd
+// over ~1024 blocks, writing up to 100 fp32 slabs of the whole OC x 9 IC
+// weight that a per-job reduce kernel then summed (≈390 launches, a quarter
+// of the kernel time in slab reductions).  Here the jobs of a flush share one
+// grid: a job's blocks are sized by ONE pixel count per block across the
+// batch (the planner below), so the small-pixel jobs (8x8 / 16x16 levels)
+// run unsplit and write the OIHW gradient straight from their epilogue; only
+// the long-reduction jobs (64x64 level) are split, into a few slabs summed by
+// the grouped reduce in a fixed order (bitwise reproducible).
+//
+// Tile engine: the pixel-major LDS-DMA + transposed-read (ds_read_b64_tr_b16)
+// weight-gradient tile of conv.hip's conv_wgrad_bufl_k (FAST addressing:
+// stride 1, power-of-two images, so a tap's input rows are the output rows
+// shifted by a wave-uniform pixel offset; 1x1 jobs are the degenerate
+// 1-tap case), with the tap count, shapes and pointers read per block from a
+// job table passed by value (no device-side table, graph-capture safe).
+#include "common.h"
+
+#include <algorithm>
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short gs16x4;
+typedef __attribute__((ext_vector_type(8))) short gs16x8;
+typedef __attribute__((address_space(3))) gs16x4 glds_s16x4;
+
+__device__ __forceinline__ gs16x4 gw_tr(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((glds_s16x4*)(p));
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gw_rsrc(const void* p, long bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)(bytes > 0 ? (bytes < 0x7fffffffL ? bytes : 0x7fffffffL) : 0));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, n, 0x00020000);
+}
+
+constexpr int GW_MAX = 16;        // jobs per launch (the sink flushes 8)
+constexpr int GW_BM = 128, GW_BN = 128;
+
+struct GwJob {
+  const bf16* dy;                 // [P][OC]
+  const bf16* x;                  // [P][C1 or IC]
+  const bf16* x2;                 // [P][IC - C1] or null
+  float* dw;                      // [OC][IC][taps] (OIHW)
+  float* db;                      // [OC] or null
+  float* slab;                    // splits > 1: [splits][OC][taps * IC]
+  float* bslab;                   // splits > 1 and db: [2 splits][OC]
+  long P;
+  int OC, IC, C1, taps, H, W, lw, lh, ncb, nmb, splits, pps, blk0, acc;
+  float scale;
+  int pad_;
+};
+struct GwTable {
+  int n, pad_;
+  GwJob j[GW_MAX];
+};
+
+struct GrJob {
+  const float* slab;
+  const float* bslab;
+  float* dw;
+  float* db;
+  int OC, IC, taps, splits, blk0, nblk_w, acc;
+  float scale;
+};
+struct GrTable {
+  int n, pad_;
+  GrJob j[GW_MAX];
+};
+
+template <int PK>
+__device__ __forceinline__ void gw_issue(bf16* sA, bf16* sB, const bf16* __restrict__ dY, const bf16* __restrict__ I,
+                                         long in_elems, long p0, long p_end, int OC, int IC, int OH, int OW, int kh,
+                                         int kw, int dpix, int lw, int wave, const int* trow, const unsigned* aoff,
+                                         const unsigned* boff, const bool* bok) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  constexpr int PPW = PK / 16;
+  const __amdgpu_buffer_rsrc_t rA = gw_rsrc(dY + p0 * OC, (p_end - p0) * OC * 2);
+#pragma unroll
+  for (int i = 0; i < PPW; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sA + (wave * PPW + i) * 4 * GW_BM), 16, aoff[i], 0, 0,
+                                             0);
+  // the base may lie before the tensor (only masked top-padding rows see it)
+  // or past its end on the last stages: the record count clamps at 0
+  const long pb = p0 + dpix;
+  const __amdgpu_buffer_rsrc_t rB = gw_rsrc(I + pb * IC, (in_elems - pb * IC) * 2);
+  // padding rows of the (wave-uniform) tap: compare against the uniform edge
+  // coordinate, branch-free per lane
+  const int wedge = kw == 0 ? 0 : OW - 1, hedge = kh == 0 ? 0 : OH - 1;
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int pp = (int)p0 + trow[i];
+    bool bad = !bok[i];
+    if (kw != 1) bad |= (pp & (OW - 1)) == wedge;
+    if (kh != 1) bad |= ((pp >> lw) & (OH - 1)) == hedge;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * PPW + i) * 4 * GW_BN), 16,
+                                             bad ? 0x80000000u : boff[i], 0, 0, 0);
+  }
+}
+
+}  // namespace
+
+// One 128 (output channels) x 128 (input channels of one tap) tile of one
+// split of one job per block; 4 waves of 64 x 64 (4 x 4 MFMA 16x16x32 tiles);
+// PK pixel rows per LDS stage, two stages, one barrier per stage.
+template <int PK>
+__global__ void __launch_bounds__(256, 2) wgrad_grp_k(GwTable tab) {
+  constexpr int BM = GW_BM, BN = GW_BN, NS = 2;
+  constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
+  constexpr int STAGE = PK * (BM + BN);
+  constexpr int PPW = PK / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
+  __shared__ float bred[BM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware remap of the flat block index: consecutive logical blocks (the
+  // taps / channel tiles of one split, which read the same dY rows) on one XCD
+  int R;
+  {
+    const int T = gridDim.x, L = blockIdx.x;
+    const int q = T / 8, r = T % 8, xcd = L % 8;
+    R = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+  }
+  int k = 0;
+  while (k + 1 < tab.n && R >= tab.j[k + 1].blk0) ++k;
+  const GwJob& J = tab.j[k];
+  const bf16* dY = J.dy;
+  const int OC = J.OC, ICt = J.IC, C1 = J.C1, taps = J.taps, OH = J.H, OW = J.W, lw = J.lw;
+  const int ncb = J.ncb, nmb = J.nmb, splits = J.splits;
+  const long P = J.P;
+  const int nt = taps * ncb;
+  const int b = R - J.blk0;
+  const int bx = b % nt, by = (b / nt) % nmb, split = b / (nt * nmb);
+  const int tap = bx / ncb;
+  const int ci0g = (bx % ncb) * BN;               // channel tile in the (possibly concatenated) input
+  const int m0 = by * BM;
+  const int kh = taps == 9 ? tap / 3 : 1, kw = taps == 9 ? tap % 3 : 1;
+  const long p_begin = (long)split * J.pps;
+  const long p_end = p_begin + J.pps < P ? p_begin + J.pps : P;
+  const int dpix = (kh - 1) * OW + (kw - 1);
+  const bool second = J.x2 != nullptr && ci0g >= C1;
+  const bf16* I = second ? J.x2 : J.x;
+  const int IC = J.x2 == nullptr ? ICt : (second ? ICt - C1 : C1);
+  const int ci0 = second ? ci0g - C1 : ci0g;
+  const long in_elems = P * IC;
+
+  const int lrow = lane >> 4, pch = lane & 15;
+  int trow[PPW];
+  unsigned aoff[PPW], boff[PPW];
+  bool bok[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    trow[i] = (wave * PPW + i) * 4 + lrow;
+    const int lc = pch ^ (2 * (trow[i] & 7));
+    const int co = m0 + lc * 8;
+    aoff[i] = co < OC ? (unsigned)((trow[i] * OC + co) * 2) : 0x80000000u;
+    const int ci = ci0 + lc * 8;
+    boff[i] = (unsigned)((trow[i] * IC + ci) * 2);
+    bok[i] = ci < IC;
+  }
+  // transpose-read lane offsets (elements): row (4g+q) + swizzled column chunk
+  const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
+  const int x7 = 2 * ((4 * g + q) & 7);
+  int la[TM], lb[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) la[i] = (4 * g + q) * 128 + ((((wm * 8 + 2 * i + (pc >> 1)) ^ x7)) << 3) + (pc & 1) * 4;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) lb[j] = (4 * g + q) * 128 + ((((wn * 8 + 2 * j + (pc >> 1)) ^ x7)) << 3) + (pc & 1) * 4;
+
+  auto issue = [&](long p0, int stage) {
+    bf16* sA = smem + stage * STAGE;
+    gw_issue<PK>(sA, sA + PK * BM, dY, I, in_elems, p0, p_end, OC, IC, OH, OW, kh, kw, dpix, lw, wave, trow, aoff,
+                 boff, bok);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const long nsteps = (p_end - p_begin + PK - 1) / PK;
+  const bool do_bias = J.db != nullptr && bx == 0;
+  float bacc = 0.f;
+  const int bcol = tid & 127, bhalf = tid >> 7;   // bias: column, half of the stage's rows
+  auto compute = [&](const bf16* a) {
+    const bf16* bb = a + PK * BM;
+    if (do_bias) {
+#pragma unroll
+      for (int r = 0; r < PK / 2; ++r) {
+        const int row = bhalf * (PK / 2) + r;
+        bacc += (float)a[row * 128 + ((((bcol >> 3) ^ (2 * (row & 7)))) << 3) + (bcol & 7)];
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < PK / 32; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        gs16x4 lo = gw_tr(a + la[i] + kk * 32 * 128);
+        gs16x4 hi = gw_tr(a + la[i] + kk * 32 * 128 + 16 * 128);
+        gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        gs16x4 lo = gw_tr(bb + lb[j] + kk * 32 * 128);
+        gs16x4 hi = gw_tr(bb + lb[j] + kk * 32 * 128 + 16 * 128);
+        gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  // one barrier per stage: wait for this stage's DMA, barrier (every wave's
+  // DMA landed AND every wave done reading the other slot), issue the next
+  // stage into the other slot, compute
+  if (nsteps > 0) issue(p_begin, 0);
+  for (long s = 0; s < nsteps; ++s) {
+    const int st = (int)(s & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nsteps) issue(p_begin + (s + 1) * PK, st ^ 1);
+    __builtin_amdgcn_s_setprio(1);
+    compute(smem + st * STAGE);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const long KW = (long)taps * ICt;
+  if (splits == 1) {
+    // unsplit: the OIHW gradient straight from the accumulators (this block
+    // is the only writer of its (co, ci, tap) elements)
+    const float sc = J.scale;
+    float* dw = J.dw;
+    const int acc_in = J.acc;
+    if (do_bias) {                                  // block-uniform: the barrier is safe
+      if (bhalf) bred[bcol] = bacc;
+      __syncthreads();
+      if (!bhalf && m0 + bcol < OC) {
+        const float v = (bacc + bred[bcol]) * sc;
+        float* d = J.db + m0 + bcol;
+        *d = acc_in ? *d + v : v;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cl = ci0 + wn * WN + j * 16 + fr;
+      if (cl >= IC) continue;
+      const int ci = ci0g - ci0 + cl;               // channel within the concatenation
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (co + e < OC) {
+            float* d = dw + ((long)(co + e) * ICt + ci) * taps + tap;
+            const float v = acc[i][j][e] * sc;
+            *d = acc_in ? *d + v : v;
+          }
+      }
+    }
+    return;
+  }
+  if (do_bias && m0 + bcol < OC) J.bslab[((long)split * 2 + bhalf) * OC + m0 + bcol] = bacc;
+  float* slab = J.slab + (long)split * OC * KW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cl = ci0 + wn * WN + j * 16 + fr;
+    if (cl >= IC) continue;
+    const int ci = ci0g - ci0 + cl;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < OC) slab[(long)(co + e) * KW + tap * ICt + ci] = acc[i][j][e];
+    }
+  }
+}
+
+// Grouped split-K reduce: block = (job, co, 64 input channels) summing every
+// tap of its channels over the job's slabs, 4 split lanes merged in a fixed
+// order through LDS, written as 64 x taps CONTIGUOUS floats of OIHW; blocks
+// past a job's nblk_w sum its bias partials.
+__global__ void __launch_bounds__(256) wgrad_grp_reduce_k(GrTable tab) {
+  __shared__ float red[4][9][64];
+  __shared__ float tile[64 * 9];
+  const int tid = threadIdx.x;
+  const int R = blockIdx.x;
+  int k = 0;
+  while (k + 1 < tab.n && R >= tab.j[k + 1].blk0) ++k;
+  const GrJob& J = tab.j[k];
+  const int b = R - J.blk0;
+  const int OC = J.OC, IC = J.IC, taps = J.taps, splits = J.splits;
+  const int ln = tid >> 6, c = tid & 63;
+  if (b >= J.nblk_w) {
+    const int co = (b - J.nblk_w) * 64 + c;
+    float a0 = 0.f, a1 = 0.f;
+    if (co < OC) {
+      int r = ln;
+      for (; r + 4 < 2 * splits; r += 8) {
+        a0 += J.bslab[(long)r * OC + co];
+        a1 += J.bslab[(long)(r + 4) * OC + co];
+      }
+      if (r < 2 * splits) a0 += J.bslab[(long)r * OC + co];
+    }
+    red[ln][0][c] = a0 + a1;
+    __syncthreads();
+    if (ln == 0 && co < OC) {
+      const float v = (((red[0][0][c] + red[1][0][c]) + red[2][0][c]) + red[3][0][c]) * J.scale;
+      J.db[co] = J.acc ? J.db[co] + v : v;
+    }
+    return;
+  }
+  const int ncg = (IC + 63) / 64;
+  const int co = b / ncg, ci0 = (b % ncg) * 64;
+  const int nci = min(64, IC - ci0);
+  const long total = (long)OC * taps * IC;
+  float a[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) a[t] = 0.f;
+  if (c < nci) {
+    const float* src = J.slab + (long)co * taps * IC + ci0 + c;
+    for (int sp = ln; sp < splits; sp += 4) {
+      const float* s = src + (long)sp * total;
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+        if (t < taps) a[t] += s[(long)t * IC];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+    if (t < taps) red[ln][t][c] = a[t];
+  __syncthreads();
+  for (int m = tid; m < taps * 64; m += 256) {
+    const int t = m >> 6, cc = m & 63;
+    tile[cc * taps + t] = (((red[0][t][cc] + red[1][t][cc]) + red[2][t][cc]) + red[3][t][cc]) * J.scale;
+  }
+  __syncthreads();
+  float* dst = J.dw + ((long)co * IC + ci0) * taps;
+  for (int m = tid; m < nci * taps; m += 256) dst[m] = J.acc ? dst[m] + tile[m] : tile[m];
+}
+
+// ------------------------------------------------------------------ host ----
+// Job description of the C ABI (mirrored by ops/hip_impl.py _WgJob).
+struct WgJobDesc {
+  const void* dy;
+  const void* x;
+  const void* x2;
+  float* dw;
+  float* db;
+  int N, H, W, OC, IC, C1, taps, acc;
+  float scale;
+  int pad_;
+};
+static_assert(sizeof(WgJobDesc) == 80, "WgJobDesc must match hip_impl._WgJob");
+
+static int g_gw_blocks = 512;      // target blocks per grouped launch (2 per CU)
+static int g_gw_pk = 32;           // pixel rows per LDS stage (32 or 64)
+static int g_gw_minpix = 512;      // lower bound of the pixels per block
+
+D3D_API int d3d_wgrad_group_cfg(int blocks, int pk, int minpix) {
+  if (blocks > 0) g_gw_blocks = blocks;
+  if (pk == 32 || pk == 64) g_gw_pk = pk;
+  if (minpix > 0) g_gw_minpix = minpix;
+  return 0;
+}
+
+static int gw_lg2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
+}
+
+// 0 when the grouped kernel takes the job, else the reason (> 0).
+D3D_API int d3d_wgrad_group_ok(const WgJobDesc* d) {
+  if (d->taps != 1 && d->taps != 9) return 1;
+  if (d->OC <= 0 || d->IC <= 0 || d->OC % 8 || d->IC % 8) return 2;
+  if (d->taps == 9 && (gw_lg2(d->H) < 0 || gw_lg2(d->W) < 0)) return 3;
+  if (d->x2 && (d->C1 <= 0 || d->C1 % GW_BN || d->C1 >= d->IC)) return 4;
+  if (((uintptr_t)d->dy | (uintptr_t)d->x | (uintptr_t)d->x2) & 15) return 5;
+  if (!d->dw) return 6;
+  const long P = (long)d->N * d->H * d->W;
+  if (P <= 0 || P >= (1L << 31) - 1) return 7;
+  return 0;
+}
+
+struct GwPlan {
+  int splits[GW_MAX], pps[GW_MAX], tiles[GW_MAX];
+  long slab_off[GW_MAX], bslab_off[GW_MAX];
+  long ws_floats;
+  long blocks;
+};
+
+static void gw_plan(const WgJobDesc* d, int n, GwPlan& pl) {
+  double work = 0;
+  for (int i = 0; i < n; ++i) {
+    const long P = (long)d[i].N * d[i].H * d[i].W;
+    pl.tiles[i] = d[i].taps * cdiv(d[i].IC, GW_BN) * cdiv(d[i].OC, GW_BM);
+    work += (double)pl.tiles[i] * P;
+  }
+  // one pixel count per block across the batch: ~g_gw_blocks equal blocks
+  long Q = (long)(work / g_gw_blocks);
+  Q = std::max<long>(Q, g_gw_minpix);
+  Q = (Q + 63) / 64 * 64;
+  long off = 0, blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const long P = (long)d[i].N * d[i].H * d[i].W;
+    long s = (P + Q - 1) / Q;
+    s = std::min<long>(std::max<long>(s, 1), 64);
+    long pps = (P + s - 1) / s;
+    pps = (pps + 63) / 64 * 64;
+    s = (P + pps - 1) / pps;
+    // the dY descriptor spans one split: 31-bit byte count
+    while ((long)pps * d[i].OC * 2 >= (1L << 31) - (1L << 20)) {
+      ++s;
+      pps = ((P + s - 1) / s + 63) / 64 * 64;
+      s = (P + pps - 1) / pps;
+    }
+    pl.splits[i] = (int)s;
+    pl.pps[i] = (int)pps;
+    pl.slab_off[i] = pl.bslab_off[i] = -1;
+    if (s > 1) {
+      pl.slab_off[i] = off;
+      off += (s * d[i].OC * d[i].taps * (long)d[i].IC + 63) / 64 * 64;
+      if (d[i].db) {
+        pl.bslab_off[i] = off;
+        off += (2 * s * d[i].OC + 63) / 64 * 64;
+      }
+    }
+    blocks += pl.tiles[i] * s;
+  }
+  pl.ws_floats = off;
+  pl.blocks = blocks;
+}
+
+// Weight gradients of n jobs (n <= 16, each d3d_wgrad_group_ok, no two jobs
+// writing the same dw / db) in one grouped launch + one grouped reduce.
+// ws == nullptr: returns the workspace size in floats (nothing launched).
+// Otherwise returns 0, or < 0 on error (nothing launched).
+D3D_API long d3d_wgrad_group(const WgJobDesc* d, int n, float* ws, long ws_floats, hipStream_t st) {
+  if (n < 1 || n > GW_MAX) return -1;
+  for (int i = 0; i < n; ++i)
+    if (d3d_wgrad_group_ok(d + i)) return -2;
+  GwPlan pl;
+  gw_plan(d, n, pl);
+  if (!ws) return pl.ws_floats;
+  if (ws_floats < pl.ws_floats || pl.blocks >= (1L << 31)) return -3;
+  GwTable tab{};
+  GrTable rt{};
+  tab.n = n;
+  long blk = 0, rblk = 0;
+  for (int i = 0; i < n; ++i) {
+    GwJob& J = tab.j[i];
+    const WgJobDesc& D = d[i];
+    J.dy = (const bf16*)D.dy;
+    J.x = (const bf16*)D.x;
+    J.x2 = (const bf16*)D.x2;
+    J.dw = D.dw;
+    J.db = D.db;
+    J.P = (long)D.N * D.H * D.W;
+    J.OC = D.OC;
+    J.IC = D.IC;
+    J.C1 = D.x2 ? D.C1 : D.IC;
+    J.taps = D.taps;
+    if (D.taps == 1) {             // per-pixel GEMM: rows only, no padding tests
+      J.H = J.W = 1;
+      J.lw = J.lh = 0;
+    } else {
+      J.H = D.H;
+      J.W = D.W;
+      J.lw = gw_lg2(D.W);
+      J.lh = gw_lg2(D.H);
+    }
+    J.ncb = cdiv(D.IC, GW_BN);
+    J.nmb = cdiv(D.OC, GW_BM);
+    J.splits = pl.splits[i];
+    J.pps = pl.pps[i];
+    J.blk0 = (int)blk;
+    J.acc = D.acc;
+    J.scale = D.scale;
+    J.slab = pl.splits[i] > 1 ? ws + pl.slab_off[i] : nullptr;
+    J.bslab = pl.splits[i] > 1 && D.db ? ws + pl.bslab_off[i] : nullptr;
+    blk += (long)pl.tiles[i] * pl.splits[i];
+    if (pl.splits[i] > 1) {
+      GrJob& Rj = rt.j[rt.n++];
+      Rj.slab = J.slab;
+      Rj.bslab = J.bslab;
+      Rj.dw = D.dw;
+      Rj.db = D.db;
+      Rj.OC = D.OC;
+      Rj.IC = D.IC;
+      Rj.taps = D.taps;
+      Rj.splits = pl.splits[i];
+      Rj.blk0 = (int)rblk;
+      Rj.nblk_w = D.OC * cdiv(D.IC, 64);
+      Rj.acc = D.acc;
+      Rj.scale = D.scale;
+      rblk += Rj.nblk_w + (D.db ? cdiv(D.OC, 64) : 0);
+    }
+  }
+  if (g_gw_pk == 64)
+    hipLaunchKernelGGL(wgrad_grp_k<64>, dim3((unsigned)blk), dim3(256), 0, st, tab);
+  else
+    hipLaunchKernelGGL(wgrad_grp_k<32>, dim3((unsigned)blk), dim3(256), 0, st, tab);
+  if (rt.n > 0) hipLaunchKernelGGL(wgrad_grp_reduce_k, dim3((unsigned)rblk), dim3(256), 0, st, rt);
+  const int e = (int)hipGetLastError();
+  return e ? -1000 - e : 0;
+}
+
+// Plan introspection for tests / tools: splits and pixels per split of job i.
+D3D_API int d3d_wgrad_group_plan(const WgJobDesc* d, int n, int* splits, int* pps, long* blocks) {
+  if (n < 1 || n > GW_MAX) return -1;
+  GwPlan pl;
+  gw_plan(d, n, pl);
+  for (int i = 0; i < n; ++i) {
+    splits[i] = pl.splits[i];
+    pps[i] = pl.pps[i];
+  }
+  if (blocks) *blocks = pl.blocks;
+  return 0;
+}

@@ -67,6 +67,9 @@ class GradSink:
         self._streams: Dict[int, "torch.cuda.Stream"] = {}
         self._forked = set()
         self._cb_queued = False
+        # grouped weight-gradient launcher (set by ops.hip_impl): runs a
+        # flush's job descriptors as one launch + one slab reduce
+        self.group_fn: Optional[Callable[[list], None]] = None
 
     def attach(self, params, views, notify: Optional[Callable[[int], None]] = None) -> None:
         # the parameter objects themselves are kept: a key is only trusted
@@ -177,11 +180,14 @@ class GradSink:
                 pass
 
     # ------------------------------------------------ weight-gradient jobs
-    def submit(self, dev: torch.device, fn: Callable[[], None], keep=(), done=()) -> None:
+    def submit(self, dev: torch.device, fn: Callable[[], None], keep=(), done=(), spec=None) -> None:
         """Run one weight-gradient job: ``fn()`` launches kernels that deposit
         into sink targets, then the parameters in ``done`` are reported.
         Eager: now, on the side stream (:meth:`producer`).  Graph capture with
-        deferral on: queued and flushed in batches behind one fork each."""
+        deferral on: queued and flushed in batches behind one fork each.
+        ``spec``: the same job as a grouped-kernel descriptor
+        (hip_impl.wgrad_job); a flush runs all queued specs as ONE grouped
+        launch (:attr:`group_fn`) instead of their closures."""
         if (self.stream_enabled and self.graph_defer and dev.type == "cuda"
                 and torch.cuda.is_current_stream_capturing()):
             # the submitting stream travels with the job: its inputs were
@@ -189,7 +195,7 @@ class GradSink:
             # (conditioning-stream jobs are often flushed from the compute
             # stream -- see flush())
             self._queue.append((fn, tuple(t for t in keep if t is not None), tuple(p for p in done if p is not None),
-                                torch.cuda.current_stream(dev.index if dev.index is not None else None)))
+                                torch.cuda.current_stream(dev.index if dev.index is not None else None), spec))
             self._queue_end_callback()
             if len(self._queue) >= self.defer_batch:
                 self.flush()
@@ -221,14 +227,20 @@ class GradSink:
             if all(st.cuda_stream != w.cuda_stream for w in waited):
                 side.wait_stream(st)
                 waited.append(st)
+        grouped = self.group_fn is not None
         with torch.cuda.stream(side):
-            for fn, _, _, _ in q:
-                fn()
-        for _, keep, _, _ in q:
+            if grouped:
+                specs = [j[4] for j in q if j[4] is not None]
+                if specs:
+                    self.group_fn(specs)
+            for fn, _, _, _, spec in q:
+                if spec is None or not grouped:
+                    fn()
+        for _, keep, _, _, _ in q:
             for t in keep:
                 t.record_stream(side)
         self._forked.add(idx)
-        for _, _, done, _ in q:
+        for _, _, done, _, _ in q:
             for p in done:
                 self.done(p)
 

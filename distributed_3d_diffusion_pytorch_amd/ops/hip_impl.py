@@ -556,7 +556,8 @@ class _CatGNDense(torch.autograd.Function):
             else:
                 _chk(rc, "wgrad_cat")
         if direct:
-            SINK.submit(g.device, job, (g2, a, b), (dwp, dbp if has_db else None))
+            spec = wgrad_job(g2, a, OC, C, rows, 1, 1, 1, dWt, dbt, 1.0, x2=b, C1=C1)
+            SINK.submit(g.device, job, (g2, a, b), (dwp, dbp if has_db else None), spec=spec)
         else:
             job()
             gW = dWt.view(dwp.shape)
@@ -670,6 +671,72 @@ def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9, want_bias=False, dW=No
     return dW, db
 
 
+# ------------------------------------------------- grouped weight gradients
+class _WgJob(ctypes.Structure):
+    """One weight-gradient job of a grouped launch (wgrad_group.hip
+    WgJobDesc): dW[co][ci][tap] (+)= scale * sum_p dY[p][co] X[p+shift][ci],
+    db[co] (+)= scale * sum_p dY[p][co]; X may be the virtual concat [x | x2]
+    split at channel C1."""
+    _fields_ = [("dy", ctypes.c_void_p), ("x", ctypes.c_void_p), ("x2", ctypes.c_void_p),
+                ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p),
+                ("N", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int), ("OC", ctypes.c_int),
+                ("IC", ctypes.c_int), ("C1", ctypes.c_int), ("taps", ctypes.c_int), ("acc", ctypes.c_int),
+                ("scale", ctypes.c_float), ("pad_", ctypes.c_int)]
+
+
+assert ctypes.sizeof(_WgJob) == 80
+# 1: weight-gradient jobs deferred inside graph capture run grouped, one
+# launch (+ one slab reduce) per sink flush; 0: one launch pair per job
+_WGRAD_GROUP = os.environ.get("D3D_WGRAD_GROUP", "1") != "0"
+
+
+def wgrad_job(dy, x, OC, IC, N, H, W, taps, dw, db=None, scale=1.0, accumulate=True, x2=None, C1=0):
+    """A grouped weight-gradient job over contiguous bf16 dY [P, OC] and X
+    [P, IC] (or [P, C1] + x2 [P, IC - C1]), or None when the grouped kernel
+    cannot take it (the caller keeps its per-job path)."""
+    if not _WGRAD_GROUP or dw is None:
+        return None
+    for t in (dy, x, x2):
+        if t is not None and (t.dtype != BF16 or not t.is_contiguous()):
+            return None
+    j = _WgJob(dy.data_ptr(), x.data_ptr(), _ptr(x2), dw.data_ptr(), _ptr(db), int(N), int(H), int(W), int(OC),
+               int(IC), int(C1 if x2 is not None else IC), int(taps), int(bool(accumulate)), float(scale), 0)
+    return j if _lib.d3d_wgrad_group_ok(ctypes.byref(j)) == 0 else None
+
+
+def wgrad_group_run(jobs) -> None:
+    """Run grouped weight-gradient jobs on the current stream: at most 16 per
+    launch and never two writing the same gradient in one launch (the
+    unsplit epilogue accumulates in place)."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    batch, seen = [], set()
+
+    def go(b):
+        arr = (_WgJob * len(b))(*b)
+        need = _lib.d3d_wgrad_group(arr, len(b), None, 0, None)
+        if need < 0:
+            raise RuntimeError(f"d3d_wgrad_group plan failed ({need})")
+        ws = torch.empty(max(int(need), 1), dtype=F32, device=dev)
+        rc = _lib.d3d_wgrad_group(arr, len(b), ws.data_ptr(), int(need), _st())
+        if rc != 0:
+            raise RuntimeError(f"d3d_wgrad_group failed ({rc})")
+        if _SYNC_CHECK:
+            _chk(0, "wgrad_group")
+
+    for j in jobs:
+        keys = {j.dw} | ({j.db} if j.db else set())
+        if len(batch) == 16 or keys & seen:
+            go(batch)
+            batch, seen = [], set()
+        batch.append(j)
+        seen |= keys
+    if batch:
+        go(batch)
+
+
+SINK.group_fn = wgrad_group_run
+
+
 def _chansum(g, per_image: bool):
     N, OH, OW, C = g.shape
     P = OH * OW
@@ -763,7 +830,9 @@ class _Conv(torch.autograd.Function):
                 def job(g=g, x=x, tw=tw, tb=tb if need_b else None, ks=ks):
                     _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, dW=tw.view(OC, IC, taps), db=tb,
                            accumulate=True, scale=ks)
-                SINK.submit(g.device, job, (g, x), (weight, bias if need_b else None))
+                spec = wgrad_job(g, x, OC, IC, N, H, W, taps, tw, tb if need_b else None, ks) \
+                    if stride == 1 and (OH, OW) == (H, W) else None
+                SINK.submit(g.device, job, (g, x), (weight, bias if need_b else None), spec=spec)
             else:
                 dW, db2 = _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps, want_bias=need_b, scale=ks)
                 dW = dW.reshape(weight.shape)
@@ -1087,7 +1156,8 @@ class _Linear(torch.autograd.Function):
                 def job(g4=g4, x4=x4, tw=tw, tb=tb, ks=ks):
                     _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, dW=tw.view(OC, IC, 1), db=tb, accumulate=True,
                            scale=ks)
-                SINK.submit(g.device, job, (g4, x4), (weight, bias if need_b else None))
+                spec = wgrad_job(g4, x4, OC, IC, rows, 1, 1, 1, tw, tb, ks)
+                SINK.submit(g.device, job, (g4, x4), (weight, bias if need_b else None), spec=spec)
             else:
                 dW, db = _wgrad(g4, x4, OC, IC, rows, 1, 1, 1, 1, 1, 1, want_bias=need_b, scale=ks)
                 dW = dW.reshape(weight.shape)

@@ -137,6 +137,13 @@ class GradReducer:
                 view.copy_(tmp)                                     # widen (persistent mirror: no recycling)
         self.reset()
 
+    def describe(self) -> dict:
+        """Bucket layout and payload, for benchmark / metrics records."""
+        sizes = [(bk["end"] - bk["start"]) * 4 / 2 ** 20 for bk in self.buckets]
+        return {"active": bool(self.active), "world_pg": int(self.world), "buckets": len(self.buckets),
+                "bucket_mib": [round(x, 2) for x in sizes], "total_mib": round(sum(sizes), 2),
+                "payload": "bf16" if self.grad_dtype == torch.bfloat16 else "fp32"}
+
     @contextlib.contextmanager
     def no_sync(self):
         """Gradient accumulation: skip communication inside the block."""

@@ -1,5 +1,6 @@
 """Numerics of every HIP kernel against the fp32 PyTorch composition of the
 same op (ops.torch_impl) on identical bf16-rounded inputs.  GPU only."""
+import ctypes
 import math
 import os
 
@@ -594,6 +595,84 @@ def test_wgrad_tn_matches_fp32(H, P, M, N, ldy, splits):
     assert (bws.sum(0) - rb).abs().max().item() <= 1e-3 * rb.abs().max().item() + 1e-3
 
 
+# grouped weight-gradient jobs: (N, H, W, IC, OC, taps, C1 of a virtual concat or 0, bias)
+WG_JOBS = [
+    (32, 64, 64, 128, 128, 9, 0, True),      # 64x64 level at 16 examples / GPU: split-K
+    (32, 8, 8, 512, 512, 9, 0, True),        # 8x8 level: unsplit, direct OIHW epilogue
+    (4, 16, 16, 384, 256, 9, 0, False),
+    (6, 8, 16, 72, 200, 9, 0, True),         # channel tails (partial tiles), non-square image
+    (2048, 1, 1, 512, 1536, 1, 0, True),     # 1x1 projection
+    (8192, 1, 1, 768, 256, 1, 256, True),    # 1x1 over the virtual concat [x | x2]
+    (32, 32, 32, 256, 256, 9, 0, True),
+]
+
+
+def _wg_ref(g, x, taps):
+    N, Hh, W, OC = g.shape
+    IC = x.shape[-1]
+    if taps == 1:
+        return (g.reshape(-1, OC).float().t() @ x.reshape(-1, IC).float()).reshape(OC, IC, 1)
+    dw = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).float(), (OC, IC, 3, 3), g.permute(0, 3, 1, 2).float(),
+                                     padding=1)
+    return dw.reshape(OC, IC, 9)
+
+
+@pytest.mark.parametrize("pk,blocks,minpix", [(32, 512, 512), (64, 512, 512), (32, 4096, 64)])
+def test_wgrad_group_matches_fp32(H, pk, blocks, minpix):
+    """Grouped weight gradients (wgrad_group.hip): one launch over a mixed
+    batch of 3x3 / 1x1 / virtual-concat jobs (+ the grouped slab reduce for
+    the split ones) == the fp32 torch weight gradients, accumulated onto the
+    existing gradient with the scale, bias sums included; bitwise equal on a
+    re-run.  The last case plans many more splits (small blocks)."""
+    torch.manual_seed(5)
+    H._lib.d3d_wgrad_group_cfg(blocks, pk, minpix)
+    try:
+        jobs, refs, outs = [], [], []
+        for (N, Hh, W, IC, OC, taps, C1, bias) in WG_JOBS:
+            g = torch.randn(N, Hh, W, OC, device=DEV).to(BF)
+            x = torch.randn(N, Hh, W, IC, device=DEV).to(BF)
+            dw0 = torch.randn(OC, IC, taps, device=DEV)
+            db0 = torch.randn(OC, device=DEV) if bias else None
+            ref_w = dw0 + 0.7 * _wg_ref(g, x, taps)
+            ref_b = db0 + 0.7 * g.reshape(-1, OC).float().sum(0) if bias else None
+            dw, db = dw0.clone(), db0.clone() if bias else None
+            if C1:
+                xa, xb = x[..., :C1].contiguous(), x[..., C1:].contiguous()
+                j = H.wgrad_job(g, xa, OC, IC, N, Hh, W, taps, dw, db, 0.7, x2=xb, C1=C1)
+                keep = (g, xa, xb)
+            else:
+                j = H.wgrad_job(g, x, OC, IC, N, Hh, W, taps, dw, db, 0.7)
+                keep = (g, x)
+            assert j is not None, (N, Hh, W, IC, OC, taps)
+            jobs.append(j)
+            refs.append((ref_w, ref_b, dw0, db0))
+            outs.append((dw, db, keep))
+        sp = (ctypes.c_int * len(jobs))()
+        pp = (ctypes.c_int * len(jobs))()
+        H._lib.d3d_wgrad_group_plan((H._WgJob * len(jobs))(*jobs), len(jobs), sp, pp, None)
+        H.wgrad_group_run(jobs)
+        torch.cuda.synchronize()
+        first = []
+        for (ref_w, ref_b, _, _), (dw, db, _), s in zip(refs, outs, sp):
+            assert rel(dw, ref_w) < 1e-4, (s, rel(dw, ref_w))
+            if ref_b is not None:
+                assert rel(db, ref_b) < 1e-4, (s, rel(db, ref_b))
+            first.append((dw.clone(), db.clone() if db is not None else None))
+        assert max(sp) > 1 and min(sp) == 1, list(sp)        # both epilogues exercised
+        for (_, _, dw0, db0), (dw, db, _) in zip(refs, outs):  # re-run: bitwise
+            dw.copy_(dw0)
+            if db is not None:
+                db.copy_(db0)
+        H.wgrad_group_run(jobs)
+        torch.cuda.synchronize()
+        for (dw, db, _), (w1, b1) in zip(outs, first):
+            assert torch.equal(dw, w1)
+            if db is not None:
+                assert torch.equal(db, b1)
+    finally:
+        H._lib.d3d_wgrad_group_cfg(512, 32, 512)
+
+
 @pytest.mark.parametrize("micro", [2, 0])
 def test_graph_train_step_matches_eager(micro):
     """HIP-graph replayed training step == eager step (dropout ON: the graph
@@ -1029,23 +1108,26 @@ def _graph_comm_1rank_worker(out_dir):
     data = SyntheticBatches(4, 32, "cuda", seed=21)
     batches = [next(data) for _ in range(3)]
     lines = []
-    for gd in ("fp32", "bf16"):
+    # (payload, micro-batch): one micro-batch (deferred update) for both
+    # payloads, and two micro-batches, where the leading one's graph gA0 is
+    # captured next to the comm graph (thread_local, no watchdog wait)
+    for gd, mb in (("fp32", 0), ("bf16", 0), ("fp32", 2)):
         res = []
         for graph in (False, True):
             cfg = make_config(None, {"model.H": 32, "model.W": 32, "data.imgsize": 32, "global_batch": 4,
-                                     "micro_batch": 0, "data.synthetic": True, "log_every": 0, "ckpt_every": 0,
+                                     "micro_batch": mb, "data.synthetic": True, "log_every": 0, "ckpt_every": 0,
                                      "graph": graph, "optim.warmup_examples": 8, "dist.bucket_mb": 16.0,
                                      "dist.grad_dtype": gd, "dist.force_comm": True})
             tr = Trainer(cfg, ctx)
             assert tr.reducer is not None and tr.reducer.active
             losses = [float(tr.train_step(*b)) for b in batches]
             g = tr._graphed
-            mode = f"{g.comm_mode}/{int(g.defer)}" if g is not None else "eager"
+            mode = f"{g.comm_mode}/{int(g.defer)}/{int(g.gA0 is not None)}" if g is not None else "eager"
             tr.sync()
             res.append((losses, tr.flat.data.clone(), mode))
             del tr
         (le, pe, _), (lg, pg, mode) = res
-        lines.append(f"{gd} {(pe - pg).abs().max().item()} {max(abs(a - b) for a, b in zip(le, lg))} {mode}")
+        lines.append(f"{gd}/{mb} {(pe - pg).abs().max().item()} {max(abs(a - b) for a, b in zip(le, lg))} {mode}")
     with open(os.path.join(out_dir, "gc1.txt"), "w") as f:
         f.write("\n".join(lines))
     cleanup()
@@ -1053,18 +1135,19 @@ def _graph_comm_1rank_worker(out_dir):
 
 def test_graph_step_captured_collectives_one_rank(tmp_path):
     """Graph A captured with the real bucketed RCCL all-reduces (1-rank
-    group), deferred update on, fp32 and bf16 payloads: comm_mode "graph",
-    parameters equal to the eager bucketed step within 5e-4."""
+    group), deferred update on, fp32 and bf16 payloads, and a two-micro-batch
+    step (leading graph gA0 captured too): comm_mode "graph", parameters equal
+    to the eager bucketed step within 5e-4.  No sleep before any capture."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from distributed_3d_diffusion_pytorch_amd.parallel import spawn
     import test_ops_gpu as me
     spawn(me._graph_comm_1rank_worker, 1, (str(tmp_path),))
     rows = open(tmp_path / "gc1.txt").read().split("\n")
-    assert [r.split()[0] for r in rows] == ["fp32", "bf16"]
+    assert [r.split()[0] for r in rows] == ["fp32/0", "bf16/0", "fp32/2"]
     for r in rows:
         gd, d, dl, mode = r.split()
-        assert mode == "graph/1", r
+        assert mode == ("graph/0/1" if gd == "fp32/2" else "graph/1/0"), r
         assert float(d) < 5e-4 and float(dl) < 2e-3, r
 
 

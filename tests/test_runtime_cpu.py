@@ -46,6 +46,21 @@ def test_bench_self_spawns_ranks():
         assert k in r
 
 
+def test_bench_reports_comm_diagnostics_four_ranks():
+    """`bench.py --gpus 4`: the JSON carries the gradient-communication record
+    a scaling run needs for diagnosis -- the process group's own world size
+    and backend, step path, bucket count / sizes / payload, and the exposed
+    all-reduce time per step (max over ranks)."""
+    r = _tiny_bench(4, ("--grad_dtype", "bf16"))
+    assert r["n_gpus"] == 4
+    c = r["comm"]
+    assert c["world_pg"] == 4 and c["backend_pg"] == "gloo" and c["active"]
+    assert c["step"] == "eager" and c["comm_mode"] == "eager" and "error" not in c, c
+    assert c["buckets"] == len(c["bucket_mib"]) >= 1 and abs(sum(c["bucket_mib"]) - c["total_mib"]) < 0.1
+    assert c["payload"] == "bf16"
+    assert c["exposed_allreduce_ms"] >= 0.0
+
+
 def test_bench_launcher_fails_when_a_rank_dies():
     env = dict(os.environ, D3D_FAULT_AT_STEP="0", D3D_FAULT_RANK="1", OMP_NUM_THREADS="2")
     env.pop("WORLD_SIZE", None)
