@@ -154,8 +154,16 @@ class Diff3D(nn.Module):
         ``model`` None -> this module's denoiser.  Returns the per-step images
         (numpy [b, 3, H, W] each, like the reference) or, with
         ``return_all=False``, the final image tensor.  The call without the
-        model argument, ``sample(img, R, T, K, w, ...)``, is accepted too."""
+        model argument, ``sample(img, R, T, K, w, timesteps)``, is accepted
+        too (every positional argument shifts by one, the step count
+        included).  Note the return type: the per-step list by default (as
+        the reference), the final tensor only with ``return_all=False``."""
         if isinstance(model, torch.Tensor):
+            if w is not None:
+                if not isinstance(w, int) or isinstance(w, bool):
+                    raise TypeError("sample(img, R, T, K, w, timesteps): timesteps must be an int, "
+                                    f"got {type(w).__name__}")
+                timesteps = w
             model, img, R, T, K, w = None, model, img, R, T, K
         net = model if model is not None else self.xunet_denoiser
         dev = next(net.parameters()).device

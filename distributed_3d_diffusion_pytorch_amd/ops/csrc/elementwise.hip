@@ -10,7 +10,7 @@
 //   diffusion_fwd2                : the whole training-input draw of one step in one launch:
 //                                   t ~ U[0,1), lambda(t), eps, z_t = q_sample, CFG drop
 //                                   (train.py:50-60,80-100) -> the stem's NHWC bf16 input
-//   diff_loss / diff_loss_bwd     : l2 / l1 epsilon loss read straight from the padded
+//   diff_loss / diff_loss_bwd     : l2 / l1 / huber epsilon loss read straight from the padded
 //                                   NHWC head output (train.py:102-112)
 #include "common.h"
 
@@ -340,7 +340,9 @@ __global__ void __launch_bounds__(256) diff_loss_part_k(const bf16* __restrict__
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const float d = (float)yp[c] - eps[(size_t)bb * 3 * HW + (size_t)c * HW + p];
-      acc += mode ? fabsf(d) : d * d;
+      // 0: l2, 1: l1, 2: huber = smooth_l1 with beta 1 (F.smooth_l1_loss, train.py:108-109)
+      const float ad = fabsf(d);
+      acc += mode == 0 ? d * d : (mode == 1 ? ad : (ad < 1.f ? 0.5f * d * d : ad - 0.5f));
     }
   }
   __shared__ float red[4];
@@ -377,7 +379,8 @@ __global__ void diff_loss_bwd_k(const bf16* __restrict__ y, const float* __restr
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const float d = (float)yp[c] - eps[(size_t)bb * 3 * HW + (size_t)c * HW + p];
-      o[c] = (bf16)(mode ? g * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) : 2.f * g * d);
+      const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+      o[c] = (bf16)(mode == 0 ? 2.f * g * d : (mode == 1 ? g * sgn : g * (fabsf(d) < 1.f ? d : sgn)));
     }
     *reinterpret_cast<bf16x8*>(dy + (size_t)i * CP) = o;
   }

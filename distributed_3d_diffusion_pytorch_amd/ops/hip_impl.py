@@ -487,7 +487,7 @@ class _CatGNDense(torch.autograd.Function):
         OC = wb.shape[0]
         a2, b2 = a.reshape(-1, C1), b.reshape(-1, C2)
         C = C1 + C2
-        if _gemm_ok(OC, a2.shape[0], C1, C, C1) and _gemm_ok(OC, b2.shape[0], C2, C, C2):
+        if _gemm_ok(OC, a2.shape[0], C1, C, C1, a2, wb) and _gemm_ok(OC, b2.shape[0], C2, C, C2, b2, wb[:, C1:]):
             # two GEMMs over the halves; the second accumulates through its residual epilogue
             skip = torch.empty(a2.shape[0], OC, dtype=BF16, device=a.device)
             gemm_nt(wb, a2, skip, OC, a2.shape[0], C1, C, C1, OC, bias=db.detach() if db is not None else None)
@@ -518,7 +518,8 @@ class _CatGNDense(torch.autograd.Function):
         g2 = g.reshape(-1, OC)
         OCp = _up(OC, 64)
         rows_ = g2.shape[0]
-        if g2.is_contiguous() and _gemm_ok(C1, rows_, OC, OCp, OC) and _gemm_ok(C2, rows_, OC, OCp, OC):
+        if g2.is_contiguous() and _gemm_ok(C1, rows_, OC, OCp, OC, g2, da, db_in) and \
+                _gemm_ok(C2, rows_, OC, OCp, OC, g2, da, db_in):
             pk = packed_weight(dw, True, 1)                      # [ICp][OCp]: rows = input channels
             d2a, d2b = da.view(-1, C1), db_in.view(-1, C2)
             gemm_nt(pk, g2, d2a, C1, rows_, OC, OCp, OC, C1, res=d2a)
@@ -1044,9 +1045,17 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         return torch.mm(a, b).float()
 
 
-def _gemm_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
-    """Shapes csrc/gemm.hip takes (K % 64 == 0 and >= 128, M % 8 == 0, 16-byte rows)."""
-    return bool(_lib.d3d_gemm_nt_ok(M, N, K, lda, ldb))
+def _gemm_ok(M: int, N: int, K: int, lda: int, ldb: int, *ops: Optional[torch.Tensor], res=None) -> bool:
+    """Shapes csrc/gemm.hip takes (K % 64 == 0 and >= 128, M % 8 == 0, 16-byte
+    rows), and -- for the operand / output tensors given -- the pointer
+    conditions d3d_gemm checks at launch (16-byte aligned operands and output,
+    8-byte aligned residual), so an odd view takes the caller's library
+    fallback instead of failing the launch."""
+    if not _lib.d3d_gemm_nt_ok(M, N, K, lda, ldb):
+        return False
+    if any(t is not None and t.data_ptr() % 16 for t in ops):
+        return False
+    return res is None or res.data_ptr() % 8 == 0
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, M: int, N: int, K: int, lda: int, ldb: int, ldo: int,
@@ -1083,7 +1092,7 @@ class _Linear(torch.autograd.Function):
         OC = weight.shape[0]
         L = shp[1] if len(shp) == 3 else 0
         r = residual.reshape(P, OC).contiguous() if residual is not None else None
-        if x2.is_contiguous() and _gemm_ok(OC, P, IC, IC, IC):
+        if x2.is_contiguous() and _gemm_ok(OC, P, IC, IC, IC, x2, res=r):
             gnp = None
             if gn is not None and L and L % 64 == 0 and OC % gn["groups"] == 0 and \
                     OC // gn["groups"] in (4, 8, 16, 32):
@@ -1137,7 +1146,7 @@ class _Linear(torch.autograd.Function):
             ks = scale
         if ctx.needs_input_grad[0]:
             OCp = _up(OC, 64)
-            if g.is_contiguous() and _gemm_ok(IC, rows, OC, OCp, OC):
+            if g.is_contiguous() and _gemm_ok(IC, rows, OC, OCp, OC, g):
                 dx = torch.empty(rows, IC, dtype=g.dtype, device=g.device)
                 gemm_nt(packed_weight(weight, True, 1), g, dx, IC, rows, OC, OCp, OC, IC, alpha=float(ks))
             else:
@@ -1262,7 +1271,7 @@ class _FiLMBatch(torch.autograd.Function):
         bcat = bf16_cat(list(Bs), "filmB")
         S = wcat.shape[0]
         y = torch.empty(P, S, dtype=BF16, device=e.device)
-        if _gemm_ok(S, P, K, K, K) and slot.want_events:
+        if _gemm_ok(S, P, K, K, K, x2) and slot.want_events:
             # one GEMM per block's column slice, each followed by an event:
             # the trunk's block i waits for its own modulation only, so the
             # conditioning stream computes slice i + 1 while block i runs
@@ -1275,7 +1284,7 @@ class _FiLMBatch(torch.autograd.Function):
                 ev.record()
                 slot.events.append(ev)
                 off += wd
-        elif _gemm_ok(S, P, K, K, K):
+        elif _gemm_ok(S, P, K, K, K, x2):
             gemm_nt(wcat, x2, y, S, P, K, K, K, S, bias=bcat)
         else:
             _fallback("film_batch", f"P={P} K={K} S={S} (library GEMM)")
@@ -1325,7 +1334,7 @@ class _FiLMBatch(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(rows, K, dtype=BF16, device=x2.device)
-            if _gemm_ok(K, rows, S, S, S):
+            if _gemm_ok(K, rows, S, S, S, dy, e2):
                 # d e = (dy @ Wcat) * dsilu(e), the SiLU derivative in the epilogue
                 gemm_nt(bf16_catT(Ws, "filmWT"), dy, dx, K, rows, S, S, S, K, dsilu_of=e2, ldr=K)
             else:
@@ -1882,7 +1891,7 @@ def diffusion_inputs(img, seed, e0=0, cond_prob=0.1, logsnr_min=-20.0, logsnr_ma
     return xz, eps, lam, keep.view(torch.bool)
 
 
-_LOSS_MODES = {"l2": 0, "l1": 1}
+_LOSS_MODES = {"l2": 0, "l1": 1, "huber": 2}
 
 
 class _DiffLoss(torch.autograd.Function):
@@ -1911,7 +1920,10 @@ class _DiffLoss(torch.autograd.Function):
 def diff_loss_nhwc(y, eps, loss_type="l2"):
     """Epsilon loss read straight from the channel-padded NHWC head output
     (two launches forward, one backward; deterministic partial sums)."""
-    if loss_type not in _LOSS_MODES or y.shape[-1] != 8 or y.dtype != BF16:
+    if loss_type not in _LOSS_MODES:
+        raise ValueError(f"loss_type {loss_type!r}: expected one of {sorted(_LOSS_MODES)}")
+    if y.shape[-1] != 8 or y.dtype != BF16:
+        _fallback("diff_loss", f"head layout {tuple(y.shape)} {y.dtype}")
         return _t.diff_loss_nhwc(y, eps, loss_type)
     return _DiffLoss.apply(y.contiguous(), eps.float().contiguous(), _LOSS_MODES[loss_type])
 

@@ -62,3 +62,8 @@ def test_diff3d_api(srn):
     torch.manual_seed(1)
     c = m.sample(None, batch[0], R2, batch[2].float(), batch[3][0].float(), 2.0, timesteps=2, return_all=False)
     assert torch.allclose(a[0], c[0]) and not torch.allclose(a[1], c[1])
+    # the legacy call without the model: the positional step count shifts with the rest
+    imgs3 = m.sample(batch[0][:, 0], batch[1].float(), batch[2].float(), batch[3][0].float(), 2.0, 3)
+    assert len(imgs3) == 3
+    with pytest.raises(TypeError):
+        m.sample(batch[0][:, 0], batch[1].float(), batch[2].float(), batch[3][0].float(), 2.0, 2.5)

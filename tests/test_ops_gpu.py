@@ -1004,7 +1004,7 @@ def test_diffusion_inputs_kernel_matches_torch(H):
     assert torch.equal(eg, ee) and torch.equal(xg, xe) and torch.equal(lg, le) and torch.equal(kg, ke)
 
 
-@pytest.mark.parametrize("loss_type", ["l2", "l1"])
+@pytest.mark.parametrize("loss_type", ["l2", "l1", "huber"])
 def test_diff_loss_kernel(H, loss_type):
     torch.manual_seed(4)
     y = torch.randn(6, 32, 32, 8, device=DEV).to(BF)

@@ -6,6 +6,13 @@ utilisation, the LDS bank-conflict share and the HBM-side read / write rate.
 
   clock   = GRBM_GUI_ACTIVE / 8 XCDs / wall time
   MFMA    = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+
+GRBM_GUI_ACTIVE counts over the profiler's counter window, which brackets the
+dispatch with a few microseconds of its own: for short dispatches the window
+is longer than the kernel and the ratio above reads as an impossible clock
+(>2.4 GHz, the part's peak).  Those rows print the clock as "-" and take the
+MFMA denominator from the wall time at the peak clock instead (a lower bound
+of the utilisation).
   LDS-cf  = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   rd, wr  = 2 x FETCH_SIZE (gfx950 tallies 128-B requests at 64 B), WRITE_SIZE;
             KiB per dispatch over its wall time; L3 (Infinity Cache) hits are
@@ -18,6 +25,8 @@ import glob
 import os
 import sys
 from collections import defaultdict
+
+PEAK_GHZ = 2.4          # MI355X peak engine clock
 
 
 def load(d):
@@ -58,7 +67,13 @@ def main(p1, p2, p3):
         a = c1[key]
         gui = a.get("GRBM_GUI_ACTIVE", 0.0)
         ghz = gui / 8 / ns if ns else 0.0
-        mfma = a.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024 * gui / 8) * 100 if gui else 0.0
+        if ghz > PEAK_GHZ * 1.02:           # counter window longer than the dispatch (see the module doc)
+            ghz_s = "    -"
+            cyc = ns * PEAK_GHZ
+        else:
+            ghz_s = f"{ghz:5.2f}"
+            cyc = gui / 8
+        mfma = a.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024 * cyc) * 100 if cyc else 0.0
         lds = a.get("SQ_LDS_IDX_ACTIVE", 0.0)
         ldscf = a.get("SQ_LDS_BANK_CONFLICT", 0.0) / lds * 100 if lds else 0.0
         rd = wr = float("nan")
@@ -66,7 +81,7 @@ def main(p1, p2, p3):
             rd = 2 * c2[key].get("FETCH_SIZE", 0.0) * 1024 / t2[key][1]
         if key in t3 and t3[key][1]:
             wr = c3[key].get("WRITE_SIZE", 0.0) * 1024 / t3[key][1]
-        print(f"{key[0]:<44} {key[1]:>7} {n:>4} {ns / n / 1e3:8.1f} {ns / total * 100:6.1f} {ghz:5.2f} {mfma:6.1f} "
+        print(f"{key[0]:<44} {key[1]:>7} {n:>4} {ns / n / 1e3:8.1f} {ns / total * 100:6.1f} {ghz_s} {mfma:6.1f} "
               f"{ldscf:6.2f} {rd:8.0f} {wr:8.0f}")
 
 
