@@ -295,7 +295,7 @@ class ConditioningProcessor(nn.Module):
             s = 2 ** i
             e_emb = ops.conv3x3(emb_img, conv.weight, None, stride=s) if emb_img is not None else None
             e = ops.cond_conv(rays_dir, orig_pe, conv.weight, conv.bias, s, row_bias=logsnr_emb, residual=e_emb,
-                              res_period=2 if e_emb is not None else 0)
+                              res_period=2 if e_emb is not None else 0, silu_out=True)
             yield e
 
 

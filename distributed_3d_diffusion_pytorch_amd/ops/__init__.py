@@ -75,9 +75,14 @@ def carry_gn_stats(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
     return dst
 
 
-def cond_conv(rays_dir, orig_pe, weight, bias, stride: int, row_bias=None, residual=None, res_period: int = 0):
+def cond_conv(rays_dir, orig_pe, weight, bias, stride: int, row_bias=None, residual=None, res_period: int = 0,
+              silu_out: bool = False):
+    """``silu_out``: (HIP) the output also carries silu(output) for the FiLM
+    projections (film_batch then skips its SiLU pass); ignored by the torch
+    composition, which film_batch handles itself."""
     if use_hip(rays_dir):
-        return _h().cond_conv(rays_dir, orig_pe, weight, bias, stride, row_bias, residual, res_period)
+        return _h().cond_conv(rays_dir, orig_pe, weight, bias, stride, row_bias, residual, res_period,
+                              silu_out=silu_out)
     return _t.cond_conv(rays_dir, orig_pe, weight, bias, stride, row_bias, residual, res_period)
 
 

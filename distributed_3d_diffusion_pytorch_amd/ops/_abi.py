@@ -20,7 +20,7 @@ SIGNATURES = {
     "d3d_gn_film": [P, P, P, P, P, P, I, I, I, I, F, U64, I, P, P],
     "d3d_gn_bwd": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, P],
     "d3d_ray_dir": [P, P, P, P, I, I, I, I, P],
-    "d3d_border_fix": [P, P, I, I, I, I, I, I, I, P],
+    "d3d_border_fix": [P, P, I, I, I, I, I, I, I, P, P],
     "d3d_border_sums": [P, P, I, I, I, I, P],
     "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, I, P, P],
     "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P, F, P],
@@ -52,6 +52,7 @@ SIGNATURES = {
     "d3d_pack_conv_weight": [P, P, I, I, I, I, I, P],
     "d3d_conv": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P],
     "d3d_conv2": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P],
+    "d3d_conv3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P, IP, P],
     "d3d_conv_plan": [I, I, I, I, I, I],
     "d3d_set_conv_korder": [I],
     "d3d_set_wgrad_impl": [I],

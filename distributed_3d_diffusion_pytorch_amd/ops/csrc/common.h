@@ -109,6 +109,16 @@ __device__ __forceinline__ Moments merge_moments(Moments a, Moments b) {
   return r;
 }
 
+// Optional second conv output: silu of the stored (bf16-rounded) output
+// values, written next to them by the conv epilogue (the conditioning convs,
+// whose output feeds the FiLM projections through a SiLU, xunet.py:84).
+__device__ __forceinline__ void silu_store4(bf16* __restrict__ O2, long off, bf16x4 o4) {
+  bf16x4 s4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) s4[e] = (bf16)siluf_((float)o4[e]);
+  *reinterpret_cast<bf16x4*>(O2 + off) = s4;
+}
+
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // ----------------------------------------- fused GroupNorm statistics -----

@@ -34,8 +34,10 @@ __device__ __forceinline__ bool border_pixel(int b, int OH, int OW, int& oh, int
   return false;
 }
 
+// y2 != nullptr: y's SiLU companion (written by the conv epilogue from the
+// uncorrected border values) is rewritten at the corrected pixels.
 __global__ void border_fix_k(bf16* __restrict__ y, const float* __restrict__ U, int IH, int IW, int OH, int OW,
-                             int OC, int stride) {
+                             int OC, int stride, bf16* __restrict__ y2) {
   const int n = blockIdx.y;
   int oh, ow;
   if (!border_pixel(blockIdx.x, OH, OW, oh, ow)) return;
@@ -58,6 +60,13 @@ __global__ void border_fix_k(bf16* __restrict__ y, const float* __restrict__ U, 
         for (int j = 0; j < 8; ++j) v[j] -= u[j];
       }
     st8(row + c, v);
+    if (y2) {
+      const f32x8 r = ld8(row + c);         // the stored (bf16-rounded) values, as the SiLU pass reads them
+      f32x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = siluf_(r[j]);
+      st8(y2 + (row - y) + c, o);
+    }
   }
 }
 
@@ -93,10 +102,10 @@ __global__ void border_sums_k(const bf16* __restrict__ dy, float* __restrict__ S
 }  // namespace
 
 D3D_API int d3d_border_fix(void* y, const float* U, int N, int IH, int IW, int OH, int OW, int OC, int stride,
-                           hipStream_t st) {
+                           void* y2, hipStream_t st) {
   if (OC % 8) return (int)hipErrorInvalidValue;
   const int nb = OW + (OH > 1 ? OW : 0) + 2 * (OH > 2 ? OH - 2 : 0);
-  hipLaunchKernelGGL(border_fix_k, dim3(nb, N), dim3(128), 0, st, (bf16*)y, U, IH, IW, OH, OW, OC, stride);
+  hipLaunchKernelGGL(border_fix_k, dim3(nb, N), dim3(128), 0, st, (bf16*)y, U, IH, IW, OH, OW, OC, stride, (bf16*)y2);
   return (int)hipGetLastError();
 }
 

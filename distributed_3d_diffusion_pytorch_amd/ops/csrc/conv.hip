@@ -421,7 +421,7 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
             int in_bytes, int w_bytes, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC,
             int ldo, int stride, float scale, int res_nmod, float* __restrict__ part, int korder,
-            float* __restrict__ gnp, int gn_groups) {
+            float* __restrict__ gnp, int gn_groups, bf16* __restrict__ O2) {
   constexpr int BM = 128, BN = 128, BKk = 64;
   constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
   constexpr int STAGE = (BM + BN) * BKk;           // elements per stage
@@ -657,11 +657,13 @@ conv_bufl_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
           gq[i][0] += y * y;
         }
         *reinterpret_cast<bf16x4*>(dst) = o4;
+        if (O2) silu_store4(O2, dst - O, o4);
       } else {
         for (int e = 0; e < 4 && co + e < OC; ++e) {
           float t = v[e];
           if (res) t += (float)res[rpix * ldo + co + e];
           dst[e] = (bf16)(t * scale);
+          if (O2) O2[(dst - O) + e] = (bf16)siluf_((float)dst[e]);
           const float y = (float)dst[e];
           gs[i][0] += y;
           gq[i][0] += y * y;
@@ -724,7 +726,8 @@ __global__ void __launch_bounds__(512, 1)
 conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
           const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
           int in_bytes, int w_bytes, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC,
-          int ldo, int stride, float scale, int res_nmod, int korder, float* __restrict__ gnp, int gn_groups) {
+          int ldo, int stride, float scale, int res_nmod, int korder, float* __restrict__ gnp, int gn_groups,
+          bf16* __restrict__ O2) {
   constexpr int BKk = 64;
   // 8 waves as 2 x 4 (M x N) over >= 256-pixel tiles; 4 x 2 over the
   // 128-pixel tile (256 x 128: the 32x32 level at 16 examples per GPU, one
@@ -896,11 +899,13 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
           gq[i][j / 4] += y * y;
         }
         *reinterpret_cast<bf16x4*>(dst) = o4;
+        if (O2) silu_store4(O2, dst - O, o4);
       } else {
         for (int e = 0; e < 4 && co + e < OC; ++e) {
           float t = v[e];
           if (res) t += (float)res[rpix * ldo + co + e];
           dst[e] = (bf16)(t * scale);
+          if (O2) O2[(dst - O) + e] = (bf16)siluf_((float)dst[e]);
           const float y = (float)dst[e];
           gs[i][j / 4] += y;
           gq[i][j / 4] += y * y;
@@ -974,7 +979,7 @@ __global__ void __launch_bounds__(512, 1)
 conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
             int w_bytes, int Nimg, int OH, int IC, int ICp, int OC, float scale, int res_nmod,
-            float* __restrict__ gnp, int gn_groups) {
+            float* __restrict__ gnp, int gn_groups, bf16* __restrict__ O2) {
   typedef HaloGeom<OWT, BNT> Gm;
   constexpr int BM = 128, BN = BNT, WM = 64, WN = BN / 4, TM = 4, TN = WN / 16;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * Gm::HBUF + 4 * Gm::ABUF];
@@ -1217,6 +1222,7 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
         gq[i][j / 4] += y * y;
       }
       *reinterpret_cast<bf16x4*>(O + pix * OC + co) = o4;
+      if (O2) silu_store4(O2, pix * OC + co, o4);
     }
   }
   if (gnp) gn_part_store<TM, NH>(gs, gq, lane, m0 + wm * WM, n0 + wn * WN, OC, gn_groups, OHW, Mpix, gnp);
@@ -1227,7 +1233,7 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
 __global__ void conv_splitk_epi_k(const float* __restrict__ part, int nsplit, long Mpix, int OC, int OHW,
                                   const float* __restrict__ bias, const float* __restrict__ row_bias,
                                   const bf16* __restrict__ res, int res_nmod, bf16* __restrict__ O, int ldo,
-                                  float scale) {
+                                  float scale, bf16* __restrict__ O2) {
   const long nv = Mpix * (OC / 4);
   const long slab = Mpix * OC;
   for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nv; v += (long)gridDim.x * blockDim.x) {
@@ -1252,6 +1258,7 @@ __global__ void conv_splitk_epi_k(const float* __restrict__ part, int nsplit, lo
 #pragma unroll
     for (int e = 0; e < 4; ++e) o4[e] = (bf16)(a[e] * scale);
     *reinterpret_cast<bf16x4*>(O + pix * ldo + co) = o4;
+    if (O2) silu_store4(O2, pix * ldo + co, o4);
   }
 }
 
@@ -1265,7 +1272,7 @@ __global__ void __launch_bounds__(256) conv_splitk_epi_gn_k(const float* __restr
                                                             const float* __restrict__ row_bias,
                                                             const bf16* __restrict__ res, int res_nmod,
                                                             bf16* __restrict__ O, float scale,
-                                                            float* __restrict__ gnp, int G) {
+                                                            float* __restrict__ gnp, int G, bf16* __restrict__ O2) {
   constexpr int CB = 64, TPC = CB / 4, PPI = 256 / TPC;   // 16 threads per pixel, 16 pixels per pass
   __shared__ float s_s[PPI][CB / 4], s_q[PPI][CB / 4];
   const int tid = threadIdx.x, r = tid / TPC, cq = tid % TPC;
@@ -1308,6 +1315,7 @@ __global__ void __launch_bounds__(256) conv_splitk_epi_gn_k(const float* __restr
       sq += y * y;
     }
     *reinterpret_cast<bf16x4*>(O + pix * OC + co) = o4;
+    if (O2) silu_store4(O2, pix * OC + co, o4);
   }
   s_s[r][cq] = sum;
   s_q[r][cq] = sq;
@@ -2640,7 +2648,7 @@ static int g_s64 = 1;
 extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias, const float* row_bias,
                                 const void* res, void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW,
                                 int OC, int ldo, int stride, int trans, float scale, int res_nmod, int taps,
-                                float* gnp, int gn_groups, int* gn_done, hipStream_t st);
+                                float* gnp, int gn_groups, int* gn_done, hipStream_t st, void* O2);
 // 64x64 no-split tiles (conv_small.hip) on grids of at most g_s64_maxb
 // 128x128 blocks (default 160): the 16x16 / 8x8 levels at 16 examples per GPU
 // and the 8x8 level at 32 (in-graph A/B: +1.1 % at bs16; the 16x16 level at
@@ -2695,12 +2703,17 @@ D3D_API int d3d_conv_plan(int N, int OH, int OW, int OC, int ICp, int taps) {
 // output (gn_part_store layout, gn_groups groups) when the chosen kernel can;
 // *gn_done reports whether it did (the caller runs the statistics pass
 // otherwise).
-D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
+// O2 != nullptr: also write silu(output) to O2 (same layout) when the chosen
+// kernel can; *silu_done reports whether it did (the caller runs the SiLU
+// pass otherwise).
+D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
                       void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
                       int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, float* gnp,
-                      int gn_groups, int* gn_done, hipStream_t st) {
+                      int gn_groups, int* gn_done, void* O2, int* silu_done, hipStream_t st) {
   long Mpix = (long)N * OH * OW;
   if (gn_done) *gn_done = 0;
+  if (silu_done) *silu_done = 0;
+  if (!silu_done) O2 = nullptr;
   // Operands beyond the kernels' 32-bit buffer offsets (2 GiB: e.g. the
   // 256-channel decoder concat of 128x128 images at one micro-batch of 128):
   // run the conv over image chunks that fit, each at full speed, instead of
@@ -2717,21 +2730,24 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
       per = per / q * q;
       if (per >= 1) {
         const int parts_per_img = (OH * OW) % 64 == 0 ? OH * OW / 64 : 0;
-        int all_gn = 1;
+        int all_gn = 1, all_silu = 1;
         for (int n0 = 0; n0 < N; n0 += (int)per) {
           const int nc = (int)std::min<long>(per, N - n0);
-          int d = 0;
-          const int rc = d3d_conv2((const char*)I + n0 * img_in, Wp, bias,
+          int d = 0, ds = 0;
+          const int rc = d3d_conv3((const char*)I + n0 * img_in, Wp, bias,
                                    row_bias ? row_bias + (long)n0 * OC : nullptr,
                                    res ? (res_nmod > 0 ? res : (const char*)res + n0 * img_out) : nullptr,
                                    (char*)O + n0 * img_out, nc, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans, scale,
                                    res_nmod, taps, ws, nsplit,
                                    gnp ? gnp + (long)n0 * gn_groups * parts_per_img * 2 : nullptr, gn_groups,
-                                   gn_done ? &d : nullptr, st);
+                                   gn_done ? &d : nullptr, O2 ? (char*)O2 + n0 * img_out : nullptr,
+                                   O2 ? &ds : nullptr, st);
           if (rc) return rc;
           all_gn &= d;
+          all_silu &= ds;
         }
         if (gn_done) *gn_done = gnp ? all_gn : 0;
+        if (silu_done) *silu_done = O2 ? all_silu : 0;
         return 0;
       }
     }
@@ -2746,7 +2762,8 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
   if (nsplit < 1 || !ws || g_conv_impl < 1) nsplit = 1;
   if (g_conv_impl >= 2 && nsplit == 1 && s64_wanted(Mpix, OC, ICp, taps)) {
     const int r = d3d_conv_s64_try(I, Wp, bias, row_bias, res, O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans,
-                                   scale, res_nmod, taps, gnp, gn_groups, gn_done, st);
+                                   scale, res_nmod, taps, gnp, gn_groups, gn_done, st, O2);
+    if (r > 0 && silu_done) *silu_done = O2 ? 1 : 0;
     if (r != 0) return r < 0 ? -r : 0;
   }
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM), (unsigned)nsplit);
@@ -2760,7 +2777,7 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
 #define HALO(OWv, TR)                                                                                              \
   hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias,     \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale,   \
-                     res_nmod, gnp, gn_groups)
+                     res_nmod, gnp, gn_groups, (bf16*)O2)
       if (OW == 64) {
         if (trans) HALO(64, true); else HALO(64, false);
       } else {
@@ -2768,6 +2785,7 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
       }
 #undef HALO
       if (gn_done && gnp) *gn_done = 1;
+      if (silu_done && O2) *silu_done = 1;
       return (int)hipGetLastError();
     }
   }
@@ -2792,7 +2810,7 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
 #define W8(TP, TR, BMv, BNv)                                                                                     \
   hipLaunchKernelGGL((conv_w8_k<TP, TR, BMv, BNv>), g8, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias, \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, \
-                     OC, ldo, stride, scale, res_nmod, g_conv_korder, gnp, gn_groups)
+                     OC, ldo, stride, scale, res_nmod, g_conv_korder, gnp, gn_groups, (bf16*)O2)
       if (bn == 128) {
         if (taps == 9) {
           if (trans) W8(9, true, 256, 128); else W8(9, false, 256, 128);
@@ -2814,6 +2832,7 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
       }
 #undef W8
       if (gn_done && gnp) *gn_done = 1;
+      if (silu_done && O2) *silu_done = 1;
       return (int)hipGetLastError();
     }
   }
@@ -2822,7 +2841,8 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
 #define BUFL(TP, TR, OB)                                                                                         \
   hipLaunchKernelGGL((conv_bufl_k<TP, TR, OB>), grid, dim3(256), 0, st, (const bf16*)I, (const bf16*)Wp, bias,    \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, \
-                     OC, ldo, stride, scale, res_nmod, part, g_conv_korder, part ? nullptr : gnp, gn_groups)
+                     OC, ldo, stride, scale, res_nmod, part, g_conv_korder, part ? nullptr : gnp, gn_groups,       \
+                     part ? nullptr : (bf16*)O2)
     if (g_conv_impl >= 3) {
       if (taps == 9) {
         if (trans) BUFL(9, true, true); else BUFL(9, false, true);
@@ -2841,17 +2861,18 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
       // gnp non-null implies ldo == OC, 64 | H*W and Cg <= 32
       hipLaunchKernelGGL(conv_splitk_epi_gn_k, dim3((unsigned)(Mpix / 64), (unsigned)(OC / 64)), dim3(256), 0, st,
                          part, nsplit, Mpix, OC, OH * OW, bias, row_bias, (const bf16*)res, res_nmod, (bf16*)O,
-                         scale, gnp, gn_groups);
+                         scale, gnp, gn_groups, (bf16*)O2);
       if (gn_done) *gn_done = 1;
     } else if (part) {
       long nv = Mpix * (OC / 4);
       long g = (nv + 255) / 256;
       if (g > 4096) g = 4096;
       hipLaunchKernelGGL(conv_splitk_epi_k, dim3((unsigned)g), dim3(256), 0, st, part, nsplit, Mpix, OC, OH * OW,
-                         bias, row_bias, (const bf16*)res, res_nmod, (bf16*)O, ldo, scale);
+                         bias, row_bias, (const bf16*)res, res_nmod, (bf16*)O, ldo, scale, (bf16*)O2);
     } else if (gn_done && gnp) {
       *gn_done = 1;
     }
+    if (silu_done && O2) *silu_done = 1;
     return (int)hipGetLastError();
   }
   if (g_conv_impl >= 1 && g_zero16) {
@@ -2871,7 +2892,7 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
       long g = (nv + 255) / 256;
       if (g > 4096) g = 4096;
       hipLaunchKernelGGL(conv_splitk_epi_k, dim3((unsigned)g), dim3(256), 0, st, part, nsplit, Mpix, OC, OH * OW,
-                         bias, row_bias, (const bf16*)res, res_nmod, (bf16*)O, ldo, scale);
+                         bias, row_bias, (const bf16*)res, res_nmod, (bf16*)O, ldo, scale, (bf16*)nullptr);
     }
     return (int)hipGetLastError();
   }
@@ -2886,6 +2907,14 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
   }
 #undef LAUNCH
   return (int)hipGetLastError();
+}
+
+D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
+                      void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
+                      int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, float* gnp,
+                      int gn_groups, int* gn_done, hipStream_t st) {
+  return d3d_conv3(I, Wp, bias, row_bias, res, O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans, scale,
+                   res_nmod, taps, ws, nsplit, gnp, gn_groups, gn_done, nullptr, nullptr, st);
 }
 
 D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,

@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256 * G, G == 1 ? 2 : 1)
 conv_s64_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
            const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
            int w_bytes, int Nimg, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
-           float scale, int res_nmod, float* __restrict__ gnp, int gn_groups) {
+           float scale, int res_nmod, float* __restrict__ gnp, int gn_groups, bf16* __restrict__ O2) {
   constexpr int BM = S64_BM, BN = S64_BN, BK = S64_BK;
   constexpr int STAGE = (BM + BN) * BK;                 // elements
   static_assert(G * NS * STAGE * 2 <= 160 * 1024 - 1024, "LDS");
@@ -247,11 +247,13 @@ conv_s64_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float*
           gq[i] += y * y;
         }
         *reinterpret_cast<bf16x4*>(dst) = o4;
+        if (O2) silu_store4(O2, dst - O, o4);
       } else {
         for (int e = 0; e < 4 && co + e < OC; ++e) {
           float t = v[e];
           if (res) t += (float)res[rpix * ldo + co + e];
           dst[e] = (bf16)(t * scale);
+          if (O2) O2[(dst - O) + e] = (bf16)siluf_((float)dst[e]);
           const float y = (float)dst[e];
           gs[i] += y;
           gq[i] += y * y;
@@ -325,7 +327,7 @@ D3D_API void d3d_conv_s64_cfg(int cfg) { g_s64_cfg = cfg; }
 extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias, const float* row_bias,
                                 const void* res, void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW,
                                 int OC, int ldo, int stride, int trans, float scale, int res_nmod, int taps,
-                                float* gnp, int gn_groups, int* gn_done, hipStream_t st) {
+                                float* gnp, int gn_groups, int* gn_done, hipStream_t st, void* O2) {
   const long Mpix = (long)N * OH * OW;
   const long in_bytes = (long)N * IH * IW * IC * 2;
   const long w_bytes = (long)((OC + 127) / 128 * 128) * taps * ICp * 2;
@@ -345,7 +347,7 @@ extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias
 #define S64(TP, TR, GV, NSV)                                                                                    \
   hipLaunchKernelGGL((conv_s64_k<TP, TR, GV, NSV>), grid, dim3(256 * GV), 0, st, (const bf16*)I, (const bf16*)Wp, \
                      bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, \
-                     OW, OC, ldo, stride, scale, res_nmod, gnp, gn_groups)
+                     OW, OC, ldo, stride, scale, res_nmod, gnp, gn_groups, (bf16*)O2)
 #define S64G(TP, TR)                                                                                            \
   do {                                                                                                          \
     if (cfg == 4) S64(TP, TR, 4, 2);                                                                            \

@@ -62,6 +62,9 @@ class GradSink:
         self.stream_enabled = os.environ.get("D3D_WGRAD_STREAM", "1") != "0"
         self.graph_defer = True      # weight gradients on the side stream inside graph capture too
         self.defer_batch = 8         # jobs per fork (4 measured 1.5 % slower at bs16)
+        # eager steps: queue the grouped-kernel jobs too and flush them 8 at a
+        # time (one grouped launch each) instead of one launch pair per job
+        self.eager_group = os.environ.get("D3D_WGRAD_EAGER_GROUP", "0") == "1"
         self._queue = []
         self._compute = []
         self._streams: Dict[int, "torch.cuda.Stream"] = {}
@@ -188,8 +191,9 @@ class GradSink:
         ``spec``: the same job as a grouped-kernel descriptor
         (hip_impl.wgrad_job); a flush runs all queued specs as ONE grouped
         launch (:attr:`group_fn`) instead of their closures."""
-        if (self.stream_enabled and self.graph_defer and dev.type == "cuda"
-                and torch.cuda.is_current_stream_capturing()):
+        capturing = dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
+        if self.stream_enabled and dev.type == "cuda" and (
+                (self.graph_defer and capturing) or (self.eager_group and spec is not None and not capturing)):
             # the submitting stream travels with the job: its inputs were
             # produced there, and it need not be the stream that flushes
             # (conditioning-stream jobs are often flushed from the compute

@@ -636,10 +636,12 @@ def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=Fa
 
 # ----------------------------------------------------------------- conv ----
 def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale, res_nmod=0,
-              taps=9, gn_groups=0):
+              taps=9, gn_groups=0, silu_out=None):
     """Launch the conv; with gn_groups > 0 the epilogue may also emit the
     GroupNorm partial statistics of ``out``: returns (part, nparts) when it
-    did (the consuming GroupNorm then skips its statistics pass), else None."""
+    did (the consuming GroupNorm then skips its statistics pass), else None.
+    ``silu_out``: also write silu(out) there -- from the epilogue when the
+    chosen kernel can, else by the SiLU pass."""
     _ensure_impl()
     ns = _lib.d3d_conv_plan(N, OH, OW, OC, ICp, taps) if ldo == OC else 1
     ws = torch.empty(ns * N * OH * OW * OC, dtype=F32, device=x.device) if ns > 1 else None
@@ -647,9 +649,13 @@ def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo
     if gn_groups and (OH * OW) % 64 == 0:
         gnp = torch.empty(N * gn_groups * (OH * OW // 64) * 2, dtype=F32, device=x.device)
     done = ctypes.c_int(0)
-    _chk(_lib.d3d_conv2(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
+    sdone = ctypes.c_int(0)
+    _chk(_lib.d3d_conv3(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
                         IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), taps, _ptr(ws), ns,
-                        _ptr(gnp), int(gn_groups), ctypes.byref(done), _st()), "conv")
+                        _ptr(gnp), int(gn_groups), ctypes.byref(done), _ptr(silu_out), ctypes.byref(sdone), _st()),
+         "conv")
+    if silu_out is not None and not sdone.value:
+        _chk(_lib.d3d_silu(out.data_ptr(), silu_out.data_ptr(), out.numel(), _st()), "silu")
     return (gnp, OH * OW // 64) if done.value else None
 
 
@@ -921,7 +927,7 @@ class _CondConv(torch.autograd.Function):
     144-channel conv; 3x fewer conv FLOPs and half the weight-gradient tiles."""
 
     @staticmethod
-    def forward(ctx, rays_dir, orig_pe, weight, bias, row_bias, residual, stride, res_period):
+    def forward(ctx, rays_dir, orig_pe, weight, bias, row_bias, residual, stride, res_period, aux=None):
         N, H, W, ICd = rays_dir.shape
         OC, IC = weight.shape[0], weight.shape[1]
         no = orig_pe.shape[1]
@@ -936,9 +942,16 @@ class _CondConv(torch.autograd.Function):
             rb = rb + row_bias.float()
         out = torch.empty(N, OH, OW, OC, dtype=BF16, device=rays_dir.device)
         res = residual.contiguous() if residual is not None else None
+        # aux: also produce silu(out) -- the FiLM projections' GEMM operand
+        # (xunet.py:84) -- from the conv epilogue + the border correction,
+        # instead of a separate SiLU pass over the level embedding
+        so = torch.empty_like(out) if aux is not None else None
         _conv_fwd(rays_dir, wp, bias, rb.contiguous(), res, out, N, H, W, ICd, ICd, OH, OW, OC, OC, stride, False,
-                  1.0, res_period, 9)
-        _chk(_lib.d3d_border_fix(out.data_ptr(), U.data_ptr(), N, H, W, OH, OW, OC, stride, _st()), "border_fix")
+                  1.0, res_period, 9, silu_out=so)
+        _chk(_lib.d3d_border_fix(out.data_ptr(), U.data_ptr(), N, H, W, OH, OW, OC, stride, _ptr(so), _st()),
+             "border_fix")
+        if aux is not None:
+            aux["silu"] = so
         ctx.save_for_backward(rays_dir, orig_pe, weight)
         ctx.cfg = (stride, residual is not None, row_bias is not None, bias is not None, res_period)
         ctx.bias_param = bias
@@ -991,13 +1004,19 @@ class _CondConv(torch.autograd.Function):
         if has_res:
             dres = g if not res_period else \
                 g.reshape(N // res_period, res_period, *g.shape[1:]).sum(0, dtype=F32).to(g.dtype)
-        return None, None, dW, db, drb, dres, None, None
+        return None, None, dW, db, drb, dres, None, None, None
 
 
-def cond_conv(rays_dir, orig_pe, weight, bias, stride, row_bias=None, residual=None, res_period=0):
+def cond_conv(rays_dir, orig_pe, weight, bias, stride, row_bias=None, residual=None, res_period=0, silu_out=False):
+    """``silu_out``: the output carries ``_d3d_silu`` = silu(output), produced
+    with it (consumed by :func:`film_batch` instead of its SiLU pass)."""
     _need_bf16(rays_dir, residual)
-    return _CondConv.apply(rays_dir, orig_pe.float().contiguous(), weight, bias, row_bias, residual, stride,
-                           res_period)
+    aux = {} if silu_out else None
+    y = _CondConv.apply(rays_dir, orig_pe.float().contiguous(), weight, bias, row_bias, residual, stride,
+                        res_period, aux)
+    if aux is not None:
+        y._d3d_silu = aux["silu"]
+    return y
 
 
 def ray_posenc_dir(R, t, K, H, W, cond_mask, rescale_from=0, ld=64):
@@ -1259,14 +1278,17 @@ class _FiLMBatch(torch.autograd.Function):
     reduction scatters rows into each block's parameter gradient."""
 
     @staticmethod
-    def forward(ctx, e, slot, n, *wb):
+    def forward(ctx, e, slot, n, se, *wb):
         Ws, Bs = wb[:n], wb[n:]
         shp = e.shape
         K = shp[-1]
         e2 = e.reshape(-1, K)
         P = e2.shape[0]
-        x2 = torch.empty_like(e2)                           # silu(e): the GEMM operand, kept for the wgrad
-        _chk(_lib.d3d_silu(e2.data_ptr(), x2.data_ptr(), e2.numel(), _st()), "silu")
+        if se is not None:
+            x2 = se.reshape(-1, K)                          # silu(e) from the producing conv's epilogue
+        else:
+            x2 = torch.empty_like(e2)                       # silu(e): the GEMM operand, kept for the wgrad
+            _chk(_lib.d3d_silu(e2.data_ptr(), x2.data_ptr(), e2.numel(), _st()), "silu")
         wcat = bf16_cat(Ws, "filmW")
         bcat = bf16_cat(list(Bs), "filmB")
         S = wcat.shape[0]
@@ -1294,8 +1316,8 @@ class _FiLMBatch(torch.autograd.Function):
         ctx.params = (Ws, Bs)
         ctx.widths = [w.shape[0] for w in Ws]
         for i, (w, b) in enumerate(zip(Ws, Bs)):
-            SINK.use(w, ctx.needs_input_grad[3 + i])
-            SINK.use(b, ctx.needs_input_grad[3 + n + i])
+            SINK.use(w, ctx.needs_input_grad[4 + i])
+            SINK.use(b, ctx.needs_input_grad[4 + n + i])
         y = y.view(*shp[:-1], S)
         outs, off = [], 0
         for wd in ctx.widths:
@@ -1343,7 +1365,7 @@ class _FiLMBatch(torch.autograd.Function):
                 _chk(_lib.d3d_dsilu(e2.data_ptr(), ds.data_ptr(), dx.data_ptr(), dx.numel(), _st()), "dsilu")
             dx = dx.view(shp)
         grads_w, grads_b = [None] * n, [None] * n
-        need_w = any(ctx.needs_input_grad[3: 3 + n])
+        need_w = any(ctx.needs_input_grad[4: 4 + n])
         if need_w:
             tw = [SINK.target(w) for w in Ws]
             tb = [SINK.target(b) for b in Bs]
@@ -1386,7 +1408,7 @@ class _FiLMBatch(torch.autograd.Function):
                 job()
                 grads_w = [t.view(w.shape) for t, w in zip(tw, Ws)]
                 grads_b = tb
-        return (dx, None, None, *grads_w, *grads_b)
+        return (dx, None, None, None, *grads_w, *grads_b)
 
 
 def film_batch(emb, weights, biases, block_events=False):
@@ -1403,7 +1425,10 @@ def film_batch(emb, weights, biases, block_events=False):
         se = silu(emb)
         return tuple(linear(se, w, b) for w, b in zip(weights, biases))
     slot = _FiLMSlot(emb.shape[:-1], sum(widths), emb.device, want_events=bool(block_events))
-    outs = _FiLMBatch.apply(emb.contiguous(), slot, len(weights), *weights, *biases)
+    se = getattr(emb, "_d3d_silu", None)          # silu(emb) written by the conditioning conv (cond_conv)
+    if se is not None and (se.shape != emb.shape or not se.is_contiguous() or not emb.is_contiguous()):
+        se = None
+    outs = _FiLMBatch.apply(emb.contiguous(), slot, len(weights), se, *weights, *biases)
     off = 0
     for i, (o, wd) in enumerate(zip(outs, widths)):
         o._d3d_slot = (slot, off)

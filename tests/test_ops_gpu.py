@@ -737,6 +737,41 @@ def test_cond_conv_split_matches_full_conv(H, s):
         assert rel(a, c) < 3e-2, (name, rel(a, c))
 
 
+@pytest.mark.parametrize("N,Hh,s", [(4, 16, 1), (4, 16, 2), (4, 16, 4), (8, 64, 1), (8, 64, 2), (4, 64, 8),
+                                    (32, 64, 4), (32, 64, 8), (64, 64, 8)])
+def test_cond_conv_silu_companion(H, N, Hh, s):
+    """cond_conv(silu_out=True): the conv epilogue (halo / w8 / bufl / split-K
+    / small-tile forms, by shape) + the border correction write silu(output)
+    next to the output -- bitwise what the SiLU pass makes of the stored
+    output -- and film_batch consumes it (same projections as from the
+    output alone)."""
+    torch.manual_seed(8)
+    OC, no = 1024, 93
+    rays_dir = torch.zeros(N, Hh, Hh, 64, device=DEV)
+    rays_dir[..., :51] = torch.randn(N, Hh, Hh, 51, device=DEV)
+    rays_dir = rays_dir.to(BF)
+    orig = torch.randn(N, no, device=DEV)
+    w = torch.randn(OC, 144, 3, 3, device=DEV) / 36
+    b = torch.randn(OC, device=DEV) * 0.1
+    rb = torch.randn(N, OC, device=DEV)
+    OHs = (Hh - 1) // s + 1
+    res = torch.randn(2, OHs, OHs, OC, device=DEV).to(BF)
+    with torch.no_grad():
+        y = H.cond_conv(rays_dir, orig, w, b, s, rb, res, 2, silu_out=True)
+        se = y._d3d_silu
+        ref = torch.empty_like(y)
+        H._chk(H._lib.d3d_silu(y.data_ptr(), ref.data_ptr(), y.numel(), H._st()), "silu")
+        torch.cuda.synchronize()
+        assert torch.equal(se, ref)
+        ws = [torch.randn(256, OC, device=DEV) / 32, torch.randn(512, OC, device=DEV) / 32]
+        bs = [torch.randn(256, device=DEV), torch.randn(512, device=DEV)]
+        a = H.film_batch(y, ws, bs)
+        y2 = y.clone()                         # no companion: film_batch runs its own SiLU pass
+        c = H.film_batch(y2, ws, bs)
+        for u, v in zip(a, c):
+            assert torch.equal(u, v)
+
+
 def test_sgemm_strided_matches_einsum(H):
     """Strided batched fp32 GEMM (small_gemm.hip) on the conditioning conv's
     three permuted products == the fp32 einsums, incl. beta accumulation."""
