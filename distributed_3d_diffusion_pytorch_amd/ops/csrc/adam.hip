@@ -145,7 +145,10 @@ __global__ void __launch_bounds__(256) adam_pack_tiles_k(float* __restrict__ p, 
                                                          float* __restrict__ ema, const float* __restrict__ hp,
                                                          const AdamTile* __restrict__ tiles,
                                                          const int* __restrict__ blk_tile) {
-  __shared__ float tile[32 * 16 * 9];
+  // rows padded by one float: the transposed reads below step through rows
+  // (stride 16 * 9 = 144 floats = 16 mod 32 banks put every row of a lane
+  // group on two banks -- 51 % LDS conflict cycles at bs16); 145 spreads them
+  __shared__ float tile[32 * (16 * 9 + 1)];
   const AdamTile d = tiles[blk_tile[blockIdx.x]];
   const int local = blockIdx.x - d.blk0, tid = threadIdx.x, T = d.taps;
   const int nct = (d.OC + 31) / 32;
@@ -155,19 +158,50 @@ __global__ void __launch_bounds__(256) adam_pack_tiles_k(float* __restrict__ p, 
               grad_scale = hp[6], ema_w = hp[7];
   // tile element k -> (row r, q = ci * T + tap); each row's 16 * T elements
   // are contiguous in the OIHW master (16 * 9 floats = 576 B)
-  const int RW = 16 * T;
-  for (int k = tid; k < 32 * RW; k += 256) {
-    const int r = k / RW, q = k - r * RW;
-    const int ci = q / T;
-    if (r >= nco || ci >= nci) continue;
-    const long i = d.off + ((long)(co0 + r) * d.IC + ci0) * T + q;
-    float mm = m[i], vv = v[i];
-    const float pn = adam_elem(p[i], g[i], mm, vv, b1, b2, eps, wd, step_size, inv_bc2, grad_scale);
-    p[i] = pn;
-    m[i] = mm;
-    v[i] = vv;
-    if (ema) ema[i] = ema[i] + ema_w * (pn - ema[i]);
-    tile[k] = pn;
+  const int RW = 16 * T, RP = RW + 1;
+  const long rowlen = (long)d.IC * T;
+  if (nci == 16 && ((d.off | rowlen) & 3) == 0) {
+    // full channel tile: every row is 16 * T contiguous, 16-byte aligned
+    // floats -- 16-byte loads / stores of p, g, m, v (and the EMA)
+    const int RW4 = RW / 4;
+    for (int k = tid; k < 32 * RW4; k += 256) {
+      const int r = k / RW4, q = (k - r * RW4) * 4;
+      if (r >= nco) continue;
+      const long i = d.off + ((long)(co0 + r) * d.IC + ci0) * T + q;
+      f32x4 pp = *reinterpret_cast<const f32x4*>(p + i), gg = *reinterpret_cast<const f32x4*>(g + i);
+      f32x4 mm = *reinterpret_cast<const f32x4*>(m + i), vv = *reinterpret_cast<const f32x4*>(v + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float mj = mm[j], vj = vv[j];
+        pp[j] = adam_elem(pp[j], gg[j], mj, vj, b1, b2, eps, wd, step_size, inv_bc2, grad_scale);
+        mm[j] = mj;
+        vv[j] = vj;
+        tile[r * RP + q + j] = pp[j];
+      }
+      *reinterpret_cast<f32x4*>(p + i) = pp;
+      *reinterpret_cast<f32x4*>(m + i) = mm;
+      *reinterpret_cast<f32x4*>(v + i) = vv;
+      if (ema) {
+        f32x4 ee = *reinterpret_cast<const f32x4*>(ema + i);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ee[j] = ee[j] + ema_w * (pp[j] - ee[j]);
+        *reinterpret_cast<f32x4*>(ema + i) = ee;
+      }
+    }
+  } else {
+    for (int k = tid; k < 32 * RW; k += 256) {
+      const int r = k / RW, q = k - r * RW;
+      const int ci = q / T;
+      if (r >= nco || ci >= nci) continue;
+      const long i = d.off + ((long)(co0 + r) * d.IC + ci0) * T + q;
+      float mm = m[i], vv = v[i];
+      const float pn = adam_elem(p[i], g[i], mm, vv, b1, b2, eps, wd, step_size, inv_bc2, grad_scale);
+      p[i] = pn;
+      m[i] = mm;
+      v[i] = vv;
+      if (ema) ema[i] = ema[i] + ema_w * (pn - ema[i]);
+      tile[r * RP + q] = pn;
+    }
   }
   __syncthreads();
   if (d.dst1) {
@@ -178,7 +212,7 @@ __global__ void __launch_bounds__(256) adam_pack_tiles_k(float* __restrict__ p, 
       if (ci >= nci || c8 >= nco) continue;
       bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (bf16)(c8 + e < nco ? tile[(c8 + e) * RW + ci * T + tap] : 0.f);
+      for (int e = 0; e < 8; ++e) o[e] = (bf16)(c8 + e < nco ? tile[(c8 + e) * RP + ci * T + tap] : 0.f);
       *reinterpret_cast<bf16x8*>(d.dst1 + ((long)(ci0 + ci) * T + tap) * d.OCp1 + co0 + c8) = o;
     }
   }
@@ -192,7 +226,7 @@ __global__ void __launch_bounds__(256) adam_pack_tiles_k(float* __restrict__ p, 
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int ci = h * 8 + e;
-        o[e] = (bf16)(ci < nci ? tile[r * RW + ci * T + tap] : 0.f);
+        o[e] = (bf16)(ci < nci ? tile[r * RP + ci * T + tap] : 0.f);
       }
       *reinterpret_cast<bf16x8*>(d.dst0 + ((long)(co0 + r) * T + tap) * d.ICp0 + ci0 + h * 8) = o;
     }
