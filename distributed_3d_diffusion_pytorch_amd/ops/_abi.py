@@ -25,6 +25,7 @@ SIGNATURES = {
     "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, I, P, P],
     "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P, F, P],
     "d3d_conv_s64_cfg": [I],
+    "d3d_conv_res_cfg": [I],
     # elementwise.hip
     "d3d_silu": [P, P, L, P],
     "d3d_dsilu": [P, P, P, L, P],

@@ -721,7 +721,11 @@ __device__ __forceinline__ void w8_issue(bf16* sA, const bf16* I, const bf16* Wp
   }
 }
 
-template <int TAPS, bool TRANS, int BM, int BN>
+// RES = false: no residual operand (res must be null) -- the prefetch
+// registers (TM x TN x 2 VGPRs) are not reserved, which the 256-VGPR budget of
+// the 8-wave tile needs for its fragment reads (the dgrad and the first conv of
+// a ResnetBlock carry no residual).
+template <int TAPS, bool TRANS, int BM, int BN, bool RES = true>
 __global__ void __launch_bounds__(512, 1)
 conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
           const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O,
@@ -801,9 +805,9 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
   const int OHW = OH * OW;
   // residual prefetch (see conv_halo_k): issued ahead of the first stage,
   // drained with it, held in registers through the K loop
-  bf16x4 rres[TM][TN];
+  bf16x4 rres[RES ? TM : 1][RES ? TN : 1];
   const bool vec_out = (ldo & 3) == 0;
-  if (res && vec_out) {
+  if (RES && res && vec_out) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const long pix = n0 + wn * WN + j * 16 + fr;
@@ -820,11 +824,13 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
   }
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (res && vec_out) {
+  if constexpr (RES) {
+    if (res && vec_out) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(__builtin_bit_cast(unsigned long long, rres[i][j])));
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(__builtin_bit_cast(unsigned long long, rres[i][j])));
+    }
   }
   __builtin_amdgcn_s_barrier();
   for (int ks = 0; ks < nk; ++ks) {
@@ -886,9 +892,11 @@ conv_w8_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* 
       }
       bf16* dst = O + pix * ldo + co;
       if (co + 3 < OC && vec_out) {
-        if (res) {
+        if constexpr (RES) {
+          if (res) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)rres[i][j][e];
+            for (int e = 0; e < 4; ++e) v[e] += (float)rres[i][j][e];
+          }
         }
         bf16x4 o4;
 #pragma unroll
@@ -974,7 +982,7 @@ __device__ __forceinline__ void halo_issue_b(bf16* sH, const bf16* I, int in_byt
                                              hoff[k] + (unsigned)cbyte, 0, 0, 0);
 }
 
-template <int OWT, bool TRANS, int BNT = 512, bool PF = false>
+template <int OWT, bool TRANS, int BNT = 512, bool PF = false, bool RES = true>   // RES: see conv_w8_k
 __global__ void __launch_bounds__(512, 1)
 conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
@@ -1047,8 +1055,8 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   // epilogue the 8-byte residual reads (16 pixels x 32 B per instruction)
   // were fully exposed -- one block per CU, nothing left to overlap them --
   // and cost +30 % on the level-0 conv (tools/kbench_conv_epi.py).
-  bf16x4 rres[TM][TN];
-  if (res) {
+  bf16x4 rres[RES ? TM : 1][RES ? TN : 1];
+  if (RES && res) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const long pix = n0 + wn * WN + j * 16 + fr;
@@ -1127,12 +1135,14 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   halo_issue_a(sAr + Gm::ABUF, Wp, w_bytes, aoff, a_soff(1), wave);
   halo_issue_a(sAr + 2 * Gm::ABUF, Wp, w_bytes, aoff, a_soff(2), wave);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (res) {
-    // pin the prefetched values here (keeps the loads ahead of the K loop)
+  if constexpr (RES) {
+    if (res) {
+      // pin the prefetched values here (keeps the loads ahead of the K loop)
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(__builtin_bit_cast(unsigned long long, rres[i][j])));
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(__builtin_bit_cast(unsigned long long, rres[i][j])));
+    }
   }
 
   for (int c = 0; c < NCH; ++c) {
@@ -1209,9 +1219,11 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + cb[i][e];
-      if (res) {
+      if constexpr (RES) {
+        if (res) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += (float)rres[i][j][e];
+          for (int e = 0; e < 4; ++e) v[e] += (float)rres[i][j][e];
+        }
       }
       bf16x4 o4;
 #pragma unroll
@@ -2659,6 +2671,13 @@ static bool s64_wanted(long Mpix, int OC, int ICp, int taps) {
   const long blocks64 = ((Mpix + 63) / 64) * (OC / 64);
   return g_s64 && OC % 64 == 0 && (taps * ICp) % 64 == 0 && blocks128 <= g_s64_maxb && blocks64 >= 128;
 }
+// 1: the residual-free convs (dgrad, conv1) still run the residual-capable
+// kernel variants (round-3 behaviour; A/B switch for the RES template)
+static int g_conv_res_always = 0;
+D3D_API int d3d_conv_res_cfg(int always) {
+  g_conv_res_always = always;
+  return 0;
+}
 static int g_conv_impl = -1;      // 0: register-staged, 1: glds pipeline, 2: buffer-descriptor LDS-DMA
 static int g_conv_korder = 1;     // glds k-step order: 1 channel-chunk major, 0 tap major
 static int g_wgrad_impl = 5;      // 0: register-staged; 1-4: glds (PK,NS) = (64,2) (32,2) (32,3) (64,3); 5: bufl
@@ -2774,14 +2793,17 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
     auto nblk = [&](int bn) { return OH % (bn / OW) ? 0L : (long)N * (OH / (bn / OW)) * (OC / 128); };
     if (OW != 32 && nblk(512) >= 256) {
       dim3 gh((unsigned)(N * (OH / (512 / OW))), (unsigned)(OC / 128), 1);
-#define HALO(OWv, TR)                                                                                              \
-  hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias,     \
+#define HALO(OWv, TR, RS)                                                                                          \
+  hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512, false, RS>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, \
+                     bias,                                                                                         \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale,   \
                      res_nmod, gnp, gn_groups, (bf16*)O2)
       if (OW == 64) {
-        if (trans) HALO(64, true); else HALO(64, false);
+        if (trans) { if (res || g_conv_res_always) HALO(64, true, true); else HALO(64, true, false); }
+        else if (res || g_conv_res_always) HALO(64, false, true); else HALO(64, false, false);
       } else {
-        if (trans) HALO(128, true); else HALO(128, false);
+        if (trans) { if (res || g_conv_res_always) HALO(128, true, true); else HALO(128, true, false); }
+        else if (res || g_conv_res_always) HALO(128, false, true); else HALO(128, false, false);
       }
 #undef HALO
       if (gn_done && gnp) *gn_done = 1;
@@ -2807,10 +2829,14 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
     }
     if ((bm == 256 || wide) && blocks >= 256) {
       dim3 g8((unsigned)ptiles, (unsigned)((OC + bm - 1) / bm), 1);
-#define W8(TP, TR, BMv, BNv)                                                                                     \
-  hipLaunchKernelGGL((conv_w8_k<TP, TR, BMv, BNv>), g8, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias, \
+#define W8R(TP, TR, BMv, BNv, RS)                                                                                \
+  hipLaunchKernelGGL((conv_w8_k<TP, TR, BMv, BNv, RS>), g8, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, bias, \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, IH, IW, IC, ICp, OH, OW, \
                      OC, ldo, stride, scale, res_nmod, g_conv_korder, gnp, gn_groups, (bf16*)O2)
+#define W8(TP, TR, BMv, BNv)                                                                                     \
+  do {                                                                                                          \
+    if (res || g_conv_res_always) W8R(TP, TR, BMv, BNv, true); else W8R(TP, TR, BMv, BNv, false);               \
+  } while (0)
       if (bn == 128) {
         if (taps == 9) {
           if (trans) W8(9, true, 256, 128); else W8(9, false, 256, 128);
@@ -2831,6 +2857,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
         }
       }
 #undef W8
+#undef W8R
       if (gn_done && gnp) *gn_done = 1;
       if (silu_done && O2) *silu_done = 1;
       return (int)hipGetLastError();

@@ -1,0 +1,63 @@
+"""3x3 convs of the four X-UNet levels in isolation, as the training step
+launches them: forward without residual (a ResnetBlock's conv1: bias + GN
+partials), forward with residual + 1/sqrt2 (conv2), and the input gradient.
+JSON lines with median device time and TF/s.
+
+    python tools/kbench_conv_levels.py [N frames ...]     (default: 32 256 = bs16, bs128)
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from distributed_3d_diffusion_pytorch_amd.ops import hip_impl as H
+
+BF = torch.bfloat16
+
+
+def timeit(fn, iters=25):
+    for _ in range(4):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    ns = [int(a) for a in sys.argv[1:]] or [32, 256]
+    H._ensure_impl()
+    H._lib.d3d_conv_res_cfg(int(os.environ.get("D3D_CONV_RES_ALWAYS", "0")))
+    for N in ns:
+        for Hh, C in ((64, 128), (32, 256), (16, 256), (8, 512)):
+            x = torch.randn(N, Hh, Hh, C, device="cuda").to(BF)
+            w = torch.randn(C, C, 3, 3, device="cuda") * 0.03
+            b = torch.randn(C, device="cuda") * 0.1
+            r = torch.randn(N, Hh, Hh, C, device="cuda").to(BF)
+            fl = 2.0 * N * Hh * Hh * C * C * 9
+            with torch.no_grad():
+                f1 = timeit(lambda: H.conv3x3(x, w, b, gn_groups=32))
+                f2 = timeit(lambda: H.conv3x3(x, w, b, residual=r, out_scale=0.7071, gn_groups=32))
+            xr = x.clone().requires_grad_(True)
+            y = H.conv3x3(xr, w, None)
+            g = torch.randn_like(y)
+            d = timeit(lambda: torch.autograd.grad(y, xr, g, retain_graph=True))
+            print(json.dumps({"res_always": os.environ.get("D3D_CONV_RES_ALWAYS", "0"), "N": N, "level": f"{Hh}x{Hh}x{C}", "fwd_us": round(f1, 1),
+                              "fwd_tfs": round(fl / f1 / 1e6, 1), "fwd_res_us": round(f2, 1),
+                              "fwd_res_tfs": round(fl / f2 / 1e6, 1), "dgrad_us": round(d, 1),
+                              "dgrad_tfs": round(fl / d / 1e6, 1)}), flush=True)
+            del x, r, xr, y, g
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
