@@ -192,8 +192,11 @@ class GradSink:
         (hip_impl.wgrad_job); a flush runs all queued specs as ONE grouped
         launch (:attr:`group_fn`) instead of their closures."""
         capturing = dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
-        if self.stream_enabled and dev.type == "cuda" and (
-                (self.graph_defer and capturing) or (self.eager_group and spec is not None and not capturing)):
+        # (queueing does not depend on the side stream: with it off the flush
+        # runs on the current stream, so the same jobs group the same way and
+        # the gradients are bitwise those of the side-stream step)
+        if dev.type == "cuda" and ((self.graph_defer and capturing) or
+                                   (self.eager_group and spec is not None and not capturing)):
             # the submitting stream travels with the job: its inputs were
             # produced there, and it need not be the stream that flushes
             # (conditioning-stream jobs are often flushed from the compute
@@ -216,6 +219,31 @@ class GradSink:
         if not self._queue:
             return
         q, self._queue = self._queue, []
+        grouped = self.group_fn is not None
+        if not self.stream_enabled:
+            # no side stream: issue in place (the queue was filled from this
+            # stream, or from a registered compute stream that the
+            # end-of-backward join covers)
+            idx = torch.cuda.current_device()
+            cur = torch.cuda.current_stream(idx)
+            for st in {j[3].cuda_stream: j[3] for j in q}.values():
+                if st.cuda_stream != cur.cuda_stream:
+                    cur.wait_stream(st)
+            if grouped:
+                specs = [j[4] for j in q if j[4] is not None]
+                if specs:
+                    self.group_fn(specs)
+            for fn, _, _, _, spec in q:
+                if spec is None or not grouped:
+                    fn()
+            for _, keep, _, st, _ in q:
+                if st.cuda_stream != cur.cuda_stream:       # read here, produced on another stream
+                    for t in keep:
+                        t.record_stream(cur)
+            for _, _, done, _, _ in q:
+                for p in done:
+                    self.done(p)
+            return
         idx = torch.cuda.current_device()
         side = self._side(idx)
         # wait for every stream a queued job was submitted from, not only the
@@ -231,7 +259,6 @@ class GradSink:
             if all(st.cuda_stream != w.cuda_stream for w in waited):
                 side.wait_stream(st)
                 waited.append(st)
-        grouped = self.group_fn is not None
         with torch.cuda.stream(side):
             if grouped:
                 specs = [j[4] for j in q if j[4] is not None]
