@@ -94,6 +94,7 @@ SIGNATURES = {
     # wgrad_group.hip (job tables: arrays of hip_impl._WgJob)
     "d3d_wgrad_group_cfg": [I, I, I],
     "d3d_wgrad_group_ok": [P],
+    "d3d_wgrad_group_wide": [I],
     "d3d_wgrad_group": [P, I, P, L, P],
     "d3d_wgrad_group_plan": [P, I, IP, IP, C.POINTER(C.c_long)],
 }

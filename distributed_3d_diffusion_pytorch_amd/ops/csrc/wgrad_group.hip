@@ -299,6 +299,227 @@ __global__ void __launch_bounds__(256, 2) wgrad_grp_k(GwTable tab) {
   }
 }
 
+// Wide tile: 128 output channels x TWO 128-column chunks of the (tap, input
+// channel) axis -- chunk c of a job is (tap c / ncb, channels (c % ncb) * 128
+// ...), so at 128 input channels a block covers two taps, at >= 256 two
+// channel slices of one tap.  Waves 2 (M) x 2 (chunk), 64 x 128 each (4 x 8
+// MFMA 16x16x32 tiles): twice the MFMAs per transposed LDS read of the 64 x 64
+// wave tile above -- that tile's per-K-step LDS traffic (fragment reads +
+// DMA) outran its 16 MFMAs per wave.
+template <int PK>
+__global__ void __launch_bounds__(256, 2) wgrad_grp2_k(GwTable tab) {
+  constexpr int BM = 128, NS = 2;
+  constexpr int WM = 64, TM = 4, TN = 8;
+  constexpr int STAGE = PK * 3 * 128;              // A | B chunk 0 | B chunk 1
+  constexpr int PPW = PK / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
+  __shared__ float bred[BM];
+  typedef __attribute__((address_space(3))) void lds_void;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int R;
+  {
+    const int T = gridDim.x, L = blockIdx.x;
+    const int q = T / 8, r = T % 8, xcd = L % 8;
+    R = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+  }
+  int k = 0;
+  while (k + 1 < tab.n && R >= tab.j[k + 1].blk0) ++k;
+  const GwJob& J = tab.j[k];
+  const bf16* dY = J.dy;
+  const int OC = J.OC, ICt = J.IC, C1 = J.C1, taps = J.taps, OH = J.H, OW = J.W, lw = J.lw;
+  const int ncb = J.ncb, nmb = J.nmb, splits = J.splits;
+  const long P = J.P;
+  const int nch = taps * ncb, npair = (nch + 1) / 2;
+  const int b = R - J.blk0;
+  const int bx = b % npair, by = (b / npair) % nmb, split = b / (npair * nmb);
+  const int m0 = by * BM;
+  const long p_begin = (long)split * J.pps;
+  const long p_end = p_begin + J.pps < P ? p_begin + J.pps : P;
+  // the two chunks of this block (chunk 1 may not exist: odd chunk count)
+  int tapc[2], ci0c[2], ci0gc[2], ICc[2], dpixc[2], khc[2], kwc[2];
+  bool validc[2];
+  const bf16* Ic[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int ch = 2 * bx + c;
+    validc[c] = ch < nch;
+    const int chv = validc[c] ? ch : 2 * bx;
+    tapc[c] = chv / ncb;
+    ci0gc[c] = (chv % ncb) * 128;
+    const bool second = J.x2 != nullptr && ci0gc[c] >= C1;
+    Ic[c] = second ? J.x2 : J.x;
+    ICc[c] = J.x2 == nullptr ? ICt : (second ? ICt - C1 : C1);
+    ci0c[c] = second ? ci0gc[c] - C1 : ci0gc[c];
+    khc[c] = taps == 9 ? tapc[c] / 3 : 1;
+    kwc[c] = taps == 9 ? tapc[c] % 3 : 1;
+    dpixc[c] = (khc[c] - 1) * OW + (kwc[c] - 1);
+  }
+
+  const int lrow = lane >> 4, pch = lane & 15;
+  int trow[PPW];
+  unsigned aoff[PPW], boff[2][PPW];
+  bool bok[2][PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    trow[i] = (wave * PPW + i) * 4 + lrow;
+    const int lc = pch ^ (2 * (trow[i] & 7));
+    const int co = m0 + lc * 8;
+    aoff[i] = co < OC ? (unsigned)((trow[i] * OC + co) * 2) : 0x80000000u;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int ci = ci0c[c] + lc * 8;
+      boff[c][i] = (unsigned)((trow[i] * ICc[c] + ci) * 2);
+      bok[c][i] = ci < ICc[c];
+    }
+  }
+  const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
+  const int x7 = 2 * ((4 * g + q) & 7);
+  int la[TM], lb[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) la[i] = (4 * g + q) * 128 + ((((wm * 8 + 2 * i + (pc >> 1)) ^ x7)) << 3) + (pc & 1) * 4;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) lb[j] = (4 * g + q) * 128 + ((((2 * j + (pc >> 1)) ^ x7)) << 3) + (pc & 1) * 4;
+
+  auto issue = [&](long p0, int stage) {
+    bf16* sA = smem + stage * STAGE;
+    const __amdgpu_buffer_rsrc_t rA = gw_rsrc(dY + p0 * OC, (p_end - p0) * OC * 2);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sA + (wave * PPW + i) * 4 * 128), 16, aoff[i], 0, 0,
+                                               0);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (!validc[c]) continue;                    // (block-uniform)
+      bf16* sB = sA + (1 + c) * PK * 128;
+      const long pb = p0 + dpixc[c];
+      const long in_elems = P * ICc[c];
+      const __amdgpu_buffer_rsrc_t rB = gw_rsrc(Ic[c] + pb * ICc[c], (in_elems - pb * ICc[c]) * 2);
+      const int wedge = kwc[c] == 0 ? 0 : OW - 1, hedge = khc[c] == 0 ? 0 : OH - 1;
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) {
+        const int pp = (int)p0 + trow[i];
+        bool bad = !bok[c][i];
+        if (kwc[c] != 1) bad |= (pp & (OW - 1)) == wedge;
+        if (khc[c] != 1) bad |= ((pp >> lw) & (OH - 1)) == hedge;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * PPW + i) * 4 * 128), 16,
+                                                 bad ? 0x80000000u : boff[c][i], 0, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const long nsteps = (p_end - p_begin + PK - 1) / PK;
+  const bool do_bias = J.db != nullptr && bx == 0;
+  const bool mine = validc[wn];                   // this wave's chunk exists (wave-uniform)
+  float bacc = 0.f;
+  const int bcol = tid & 127, bhalf = tid >> 7;
+  auto compute = [&](const bf16* a) {
+    const bf16* bb = a + (1 + wn) * PK * 128;
+    if (do_bias) {
+#pragma unroll
+      for (int r = 0; r < PK / 2; ++r) {
+        const int row = bhalf * (PK / 2) + r;
+        bacc += (float)a[row * 128 + ((((bcol >> 3) ^ (2 * (row & 7)))) << 3) + (bcol & 7)];
+      }
+    }
+    if (!mine) return;
+#pragma unroll
+    for (int kk = 0; kk < PK / 32; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        gs16x4 lo = gw_tr(bb + lb[j] + kk * 32 * 128);
+        gs16x4 hi = gw_tr(bb + lb[j] + kk * 32 * 128 + 16 * 128);
+        gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        gs16x4 lo = gw_tr(a + la[i] + kk * 32 * 128);
+        gs16x4 hi = gw_tr(a + la[i] + kk * 32 * 128 + 16 * 128);
+        gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  if (nsteps > 0) issue(p_begin, 0);
+  for (long s = 0; s < nsteps; ++s) {
+    const int st = (int)(s & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nsteps) issue(p_begin + (s + 1) * PK, st ^ 1);
+    __builtin_amdgcn_s_setprio(1);
+    compute(smem + st * STAGE);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const long KW = (long)taps * ICt;
+  const int tap = tapc[wn], ci0 = ci0c[wn], ci0g = ci0gc[wn], IC = ICc[wn];
+  if (splits == 1) {
+    const float sc = J.scale;
+    float* dw = J.dw;
+    const int acc_in = J.acc;
+    if (do_bias) {                                  // block-uniform: the barrier is safe
+      if (bhalf) bred[bcol] = bacc;
+      __syncthreads();
+      if (!bhalf && m0 + bcol < OC) {
+        const float v = (bacc + bred[bcol]) * sc;
+        float* d = J.db + m0 + bcol;
+        *d = acc_in ? *d + v : v;
+      }
+    }
+    if (!mine) return;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cl = ci0 + j * 16 + fr;
+      if (cl >= IC || cl >= ci0 + 128) continue;
+      const int ci = ci0g - ci0 + cl;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (co + e < OC) {
+            float* d = dw + ((long)(co + e) * ICt + ci) * taps + tap;
+            const float v = acc[i][j][e] * sc;
+            *d = acc_in ? *d + v : v;
+          }
+      }
+    }
+    return;
+  }
+  if (do_bias && m0 + bcol < OC) J.bslab[((long)split * 2 + bhalf) * OC + m0 + bcol] = bacc;
+  if (!mine) return;
+  float* slab = J.slab + (long)split * OC * KW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cl = ci0 + j * 16 + fr;
+    if (cl >= IC || cl >= ci0 + 128) continue;
+    const int ci = ci0g - ci0 + cl;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int co = m0 + wm * WM + i * 16 + fq * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < OC) slab[(long)(co + e) * KW + tap * ICt + ci] = acc[i][j][e];
+    }
+  }
+}
+
 // Grouped split-K reduce: block = (job, co, 64 input channels) summing every
 // tap of its channels over the job's slabs, 4 split lanes merged in a fixed
 // order through LDS, written as 64 x taps CONTIGUOUS floats of OIHW; blocks
@@ -379,11 +600,16 @@ static_assert(sizeof(WgJobDesc) == 80, "WgJobDesc must match hip_impl._WgJob");
 static int g_gw_blocks = 512;      // target blocks per grouped launch (2 per CU)
 static int g_gw_pk = 32;           // pixel rows per LDS stage (32 or 64)
 static int g_gw_minpix = 512;      // lower bound of the pixels per block
+static int g_gw_wide = 1;          // 1: 128 x 256 chunk-pair tiles (wgrad_grp2_k), 0: 128 x 128 (wgrad_grp_k)
 
 D3D_API int d3d_wgrad_group_cfg(int blocks, int pk, int minpix) {
   if (blocks > 0) g_gw_blocks = blocks;
   if (pk == 32 || pk == 64) g_gw_pk = pk;
   if (minpix > 0) g_gw_minpix = minpix;
+  return 0;
+}
+D3D_API int d3d_wgrad_group_wide(int wide) {
+  g_gw_wide = wide ? 1 : 0;
   return 0;
 }
 
@@ -417,7 +643,8 @@ static void gw_plan(const WgJobDesc* d, int n, GwPlan& pl) {
   double work = 0;
   for (int i = 0; i < n; ++i) {
     const long P = (long)d[i].N * d[i].H * d[i].W;
-    pl.tiles[i] = d[i].taps * cdiv(d[i].IC, GW_BN) * cdiv(d[i].OC, GW_BM);
+    const int nch = d[i].taps * cdiv(d[i].IC, GW_BN);
+    pl.tiles[i] = (g_gw_wide ? (nch + 1) / 2 : nch) * cdiv(d[i].OC, GW_BM);
     work += (double)pl.tiles[i] * P;
   }
   // one pixel count per block across the batch: ~g_gw_blocks equal blocks
@@ -520,10 +747,16 @@ D3D_API long d3d_wgrad_group(const WgJobDesc* d, int n, float* ws, long ws_float
       rblk += Rj.nblk_w + (D.db ? cdiv(D.OC, 64) : 0);
     }
   }
-  if (g_gw_pk == 64)
+  if (g_gw_wide) {
+    if (g_gw_pk == 64)
+      hipLaunchKernelGGL(wgrad_grp2_k<64>, dim3((unsigned)blk), dim3(256), 0, st, tab);
+    else
+      hipLaunchKernelGGL(wgrad_grp2_k<32>, dim3((unsigned)blk), dim3(256), 0, st, tab);
+  } else if (g_gw_pk == 64) {
     hipLaunchKernelGGL(wgrad_grp_k<64>, dim3((unsigned)blk), dim3(256), 0, st, tab);
-  else
+  } else {
     hipLaunchKernelGGL(wgrad_grp_k<32>, dim3((unsigned)blk), dim3(256), 0, st, tab);
+  }
   if (rt.n > 0) hipLaunchKernelGGL(wgrad_grp_reduce_k, dim3((unsigned)rblk), dim3(256), 0, st, rt);
   const int e = (int)hipGetLastError();
   return e ? -1000 - e : 0;

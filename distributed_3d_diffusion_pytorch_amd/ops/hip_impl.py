@@ -695,6 +695,10 @@ assert ctypes.sizeof(_WgJob) == 80
 # 1: weight-gradient jobs deferred inside graph capture run grouped, one
 # launch (+ one slab reduce) per sink flush; 0: one launch pair per job
 _WGRAD_GROUP = os.environ.get("D3D_WGRAD_GROUP", "1") != "0"
+if os.environ.get("D3D_WGRAD_GROUP_BLOCKS"):           # planner target (A/B knob): blocks per grouped launch
+    _lib.d3d_wgrad_group_cfg(int(os.environ["D3D_WGRAD_GROUP_BLOCKS"]), 0, 0)
+if os.environ.get("D3D_WGRAD_GROUP_WIDE"):             # A/B knob: 128 x 256 (1) or 128 x 128 (0) tiles
+    _lib.d3d_wgrad_group_wide(int(os.environ["D3D_WGRAD_GROUP_WIDE"]))
 
 
 def wgrad_job(dy, x, OC, IC, N, H, W, taps, dw, db=None, scale=1.0, accumulate=True, x2=None, C1=0):

@@ -617,8 +617,9 @@ def _wg_ref(g, x, taps):
     return dw.reshape(OC, IC, 9)
 
 
+@pytest.mark.parametrize("wide", [1, 0])
 @pytest.mark.parametrize("pk,blocks,minpix", [(32, 512, 512), (64, 512, 512), (32, 4096, 64)])
-def test_wgrad_group_matches_fp32(H, pk, blocks, minpix):
+def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide):
     """Grouped weight gradients (wgrad_group.hip): one launch over a mixed
     batch of 3x3 / 1x1 / virtual-concat jobs (+ the grouped slab reduce for
     the split ones) == the fp32 torch weight gradients, accumulated onto the
@@ -626,6 +627,7 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix):
     re-run.  The last case plans many more splits (small blocks)."""
     torch.manual_seed(5)
     H._lib.d3d_wgrad_group_cfg(blocks, pk, minpix)
+    H._lib.d3d_wgrad_group_wide(wide)
     try:
         jobs, refs, outs = [], [], []
         for (N, Hh, W, IC, OC, taps, C1, bias) in WG_JOBS:
@@ -671,6 +673,7 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix):
                 assert torch.equal(db, b1)
     finally:
         H._lib.d3d_wgrad_group_cfg(512, 32, 512)
+        H._lib.d3d_wgrad_group_wide(1)
 
 
 @pytest.mark.parametrize("micro", [2, 0])
