@@ -112,6 +112,27 @@ __device__ __forceinline__ void gw_issue(bf16* sA, bf16* sB, const bf16* __restr
   }
 }
 
+// the input (B) half of gw_issue alone: the second chunk of a wide tile
+template <int PK>
+__device__ __forceinline__ void gw_issue_b(bf16* sB, const bf16* __restrict__ I, long in_elems, long p0, int IC,
+                                           int OH, int OW, int kh, int kw, int dpix, int lw, int wave,
+                                           const int* trow, const unsigned* boff, const bool* bok) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  constexpr int PPW = PK / 16;
+  const long pb = p0 + dpix;
+  const __amdgpu_buffer_rsrc_t rB = gw_rsrc(I + pb * IC, (in_elems - pb * IC) * 2);
+  const int wedge = kw == 0 ? 0 : OW - 1, hedge = kh == 0 ? 0 : OH - 1;
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int pp = (int)p0 + trow[i];
+    bool bad = !bok[i];
+    if (kw != 1) bad |= (pp & (OW - 1)) == wedge;
+    if (kh != 1) bad |= ((pp >> lw) & (OH - 1)) == hedge;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * PPW + i) * 4 * GW_BN), 16,
+                                             bad ? 0x80000000u : boff[i], 0, 0, 0);
+  }
+}
+
 }  // namespace
 
 // One 128 (output channels) x 128 (input channels of one tap) tile of one
@@ -314,7 +335,6 @@ __global__ void __launch_bounds__(256, 2) wgrad_grp2_k(GwTable tab) {
   constexpr int PPW = PK / 16;
   __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
   __shared__ float bred[BM];
-  typedef __attribute__((address_space(3))) void lds_void;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -382,31 +402,15 @@ __global__ void __launch_bounds__(256, 2) wgrad_grp2_k(GwTable tab) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) lb[j] = (4 * g + q) * 128 + ((((2 * j + (pc >> 1)) ^ x7)) << 3) + (pc & 1) * 4;
 
+  // (a __device__ function, not a lambda body: buffer-resource values must
+  // not appear in host-visible code, or the host pass drops the kernel stub)
   auto issue = [&](long p0, int stage) {
     bf16* sA = smem + stage * STAGE;
-    const __amdgpu_buffer_rsrc_t rA = gw_rsrc(dY + p0 * OC, (p_end - p0) * OC * 2);
-#pragma unroll
-    for (int i = 0; i < PPW; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sA + (wave * PPW + i) * 4 * 128), 16, aoff[i], 0, 0,
-                                               0);
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      if (!validc[c]) continue;                    // (block-uniform)
-      bf16* sB = sA + (1 + c) * PK * 128;
-      const long pb = p0 + dpixc[c];
-      const long in_elems = P * ICc[c];
-      const __amdgpu_buffer_rsrc_t rB = gw_rsrc(Ic[c] + pb * ICc[c], (in_elems - pb * ICc[c]) * 2);
-      const int wedge = kwc[c] == 0 ? 0 : OW - 1, hedge = khc[c] == 0 ? 0 : OH - 1;
-#pragma unroll
-      for (int i = 0; i < PPW; ++i) {
-        const int pp = (int)p0 + trow[i];
-        bool bad = !bok[c][i];
-        if (kwc[c] != 1) bad |= (pp & (OW - 1)) == wedge;
-        if (khc[c] != 1) bad |= ((pp >> lw) & (OH - 1)) == hedge;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * PPW + i) * 4 * 128), 16,
-                                                 bad ? 0x80000000u : boff[c][i], 0, 0, 0);
-      }
-    }
+    gw_issue<PK>(sA, sA + PK * 128, dY, Ic[0], P * ICc[0], p0, p_end, OC, ICc[0], OH, OW, khc[0], kwc[0], dpixc[0],
+                 lw, wave, trow, aoff, boff[0], bok[0]);
+    if (validc[1])                                 // (block-uniform)
+      gw_issue_b<PK>(sA + 2 * PK * 128, Ic[1], P * ICc[1], p0, ICc[1], OH, OW, khc[1], kwc[1], dpixc[1], lw, wave,
+                     trow, boff[1], bok[1]);
   };
 
   f32x4 acc[TM][TN];

@@ -70,6 +70,16 @@ def build(force: bool = False, jobs: int = 8, debug: bool = False, verbose: bool
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stderr}")
         if verbose:
             print(f"[build] linked {OUT_}", flush=True)
+        # a kernel whose host pass silently failed (e.g. a buffer-resource value
+        # in a lambda) leaves its launch stub undefined: the library would only
+        # fail to load on the GPU box
+        nm = shutil.which("nm")
+        if nm:
+            r = subprocess.run([nm, "-D", "--undefined-only", OUT_], capture_output=True, text=True)
+            bad = [l.split()[-1] for l in r.stdout.splitlines() if "__device_stub__" in l]
+            if bad:
+                os.remove(OUT_)
+                raise RuntimeError(f"undefined kernel launch stubs in {OUT_}: {bad}")
     return OUT_
 
 
