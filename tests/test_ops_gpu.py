@@ -660,7 +660,9 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide):
             if ref_b is not None:
                 assert rel(db, ref_b) < 1e-4, (s, rel(db, ref_b))
             first.append((dw.clone(), db.clone() if db is not None else None))
-        assert max(sp) > 1 and min(sp) == 1, list(sp)        # both epilogues exercised
+        assert max(sp) > 1, list(sp)                          # split-K slabs + grouped reduce exercised
+        if blocks <= 1024:
+            assert min(sp) == 1, list(sp)                     # ... and the direct OIHW epilogue
         for (_, _, dw0, db0), (dw, db, _) in zip(refs, outs):  # re-run: bitwise
             dw.copy_(dw0)
             if db is not None:
