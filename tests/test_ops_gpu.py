@@ -675,7 +675,7 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide):
                 assert torch.equal(db, b1)
     finally:
         H._lib.d3d_wgrad_group_cfg(512, 32, 512)
-        H._lib.d3d_wgrad_group_wide(1)
+        H._lib.d3d_wgrad_group_wide(0)
 
 
 @pytest.mark.parametrize("micro", [2, 0])
