@@ -95,6 +95,7 @@ SIGNATURES = {
     "d3d_wgrad_group_cfg": [I, I, I],
     "d3d_wgrad_group_ok": [P],
     "d3d_wgrad_group_wide": [I],
+    "d3d_wgrad_group_stages": [I],
     "d3d_wgrad_group": [P, I, P, L, P],
     "d3d_wgrad_group_plan": [P, I, IP, IP, C.POINTER(C.c_long)],
 }

@@ -40,6 +40,31 @@ __device__ __forceinline__ gs16x4 gw_tr(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((glds_s16x4*)(p));
 }
 
+// The same transposed read as inline asm: the compiler's wait-count pass
+// cannot tell an LDS read from the LDS-DMA writes still in flight to the
+// OTHER ring slots, and put "s_waitcnt vmcnt(0)" in front of the first read
+// of every stage -- every stage waited for the stages issued after it, so no
+// DMA ever overlapped compute (the 59 % wait-parked cycles of the 2-stage
+// weight-gradient kernel).  Hidden from the pass, the reads are retired by an
+// explicit lgkmcnt wait (gw_tr_wait) that also pins the fragment registers.
+__device__ __forceinline__ gs16x4 gw_tr_asm(const bf16* p) {
+  gs16x4 v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+template <int TM, int TN>
+__device__ __forceinline__ void gw_tr_wait(bf16x8 (&a)[TM], bf16x8 (&b)[TN]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(a[i]));
+#pragma unroll
+  for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(b[j]));
+}
+__device__ __forceinline__ float gw_dot2(unsigned a, unsigned b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, a), __builtin_bit_cast(bf16x2, b), c, false);
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t gw_rsrc(const void* p, long bytes) {
   const unsigned long long a = (unsigned long long)p;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
@@ -86,10 +111,13 @@ template <int PK>
 __device__ __forceinline__ void gw_issue(bf16* sA, bf16* sB, const bf16* __restrict__ dY, const bf16* __restrict__ I,
                                          long in_elems, long p0, long p_end, int OC, int IC, int OH, int OW, int kh,
                                          int kw, int dpix, int lw, int wave, const int* trow, const unsigned* aoff,
-                                         const unsigned* boff, const bool* bok) {
+                                         const unsigned* boff, const bool* bok, bool on = true) {
   typedef __attribute__((address_space(3))) void lds_void;
   constexpr int PPW = PK / 16;
-  const __amdgpu_buffer_rsrc_t rA = gw_rsrc(dY + p0 * OC, (p_end - p0) * OC * 2);
+  // on = false: a pipeline-tail dummy -- zero-record descriptors, so the same
+  // number of DMAs is in flight at every wait (the data land in a slot no one
+  // reads)
+  const __amdgpu_buffer_rsrc_t rA = gw_rsrc(dY + p0 * OC, on ? (p_end - p0) * OC * 2 : 0);
 #pragma unroll
   for (int i = 0; i < PPW; ++i)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sA + (wave * PPW + i) * 4 * GW_BM), 16, aoff[i], 0, 0,
@@ -97,7 +125,7 @@ __device__ __forceinline__ void gw_issue(bf16* sA, bf16* sB, const bf16* __restr
   // the base may lie before the tensor (only masked top-padding rows see it)
   // or past its end on the last stages: the record count clamps at 0
   const long pb = p0 + dpix;
-  const __amdgpu_buffer_rsrc_t rB = gw_rsrc(I + pb * IC, (in_elems - pb * IC) * 2);
+  const __amdgpu_buffer_rsrc_t rB = gw_rsrc(I + pb * IC, on ? (in_elems - pb * IC) * 2 : 0);
   // padding rows of the (wave-uniform) tap: compare against the uniform edge
   // coordinate, branch-free per lane
   const int wedge = kw == 0 ? 0 : OW - 1, hedge = kh == 0 ? 0 : OH - 1;
@@ -138,14 +166,18 @@ __device__ __forceinline__ void gw_issue_b(bf16* sB, const bf16* __restrict__ I,
 // One 128 (output channels) x 128 (input channels of one tap) tile of one
 // split of one job per block; 4 waves of 64 x 64 (4 x 4 MFMA 16x16x32 tiles);
 // PK pixel rows per LDS stage, two stages, one barrier per stage.
-template <int PK>
+// NS-stage LDS ring, NS - 1 stages in flight: with two stages (one landing
+// while the other is read) the waves sat 59 % of their cycles in s_waitcnt /
+// s_barrier (profiles/pmc_wgrad): a 32-pixel stage is 16 MFMAs per wave,
+// far shorter than a DMA round trip.
+template <int PK, int NS>
 __global__ void __launch_bounds__(256, 2) wgrad_grp_k(GwTable tab) {
-  constexpr int BM = GW_BM, BN = GW_BN, NS = 2;
+  constexpr int BM = GW_BM, BN = GW_BN;
+  constexpr int PER = 2 * (PK / 16);              // DMA instructions per wave per stage
   constexpr int WM = 64, WN = 64, TM = 4, TN = 4;
   constexpr int STAGE = PK * (BM + BN);
   constexpr int PPW = PK / 16;
   __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
-  __shared__ float bred[BM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -203,10 +235,10 @@ __global__ void __launch_bounds__(256, 2) wgrad_grp_k(GwTable tab) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) lb[j] = (4 * g + q) * 128 + ((((wn * 8 + 2 * j + (pc >> 1)) ^ x7)) << 3) + (pc & 1) * 4;
 
-  auto issue = [&](long p0, int stage) {
+  auto issue = [&](long p0, int stage, bool on) {
     bf16* sA = smem + stage * STAGE;
     gw_issue<PK>(sA, sA + PK * BM, dY, I, in_elems, p0, p_end, OC, IC, OH, OW, kh, kw, dpix, lw, wave, trow, aoff,
-                 boff, bok);
+                 boff, bok, on);
   };
 
   f32x4 acc[TM][TN];
@@ -216,72 +248,95 @@ __global__ void __launch_bounds__(256, 2) wgrad_grp_k(GwTable tab) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const long nsteps = (p_end - p_begin + PK - 1) / PK;
+  // bias (column sums of dY): from the A fragments the MFMAs read anyway --
+  // lane l of fragment i holds 8 pixels of channel wm*64 + 16i + l%16, so a
+  // dot product with (1, 1) per bf16 pair sums them (the wn = 1 waves read the
+  // same fragments and skip it)
   const bool do_bias = J.db != nullptr && bx == 0;
-  float bacc = 0.f;
-  const int bcol = tid & 127, bhalf = tid >> 7;   // bias: column, half of the stage's rows
+  const bool bias_wave = do_bias && wn == 0;
+  float bsum[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) bsum[i] = 0.f;
+  const unsigned ones = 0x3F803F80u;              // bf16 (1, 1)
   auto compute = [&](const bf16* a) {
     const bf16* bb = a + PK * BM;
-    if (do_bias) {
-#pragma unroll
-      for (int r = 0; r < PK / 2; ++r) {
-        const int row = bhalf * (PK / 2) + r;
-        bacc += (float)a[row * 128 + ((((bcol >> 3) ^ (2 * (row & 7)))) << 3) + (bcol & 7)];
-      }
-    }
 #pragma unroll
     for (int kk = 0; kk < PK / 32; ++kk) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        gs16x4 lo = gw_tr(a + la[i] + kk * 32 * 128);
-        gs16x4 hi = gw_tr(a + la[i] + kk * 32 * 128 + 16 * 128);
-        gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
       for (int j = 0; j < TN; ++j) {
-        gs16x4 lo = gw_tr(bb + lb[j] + kk * 32 * 128);
-        gs16x4 hi = gw_tr(bb + lb[j] + kk * 32 * 128 + 16 * 128);
+        gs16x4 lo = gw_tr_asm(bb + lb[j] + kk * 32 * 128);
+        gs16x4 hi = gw_tr_asm(bb + lb[j] + kk * 32 * 128 + 16 * 128);
         gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         bfr[j] = __builtin_bit_cast(bf16x8, v);
       }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        gs16x4 lo = gw_tr_asm(a + la[i] + kk * 32 * 128);
+        gs16x4 hi = gw_tr_asm(a + la[i] + kk * 32 * 128 + 16 * 128);
+        gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+      gw_tr_wait<TM, TN>(af, bfr);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (bias_wave) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const auto u = __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, af[i]);
+#pragma unroll
+          for (int w = 0; w < 4; ++w) bsum[i] = gw_dot2(u[w], ones, bsum[i]);
+        }
+      }
     }
   };
-  // one barrier per stage: wait for this stage's DMA, barrier (every wave's
-  // DMA landed AND every wave done reading the other slot), issue the next
-  // stage into the other slot, compute
-  if (nsteps > 0) issue(p_begin, 0);
+  // one barrier per stage: wait for this stage's DMA (NS - 2 newer stages may
+  // stay in flight), barrier (every wave's DMA landed AND every wave done
+  // reading the slot refilled next), issue stage s + NS - 1 into that slot,
+  // compute.  Past the last stage the issues are zero-record dummies, so the
+  // wait counts stay uniform.
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) issue(p_begin + t * PK, t, t < nsteps);
   for (long s = 0; s < nsteps; ++s) {
-    const int st = (int)(s & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int st = (int)(s % NS);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PER) : "memory");
     __builtin_amdgcn_s_barrier();
-    if (s + 1 < nsteps) issue(p_begin + (s + 1) * PK, st ^ 1);
+    const long nx = s + NS - 1;
+    issue(p_begin + (nx < nsteps ? nx : s) * PK, (int)(nx % NS), nx < nsteps);
     __builtin_amdgcn_s_setprio(1);
     compute(smem + st * STAGE);
     __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail dummies drained before exit
 
   const int fr = lane & 15, fq = lane >> 4;
   const long KW = (long)taps * ICt;
+  if (bias_wave) {                                // the four 8-pixel lane groups -> lanes 0..15
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      bsum[i] += __shfl_xor(bsum[i], 16);
+      bsum[i] += __shfl_xor(bsum[i], 32);
+    }
+  }
   if (splits == 1) {
     // unsplit: the OIHW gradient straight from the accumulators (this block
     // is the only writer of its (co, ci, tap) elements)
     const float sc = J.scale;
     float* dw = J.dw;
     const int acc_in = J.acc;
-    if (do_bias) {                                  // block-uniform: the barrier is safe
-      if (bhalf) bred[bcol] = bacc;
-      __syncthreads();
-      if (!bhalf && m0 + bcol < OC) {
-        const float v = (bacc + bred[bcol]) * sc;
-        float* d = J.db + m0 + bcol;
-        *d = acc_in ? *d + v : v;
+    if (bias_wave && fq == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int co = m0 + wm * WM + i * 16 + fr;
+        if (co < OC) {
+          float* d = J.db + co;
+          const float v = bsum[i] * sc;
+          *d = acc_in ? *d + v : v;
+        }
       }
     }
 #pragma unroll
@@ -303,7 +358,16 @@ __global__ void __launch_bounds__(256, 2) wgrad_grp_k(GwTable tab) {
     }
     return;
   }
-  if (do_bias && m0 + bcol < OC) J.bslab[((long)split * 2 + bhalf) * OC + m0 + bcol] = bacc;
+  if (bias_wave && fq == 0) {                      // bias partial rows (2 split, 2 split + 1) = (sum, 0)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int co = m0 + wm * WM + i * 16 + fr;
+      if (co < OC) {
+        J.bslab[((long)split * 2) * OC + co] = bsum[i];
+        J.bslab[((long)split * 2 + 1) * OC + co] = 0.f;
+      }
+    }
+  }
   float* slab = J.slab + (long)split * OC * KW;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -604,6 +668,7 @@ static_assert(sizeof(WgJobDesc) == 80, "WgJobDesc must match hip_impl._WgJob");
 static int g_gw_blocks = 512;      // target blocks per grouped launch (2 per CU)
 static int g_gw_pk = 32;           // pixel rows per LDS stage (32 or 64)
 static int g_gw_minpix = 512;      // lower bound of the pixels per block
+static int g_gw_ns = 4;            // LDS ring stages of wgrad_grp_k (2, 3 or 4)
 static int g_gw_wide = 0;          // 1: 128 x 256 chunk-pair tiles (wgrad_grp2_k; measured slower: profiles/r4/kb_w1_*), 0: 128 x 128
 
 D3D_API int d3d_wgrad_group_cfg(int blocks, int pk, int minpix) {
@@ -614,6 +679,10 @@ D3D_API int d3d_wgrad_group_cfg(int blocks, int pk, int minpix) {
 }
 D3D_API int d3d_wgrad_group_wide(int wide) {
   g_gw_wide = wide ? 1 : 0;
+  return 0;
+}
+D3D_API int d3d_wgrad_group_stages(int ns) {
+  if (ns >= 2 && ns <= 4) g_gw_ns = ns;
   return 0;
 }
 
@@ -757,9 +826,13 @@ D3D_API long d3d_wgrad_group(const WgJobDesc* d, int n, float* ws, long ws_float
     else
       hipLaunchKernelGGL(wgrad_grp2_k<32>, dim3((unsigned)blk), dim3(256), 0, st, tab);
   } else if (g_gw_pk == 64) {
-    hipLaunchKernelGGL(wgrad_grp_k<64>, dim3((unsigned)blk), dim3(256), 0, st, tab);
+    hipLaunchKernelGGL((wgrad_grp_k<64, 2>), dim3((unsigned)blk), dim3(256), 0, st, tab);
+  } else if (g_gw_ns == 4) {
+    hipLaunchKernelGGL((wgrad_grp_k<32, 4>), dim3((unsigned)blk), dim3(256), 0, st, tab);
+  } else if (g_gw_ns == 3) {
+    hipLaunchKernelGGL((wgrad_grp_k<32, 3>), dim3((unsigned)blk), dim3(256), 0, st, tab);
   } else {
-    hipLaunchKernelGGL(wgrad_grp_k<32>, dim3((unsigned)blk), dim3(256), 0, st, tab);
+    hipLaunchKernelGGL((wgrad_grp_k<32, 2>), dim3((unsigned)blk), dim3(256), 0, st, tab);
   }
   if (rt.n > 0) hipLaunchKernelGGL(wgrad_grp_reduce_k, dim3((unsigned)rblk), dim3(256), 0, st, rt);
   const int e = (int)hipGetLastError();

@@ -699,6 +699,8 @@ if os.environ.get("D3D_WGRAD_GROUP_BLOCKS"):           # planner target (A/B kno
     _lib.d3d_wgrad_group_cfg(int(os.environ["D3D_WGRAD_GROUP_BLOCKS"]), 0, 0)
 if os.environ.get("D3D_WGRAD_GROUP_WIDE"):             # A/B knob: 128 x 256 (1) or 128 x 128 (0) tiles
     _lib.d3d_wgrad_group_wide(int(os.environ["D3D_WGRAD_GROUP_WIDE"]))
+if os.environ.get("D3D_WGRAD_GROUP_NS"):               # A/B knob: LDS ring stages (2-4)
+    _lib.d3d_wgrad_group_stages(int(os.environ["D3D_WGRAD_GROUP_NS"]))
 
 
 def wgrad_job(dy, x, OC, IC, N, H, W, taps, dw, db=None, scale=1.0, accumulate=True, x2=None, C1=0):
