@@ -668,7 +668,10 @@ static_assert(sizeof(WgJobDesc) == 80, "WgJobDesc must match hip_impl._WgJob");
 static int g_gw_blocks = 512;      // target blocks per grouped launch (2 per CU)
 static int g_gw_pk = 32;           // pixel rows per LDS stage (32 or 64)
 static int g_gw_minpix = 512;      // lower bound of the pixels per block
-static int g_gw_ns = 4;            // LDS ring stages of wgrad_grp_k (2, 3 or 4)
+// LDS ring stages of wgrad_grp_k (2, 3 or 4): 2 (32 KB, up to four blocks per
+// CU) beat the deeper rings (64 KB, two blocks) once the fragment reads stopped
+// waiting on the ring's DMAs (profiles/r4/kb_ns*.jsonl, b16_ns_blocks_ab.txt)
+static int g_gw_ns = 2;
 static int g_gw_wide = 0;          // 1: 128 x 256 chunk-pair tiles (wgrad_grp2_k; measured slower: profiles/r4/kb_w1_*), 0: 128 x 128
 
 D3D_API int d3d_wgrad_group_cfg(int blocks, int pk, int minpix) {

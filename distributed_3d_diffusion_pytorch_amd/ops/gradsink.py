@@ -64,7 +64,9 @@ class GradSink:
         self.defer_batch = 8         # jobs per fork (4 measured 1.5 % slower at bs16)
         # eager steps: queue the grouped-kernel jobs too and flush them 8 at a
         # time (one grouped launch each) instead of one launch pair per job
+        # (2: eager jobs run immediately, each as a one-job grouped launch)
         self.eager_group = os.environ.get("D3D_WGRAD_EAGER_GROUP", "0") == "1"
+        self.eager_single = os.environ.get("D3D_WGRAD_EAGER_GROUP", "0") == "2"
         self._queue = []
         self._compute = []
         self._streams: Dict[int, "torch.cuda.Stream"] = {}
@@ -208,7 +210,10 @@ class GradSink:
                 self.flush()
             return
         with self.producer(dev, *keep):
-            fn()
+            if self.eager_single and spec is not None and self.group_fn is not None:
+                self.group_fn([spec])
+            else:
+                fn()
         for p in done:
             if p is not None:
                 self.done(p)
