@@ -64,9 +64,14 @@ class GradSink:
         self.defer_batch = 8         # jobs per fork (4 measured 1.5 % slower at bs16)
         # eager steps: queue the grouped-kernel jobs too and flush them 8 at a
         # time (one grouped launch each) instead of one launch pair per job
-        # (2: eager jobs run immediately, each as a one-job grouped launch)
-        self.eager_group = os.environ.get("D3D_WGRAD_EAGER_GROUP", "0") == "1"
-        self.eager_single = os.environ.get("D3D_WGRAD_EAGER_GROUP", "0") == "2"
+        # (default "2": eager jobs run immediately, each as a one-job grouped
+        # launch -- the 128x128 grouped tile with its planner beat the per-job
+        # split-K kernels at bs128, 965 -> 973 examples/s; "1" (deferred
+        # batches of 8 in eager steps) measured 940, "0" keeps the per-job
+        # kernels: profiles/r4/b128_eager_ab.txt)
+        mode = os.environ.get("D3D_WGRAD_EAGER_GROUP", "2")
+        self.eager_group = mode == "1"
+        self.eager_single = mode == "2"
         self._queue = []
         self._compute = []
         self._streams: Dict[int, "torch.cuda.Stream"] = {}
