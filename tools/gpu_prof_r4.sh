@@ -3,7 +3,7 @@
 # streams on); rpstats summaries (stats, grid, exposed/solo, gaps) on the box.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
-O=/root/repo/gpurun_out/prof4
+O=/root/repo/gpurun_out/prof5
 mkdir -p $O
 timeout -k 10 600 rocprofv3 --kernel-trace -d $O/db128 -o run -- python3 /root/repo/bench.py --steps 8 --warmup 3 > $O/b128.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace -d $O/db16 -o run -- python3 /root/repo/bench.py --steps 20 --warmup 3 --global_batch 16 > $O/b16.log 2>&1 || exit $?
