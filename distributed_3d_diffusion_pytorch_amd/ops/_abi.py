@@ -53,7 +53,8 @@ SIGNATURES = {
     "d3d_pack_conv_weight": [P, P, I, I, I, I, I, P],
     "d3d_conv": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P],
     "d3d_conv2": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P],
-    "d3d_conv3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P, IP, P],
+    "d3d_conv3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P, IP, P, IP, P],
+    "d3d_gn_bwd_apply_parts": [I, P, P, P, P, P, I, I, I, I, P, P, P, P, P, I, I, P, P, I, P, F, P],
     "d3d_conv_plan": [I, I, I, I, I, I],
     "d3d_set_conv_korder": [I],
     "d3d_set_wgrad_impl": [I],

@@ -185,3 +185,92 @@ __device__ __forceinline__ void gn_part_store(float (&s)[TM][NH], float (&q)[TM]
     }
   }
 }
+
+// --------------------------------- GroupNorm-backward partials in a dgrad ----
+// The input gradient of a conv whose input is a GroupNorm(+SiLU) output
+// (ResnetBlock conv1 after GN0, `xunet.py:139-140`; the head conv after the
+// last GN) IS the GroupNorm's output gradient dy.  The conv's epilogue holds dy
+// in registers, so it also forms the backward's reductions -- per (image,
+// group): sum dA*gamma and sum dA*gamma*xhat; per channel: sum dA*xhat
+// (dgamma) and sum dA (dbeta), dA = dy * [dsilu(gamma*xhat + beta)] -- from
+// the GroupNorm input x and its statistics, instead of a separate pass that
+// re-reads x and dy (gn_bwd_reduce_k).  Granularity: 64 pixels of one image
+// (a "part"); every slot is written by exactly one wave, fixed shuffle
+// order: deterministic, no atomics.
+//   grp  [N][G][nparts][2]          (gn_part_store layout)
+//   chan [2C][R], R = N * nparts    (row 2c: dgamma partials, 2c+1: dbeta)
+struct GnbArgs {
+  const bf16* x;          // GroupNorm input [N, HW, C1] (or all C channels when x2 is null)
+  const bf16* x2;         // channels [C1, C) of a virtual concat, [N, HW, C - C1]
+  const float* stats;     // [N][G] (mean, rstd)
+  const float* gamma;
+  const float* beta;
+  float* chan;
+  float* grp;
+  int C1, G, mode, R;     // mode 1: GroupNorm + SiLU, 0: GroupNorm
+};
+
+// acc: the wave's fp32 tile (TM row tiles of 16 channels x TN fragments of 16
+// pixels), dy = bf16(acc * scale) as stored; co_base / pix_base: the wave's
+// first channel / pixel (TN % 4 == 0: whole 64-pixel parts).
+template <int TM, int TN>
+__device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale, const GnbArgs& a, int lane,
+                                         int co_base, long pix_base, int C, int HW, long Mpix) {
+  const int fr = lane & 15, fq = lane >> 4;
+  const int Cg = C / a.G, nparts = HW / 64;
+#pragma unroll
+  for (int h = 0; h < TN / 4; ++h) {
+    const long p0 = pix_base + h * 64;
+    if (p0 >= Mpix) continue;                      // (wave-uniform)
+    const int n = (int)(p0 / HW);
+    const int t = (int)(p0 - (long)n * HW) / 64;
+    bf16x4 xr[TM][4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const long pix = p0 + jj * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int co = co_base + i * 16 + fq * 4;
+        const bf16* src = (a.x2 == nullptr || co < a.C1) ? a.x + pix * (a.x2 ? a.C1 : C) + co
+                                                          : a.x2 + pix * (C - a.C1) + (co - a.C1);
+        xr[i][jj] = co < C ? *reinterpret_cast<const bf16x4*>(src) : bf16x4{};
+      }
+    }
+    float ga[TM][1], gb[TM][1];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      ga[i][0] = gb[i][0] = 0.f;
+      const int cq = co_base + i * 16 + fq * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = cq + e < C ? cq + e : C - 1;
+        const int g = c / Cg;
+        const float mean = a.stats[(n * a.G + g) * 2], rstd = a.stats[(n * a.G + g) * 2 + 1];
+        const float gm = a.gamma[c], bt = a.beta[c];
+        float cdg = 0.f, cdb = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float dy = (float)(bf16)(acc[i][h * 4 + jj][e] * scale);
+          const float xhat = ((float)xr[i][jj][e] - mean) * rstd;
+          const float dA = a.mode ? dy * dsiluf_(xhat * gm + bt) : dy;
+          cdg += dA * xhat;
+          cdb += dA;
+        }
+        if (cq + e >= C) cdg = cdb = 0.f;
+        ga[i][0] += cdb * gm;                        // sum dA*gamma over the lane's pixels
+        gb[i][0] += cdg * gm;                        // sum dA*gamma*xhat
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {           // the 16 pixels of a fragment column
+          cdg += __shfl_xor(cdg, m, 64);
+          cdb += __shfl_xor(cdb, m, 64);
+        }
+        if (fr == 0 && cq + e < C) {
+          const long row = (long)n * nparts + t;
+          a.chan[(2L * (cq + e)) * a.R + row] = cdg;
+          a.chan[(2L * (cq + e) + 1) * a.R + row] = cdb;
+        }
+      }
+    }
+    gn_part_store<TM, 1>(ga, gb, lane, co_base, p0, C, a.G, HW, Mpix, a.grp);
+  }
+}

@@ -987,7 +987,7 @@ __global__ void __launch_bounds__(512, 1)
 conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
             int w_bytes, int Nimg, int OH, int IC, int ICp, int OC, float scale, int res_nmod,
-            float* __restrict__ gnp, int gn_groups, bf16* __restrict__ O2) {
+            float* __restrict__ gnp, int gn_groups, bf16* __restrict__ O2, GnbArgs gb) {
   typedef HaloGeom<OWT, BNT> Gm;
   constexpr int BM = 128, BN = BNT, WM = 64, WN = BN / 4, TM = 4, TN = WN / 16;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * Gm::HBUF + 4 * Gm::ABUF];
@@ -1238,6 +1238,9 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     }
   }
   if (gnp) gn_part_store<TM, NH>(gs, gq, lane, m0 + wm * WM, n0 + wn * WN, OC, gn_groups, OHW, Mpix, gnp);
+  // the output is a GroupNorm's output gradient (input gradient of the conv
+  // after GN0 / the last GN): its backward partials (common.h gnb_tile)
+  if (gb.chan) gnb_tile<TM, TN>(acc, scale, gb, lane, m0 + wm * WM, n0 + wn * WN, OC, OHW, Mpix);
 }
 
 // split-K epilogue: O[pix][co] = (sum_s part[s][pix][co] + bias + row_bias
@@ -2725,14 +2728,25 @@ D3D_API int d3d_conv_plan(int N, int OH, int OW, int OC, int ICp, int taps) {
 // O2 != nullptr: also write silu(output) to O2 (same layout) when the chosen
 // kernel can; *silu_done reports whether it did (the caller runs the SiLU
 // pass otherwise).
+// gnb != nullptr: the output is a GroupNorm's output gradient -- also produce
+// the GroupNorm backward's partials (common.h GnbArgs / gnb_tile) when the
+// chosen kernel can (*gnb_done = 1; the caller runs the reduce pass otherwise).
 D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
                       void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
                       int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, float* gnp,
-                      int gn_groups, int* gn_done, void* O2, int* silu_done, hipStream_t st) {
+                      int gn_groups, int* gn_done, void* O2, int* silu_done, const GnbArgs* gnb, int* gnb_done,
+                      hipStream_t st) {
   long Mpix = (long)N * OH * OW;
   if (gn_done) *gn_done = 0;
   if (silu_done) *silu_done = 0;
+  if (gnb_done) *gnb_done = 0;
   if (!silu_done) O2 = nullptr;
+  GnbArgs gb{};
+  if (gnb && gnb_done && gnb->chan && gnb->grp && !bias && !row_bias && !res && ldo == OC && gnb->G > 0 &&
+      OC % gnb->G == 0 && (OH * OW) % 64 == 0 && (gnb->mode == 0 || gnb->mode == 1)) {
+    const int cg = OC / gnb->G;
+    if (cg == 4 || cg == 8 || cg == 16 || cg == 32) gb = *gnb;
+  }
   // Operands beyond the kernels' 32-bit buffer offsets (2 GiB: e.g. the
   // 256-channel decoder concat of 128x128 images at one micro-batch of 128):
   // run the conv over image chunks that fit, each at full speed, instead of
@@ -2760,7 +2774,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
                                    res_nmod, taps, ws, nsplit,
                                    gnp ? gnp + (long)n0 * gn_groups * parts_per_img * 2 : nullptr, gn_groups,
                                    gn_done ? &d : nullptr, O2 ? (char*)O2 + n0 * img_out : nullptr,
-                                   O2 ? &ds : nullptr, st);
+                                   O2 ? &ds : nullptr, nullptr, nullptr, st);
           if (rc) return rc;
           all_gn &= d;
           all_silu &= ds;
@@ -2797,7 +2811,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
   hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512, false, RS>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, \
                      bias,                                                                                         \
                      row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale,   \
-                     res_nmod, gnp, gn_groups, (bf16*)O2)
+                     res_nmod, gnp, gn_groups, (bf16*)O2, gb)
       if (OW == 64) {
         if (trans) { if (res || g_conv_res_always) HALO(64, true, true); else HALO(64, true, false); }
         else if (res || g_conv_res_always) HALO(64, false, true); else HALO(64, false, false);
@@ -2808,6 +2822,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
 #undef HALO
       if (gn_done && gnp) *gn_done = 1;
       if (silu_done && O2) *silu_done = 1;
+      if (gnb_done && gb.chan) *gnb_done = 1;
       return (int)hipGetLastError();
     }
   }
@@ -2941,7 +2956,7 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
                       int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, float* gnp,
                       int gn_groups, int* gn_done, hipStream_t st) {
   return d3d_conv3(I, Wp, bias, row_bias, res, O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans, scale,
-                   res_nmod, taps, ws, nsplit, gnp, gn_groups, gn_done, nullptr, nullptr, st);
+                   res_nmod, taps, ws, nsplit, gnp, gn_groups, gn_done, nullptr, nullptr, nullptr, nullptr, st);
 }
 
 D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,

@@ -387,6 +387,39 @@ __device__ __forceinline__ void sum_group_parts(const float* __restrict__ grp_pa
   __syncthreads();
 }
 
+// Group sums of image n from the dgrad-epilogue partials (common.h gnb_tile:
+// [N][G][nparts][2]): NT / G threads per group each sum a strided share of the
+// group's contiguous parts, merged in a fixed order through LDS.
+__device__ __forceinline__ void sum_group_parts_epi(const float* __restrict__ grp, int n, int G, int nparts,
+                                                    float* s_out) {
+  __shared__ float s_sub[2 * NT];
+  const int tpg = G <= NT ? NT / G : 1;
+  for (int g0 = 0; g0 < G; g0 += NT / tpg) {
+    const int g = g0 + threadIdx.x / tpg, sub = threadIdx.x % tpg;
+    float a = 0.f, b = 0.f;
+    if (g < G) {
+      const float* pp = grp + ((long)n * G + g) * nparts * 2;
+      for (int t = sub; t < nparts; t += tpg) {
+        a += pp[2 * t];
+        b += pp[2 * t + 1];
+      }
+    }
+    s_sub[threadIdx.x * 2] = a;
+    s_sub[threadIdx.x * 2 + 1] = b;
+    __syncthreads();
+    if (sub == 0 && g < G) {
+      float x = 0.f, y = 0.f;
+      for (int k = 0; k < tpg; ++k) {
+        x += s_sub[(threadIdx.x + k) * 2];
+        y += s_sub[(threadIdx.x + k) * 2 + 1];
+      }
+      s_out[g * 2] = x;
+      s_out[g * 2 + 1] = y;
+    }
+    __syncthreads();
+  }
+}
+
 // MODE 0: GN, 1: GN+SiLU, 2: GN+FiLM(+dropout)
 template <int MODE>
 __global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, const float* __restrict__ part,
@@ -699,11 +732,13 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
                                                       const float* __restrict__ chan_part,
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                       int accumulate, int trows, const bf16* __restrict__ dres,
-                                                      float dres_scale) {
+                                                      float dres_scale, long chan_R, int gparts) {
+  // chan_R: rows of chan_part; gparts > 0: grp_part holds the consumer conv's
+  // dgrad-epilogue partials ([N][G][gparts][2], common.h gnb_tile) instead of
+  // the reduce pass's [N][nchunks][G][2]
   if ((int)blockIdx.y < trows) {        // leading grid rows: dgamma / dbeta, 4 rows (waves) per block
     const int blk = blockIdx.y * nchunks + blockIdx.x;
-    dgb_rowsum(chan_part, (long)(gridDim.y - trows) * nchunks, 2 * C, blk * (NT / 64) + (threadIdx.x >> 6), dgamma,
-               dbeta, accumulate);
+    dgb_rowsum(chan_part, chan_R, 2 * C, blk * (NT / 64) + (threadIdx.x >> 6), dgamma, dbeta, accumulate);
     return;
   }
   constexpr int U = 2;      // rows in flight per thread
@@ -712,7 +747,10 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
   const int Cg = C / G;
   const float inv = 1.f / (float)((long)P * Cg);
   __shared__ float s_ab[2 * 1024];
-  sum_group_parts(grp_part, n, nchunks, G, s_ab);
+  if (gparts > 0)
+    sum_group_parts_epi(grp_part, n, G, gparts, s_ab);
+  else
+    sum_group_parts(grp_part, n, nchunks, G, s_ab);
   for (int g = threadIdx.x; g < G; g += NT) {
     s_c[g * 4 + 0] = stats[(n * G + g) * 2];
     s_c[g * 4 + 1] = stats[(n * G + g) * 2 + 1];
@@ -893,10 +931,36 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
   hipLaunchKernelGGL(gn_bwd_apply2_k<M>, dim3(p.nchunks, N + trows), dim3(NT), 0, st, (const bf16*)x,             \
                      (const bf16*)dy, (const bf16*)ss, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows,    \
                      p.nchunks, p_drop, (uint64_t)seed, ssld, (const uint64_t*)seed_dev, cat, chan_part, dgamma,    \
-                     dbeta, accumulate, trows, (const bf16*)dres, dres_scale)
+                     dbeta, accumulate, trows, (const bf16*)dres, dres_scale, (long)N * p.nchunks, 0)
   if (mode == 0) APP(0);
   else if (mode == 1) APP(1);
   else APP(2);
+#undef APP
+  return (int)hipGetLastError();
+}
+
+// Backward apply over partials the consumer conv's dgrad epilogue produced
+// (conv.hip, GnbArgs): chan_part [2C][N * nparts], grp_part [N][G][nparts][2];
+// no reduce pass.  mode 0 / 1 (GroupNorm [+ SiLU]).
+D3D_API int d3d_gn_bwd_apply_parts(int mode, const void* x, const void* dy, const float* stats, const float* gamma,
+                                   const float* beta, int N, int P, int C, int G, void* dx, float* dgamma,
+                                   float* dbeta, const float* chan_part, const float* grp_part, int nparts,
+                                   int accumulate, const void* x2, void* dx2, int C1, const void* dres,
+                                   float dres_scale, hipStream_t st) {
+  if (mode != 0 && mode != 1) return (int)hipErrorInvalidValue;
+  if (G > 1024 || nparts < 1) return (int)hipErrorInvalidValue;
+  Plan p = make_plan(N, P, C);
+  Cat cat{(const bf16*)x2, (bf16*)dx2, C1};
+  if (x2) dres = nullptr;
+  const int tblocks = (2 * C + NT / 64 - 1) / (NT / 64);
+  const int trows = (tblocks + p.nchunks - 1) / p.nchunks;
+#define APP(M)                                                                                                    \
+  hipLaunchKernelGGL(gn_bwd_apply2_k<M>, dim3(p.nchunks, N + trows), dim3(NT), 0, st, (const bf16*)x,             \
+                     (const bf16*)dy, (const bf16*)nullptr, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G,      \
+                     p.rows, p.nchunks, 0.f, (uint64_t)0, 2 * C, (const uint64_t*)nullptr, cat, chan_part, dgamma,  \
+                     dbeta, accumulate, trows, (const bf16*)dres, dres_scale, (long)N * nparts, nparts)
+  if (mode == 0) APP(0);
+  else APP(1);
 #undef APP
   return (int)hipGetLastError();
 }

@@ -443,6 +443,32 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None,
     return dx, dss, dg, db
 
 
+def _gn_bwd_parts(mode, x, dy, stats, w, b, G, parts, x2=None, dres=None, dres_scale=1.0):
+    """GroupNorm backward apply over the consumer conv's epilogue partials
+    (no reduce pass)."""
+    chan, grp, nparts, _ = parts
+    N, H, W, C1 = x.shape
+    C = C1 + (x2.shape[-1] if x2 is not None else 0)
+    dev = x.device
+    dx = torch.empty_like(x)
+    dx2 = torch.empty_like(x2) if x2 is not None else None
+    tg, tb = SINK.target(w), SINK.target(b)
+    direct = tg is not None and tb is not None
+    dg = tg if direct else torch.empty(C, dtype=F32, device=dev)
+    db = tb if direct else torch.empty(C, dtype=F32, device=dev)
+    _chk(_lib.d3d_gn_bwd_apply_parts(mode, x.data_ptr(), dy.data_ptr(), stats.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                     N, H * W, C, G, dx.data_ptr(), dg.data_ptr(), db.data_ptr(), chan.data_ptr(),
+                                     grp.data_ptr(), int(nparts), int(direct), _ptr(x2), _ptr(dx2), C1, _ptr(dres),
+                                     float(dres_scale), _st()), "gn_bwd_apply_parts")
+    if x2 is not None:
+        dx = (dx, dx2)
+    if direct:
+        SINK.done(w)
+        SINK.done(b)
+        return dx, None, None
+    return dx, dg, db
+
+
 class _GroupNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, groups, eps, silu, slot=None):
@@ -452,6 +478,10 @@ class _GroupNorm(torch.autograd.Function):
         ctx.save_for_backward(x, weight, bias, stats)
         ctx.cfg = (groups, 1 if silu else 0)
         ctx.slot = slot
+        ctx.gnb = None
+        if silu and any(ctx.needs_input_grad[:3]):
+            ctx.gnb = _GnbHolder(x, None, C, stats, weight, bias, groups, 1)
+            y._d3d_gnb = ctx.gnb
         SINK.use(weight, ctx.needs_input_grad[1])
         SINK.use(bias, ctx.needs_input_grad[2])
         return y
@@ -463,7 +493,12 @@ class _GroupNorm(torch.autograd.Function):
         dres, rsc = ctx.slot.take() if ctx.slot is not None else (None, 1.0)
         if dres is not None:
             dres = dres.reshape(x.shape).contiguous()
-        dx, _, dg, db = _gn_bwd(mode, x, dy.contiguous(), None, stats, w, b, G, 0.0, 0, dres=dres, dres_scale=rsc)
+        dy = dy.contiguous()
+        parts = ctx.gnb.take(dy) if ctx.gnb is not None else None
+        if parts is not None:
+            dx, dg, db = _gn_bwd_parts(mode, x, dy, stats, w, b, G, parts, dres=dres, dres_scale=rsc)
+        else:
+            dx, _, dg, db = _gn_bwd(mode, x, dy, None, stats, w, b, G, 0.0, 0, dres=dres, dres_scale=rsc)
         return dx, dg, db, None, None, None, None
 
 
@@ -500,6 +535,10 @@ class _CatGNDense(torch.autograd.Function):
         ctx.save_for_backward(a, b, gw, gb, stats, dw)
         ctx.cfg = (groups, db is not None)
         ctx.params = (dw, db)
+        ctx.gnb = None
+        if any(ctx.needs_input_grad[:4]):
+            ctx.gnb = _GnbHolder(a, b, C1, stats, gw, gb, groups, 1)
+            y._d3d_gnb = ctx.gnb
         SINK.use(gw, ctx.needs_input_grad[2])
         SINK.use(gb, ctx.needs_input_grad[3])
         SINK.use(dw, ctx.needs_input_grad[4])
@@ -512,7 +551,12 @@ class _CatGNDense(torch.autograd.Function):
         G, has_db = ctx.cfg
         N, H, W, C1 = a.shape
         C2 = b.shape[-1]
-        (da, db_in), _, dgw, dgb = _gn_bwd(1, a, dy.contiguous(), None, stats, gw, gb, G, 0.0, 0, x2=b)
+        dy = dy.contiguous()
+        parts = ctx.gnb.take(dy) if ctx.gnb is not None else None
+        if parts is not None:
+            (da, db_in), dgw, dgb = _gn_bwd_parts(1, a, dy, stats, gw, gb, G, parts, x2=b)
+        else:
+            (da, db_in), _, dgw, dgb = _gn_bwd(1, a, dy, None, stats, gw, gb, G, 0.0, 0, x2=b)
         g = dskip.contiguous()
         OC = g.shape[-1]
         g2 = g.reshape(-1, OC)
@@ -635,8 +679,39 @@ def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=Fa
 
 
 # ----------------------------------------------------------------- conv ----
+class _GnbArgs(ctypes.Structure):
+    """common.h GnbArgs: GroupNorm-backward partials from a dgrad epilogue."""
+    _fields_ = [("x", ctypes.c_void_p), ("x2", ctypes.c_void_p), ("stats", ctypes.c_void_p),
+                ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("chan", ctypes.c_void_p),
+                ("grp", ctypes.c_void_p), ("C1", ctypes.c_int), ("G", ctypes.c_int), ("mode", ctypes.c_int),
+                ("R", ctypes.c_int)]
+
+
+assert ctypes.sizeof(_GnbArgs) == 72
+_GNB_EPI = os.environ.get("D3D_GNB_EPI", "1") != "0"
+
+
+class _GnbHolder:
+    """Links a GroupNorm(+SiLU) output to the conv that consumes it: the conv's
+    input-gradient launch may produce the GroupNorm backward's partial sums
+    in its epilogue (``parts``), which the GroupNorm backward then uses
+    instead of its reduce pass (`xunet.py:139-140` GN0 -> conv1)."""
+    __slots__ = ("x", "x2", "C1", "stats", "w", "b", "G", "mode", "parts")
+
+    def __init__(self, x, x2, C1, stats, w, b, G, mode):
+        self.x, self.x2, self.C1, self.stats, self.w, self.b, self.G, self.mode = x, x2, C1, stats, w, b, G, mode
+        self.parts = None
+
+    def take(self, dy):
+        """The partials, when they were made from exactly this gradient."""
+        p, self.parts = self.parts, None
+        if p is None or p[3] != dy.data_ptr():
+            return None
+        return p
+
+
 def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale, res_nmod=0,
-              taps=9, gn_groups=0, silu_out=None):
+              taps=9, gn_groups=0, silu_out=None, gnb=None):
     """Launch the conv; with gn_groups > 0 the epilogue may also emit the
     GroupNorm partial statistics of ``out``: returns (part, nparts) when it
     did (the consuming GroupNorm then skips its statistics pass), else None.
@@ -650,12 +725,24 @@ def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo
         gnp = torch.empty(N * gn_groups * (OH * OW // 64) * 2, dtype=F32, device=x.device)
     done = ctypes.c_int(0)
     sdone = ctypes.c_int(0)
+    bdone = ctypes.c_int(0)
+    ga = None
+    if gnb is not None and _GNB_EPI and (OH * OW) % 64 == 0 and ldo == OC:
+        nparts = OH * OW // 64
+        R = N * nparts
+        chan = torch.empty(2 * OC * R, dtype=F32, device=x.device)
+        grp = torch.empty(N * gnb.G * nparts * 2, dtype=F32, device=x.device)
+        ga = _GnbArgs(gnb.x.data_ptr(), _ptr(gnb.x2), gnb.stats.data_ptr(), gnb.w.data_ptr(), gnb.b.data_ptr(),
+                      chan.data_ptr(), grp.data_ptr(), int(gnb.C1), int(gnb.G), int(gnb.mode), int(R))
     _chk(_lib.d3d_conv3(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
                         IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), taps, _ptr(ws), ns,
-                        _ptr(gnp), int(gn_groups), ctypes.byref(done), _ptr(silu_out), ctypes.byref(sdone), _st()),
+                        _ptr(gnp), int(gn_groups), ctypes.byref(done), _ptr(silu_out), ctypes.byref(sdone),
+                        ctypes.byref(ga) if ga is not None else None, ctypes.byref(bdone), _st()),
          "conv")
     if silu_out is not None and not sdone.value:
         _chk(_lib.d3d_silu(out.data_ptr(), silu_out.data_ptr(), out.numel(), _st()), "silu")
+    if ga is not None and bdone.value:
+        gnb.parts = (chan, grp, nparts, out.data_ptr())
     return (gnp, OH * OW // 64) if done.value else None
 
 
@@ -769,6 +856,7 @@ class _Conv(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias, res_period, taps, gn=None, res_slot=None):
+        gnb = getattr(x, "_d3d_gnb", None)          # x is a GroupNorm(+SiLU) output (see _GnbHolder)
         x = x.contiguous()
         N, H, W, IC = x.shape
         OC = weight.shape[0]
@@ -790,6 +878,7 @@ class _Conv(torch.autograd.Function):
         ctx.cfg = (stride, out_scale, residual is not None, row_bias is not None, bias is not None, res_period, taps)
         ctx.bias_param = bias
         ctx.res_slot = res_slot
+        ctx.gnb = gnb if stride == 1 else None
         SINK.use(weight, ctx.needs_input_grad[1])
         SINK.use(bias, ctx.needs_input_grad[2])
         return out
@@ -822,7 +911,7 @@ class _Conv(torch.autograd.Function):
             wt = packed_weight(weight, True, taps)
             dx = torch.empty_like(x)
             _conv_fwd(g, wt, None, None, None, dx, N, OH, OW, OC, _up(OC, 64), H, W, IC, IC, stride, True, ks, 0,
-                      taps)
+                      taps, gnb=ctx.gnb)
         dW = db = drb = None
         tw = SINK.target(weight) if need_w else None
         tb = SINK.target(bias) if need_b else None

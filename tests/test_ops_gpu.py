@@ -717,6 +717,53 @@ def test_graph_train_step_matches_eager(micro):
     hip_impl.set_device_seed(None)
 
 
+@pytest.mark.parametrize("N,Hh,C1,C2,OC", [(32, 64, 128, 0, 128), (12, 64, 256, 128, 128), (8, 128, 128, 0, 128)])
+def test_gn_silu_conv_backward_partials_from_dgrad(H, N, Hh, C1, C2, OC):
+    """GN0 + SiLU -> conv1 (`xunet.py:139-140`; C2 > 0: the decoder's virtual
+    concat): the conv's input-gradient epilogue forms the GroupNorm backward's
+    partial sums (halo dgrad), the GroupNorm backward skips its reduce pass --
+    against the fp32 composition, and against the unfused HIP path."""
+    torch.manual_seed(9)
+    C = C1 + C2
+    xa = (torch.randn(N, Hh, Hh, C1, device=DEV) * 1.5 + 0.3).to(BF)
+    xb = (torch.randn(N, Hh, Hh, C2, device=DEV) - 0.2).to(BF) if C2 else None
+    gw = torch.randn(C, device=DEV) * 0.3 + 1
+    gb = torch.randn(C, device=DEV) * 0.2
+    w = torch.randn(OC, C, 3, 3, device=DEV) / math.sqrt(9 * C)
+    dw_ = torch.randn(OC, C, device=DEV) / math.sqrt(C)
+    go = torch.randn(N, Hh, Hh, OC, device=DEV)
+
+    def hip(xa, xb, gw, gb, w):
+        if xb is None:
+            h = H.group_norm(xa, gw, gb, 32, 1e-5, True)
+        else:
+            h, _ = H.cat_gn_silu_dense(xa, xb, gw, gb, dw_, None)
+        return H.conv3x3(h, w, None)
+
+    def ref(xa, xb, gw, gb, w):
+        x = xa if xb is None else torch.cat([xa, xb], -1)
+        return T.conv3x3(T.group_norm(x, gw, gb, 32, 1e-5, True), w, None)
+
+    ins = [xa, xb, gw, gb, w] if C2 else [xa, gw, gb, w]
+    fh = hip if C2 else (lambda xa, gw, gb, w: hip(xa, None, gw, gb, w))
+    fr = ref if C2 else (lambda xa, gw, gb, w: ref(xa, None, gw, gb, w))
+    calls = []
+    orig = H._gn_bwd_parts
+    H._gn_bwd_parts = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+    try:
+        yh, yr, gh, gr = run_both(fh, fr, ins, go)
+        H._GNB_EPI = False
+        _, _, gu, _ = run_both(fh, fr, ins, go)
+    finally:
+        H._GNB_EPI = True
+        H._gn_bwd_parts = orig
+    assert calls, "the fused GroupNorm-backward path did not run"
+    assert rel(yh, yr) < 2e-2
+    for a, b, c in zip(gh, gr, gu):
+        assert rel(a, b) < 3e-2, rel(a, b)
+        assert rel(a, c) < 2e-2, rel(a, c)
+
+
 @pytest.mark.parametrize("s", [1, 2, 4, 8])
 def test_cond_conv_split_matches_full_conv(H, s):
     """Origin/direction split conditioning conv == 144-channel conv on the
