@@ -196,8 +196,11 @@ __device__ __forceinline__ void gn_part_store(float (&s)[TM][NH], float (&q)[TM]
 // the GroupNorm input x and its statistics, instead of a separate pass that
 // re-reads x and dy (gn_bwd_reduce_k).  Granularity: 64 pixels of one image
 // (a "part"); every slot is written by exactly one wave, fixed shuffle
-// order: deterministic, no atomics.
-//   grp  [N][G][nparts][2]          (gn_part_store layout)
+// order: deterministic, no atomics.  The group sums are kept per 4-channel
+// quad (the lane's channels), so any group width that is a multiple of 4 works
+// (the decoder's concat GroupNorms have 12 and 24 channels per group); the
+// apply kernel folds quads into groups.
+//   grp  [N][C/4][nparts][2]
 //   chan [2C][R], R = N * nparts    (row 2c: dgamma partials, 2c+1: dbeta)
 struct GnbArgs {
   const bf16* x;          // GroupNorm input [N, HW, C1] (or all C channels when x2 is null)
@@ -271,6 +274,20 @@ __device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale
         }
       }
     }
-    gn_part_store<TM, 1>(ga, gb, lane, co_base, p0, C, a.G, HW, Mpix, a.grp);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float u = ga[i][0], v = gb[i][0];
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        u += __shfl_xor(u, m, 64);
+        v += __shfl_xor(v, m, 64);
+      }
+      const int q = (co_base + i * 16 + fq * 4) / 4;
+      if (fr == 0 && q * 4 < C) {
+        float* d = a.grp + (((long)n * (C / 4) + q) * nparts + t) * 2;
+        d[0] = u;
+        d[1] = v;
+      }
+    }
   }
 }

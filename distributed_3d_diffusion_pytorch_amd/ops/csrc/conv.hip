@@ -2743,10 +2743,8 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
   if (!silu_done) O2 = nullptr;
   GnbArgs gb{};
   if (gnb && gnb_done && gnb->chan && gnb->grp && !bias && !row_bias && !res && ldo == OC && gnb->G > 0 &&
-      OC % gnb->G == 0 && (OH * OW) % 64 == 0 && (gnb->mode == 0 || gnb->mode == 1)) {
-    const int cg = OC / gnb->G;
-    if (cg == 4 || cg == 8 || cg == 16 || cg == 32) gb = *gnb;
-  }
+      OC % gnb->G == 0 && (OC / gnb->G) % 4 == 0 && (OH * OW) % 64 == 0 && (gnb->mode == 0 || gnb->mode == 1))
+    gb = *gnb;
   // Operands beyond the kernels' 32-bit buffer offsets (2 GiB: e.g. the
   // 256-channel decoder concat of 128x128 images at one micro-batch of 128):
   // run the conv over image chunks that fit, each at full speed, instead of

@@ -388,18 +388,20 @@ __device__ __forceinline__ void sum_group_parts(const float* __restrict__ grp_pa
 }
 
 // Group sums of image n from the dgrad-epilogue partials (common.h gnb_tile:
-// [N][G][nparts][2]): NT / G threads per group each sum a strided share of the
-// group's contiguous parts, merged in a fixed order through LDS.
-__device__ __forceinline__ void sum_group_parts_epi(const float* __restrict__ grp, int n, int G, int nparts,
+// [N][C/4][nparts][2], quads of a group contiguous): NT / G threads per group
+// each sum a strided share of the group's Cg/4 x nparts pairs, merged in a
+// fixed order through LDS.
+__device__ __forceinline__ void sum_group_parts_epi(const float* __restrict__ grp, int n, int G, int C, int nparts,
                                                     float* s_out) {
   __shared__ float s_sub[2 * NT];
   const int tpg = G <= NT ? NT / G : 1;
+  const int cnt = (C / G / 4) * nparts;            // pairs per group
   for (int g0 = 0; g0 < G; g0 += NT / tpg) {
     const int g = g0 + threadIdx.x / tpg, sub = threadIdx.x % tpg;
     float a = 0.f, b = 0.f;
     if (g < G) {
-      const float* pp = grp + ((long)n * G + g) * nparts * 2;
-      for (int t = sub; t < nparts; t += tpg) {
+      const float* pp = grp + ((long)n * (C / 4) + (long)g * (C / G / 4)) * nparts * 2;
+      for (int t = sub; t < cnt; t += tpg) {
         a += pp[2 * t];
         b += pp[2 * t + 1];
       }
@@ -748,7 +750,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
   const float inv = 1.f / (float)((long)P * Cg);
   __shared__ float s_ab[2 * 1024];
   if (gparts > 0)
-    sum_group_parts_epi(grp_part, n, G, gparts, s_ab);
+    sum_group_parts_epi(grp_part, n, G, C, gparts, s_ab);
   else
     sum_group_parts(grp_part, n, nchunks, G, s_ab);
   for (int g = threadIdx.x; g < G; g += NT) {
@@ -940,7 +942,7 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
 }
 
 // Backward apply over partials the consumer conv's dgrad epilogue produced
-// (conv.hip, GnbArgs): chan_part [2C][N * nparts], grp_part [N][G][nparts][2];
+// (conv.hip, GnbArgs): chan_part [2C][N * nparts], grp_part [N][C/4][nparts][2];
 // no reduce pass.  mode 0 / 1 (GroupNorm [+ SiLU]).
 D3D_API int d3d_gn_bwd_apply_parts(int mode, const void* x, const void* dy, const float* stats, const float* gamma,
                                    const float* beta, int N, int P, int C, int G, void* dx, float* dgamma,
@@ -948,7 +950,7 @@ D3D_API int d3d_gn_bwd_apply_parts(int mode, const void* x, const void* dy, cons
                                    int accumulate, const void* x2, void* dx2, int C1, const void* dres,
                                    float dres_scale, hipStream_t st) {
   if (mode != 0 && mode != 1) return (int)hipErrorInvalidValue;
-  if (G > 1024 || nparts < 1) return (int)hipErrorInvalidValue;
+  if (G > 1024 || nparts < 1 || C % G || (C / G) % 4) return (int)hipErrorInvalidValue;
   Plan p = make_plan(N, P, C);
   Cat cat{(const bf16*)x2, (bf16*)dx2, C1};
   if (x2) dres = nullptr;

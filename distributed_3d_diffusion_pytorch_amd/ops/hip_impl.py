@@ -731,7 +731,7 @@ def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo
         nparts = OH * OW // 64
         R = N * nparts
         chan = torch.empty(2 * OC * R, dtype=F32, device=x.device)
-        grp = torch.empty(N * gnb.G * nparts * 2, dtype=F32, device=x.device)
+        grp = torch.empty(N * (OC // 4) * nparts * 2, dtype=F32, device=x.device)
         ga = _GnbArgs(gnb.x.data_ptr(), _ptr(gnb.x2), gnb.stats.data_ptr(), gnb.w.data_ptr(), gnb.b.data_ptr(),
                       chan.data_ptr(), grp.data_ptr(), int(gnb.C1), int(gnb.G), int(gnb.mode), int(R))
     _chk(_lib.d3d_conv3(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
