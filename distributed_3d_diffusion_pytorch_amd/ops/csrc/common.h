@@ -190,37 +190,31 @@ __device__ __forceinline__ void gn_part_store(float (&s)[TM][NH], float (&q)[TM]
 // The input gradient of a conv whose input is a GroupNorm(+SiLU) output
 // (ResnetBlock conv1 after GN0, `xunet.py:139-140`; the head conv after the
 // last GN) IS the GroupNorm's output gradient dy.  The conv's epilogue holds dy
-// in registers, so it also forms the backward's reductions -- per (image,
-// group): sum dA*gamma and sum dA*gamma*xhat; per channel: sum dA*xhat
-// (dgamma) and sum dA (dbeta), dA = dy * [dsilu(gamma*xhat + beta)] -- from
-// the GroupNorm input x and its statistics, instead of a separate pass that
-// re-reads x and dy (gn_bwd_reduce_k).  Granularity: 64 pixels of one image
-// (a "part"); every slot is written by exactly one wave, fixed shuffle
-// order: deterministic, no atomics.  The group sums are kept per 4-channel
-// quad (the lane's channels), so any group width that is a multiple of 4 works
-// (the decoder's concat GroupNorms have 12 and 24 channels per group); the
-// apply kernel folds quads into groups.
-//   grp  [N][C/4][nparts][2]
-//   chan [2C][R], R = N * nparts    (row 2c: dgamma partials, 2c+1: dbeta)
+// in registers, so it also forms the backward's per-(image, group)
+// reductions -- sum dA*gamma and sum dA*gamma*xhat, dA = dy *
+// [dsilu(gamma*xhat + beta)] -- from the GroupNorm input x and its statistics,
+// instead of a separate pass that re-reads x and dy (gn_bwd_reduce_k).  The
+// per-channel dgamma / dbeta sums come out of the apply pass, which forms dA
+// anyway.  Granularity: 64 pixels of one image x one 4-channel quad (the
+// lane's channels; any group width that is a multiple of 4 works -- the
+// decoder's concat GroupNorms have 12 / 24 channels per group); every slot is
+// written by exactly one lane after a fixed shuffle order: deterministic, no
+// atomics.   grp [N][C/4][nparts][2]
 struct GnbArgs {
   const bf16* x;          // GroupNorm input [N, HW, C1] (or all C channels when x2 is null)
   const bf16* x2;         // channels [C1, C) of a virtual concat, [N, HW, C - C1]
   const float* stats;     // [N][G] (mean, rstd)
   const float* gamma;
   const float* beta;
-  float* chan;
   float* grp;
-  int C1, G, mode, R;     // mode 1: GroupNorm + SiLU, 0: GroupNorm
+  int C1, G, mode, pad_;  // mode 1: GroupNorm + SiLU, 0: GroupNorm
 };
 
 // acc: the wave's fp32 tile (TM row tiles of 16 channels x TN fragments of 16
 // pixels), dy = bf16(acc * scale) as stored; co_base / pix_base: the wave's
-// first channel / pixel (TN % 4 == 0: whole 64-pixel parts).
-// Loads are issued before any store (restrict-qualified locals: the partial
-// stores cannot alias the inputs, so the compiler need not serialise every
-// parameter load behind the previous channel's stores -- which cost a memory
-// round trip per channel, +44 % on the level-0 dgrad at bs128), the per-lane
-// channels of a 4-channel quad share one group (4 | Cg), and the SiLU
+// first channel / pixel (TN % 4 == 0: whole 64-pixel parts).  Loads are issued
+// before any store, through restrict-qualified locals (otherwise every load
+// waits behind the previous stores: a memory round trip per channel); the SiLU
 // derivative uses the hardware reciprocal.
 template <int TM, int TN>
 __device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale, const GnbArgs& a, int lane,
@@ -230,7 +224,6 @@ __device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale
   const bf16* __restrict__ x1 = a.x;
   const bf16* __restrict__ x2 = a.x2;
   const float* __restrict__ stats = a.stats;
-  float* __restrict__ chan = a.chan;
   float* __restrict__ grp = a.grp;
   const int C1 = x2 ? a.C1 : C;
   float gm[TM][4], bt[TM][4];
@@ -263,7 +256,7 @@ __device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale
         xr[i][jj] = co < C ? *reinterpret_cast<const bf16x4*>(src) : bf16x4{};
       }
     }
-    float cdg[TM][4], cdb[TM][4], ga[TM], gb[TM];
+    float ga[TM], gb[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       ga[i] = gb[i] = 0.f;
@@ -285,34 +278,17 @@ __device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale
         }
         ga[i] += sb * gm[i][e];                      // sum dA*gamma over the lane's pixels
         gb[i] += sg * gm[i][e];                      // sum dA*gamma*xhat
-        cdg[i][e] = sg;
-        cdb[i][e] = sb;
       }
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int m = 1; m < 16; m <<= 1) {           // the 16 pixels of a fragment column
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          cdg[i][e] += __shfl_xor(cdg[i][e], m, 64);
-          cdb[i][e] += __shfl_xor(cdb[i][e], m, 64);
-        }
         ga[i] += __shfl_xor(ga[i], m, 64);
         gb[i] += __shfl_xor(gb[i], m, 64);
       }
-    }
-    if (fr == 0) {
-      const long row = (long)n * nparts + t;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int co = co_base + i * 16 + fq * 4;
-        if (co >= C) continue;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          chan[(2L * (co + e)) * a.R + row] = cdg[i][e];
-          chan[(2L * (co + e) + 1) * a.R + row] = cdb[i][e];
-        }
+      const int co = co_base + i * 16 + fq * 4;
+      if (fr == 0 && co < C) {
         float* d = grp + (((long)n * (C / 4) + co / 4) * nparts + t) * 2;
         d[0] = ga[i];
         d[1] = gb[i];

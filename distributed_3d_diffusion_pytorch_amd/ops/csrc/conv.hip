@@ -1240,7 +1240,7 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   if (gnp) gn_part_store<TM, NH>(gs, gq, lane, m0 + wm * WM, n0 + wn * WN, OC, gn_groups, OHW, Mpix, gnp);
   // the output is a GroupNorm's output gradient (input gradient of the conv
   // after GN0 / the last GN): its backward partials (common.h gnb_tile)
-  if (gb.chan) gnb_tile<TM, TN>(acc, scale, gb, lane, m0 + wm * WM, n0 + wn * WN, OC, OHW, Mpix);
+  if (gb.grp) gnb_tile<TM, TN>(acc, scale, gb, lane, m0 + wm * WM, n0 + wn * WN, OC, OHW, Mpix);
 }
 
 // split-K epilogue: O[pix][co] = (sum_s part[s][pix][co] + bias + row_bias
@@ -2742,7 +2742,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
   if (gnb_done) *gnb_done = 0;
   if (!silu_done) O2 = nullptr;
   GnbArgs gb{};
-  if (gnb && gnb_done && gnb->chan && gnb->grp && !bias && !row_bias && !res && ldo == OC && gnb->G > 0 &&
+  if (gnb && gnb_done && gnb->grp && !bias && !row_bias && !res && ldo == OC && gnb->G > 0 &&
       OC % gnb->G == 0 && (OC / gnb->G) % 4 == 0 && (OH * OW) % 64 == 0 && (gnb->mode == 0 || gnb->mode == 1))
     gb = *gnb;
   // Operands beyond the kernels' 32-bit buffer offsets (2 GiB: e.g. the
@@ -2820,7 +2820,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
 #undef HALO
       if (gn_done && gnp) *gn_done = 1;
       if (silu_done && O2) *silu_done = 1;
-      if (gnb_done && gb.chan) *gnb_done = 1;
+      if (gnb_done && gb.grp) *gnb_done = 1;
       return (int)hipGetLastError();
     }
   }

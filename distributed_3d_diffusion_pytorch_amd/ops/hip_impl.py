@@ -446,10 +446,12 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None,
 def _gn_bwd_parts(mode, x, dy, stats, w, b, G, parts, x2=None, dres=None, dres_scale=1.0):
     """GroupNorm backward apply over the consumer conv's epilogue partials
     (no reduce pass)."""
-    chan, grp, nparts, _ = parts
+    _, grp, nparts, _ = parts
     N, H, W, C1 = x.shape
     C = C1 + (x2.shape[-1] if x2 is not None else 0)
     dev = x.device
+    nch, _ = _gn_plan(N, H * W, C)
+    chan = torch.empty(N * nch * 2 * C + 64 * 2 * C, dtype=F32, device=dev)
     dx = torch.empty_like(x)
     dx2 = torch.empty_like(x2) if x2 is not None else None
     tg, tb = SINK.target(w), SINK.target(b)
@@ -682,12 +684,11 @@ def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=Fa
 class _GnbArgs(ctypes.Structure):
     """common.h GnbArgs: GroupNorm-backward partials from a dgrad epilogue."""
     _fields_ = [("x", ctypes.c_void_p), ("x2", ctypes.c_void_p), ("stats", ctypes.c_void_p),
-                ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("chan", ctypes.c_void_p),
-                ("grp", ctypes.c_void_p), ("C1", ctypes.c_int), ("G", ctypes.c_int), ("mode", ctypes.c_int),
-                ("R", ctypes.c_int)]
+                ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("grp", ctypes.c_void_p),
+                ("C1", ctypes.c_int), ("G", ctypes.c_int), ("mode", ctypes.c_int), ("pad_", ctypes.c_int)]
 
 
-assert ctypes.sizeof(_GnbArgs) == 72
+assert ctypes.sizeof(_GnbArgs) == 64
 _GNB_EPI = os.environ.get("D3D_GNB_EPI", "1") != "0"
 
 
@@ -729,11 +730,9 @@ def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo
     ga = None
     if gnb is not None and _GNB_EPI and (OH * OW) % 64 == 0 and ldo == OC:
         nparts = OH * OW // 64
-        R = N * nparts
-        chan = torch.empty(2 * OC * R, dtype=F32, device=x.device)
         grp = torch.empty(N * (OC // 4) * nparts * 2, dtype=F32, device=x.device)
         ga = _GnbArgs(gnb.x.data_ptr(), _ptr(gnb.x2), gnb.stats.data_ptr(), gnb.w.data_ptr(), gnb.b.data_ptr(),
-                      chan.data_ptr(), grp.data_ptr(), int(gnb.C1), int(gnb.G), int(gnb.mode), int(R))
+                      grp.data_ptr(), int(gnb.C1), int(gnb.G), int(gnb.mode), 0)
     _chk(_lib.d3d_conv3(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
                         IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), taps, _ptr(ws), ns,
                         _ptr(gnp), int(gn_groups), ctypes.byref(done), _ptr(silu_out), ctypes.byref(sdone),
@@ -742,7 +741,7 @@ def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo
     if silu_out is not None and not sdone.value:
         _chk(_lib.d3d_silu(out.data_ptr(), silu_out.data_ptr(), out.numel(), _st()), "silu")
     if ga is not None and bdone.value:
-        gnb.parts = (chan, grp, nparts, out.data_ptr())
+        gnb.parts = (None, grp, nparts, out.data_ptr())
     return (gnp, OH * OW // 64) if done.value else None
 
 
