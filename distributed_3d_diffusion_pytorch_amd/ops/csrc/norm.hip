@@ -441,11 +441,7 @@ __global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, co
   const uint32_t dkey = drop_key(seed), dthr = drop_threshold(p_drop);
   const int cv = C / 8, rpi = NT / cv;
   const int tid = threadIdx.x, roff = tid / cv;
-  // chan_out: this block's per-channel dgamma / dbeta partials (the reduce
-  // pass that made them is gone when the consumer conv's epilogue supplied
-  // the group sums): row (n, chunk) of [N * nchunks][C][2], summed by colsum
-  if (roff >= rpi && chan_out == nullptr) return;
-  const bool act = roff < rpi;
+  if (roff >= rpi) return;
   const int c0 = (tid % cv) * 8;
   // y = x * A + B with A = rstd * gamma, B = beta - mean * rstd * gamma
   float A[8], Bc[8];
