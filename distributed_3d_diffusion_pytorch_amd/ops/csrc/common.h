@@ -212,29 +212,25 @@ struct GnbArgs {
 
 // acc: the wave's fp32 tile (TM row tiles of 16 channels x TN fragments of 16
 // pixels), dy = bf16(acc * scale) as stored; co_base / pix_base: the wave's
-// first channel / pixel (TN % 4 == 0: whole 64-pixel parts).  Loads are issued
-// before any store, through restrict-qualified locals (otherwise every load
-// waits behind the previous stores: a memory round trip per channel); the SiLU
-// derivative uses the hardware reciprocal.
+// first channel / pixel (TN % 4 == 0: whole 64-pixel parts).  The caller
+// guarantees co_base + 16 TM <= C and that the wave's channels lie in one
+// concat source (C1 % 64 == 0): every load is unconditional with a
+// wave-uniform base (per-lane conditional loads became one exec-masked branch
+// and a vmcnt(0) per load).  Loads go through restrict-qualified locals, so no
+// load waits behind the partial stores; the SiLU derivative uses the hardware
+// reciprocal.
 template <int TM, int TN>
 __device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale, const GnbArgs& a, int lane,
                                          int co_base, long pix_base, int C, int HW, long Mpix) {
   const int fr = lane & 15, fq = lane >> 4;
   const int Cg = C / a.G, nparts = HW / 64;
-  const bf16* __restrict__ x1 = a.x;
-  const bf16* __restrict__ x2 = a.x2;
+  const bool second = a.x2 != nullptr && co_base >= a.C1;       // wave-uniform
+  const bf16* __restrict__ xs = second ? a.x2 + (co_base - a.C1) : a.x + co_base;
+  const int ld = a.x2 == nullptr ? C : (second ? C - a.C1 : a.C1);
   const float* __restrict__ stats = a.stats;
+  const float* __restrict__ gam = a.gamma + co_base + fq * 4;
+  const float* __restrict__ bet = a.beta + co_base + fq * 4;
   float* __restrict__ grp = a.grp;
-  const int C1 = x2 ? a.C1 : C;
-  float gm[TM][4], bt[TM][4];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = co_base + i * 16 + fq * 4 + e;
-      gm[i][e] = c < C ? a.gamma[c] : 0.f;
-      bt[i][e] = c < C ? a.beta[c] : 0.f;
-    }
 #pragma unroll
   for (int h = 0; h < TN / 4; ++h) {
     const long p0 = pix_base + h * 64;
@@ -242,23 +238,18 @@ __device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale
     const int n = (int)(p0 / HW);
     const int t = (int)(p0 - (long)n * HW) / 64;
     bf16x4 xr[TM][4];
-    float mean[TM], rstd[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int co = co_base + i * 16 + fq * 4;
-      const int g = (co < C ? co : C - 1) / Cg;
-      mean[i] = stats[(n * a.G + g) * 2];
-      rstd[i] = stats[(n * a.G + g) * 2 + 1];
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const long pix = p0 + jj * 16 + fr;
-        const bf16* src = co < C1 ? x1 + pix * C1 + co : x2 + pix * (C - C1) + (co - C1);
-        xr[i][jj] = co < C ? *reinterpret_cast<const bf16x4*>(src) : bf16x4{};
-      }
-    }
+      for (int jj = 0; jj < 4; ++jj)
+        xr[i][jj] = *reinterpret_cast<const bf16x4*>(xs + (p0 + jj * 16 + fr) * ld + i * 16 + fq * 4);
     float ga[TM], gb[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      const f32x4 gm = *reinterpret_cast<const f32x4*>(gam + i * 16);
+      const f32x4 bt = *reinterpret_cast<const f32x4*>(bet + i * 16);
+      const int g = (co_base + i * 16 + fq * 4) / Cg;
+      const float mean = stats[(n * a.G + g) * 2], rstd = stats[(n * a.G + g) * 2 + 1];
       ga[i] = gb[i] = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -266,18 +257,18 @@ __device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const float dy = (float)(bf16)(acc[i][h * 4 + jj][e] * scale);
-          const float xhat = ((float)xr[i][jj][e] - mean[i]) * rstd[i];
+          const float xhat = ((float)xr[i][jj][e] - mean) * rstd;
           float dA = dy;
           if (a.mode) {
-            const float z = xhat * gm[i][e] + bt[i][e];
+            const float z = xhat * gm[e] + bt[e];
             const float sgm = __builtin_amdgcn_rcpf(1.0f + __expf(-z));
             dA = dy * sgm * (1.0f + z * (1.0f - sgm));
           }
           sg += dA * xhat;
           sb += dA;
         }
-        ga[i] += sb * gm[i][e];                      // sum dA*gamma over the lane's pixels
-        gb[i] += sg * gm[i][e];                      // sum dA*gamma*xhat
+        ga[i] += sb * gm[e];                       // sum dA*gamma over the lane's pixels
+        gb[i] += sg * gm[e];                       // sum dA*gamma*xhat
       }
     }
 #pragma unroll
@@ -287,9 +278,8 @@ __device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale
         ga[i] += __shfl_xor(ga[i], m, 64);
         gb[i] += __shfl_xor(gb[i], m, 64);
       }
-      const int co = co_base + i * 16 + fq * 4;
-      if (fr == 0 && co < C) {
-        float* d = grp + (((long)n * (C / 4) + co / 4) * nparts + t) * 2;
+      if (fr == 0) {
+        float* d = grp + (((long)n * (C / 4) + (co_base + i * 16 + fq * 4) / 4) * nparts + t) * 2;
         d[0] = ga[i];
         d[1] = gb[i];
       }

@@ -2742,8 +2742,10 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
   if (gnb_done) *gnb_done = 0;
   if (!silu_done) O2 = nullptr;
   GnbArgs gb{};
-  if (gnb && gnb_done && gnb->grp && !bias && !row_bias && !res && ldo == OC && gnb->G > 0 &&
-      OC % gnb->G == 0 && (OC / gnb->G) % 4 == 0 && (OH * OW) % 64 == 0 && (gnb->mode == 0 || gnb->mode == 1))
+  // (gnb_tile wants whole 64-channel wave slices in one concat source)
+  if (gnb && gnb_done && gnb->grp && !bias && !row_bias && !res && ldo == OC && gnb->G > 0 && OC % 64 == 0 &&
+      OC % gnb->G == 0 && (OC / gnb->G) % 4 == 0 && (OH * OW) % 64 == 0 && (gnb->mode == 0 || gnb->mode == 1) &&
+      (gnb->x2 == nullptr || gnb->C1 % 64 == 0))
     gb = *gnb;
   // Operands beyond the kernels' 32-bit buffer offsets (2 GiB: e.g. the
   // 256-channel decoder concat of 128x128 images at one micro-batch of 128):
