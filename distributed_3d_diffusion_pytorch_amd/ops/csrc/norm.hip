@@ -31,7 +31,9 @@ struct Plan {
 // blocks per GroupNorm launch: 1024 beat 2048 and 512 by 0.5-1 % on both
 // headline configs (the per-block merge / LDS epilogue amortises over more
 // rows; profiles/ab_gn_target.txt)
-static int gn_target_blocks() { return 1024; }
+static int g_gn_blocks = 1024;
+static int g_gn_red_u = 1, g_gn_app_u = 2;    // rows in flight per thread: backward reduce / apply
+static int gn_target_blocks() { return g_gn_blocks; }
 
 Plan make_plan(int N, int P, int C) {
   Plan p;
@@ -515,7 +517,7 @@ __device__ __forceinline__ void bwd_elem(float xv, float dyv, float mean, float 
   }
 }
 
-template <int MODE>
+template <int MODE, int U>
 __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                       const bf16* __restrict__ ss, const float* __restrict__ stats,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -523,7 +525,6 @@ __global__ void __launch_bounds__(NT) gn_bwd_reduce_k(const bf16* __restrict__ x
                                                       uint64_t seed, bf16* __restrict__ dss,
                                                       float* __restrict__ chan_part, float* __restrict__ grp_part,
                                                       int ssld, const uint64_t* __restrict__ seed_dev, Cat cat) {
-  constexpr int U = 1;      // rows in flight per thread (more: VGPR-bound occupancy, measured slower)
   if (seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][rpi][C]
   const int chunk = blockIdx.x, n = blockIdx.y;
@@ -723,7 +724,7 @@ __device__ __forceinline__ void dgb_rowsum(const float* __restrict__ part, long 
   }
 }
 
-template <int MODE>
+template <int MODE, int U>
 __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                       const bf16* __restrict__ ss, const float* __restrict__ stats,
                                                       const float* __restrict__ grp_part,
@@ -744,7 +745,6 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
     dgb_rowsum(chan_part, chan_R, 2 * C, blk * (NT / 64) + (threadIdx.x >> 6), dgamma, dbeta, accumulate);
     return;
   }
-  constexpr int U = 2;      // rows in flight per thread
   __shared__ __attribute__((aligned(16))) float s_c[4 * 1024];      // per group: mean, rstd, c1, c2
   const int chunk = blockIdx.x, n = blockIdx.y - trows;
   const int Cg = C / G;
@@ -872,6 +872,15 @@ inline int ew_grid(long nvec) {
 }  // namespace
 
 // =============================================================== C ABI ====
+// Launch-shape knobs (kbench sweeps): blocks per launch, rows in flight per
+// thread of the backward reduce (1, 2) and apply (1, 2, 4).  0 keeps a value.
+D3D_API int d3d_gn_cfg(int blocks, int red_u, int app_u) {
+  if (blocks > 0) g_gn_blocks = blocks;
+  if (red_u > 0) g_gn_red_u = red_u;
+  if (app_u > 0) g_gn_app_u = app_u;
+  return 0;
+}
+
 D3D_API int d3d_gn_plan(int N, int P, int C, int* nchunks, int* rows) {
   Plan p = make_plan(N, P, C);
   *nchunks = p.nchunks;
@@ -953,28 +962,32 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
   if (x2) dres = nullptr;                  // (the caller never combines the two)
   size_t lds = (size_t)p.rpi * C * 4 * sizeof(float);
   dim3 g(p.nchunks, N);
-#define RED(M)                                                                                                    \
-  hipLaunchKernelGGL(gn_bwd_reduce_k<M>, g, dim3(NT), lds, st, (const bf16*)x, (const bf16*)dy, (const bf16*)ss, \
+#define RED1(M, U)                                                                                                \
+  hipLaunchKernelGGL((gn_bwd_reduce_k<M, U>), g, dim3(NT), lds, st, (const bf16*)x, (const bf16*)dy, (const bf16*)ss, \
                      stats, gamma, beta, P, C, G, p.rows, p.nchunks, p_drop, (uint64_t)seed, (bf16*)dss,          \
                      chan_part, grp_part, ssld, (const uint64_t*)seed_dev, cat)
+#define RED(M) if (g_gn_red_u == 2) RED1(M, 2); else RED1(M, 1)
   if (mode == 0) RED(0);
   else if (mode == 1) RED(1);
   else RED(2);
 #undef RED
+#undef RED1
   // dgamma/dbeta: chan_part is [2C][N*nchunks] -> 2C row sums, 4 per block,
   // by `trows` leading rows of the apply grid
   if (G > 1024) return (int)hipErrorInvalidValue;
   const int tblocks = (2 * C + NT / 64 - 1) / (NT / 64);
   const int trows = (tblocks + p.nchunks - 1) / p.nchunks;
-#define APP(M)                                                                                                    \
-  hipLaunchKernelGGL(gn_bwd_apply2_k<M>, dim3(p.nchunks, N + trows), dim3(NT), 0, st, (const bf16*)x,             \
+#define APP1(M, U)                                                                                                \
+  hipLaunchKernelGGL((gn_bwd_apply2_k<M, U>), dim3(p.nchunks, N + trows), dim3(NT), 0, st, (const bf16*)x,             \
                      (const bf16*)dy, (const bf16*)ss, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows,    \
                      p.nchunks, p_drop, (uint64_t)seed, ssld, (const uint64_t*)seed_dev, cat, chan_part, dgamma,    \
                      dbeta, accumulate, trows, (const bf16*)dres, dres_scale, (long)N * p.nchunks, 0, nullptr)
+#define APP(M) if (g_gn_app_u == 4) APP1(M, 4); else if (g_gn_app_u == 1) APP1(M, 1); else APP1(M, 2)
   if (mode == 0) APP(0);
   else if (mode == 1) APP(1);
   else APP(2);
 #undef APP
+#undef APP1
   return (int)hipGetLastError();
 }
 
@@ -995,7 +1008,7 @@ D3D_API int d3d_gn_bwd_apply_parts(int mode, const void* x, const void* dy, cons
   Cat cat{(const bf16*)x2, (bf16*)dx2, C1};
   if (x2) dres = nullptr;
 #define APP(M)                                                                                                    \
-  hipLaunchKernelGGL(gn_bwd_apply2_k<M>, dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, (const bf16*)dy,   \
+  hipLaunchKernelGGL((gn_bwd_apply2_k<M, 2>), dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, (const bf16*)dy,   \
                      (const bf16*)nullptr, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows, p.nchunks,    \
                      0.f, (uint64_t)0, 2 * C, (const uint64_t*)nullptr, cat, (const float*)nullptr, dgamma, dbeta,  \
                      accumulate, 0, (const bf16*)dres, dres_scale, 0L, nparts, chan_ws)

@@ -689,7 +689,12 @@ class _GnbArgs(ctypes.Structure):
 
 
 assert ctypes.sizeof(_GnbArgs) == 64
-_GNB_EPI = os.environ.get("D3D_GNB_EPI", "1") != "0"
+# Off by default: measured slower end to end (profiles/r4/gnb_epi_ab.txt --
+# the epilogue costs the halo dgrad +25-40 % while the reduce pass it
+# replaces is a bandwidth-bound 30-160 us); kept for A/B and its tests.
+_GNB_EPI = os.environ.get("D3D_GNB_EPI", "0") != "0"
+if os.environ.get("D3D_GN_CFG"):        # A/B knob "blocks,red_u,app_u": GroupNorm launch shapes
+    _lib.d3d_gn_cfg(*[int(v) for v in os.environ["D3D_GN_CFG"].split(",")])
 
 
 class _GnbHolder:

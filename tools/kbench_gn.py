@@ -1,34 +1,26 @@
-"""GroupNorm roofline: every gn_* launch of the X-UNet step at its real
-level shapes, timed in isolation, with the HBM bytes it must move and the
-achieved TB/s.  Forward = statistics pass (when not fused into the producer)
-+ fused finalize/apply; backward = reduce + apply (d3d_gn_bwd2).
+"""GroupNorm backward (reduce + apply) in isolation on the X-UNet level shapes,
+as the training step launches it: GN+SiLU with a residual-branch gradient
+(dres), GN+FiLM(+dropout) and the decoder's virtual-concat GN+SiLU.  JSON lines
+with median device time and achieved HBM bandwidth (bytes the two passes must
+move: reduce reads x, dy (, ss); apply reads x, dy (, ss, dres), writes dx).
 
-Bytes counted (bf16 = 2 B, C-wide rows, N*P pixels):
-  stats      : read x                                   (1 unit)
-  apply m0/1 : read x, write y                          (2 units)
-  apply m2   : read x, ss scale+shift (2C), write y     (4 units)
-  bwd m0/1   : reduce read x, dy; apply read x, dy, write dx         (5 units)
-  bwd m2     : reduce read x, dy, ss scale, write dss (2C);
-               apply read x, dy, ss scale, write dx                   (9 units)
-  (+1 unit when the residual-branch gradient dres is folded into the apply)
-
-usage: python tools/kbench_gn.py [frames ...]   (default 256 = bs128, 32 = bs16)
-Prints one JSON line per (frames, level, pass, mode)."""
+    python tools/kbench_gn.py [N frames ...]     (default: 32 256 = bs16, bs128)
+    D3D_GN_CFG=blocks,red_u,app_u  selects the launch shape (ops/csrc/norm.hip)
+"""
 import json
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import torch  # noqa: E402
+import torch
 
 from distributed_3d_diffusion_pytorch_amd.ops import hip_impl as H
 
 BF = torch.bfloat16
-dev = "cuda"
 
 
-def timeit(fn, iters=20):
-    for _ in range(3):
+def timeit(fn, iters=25):
+    for _ in range(4):
         fn()
     torch.cuda.synchronize()
     ts = []
@@ -44,54 +36,35 @@ def timeit(fn, iters=20):
 
 
 def main():
-    frames = [int(a) for a in sys.argv[1:]] or [256, 32]
-    torch.manual_seed(0)
-    # (H, C, concat-C2): encoder level shapes and the decoder's widest concat
-    levels = ((64, 128, 0), (64, 128, 128), (32, 256, 0), (32, 256, 256), (16, 256, 0), (8, 512, 0))
-    for N in frames:
-        for Hh, C1, C2 in levels:
-            C = C1 + C2
-            x = torch.randn(N, Hh, Hh, C1, device=dev).to(BF)
-            x2 = torch.randn(N, Hh, Hh, C2, device=dev).to(BF) if C2 else None
-            dy = torch.randn(N, Hh, Hh, C, device=dev).to(BF)
-            dres = torch.randn(N, Hh, Hh, C, device=dev).to(BF)
-            w = torch.rand(C, device=dev) + 0.5
-            b = torch.randn(C, device=dev) * 0.1
-            ss = (torch.randn(N, Hh, Hh, 2 * C, device=dev) * 0.3).to(BF) if not C2 else None
-            unit = N * Hh * Hh * C * 2
-            tag = f"{Hh}x{Hh}x{C1}" + (f"+{C2}" if C2 else "")
-            modes = (1,) if C2 else (0, 1, 2)
-            for mode in modes:
-                sarg = ss if mode == 2 else None
-                _, stats = H._gn_fwd(mode, x, w, b, 32, 1e-5, sarg, 0, 0.1 if mode == 2 else 0.0, 7, x2=x2)
-                us = timeit(lambda: H._gn_fwd(mode, x, w, b, 32, 1e-5, sarg, 0, 0.1 if mode == 2 else 0.0, 7,
-                                              x2=x2))
-                units = 3 if mode < 2 else 5          # stats read + apply
-                print(json.dumps({"frames": N, "level": tag, "pass": "fwd(stats+apply)", "mode": mode,
-                                  "us": round(us, 1), "GB": round(units * unit / 1e9, 3),
-                                  "TBps": round(units * unit / us / 1e6, 2)}), flush=True)
-                if not C2:
-                    # apply alone, statistics partials handed over as if from the producer's epilogue
-                    P = Hh * Hh
-                    nch, _ = H._gn_plan(N, P, C)
-                    part = torch.empty(N * nch * 32 * 2, dtype=torch.float32, device=dev)
-                    H._chk(H._lib.d3d_gn_stats(x.data_ptr(), N, P, C, 32, 1e-5, part.data_ptr(), None, None, 0,
-                                               H._st()), "gn_stats")
-                    x._d3d_gnpart = (part, 32, 0)
-                    us = timeit(lambda: H._gn_fwd(mode, x, w, b, 32, 1e-5, sarg, 0, 0.1 if mode == 2 else 0.0, 7))
-                    del x._d3d_gnpart
-                    units = 2 if mode < 2 else 4
-                    print(json.dumps({"frames": N, "level": tag, "pass": "fwd(apply)", "mode": mode,
-                                      "us": round(us, 1), "GB": round(units * unit / 1e9, 3),
-                                      "TBps": round(units * unit / us / 1e6, 2)}), flush=True)
-                for use_dres in ((False, True) if mode < 2 and not C2 else (False,)):
-                    dr = dres if use_dres else None
-                    us = timeit(lambda: H._gn_bwd(mode, x, dy, sarg, stats, w, b, 32, 0.1 if mode == 2 else 0.0, 7,
-                                                  x2=x2, dres=dr))
-                    units = (5 if mode < 2 else 9) + (1 if use_dres else 0)
-                    print(json.dumps({"frames": N, "level": tag, "pass": "bwd(reduce+apply)" + ("+dres" if dr is not None else ""),
-                                      "mode": mode, "us": round(us, 1), "GB": round(units * unit / 1e9, 3),
-                                      "TBps": round(units * unit / us / 1e6, 2)}), flush=True)
+    ns = [int(a) for a in sys.argv[1:]] or [32, 256]
+    H._ensure_impl()
+    G = 32
+    cfg = os.environ.get("D3D_GN_CFG", "default")
+    for N in ns:
+        for Hh, C, C1 in ((64, 128, 0), (32, 256, 0), (16, 256, 0), (8, 512, 0), (64, 256, 128), (32, 512, 256)):
+            P = Hh * Hh
+            x = torch.randn(N, Hh, Hh, C if not C1 else C1, device="cuda").to(BF)
+            x2 = torch.randn(N, Hh, Hh, C - C1, device="cuda").to(BF) if C1 else None
+            w = torch.rand(C, device="cuda") + 0.5
+            b = torch.randn(C, device="cuda") * 0.1
+            dy = torch.randn(N, Hh, Hh, C, device="cuda").to(BF)
+            dres = torch.randn(N, Hh, Hh, C, device="cuda").to(BF) if not C1 else None
+            ss = torch.randn(N, Hh, Hh, 2 * C, device="cuda").to(BF) * 0.1
+            t = N * P * C * 2
+            stats = torch.stack([torch.zeros(N * G), torch.ones(N * G)], 1).reshape(-1).cuda()
+            rows = []
+            for mode in ((1, 2) if not C1 else (1,)):
+                if mode == 1:
+                    fn = lambda: H._gn_bwd(1, x, dy, None, stats, w, b, G, 0.0, 0, x2=x2, dres=dres, dres_scale=0.7)
+                    nbytes = 2 * t + (4 * t if dres is not None else 3 * t)
+                else:
+                    fn = lambda: H._gn_bwd(2, x, dy, ss, stats, w, b, G, 0.1, 7, ssld=2 * C)
+                    nbytes = 3 * t + 2 * t + 4 * t      # reduce: x, dy, ss + dss (2t); apply: x, dy, ss, dx
+                us = timeit(fn)
+                rows.append({"cfg": cfg, "N": N, "level": f"{Hh}x{Hh}x{C}" + (f" cat{C1}" if C1 else ""),
+                             "mode": mode, "us": round(us, 1), "TBps": round(nbytes / us / 1e6, 2)})
+            for r in rows:
+                print(json.dumps(r), flush=True)
             del x, x2, dy, dres, ss
             torch.cuda.empty_cache()
 
