@@ -475,11 +475,18 @@ class XUNet(nn.Module):
         if not (self.batch_film and _COND_STREAM and ref is not None and ref.is_cuda
                 and (self.compute_dtype or ref.dtype) == torch.bfloat16 and ops.use_hip(ref, any_dtype=True)):
             return None
-        # measured gain at 64x64 (bs16 / bs128); at 128x128 (two micro-batches
-        # of 64, multi-GB conditioning tensors) the second stream made the
-        # eager step 4.5x slower (profiles/ab_cond_stream_r2.txt): only the
-        # measured regime uses it unless D3D_COND_STREAM=2
-        if self.H * self.W > 64 * 64 and os.environ.get("D3D_COND_STREAM", "1") != "2":
+        # measured gain at 64x64 (bs16 / bs128).  At 128x128 the EAGER step
+        # (multi-GB conditioning tensors) ran 4.5x slower with the second
+        # stream (profiles/ab_cond_stream_r2.txt): the caching allocator keeps
+        # one block cache per stream, so the side stream's freed blocks were
+        # unusable by the trunk and every step hit allocation retries (a full
+        # cache flush + device sync each).  Inside a HIP-graph capture every
+        # stream of the capture allocates from the graph's one private pool
+        # and replays allocate nothing, so the side stream is safe there at
+        # any size; eager steps above 64x64 keep one stream unless
+        # D3D_COND_STREAM=2.
+        if (self.H * self.W > 64 * 64 and os.environ.get("D3D_COND_STREAM", "1") != "2"
+                and not torch.cuda.is_current_stream_capturing()):
             return None
         idx = ref.device.index if ref.device.index is not None else torch.cuda.current_device()
         st = _COND_STREAMS.get(idx)

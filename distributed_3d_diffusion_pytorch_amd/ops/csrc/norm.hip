@@ -97,7 +97,7 @@ __device__ __forceinline__ RowSrc row_src(const bf16* x, const Cat& k, int c0, i
 __global__ void __launch_bounds__(NT) gn_stats_partial_k(const bf16* __restrict__ x, int P, int C, int G,
                                                          int rows, int nchunks, float* __restrict__ part, Cat cat) {
   constexpr int U = 2;      // rows in flight per thread
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][C][3]
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [2][rpi][C] + [rpi]
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int tpr = C / 8, rpi = NT / tpr;
   const int tid = threadIdx.x;
@@ -137,29 +137,52 @@ __global__ void __launch_bounds__(NT) gn_stats_partial_k(const bf16* __restrict_
       }
     }
   }
+  // structure of arrays: mean [rpi][C] | m2 [rpi][C] | count [rpi] (one per
+  // row lane), each thread's 8 channels two 16-byte stores (the interleaved
+  // [rpi][C][3] layout was 84-86 % LDS bank-conflict cycles,
+  // profiles/r3/pmc_step/table_bs128.txt)
+  const int SL = rpi * C;
   if (active) {
+    float mn[8], m2[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float* o = lds + ((roff * C) + c0 + j) * 3;
-      float m = cnt > 0.f ? s[j] / cnt : 0.f;
-      o[0] = cnt;
-      o[1] = sh[j] + m;
-      o[2] = fmaxf(q[j] - s[j] * m, 0.f);
+      const float m = cnt > 0.f ? s[j] / cnt : 0.f;
+      mn[j] = sh[j] + m;
+      m2[j] = fmaxf(q[j] - s[j] * m, 0.f);
     }
+    float* o = lds + roff * C + c0;
+    *reinterpret_cast<f32x4*>(o) = f32x4{mn[0], mn[1], mn[2], mn[3]};
+    *reinterpret_cast<f32x4*>(o + 4) = f32x4{mn[4], mn[5], mn[6], mn[7]};
+    *reinterpret_cast<f32x4*>(o + SL) = f32x4{m2[0], m2[1], m2[2], m2[3]};
+    *reinterpret_cast<f32x4*>(o + SL + 4) = f32x4{m2[4], m2[5], m2[6], m2[7]};
+    if (v == 0) lds[2 * SL + roff] = cnt;
   }
   __syncthreads();
+  // per group: TPG consecutive lanes (a power of two <= 64: a group never
+  // straddles a wave) each merge a strided share of the rpi x Cg entries, then
+  // a fixed-order butterfly of Chan merges (deterministic)
   const int Cg = C / G;
-  for (int g = tid; g < G; g += NT) {
+  int TPG = 1;
+  while (TPG < 64 && TPG * 2 * G <= NT) TPG <<= 1;
+  const int E = rpi * Cg;
+  for (int g0 = 0; g0 < G; g0 += NT / TPG) {
+    const int g = g0 + tid / TPG, sub = tid % TPG;
     Moments acc = {0.f, 0.f, 0.f};
-    for (int rr = 0; rr < rpi; ++rr)
-      for (int cc = 0; cc < Cg; ++cc) {
-        const float* o = lds + ((rr * C) + g * Cg + cc) * 3;
-        Moments b = {o[0], o[1], o[2]};
+    if (g < G)
+      for (int e = sub; e < E; e += TPG) {
+        const int rr = e / Cg, cc = e - rr * Cg;
+        const Moments b = {lds[2 * SL + rr], lds[rr * C + g * Cg + cc], lds[SL + rr * C + g * Cg + cc]};
         if (b.n > 0.f) acc = merge_moments(acc, b);
       }
-    float* dst = part + (((long)n * nchunks + chunk) * G + g) * 2;
-    dst[0] = acc.mean;
-    dst[1] = acc.m2;
+    for (int w = 1; w < TPG; w <<= 1) {
+      const Moments b = {__shfl_xor(acc.n, w), __shfl_xor(acc.mean, w), __shfl_xor(acc.m2, w)};
+      acc = merge_moments(acc, b);
+    }
+    if (g < G && sub == 0) {
+      float* dst = part + (((long)n * nchunks + chunk) * G + g) * 2;
+      dst[0] = acc.mean;
+      dst[1] = acc.m2;
+    }
   }
 }
 

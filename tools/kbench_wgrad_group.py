@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=512)
     ap.add_argument("--minpix", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated batch-name prefixes")
+    ap.add_argument("--skip_old", action="store_true", help="time the grouped launch only")
     a = ap.parse_args()
     H._ensure_impl()
     H._lib.d3d_wgrad_group_cfg(a.blocks, a.pk, a.minpix)
@@ -69,6 +71,8 @@ def main():
     dev = torch.device("cuda")
     torch.manual_seed(0)
     for name, spec in batches(2 * a.examples):
+        if a.only and not any(name.startswith(o) for o in a.only.split(",")):
+            continue
         tens = []
         flops = 0.0
         for (N, Hh, W, IC, OC, taps) in spec:
@@ -89,7 +93,7 @@ def main():
         def new():
             H.wgrad_group_run(jobs)
 
-        t_old = timeit(old, a.iters)
+        t_old = float("nan") if a.skip_old else timeit(old, a.iters)
         t_new = timeit(new, a.iters)
         print(json.dumps({"batch": name, "gflop": round(flops / 1e9, 1), "old_us": round(t_old, 1),
                           "new_us": round(t_new, 1), "old_tfs": round(flops / t_old / 1e6, 1),
