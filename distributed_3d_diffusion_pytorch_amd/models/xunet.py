@@ -117,6 +117,9 @@ class ResnetBlock(nn.Module):
             # x's two consumers here (GN0 and the residual / NIN branch) hand
             # their gradients over inside the GN0 backward kernel
             slot = ops.res_slot(x) if torch.is_grad_enabled() and x.requires_grad else None
+            if slot is not None:
+                # a decoder skip concat that also reads x deposits its gradient here (ops _CatGNDense)
+                x._d3d_res_slot = slot
             h = self.groupnorm0(x, silu=True, res_slot=slot)
         # the conv epilogues also emit the partial statistics of the GroupNorm
         # that reads their output (GN1 here; the next block's GN0 below)

@@ -24,7 +24,7 @@ SIGNATURES = {
     "d3d_border_fix": [P, P, I, I, I, I, I, I, I, P, P],
     "d3d_border_sums": [P, P, I, I, I, I, P],
     "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, I, P, P],
-    "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P, F, P],
+    "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P, F, P, F, P],
     "d3d_conv_s64_cfg": [I],
     "d3d_conv_res_cfg": [I],
     # elementwise.hip
@@ -55,7 +55,7 @@ SIGNATURES = {
     "d3d_conv": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P],
     "d3d_conv2": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P],
     "d3d_conv3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P, IP, P, IP, P],
-    "d3d_gn_bwd_apply_parts": [I, P, P, P, P, P, I, I, I, I, P, P, P, P, P, I, I, P, P, I, P, F, P],
+    "d3d_gn_bwd_apply_parts": [I, P, P, P, P, P, I, I, I, I, P, P, P, P, P, I, I, P, P, I, P, F, P, F, P],
     "d3d_conv_plan": [I, I, I, I, I, I],
     "d3d_set_conv_korder": [I],
     "d3d_set_wgrad_impl": [I],
@@ -98,6 +98,8 @@ SIGNATURES = {
     "d3d_wgrad_group_ok": [P],
     "d3d_wgrad_group_wide": [I],
     "d3d_wgrad_group_stages": [I],
+    "d3d_wgrad_group_halo": [I, I, I],
+    "d3d_wgrad_group_engine": [P],
     "d3d_wgrad_group": [P, I, P, L, P],
     "d3d_wgrad_group_plan": [P, I, IP, IP, C.POINTER(C.c_long)],
 }

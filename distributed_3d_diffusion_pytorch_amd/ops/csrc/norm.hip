@@ -759,7 +759,8 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                       int accumulate, int trows, const bf16* __restrict__ dres,
                                                       float dres_scale, long chan_R, int gparts,
-                                                      float* __restrict__ chan_out) {
+                                                      float* __restrict__ chan_out, const bf16* __restrict__ dres2,
+                                                      float dres2_scale) {
   // chan_R: rows of chan_part; gparts > 0: grp_part holds the consumer conv's
   // dgrad-epilogue partials ([N][G][gparts][2], common.h gnb_tile) instead of
   // the reduce pass's [N][nchunks][G][2]
@@ -821,7 +822,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
 #pragma unroll
   for (int j = 0; j < 8; ++j) pg[j] = pb[j] = 0.f;
   for (int r = chunk * rows + roff; r < r1; r += U * rpi) {
-    f32x8 xv[U], dv[U], sc[U], rv[U];
+    f32x8 xv[U], dv[U], sc[U], rv[U], rv2[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int rr = r + u * rpi;
@@ -831,6 +832,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
         dv[u] = ld8(dy + pix * C + c0);
         if (MODE == 2) sc[u] = ld8(ss + pix * ssld + c0);
         if (dres) rv[u] = ld8(dres + pix * C + c0);
+        if (dres2) rv2[u] = ld8(dres2 + pix * C + c0);
       }
     }
 #pragma unroll
@@ -853,6 +855,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
         pb[j] += dA;
       }
       if (dres) o += rv[u] * dres_scale;    // the residual branch's gradient of the same input
+      if (dres2) o += rv2[u] * dres2_scale;  // ... and a second consumer's (a decoder skip, models/xunet.py)
       st8(dst + pix * dld, o);
     }
   }
@@ -978,11 +981,12 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
                         const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
                         unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
                         float* grp_part, float* coef, int accumulate, int ssld, const void* seed_dev,
-                        const void* x2, void* dx2, int C1, const void* dres, float dres_scale, hipStream_t st) {
+                        const void* x2, void* dx2, int C1, const void* dres, float dres_scale, const void* dres2,
+                        float dres2_scale, hipStream_t st) {
   Plan p = make_plan(N, P, C);
   Cat cat{(const bf16*)x2, (bf16*)dx2, C1};
   if (ssld == 0) ssld = 2 * C;
-  if (x2) dres = nullptr;                  // (the caller never combines the two)
+  if (x2) dres = dres2 = nullptr;          // (the caller never combines the two)
   size_t lds = (size_t)p.rpi * C * 4 * sizeof(float);
   dim3 g(p.nchunks, N);
 #define RED1(M, U)                                                                                                \
@@ -1004,7 +1008,8 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
   hipLaunchKernelGGL((gn_bwd_apply2_k<M, U>), dim3(p.nchunks, N + trows), dim3(NT), 0, st, (const bf16*)x,             \
                      (const bf16*)dy, (const bf16*)ss, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows,    \
                      p.nchunks, p_drop, (uint64_t)seed, ssld, (const uint64_t*)seed_dev, cat, chan_part, dgamma,    \
-                     dbeta, accumulate, trows, (const bf16*)dres, dres_scale, (long)N * p.nchunks, 0, nullptr)
+                     dbeta, accumulate, trows, (const bf16*)dres, dres_scale, (long)N * p.nchunks, 0, nullptr,        \
+                     (const bf16*)dres2, dres2_scale)
 #define APP(M) if (g_gn_app_u == 4) APP1(M, 4); else if (g_gn_app_u == 1) APP1(M, 1); else APP1(M, 2)
   if (mode == 0) APP(0);
   else if (mode == 1) APP(1);
@@ -1023,18 +1028,19 @@ D3D_API int d3d_gn_bwd_apply_parts(int mode, const void* x, const void* dy, cons
                                    const float* beta, int N, int P, int C, int G, void* dx, float* dgamma,
                                    float* dbeta, float* chan_ws, const float* grp_part, int nparts,
                                    int accumulate, const void* x2, void* dx2, int C1, const void* dres,
-                                   float dres_scale, hipStream_t st) {
+                                   float dres_scale, const void* dres2, float dres2_scale, hipStream_t st) {
   if (mode != 0 && mode != 1) return (int)hipErrorInvalidValue;
   if (G > 1024 || nparts < 1 || C % G || (C / G) % 4 || C > 2048) return (int)hipErrorInvalidValue;
   Plan p = make_plan(N, P, C);
   if (p.rpi * C > 2048) return (int)hipErrorInvalidValue;
   Cat cat{(const bf16*)x2, (bf16*)dx2, C1};
-  if (x2) dres = nullptr;
+  if (x2) dres = dres2 = nullptr;
 #define APP(M)                                                                                                    \
   hipLaunchKernelGGL((gn_bwd_apply2_k<M, 2>), dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, (const bf16*)dy,   \
                      (const bf16*)nullptr, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows, p.nchunks,    \
                      0.f, (uint64_t)0, 2 * C, (const uint64_t*)nullptr, cat, (const float*)nullptr, dgamma, dbeta,  \
-                     accumulate, 0, (const bf16*)dres, dres_scale, 0L, nparts, chan_ws)
+                     accumulate, 0, (const bf16*)dres, dres_scale, 0L, nparts, chan_ws, (const bf16*)dres2,       \
+                     dres2_scale)
   if (mode == 0) APP(0);
   else APP(1);
 #undef APP
@@ -1047,5 +1053,5 @@ D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, 
                        unsigned long long seed, void* dx, void* dss, float* dgamma, float* dbeta, float* chan_part,
                        float* grp_part, float* coef, hipStream_t st) {
   return d3d_gn_bwd2(mode, x, dy, ss, stats, gamma, beta, N, P, C, G, p_drop, seed, dx, dss, dgamma, dbeta,
-                     chan_part, grp_part, coef, 0, 0, nullptr, nullptr, nullptr, 0, nullptr, 1.f, st);
+                     chan_part, grp_part, coef, 0, 0, nullptr, nullptr, nullptr, 0, nullptr, 1.f, nullptr, 1.f, st);
 }

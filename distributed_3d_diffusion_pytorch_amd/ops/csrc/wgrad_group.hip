@@ -588,6 +588,235 @@ __global__ void __launch_bounds__(256, 2) wgrad_grp2_k(GwTable tab) {
   }
 }
 
+// ---------------------------------------------------------- halo tiles ----
+// 3x3 stride-1 jobs on images W % 32 == 0 (the 64x64 / 32x32 levels, ~80 % of
+// the weight-gradient FLOPs): one block = 128 output channels x 64 input
+// channels x ALL NINE taps of one pixel split.  Eight waves (two per SIMD);
+// wave (wm, wn) owns output channels 64wm.. +63 x input channels 16wn.. +15 x
+// the nine taps (4 x 9 = 36 MFMA 16x16x32 tiles, 144 accumulator registers).
+// A 32-pixel K-step (half or one image row) stages the dY rows [32][128 co]
+// and the input WINDOW [3 rows][34 px][64 ci] -- the step's pixels with the
+// one-pixel border around them, zero-filled outside the image -- so the B
+// fragment of tap (kh, kw) is window rows kh*34 + kw + k: one window feeds the
+// nine taps, and the step's dY fragments are read once for all nine.  Per MFMA
+// that is 0.72 transposed LDS reads and 0.07 KB of DMA, against 1.0 and 0.25 KB
+// for the per-tap 128 x 128 tile above (which re-reads dY and X once per tap).
+constexpr int GH_BM = 128, GH_BN = 64, GH_PK = 32, GH_WR = 34;
+constexpr int GH_BROWS = 128;                          // window rows, 3 x 34 = 102 padded to 16 DMAs of 8
+constexpr int GH_STAGE = GH_PK * GH_BM + GH_BROWS * GH_BN;   // bf16: 4096 (dY) + 8192 (window) = 24 KB
+
+// 16-byte chunk swizzle of the 128-byte window rows: the 8 consecutive rows a
+// transposed read's 32-lane group touches (any tap offset) land on 64 distinct
+// banks
+__device__ __forceinline__ int gh_swz(int row) { return 2 * ((row >> 1) & 3); }
+
+__device__ __forceinline__ void gh_issue(bf16* sA, bf16* sB, const bf16* __restrict__ dY, const bf16* __restrict__ I,
+                                         long in_elems, long p0, long p_end, int OC, int IC, int OH, int OW, int lw,
+                                         int wave, const unsigned* aoff, const unsigned* boff, const unsigned* bfl,
+                                         bool on) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  const __amdgpu_buffer_rsrc_t rA = gw_rsrc(dY + p0 * OC, on ? (p_end - p0) * OC * 2 : 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sA + wave * 4 * GH_BM), 16, aoff[0], 0, 0, 0);
+  // window origin: pixel (y - 1, x0 - 1); it may lie before the tensor, and
+  // only masked lanes (top row, left column) ever address below the tensor
+  const long pb = p0 - OW - 1;
+  const __amdgpu_buffer_rsrc_t rB = gw_rsrc(I + pb * IC, on ? (in_elems - pb * IC) * 2 : 0);
+  const int x0 = (int)(p0 & (OW - 1)), y = (int)((p0 >> lw) & (OH - 1));
+  const unsigned bad = 1u | (y == 0 ? 2u : 0u) | (y == OH - 1 ? 4u : 0u) | (x0 == 0 ? 8u : 0u) |
+                       (x0 + GH_PK == OW ? 16u : 0u);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * 2 + j) * 8 * GH_BN), 16,
+                                             (bfl[j] & bad) ? 0x80000000u : boff[j], 0, 0, 0);
+}
+
+template <int NS>
+__global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
+  constexpr int PER = 1 + 2;                     // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * GH_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int R;
+  {
+    const int T = gridDim.x, L = blockIdx.x;
+    const int q = T / 8, r = T % 8, xcd = L % 8;
+    R = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+  }
+  int k = 0;
+  while (k + 1 < tab.n && R >= tab.j[k + 1].blk0) ++k;
+  const GwJob& J = tab.j[k];
+  const bf16* dY = J.dy;
+  const int OC = J.OC, ICt = J.IC, C1 = J.C1, OH = J.H, OW = J.W, lw = J.lw;
+  const int ncb = J.ncb, nmb = J.nmb, splits = J.splits;
+  const long P = J.P;
+  const int b = R - J.blk0;
+  const int bx = b % ncb, by = (b / ncb) % nmb, split = b / (ncb * nmb);
+  const int m0 = by * GH_BM, ci0g = bx * GH_BN;
+  const bool second = J.x2 != nullptr && ci0g >= C1;
+  const bf16* I = second ? J.x2 : J.x;
+  const int IC = J.x2 == nullptr ? ICt : (second ? ICt - C1 : C1);
+  const int ci0 = second ? ci0g - C1 : ci0g;
+  const long in_elems = P * IC;
+  const long p_begin = (long)split * J.pps;
+  const long p_end = p_begin + J.pps < P ? p_begin + J.pps : P;
+
+  unsigned aoff[1], boff[2], bfl[2];
+  {
+    const int lrow = lane >> 4, pch = lane & 15;
+    {
+      const int trow = wave * 4 + lrow;
+      const int lc = pch ^ (2 * (trow & 7));
+      aoff[0] = (unsigned)((trow * OC + m0 + lc * 8) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int wr = (wave * 2 + j) * 8 + (lane >> 3);
+      const int kh = wr / GH_WR, px = wr - kh * GH_WR;
+      const int chunk = (lane & 7) ^ gh_swz(wr);
+      const bool valid = wr < 3 * GH_WR;
+      boff[j] = valid ? (unsigned)(((kh * OW + px) * IC + ci0 + chunk * 8) * 2) : 0u;
+      bfl[j] = (valid ? 0u : 1u) | (kh == 0 ? 2u : 0u) | (kh == 2 ? 4u : 0u) | (px == 0 ? 8u : 0u) |
+               (px == GH_WR - 1 ? 16u : 0u);
+    }
+  }
+  // transposed-read offsets (elements in a stage): lane (g, q, pc) reads K row
+  // 4g + q (and + 16), 8-element chunk pc >> 1 of its 16 columns, half pc & 1
+  int la[4], lb[9];
+  {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
+    const int kr = 4 * g + q, x7 = 2 * (kr & 7);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) la[i] = kr * GH_BM + (((wm * 8 + 2 * i + (pc >> 1)) ^ x7) << 3) + (pc & 1) * 4;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int row = (t / 3) * GH_WR + (t % 3) + kr;
+      lb[t] = GH_PK * GH_BM + row * GH_BN + (((2 * wn + (pc >> 1)) ^ gh_swz(row)) << 3) + (pc & 1) * 4;
+    }
+  }
+  auto issue = [&](long p0, int stage, bool on) {
+    bf16* sA = smem + stage * GH_STAGE;
+    gh_issue(sA, sA + GH_PK * GH_BM, dY, I, in_elems, p0, p_end, OC, IC, OH, OW, lw, wave, aoff, boff, bfl, on);
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const long nsteps = (p_end - p_begin) / GH_PK;          // (the planner keeps splits on 64-pixel bounds)
+  const bool bias_wave = J.db != nullptr && bx == 0 && wn == 0;
+  float bsum[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bsum[i] = 0.f;
+  const unsigned ones = 0x3F803F80u;
+  // the dY fragments once per step; the window fragment of tap t + 1 is read
+  // while tap t's eight MFMAs run (register budget: 288 accumulators)
+  auto rd_b = [&](const bf16* s, int t) {
+    gs16x4 lo = gw_tr_asm(s + lb[t]);
+    gs16x4 hi = gw_tr_asm(s + lb[t] + 16 * GH_BN);
+    gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  auto compute = [&](const bf16* s) {
+    bf16x8 af[4], bcur[1], bnext[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      gs16x4 lo = gw_tr_asm(s + la[i]);
+      gs16x4 hi = gw_tr_asm(s + la[i] + 16 * GH_BM);
+      gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[i] = __builtin_bit_cast(bf16x8, v);
+    }
+    bcur[0] = rd_b(s, 0);
+    gw_tr_wait<4, 1>(af, bcur);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t < 8) bnext[0] = rd_b(s, t + 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[0], acc[i][t], 0, 0, 0);
+      if (t < 8) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("" : "+v"(bnext[0]));
+        bcur[0] = bnext[0];
+      }
+    }
+    if (bias_wave) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto u = __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, af[i]);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) bsum[i] = gw_dot2(u[w], ones, bsum[i]);
+      }
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) issue(p_begin + t * GH_PK, t, t < nsteps);
+  for (long s = 0; s < nsteps; ++s) {
+    const int st = (int)(s % NS);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PER) : "memory");
+    __builtin_amdgcn_s_barrier();
+    const long nx = s + NS - 1;
+    issue(p_begin + (nx < nsteps ? nx : s) * GH_PK, (int)(nx % NS), nx < nsteps);
+    __builtin_amdgcn_s_setprio(1);
+    compute(smem + st * GH_STAGE);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int cig = ci0g + 16 * wn + fr;             // input channel within the (concatenated) input
+  const int cw = m0 + 64 * wm;                      // this wave's first output channel
+  if (bias_wave) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bsum[i] += __shfl_xor(bsum[i], 16);
+      bsum[i] += __shfl_xor(bsum[i], 32);
+    }
+  }
+  if (splits == 1) {
+    const float sc = J.scale;
+    const int acc_in = J.acc;
+    if (bias_wave && fq == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float* d = J.db + cw + i * 16 + fr;
+        const float v = bsum[i] * sc;
+        *d = acc_in ? *d + v : v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float* d = J.dw + ((long)(cw + i * 16 + fq * 4 + e) * ICt + cig) * 9;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const float v = acc[i][t][e] * sc;
+          d[t] = acc_in ? d[t] + v : v;
+        }
+      }
+    return;
+  }
+  if (bias_wave && fq == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      J.bslab[((long)split * 2) * OC + cw + i * 16 + fr] = bsum[i];
+      J.bslab[((long)split * 2 + 1) * OC + cw + i * 16 + fr] = 0.f;
+    }
+  }
+  const long KW = 9L * ICt;
+  float* slab = J.slab + (long)split * OC * KW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float* d = slab + (long)(cw + i * 16 + fq * 4 + e) * KW + cig;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) d[(long)t * ICt] = acc[i][t][e];
+    }
+}
+
 // Grouped split-K reduce: block = (job, co, 64 input channels) summing every
 // tap of its channels over the job's slabs, 4 split lanes merged in a fixed
 // order through LDS, written as 64 x taps CONTIGUOUS floats of OIHW; blocks
@@ -673,6 +902,14 @@ static int g_gw_minpix = 512;      // lower bound of the pixels per block
 // waiting on the ring's DMAs (profiles/r4/kb_ns*.jsonl, b16_ns_blocks_ab.txt)
 static int g_gw_ns = 2;
 static int g_gw_wide = 0;          // 1: 128 x 256 chunk-pair tiles (wgrad_grp2_k; measured slower: profiles/r4/kb_w1_*), 0: 128 x 128
+static int g_gh_on = 1;            // 3x3 jobs on W % 32 == 0 images -> wgrad_halo_k
+// target blocks per halo launch: one block per CU runs at a time, so the
+// planner fits the batch into at most this many blocks rounded DOWN to whole
+// rounds of the CU count -- 522 blocks on 256 CUs ran as three rounds, the last
+// one 2 % full (the mixed decoder batch at 622 instead of ~990 TF/s,
+// profiles/r4/halo_wgrad/)
+static int g_gh_blocks = 256;
+static int g_gh_ns = 2;            // LDS ring stages of wgrad_halo_k (2 or 3)
 
 D3D_API int d3d_wgrad_group_cfg(int blocks, int pk, int minpix) {
   if (blocks > 0) g_gw_blocks = blocks;
@@ -686,6 +923,13 @@ D3D_API int d3d_wgrad_group_wide(int wide) {
 }
 D3D_API int d3d_wgrad_group_stages(int ns) {
   if (ns >= 2 && ns <= 4) g_gw_ns = ns;
+  return 0;
+}
+// halo (all-taps) tiles for 3x3 jobs: on (0/1), target blocks, ring stages (2/3); < 0 keeps a value
+D3D_API int d3d_wgrad_group_halo(int on, int blocks, int ns) {
+  if (on >= 0) g_gh_on = on ? 1 : 0;
+  if (blocks > 0) g_gh_blocks = blocks;
+  if (ns == 2 || ns == 3) g_gh_ns = ns;
   return 0;
 }
 
@@ -715,18 +959,49 @@ struct GwPlan {
   long blocks;
 };
 
-static void gw_plan(const WgJobDesc* d, int n, GwPlan& pl) {
+// the all-taps halo tile takes the job (block-shape and alignment conditions)
+static bool gh_takes(const WgJobDesc& d) {
+  return g_gh_on && d.taps == 9 && d.W >= GH_PK && d.W % GH_PK == 0 && d.OC % GH_BM == 0 && d.IC % GH_BN == 0 &&
+         (!d.x2 || d.C1 % GH_BN == 0) && (long)(2 * d.W + GH_WR) * d.IC * 2 < (1L << 30);
+}
+
+// halo: every job of d is a halo job (tiles = 128 x 64 x 9 taps)
+static void gw_plan(const WgJobDesc* d, int n, GwPlan& pl, bool halo = false) {
   double work = 0;
   for (int i = 0; i < n; ++i) {
     const long P = (long)d[i].N * d[i].H * d[i].W;
-    const int nch = d[i].taps * cdiv(d[i].IC, GW_BN);
-    pl.tiles[i] = (g_gw_wide ? (nch + 1) / 2 : nch) * cdiv(d[i].OC, GW_BM);
+    if (halo) {
+      pl.tiles[i] = (d[i].OC / GH_BM) * (d[i].IC / GH_BN);
+    } else {
+      const int nch = d[i].taps * cdiv(d[i].IC, GW_BN);
+      pl.tiles[i] = (g_gw_wide ? (nch + 1) / 2 : nch) * cdiv(d[i].OC, GW_BM);
+    }
     work += (double)pl.tiles[i] * P;
   }
   // one pixel count per block across the batch: ~g_gw_blocks equal blocks
-  long Q = (long)(work / g_gw_blocks);
+  long Q = (long)(work / (halo ? g_gh_blocks : g_gw_blocks));
   Q = std::max<long>(Q, g_gw_minpix);
   Q = (Q + 63) / 64 * 64;
+  if (halo) {
+    // whole rounds: the smallest Q whose block count fits the round-down target
+    static int cus = 0;
+    if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0))
+      cus = 256;
+    const long T = std::max<long>(cus, (long)g_gh_blocks / cus * cus);
+    auto nblk = [&](long q) {
+      long t = 0;
+      for (int i = 0; i < n; ++i) {
+        const long P = (long)d[i].N * d[i].H * d[i].W;
+        long s = std::min<long>(std::max<long>((P + q - 1) / q, 1), 64);
+        const long pps = ((P + s - 1) / s + 63) / 64 * 64;
+        t += (long)pl.tiles[i] * ((P + pps - 1) / pps);
+      }
+      return t;
+    };
+    long Pmax = 0;
+    for (int i = 0; i < n; ++i) Pmax = std::max<long>(Pmax, (long)d[i].N * d[i].H * d[i].W);
+    while (Q < Pmax && nblk(Q) > T) Q += std::max<long>(64, Q / 256 / 64 * 64);   // (unsplit jobs: stop)
+  }
   long off = 0, blocks = 0;
   for (int i = 0; i < n; ++i) {
     const long P = (long)d[i].N * d[i].H * d[i].W;
@@ -758,22 +1033,40 @@ static void gw_plan(const WgJobDesc* d, int n, GwPlan& pl) {
   pl.blocks = blocks;
 }
 
-// Weight gradients of n jobs (n <= 16, each d3d_wgrad_group_ok, no two jobs
-// writing the same dw / db) in one grouped launch + one grouped reduce.
-// ws == nullptr: returns the workspace size in floats (nothing launched).
-// Otherwise returns 0, or < 0 on error (nothing launched).
-D3D_API long d3d_wgrad_group(const WgJobDesc* d, int n, float* ws, long ws_floats, hipStream_t st) {
-  if (n < 1 || n > GW_MAX) return -1;
-  for (int i = 0; i < n; ++i)
-    if (d3d_wgrad_group_ok(d + i)) return -2;
-  GwPlan pl;
-  gw_plan(d, n, pl);
-  if (!ws) return pl.ws_floats;
-  if (ws_floats < pl.ws_floats || pl.blocks >= (1L << 31)) return -3;
-  GwTable tab{};
-  GrTable rt{};
+// Jobs split by tile engine: the all-taps halo tile (3x3 on W % 32 == 0) and
+// the per-tap 128 x 128 tile (everything else); one launch each, planned
+// separately (each fills the GPU on its own), one reduce for both.
+struct GwSplit {
+  WgJobDesc hd[GW_MAX], od[GW_MAX];
+  int hidx[GW_MAX], oidx[GW_MAX];
+  int hn = 0, on = 0;
+  GwPlan hp, op;
+  long ws_floats;
+};
+
+static void gw_split_plan(const WgJobDesc* d, int n, GwSplit& S) {
+  for (int i = 0; i < n; ++i) {
+    if (gh_takes(d[i])) {
+      S.hidx[S.hn] = i;
+      S.hd[S.hn++] = d[i];
+    } else {
+      S.oidx[S.on] = i;
+      S.od[S.on++] = d[i];
+    }
+  }
+  S.hp.ws_floats = S.op.ws_floats = 0;
+  S.hp.blocks = S.op.blocks = 0;
+  if (S.hn) gw_plan(S.hd, S.hn, S.hp, true);
+  if (S.on) gw_plan(S.od, S.on, S.op, false);
+  S.ws_floats = S.hp.ws_floats + S.op.ws_floats;
+}
+
+// fills tab (and appends the split jobs to rt) for the jobs of one engine
+static long gw_tables(const WgJobDesc* d, int n, const GwPlan& pl, float* ws, bool halo, GwTable& tab, GrTable& rt,
+                      long& rblk) {
+  tab = GwTable{};
   tab.n = n;
-  long blk = 0, rblk = 0;
+  long blk = 0;
   for (int i = 0; i < n; ++i) {
     GwJob& J = tab.j[i];
     const WgJobDesc& D = d[i];
@@ -796,8 +1089,8 @@ D3D_API long d3d_wgrad_group(const WgJobDesc* d, int n, float* ws, long ws_float
       J.lw = gw_lg2(D.W);
       J.lh = gw_lg2(D.H);
     }
-    J.ncb = cdiv(D.IC, GW_BN);
-    J.nmb = cdiv(D.OC, GW_BM);
+    J.ncb = halo ? D.IC / GH_BN : cdiv(D.IC, GW_BN);
+    J.nmb = halo ? D.OC / GH_BM : cdiv(D.OC, GW_BM);
     J.splits = pl.splits[i];
     J.pps = pl.pps[i];
     J.blk0 = (int)blk;
@@ -823,19 +1116,48 @@ D3D_API long d3d_wgrad_group(const WgJobDesc* d, int n, float* ws, long ws_float
       rblk += Rj.nblk_w + (D.db ? cdiv(D.OC, 64) : 0);
     }
   }
-  if (g_gw_wide) {
-    if (g_gw_pk == 64)
-      hipLaunchKernelGGL(wgrad_grp2_k<64>, dim3((unsigned)blk), dim3(256), 0, st, tab);
+  return blk;
+}
+
+// Weight gradients of n jobs (n <= 16, each d3d_wgrad_group_ok, no two jobs
+// writing the same dw / db) in one grouped launch per tile engine + one
+// grouped reduce.  ws == nullptr: returns the workspace size in floats
+// (nothing launched).  Otherwise returns 0, or < 0 on error (nothing launched).
+D3D_API long d3d_wgrad_group(const WgJobDesc* d, int n, float* ws, long ws_floats, hipStream_t st) {
+  if (n < 1 || n > GW_MAX) return -1;
+  for (int i = 0; i < n; ++i)
+    if (d3d_wgrad_group_ok(d + i)) return -2;
+  GwSplit S;
+  gw_split_plan(d, n, S);
+  if (!ws) return S.ws_floats;
+  if (ws_floats < S.ws_floats || S.hp.blocks >= (1L << 31) || S.op.blocks >= (1L << 31)) return -3;
+  GrTable rt{};
+  long rblk = 0;
+  if (S.hn) {
+    GwTable tab;
+    const long blk = gw_tables(S.hd, S.hn, S.hp, ws, true, tab, rt, rblk);
+    if (g_gh_ns == 3)
+      hipLaunchKernelGGL(wgrad_halo_k<3>, dim3((unsigned)blk), dim3(512), 0, st, tab);
     else
-      hipLaunchKernelGGL(wgrad_grp2_k<32>, dim3((unsigned)blk), dim3(256), 0, st, tab);
-  } else if (g_gw_pk == 64) {
-    hipLaunchKernelGGL((wgrad_grp_k<64, 2>), dim3((unsigned)blk), dim3(256), 0, st, tab);
-  } else if (g_gw_ns == 4) {
-    hipLaunchKernelGGL((wgrad_grp_k<32, 4>), dim3((unsigned)blk), dim3(256), 0, st, tab);
-  } else if (g_gw_ns == 3) {
-    hipLaunchKernelGGL((wgrad_grp_k<32, 3>), dim3((unsigned)blk), dim3(256), 0, st, tab);
-  } else {
-    hipLaunchKernelGGL((wgrad_grp_k<32, 2>), dim3((unsigned)blk), dim3(256), 0, st, tab);
+      hipLaunchKernelGGL(wgrad_halo_k<2>, dim3((unsigned)blk), dim3(512), 0, st, tab);
+  }
+  if (S.on) {
+    GwTable tab;
+    const long blk = gw_tables(S.od, S.on, S.op, ws + S.hp.ws_floats, false, tab, rt, rblk);
+    if (g_gw_wide) {
+      if (g_gw_pk == 64)
+        hipLaunchKernelGGL(wgrad_grp2_k<64>, dim3((unsigned)blk), dim3(256), 0, st, tab);
+      else
+        hipLaunchKernelGGL(wgrad_grp2_k<32>, dim3((unsigned)blk), dim3(256), 0, st, tab);
+    } else if (g_gw_pk == 64) {
+      hipLaunchKernelGGL((wgrad_grp_k<64, 2>), dim3((unsigned)blk), dim3(256), 0, st, tab);
+    } else if (g_gw_ns == 4) {
+      hipLaunchKernelGGL((wgrad_grp_k<32, 4>), dim3((unsigned)blk), dim3(256), 0, st, tab);
+    } else if (g_gw_ns == 3) {
+      hipLaunchKernelGGL((wgrad_grp_k<32, 3>), dim3((unsigned)blk), dim3(256), 0, st, tab);
+    } else {
+      hipLaunchKernelGGL((wgrad_grp_k<32, 2>), dim3((unsigned)blk), dim3(256), 0, st, tab);
+    }
   }
   if (rt.n > 0) hipLaunchKernelGGL(wgrad_grp_reduce_k, dim3((unsigned)rblk), dim3(256), 0, st, rt);
   const int e = (int)hipGetLastError();
@@ -843,14 +1165,20 @@ D3D_API long d3d_wgrad_group(const WgJobDesc* d, int n, float* ws, long ws_float
 }
 
 // Plan introspection for tests / tools: splits and pixels per split of job i.
+// (blocks: both launches' blocks; engine[i], when given: 1 = halo tile)
 D3D_API int d3d_wgrad_group_plan(const WgJobDesc* d, int n, int* splits, int* pps, long* blocks) {
   if (n < 1 || n > GW_MAX) return -1;
-  GwPlan pl;
-  gw_plan(d, n, pl);
-  for (int i = 0; i < n; ++i) {
-    splits[i] = pl.splits[i];
-    pps[i] = pl.pps[i];
+  GwSplit S;
+  gw_split_plan(d, n, S);
+  for (int i = 0; i < S.hn; ++i) {
+    splits[S.hidx[i]] = S.hp.splits[i];
+    pps[S.hidx[i]] = S.hp.pps[i];
   }
-  if (blocks) *blocks = pl.blocks;
+  for (int i = 0; i < S.on; ++i) {
+    splits[S.oidx[i]] = S.op.splits[i];
+    pps[S.oidx[i]] = S.op.pps[i];
+  }
+  if (blocks) *blocks = S.hp.blocks + S.op.blocks;
   return 0;
 }
+D3D_API int d3d_wgrad_group_engine(const WgJobDesc* d) { return gh_takes(*d) ? 1 : 0; }

@@ -389,29 +389,36 @@ class ResGradSlot:
     normally (``consumed``), so any order stays correct.  The deposit is
     ``scale * g`` kept unscaled (the kernel applies the scale), so the
     branch's own backward never materialises its scaled output gradient."""
-    __slots__ = ("g", "scale", "consumed")
+    __slots__ = ("g", "scale", "g2", "scale2", "consumed")
 
     def __init__(self):
-        self.g = None
-        self.scale = 1.0
+        self.g = self.g2 = None
+        self.scale = self.scale2 = 1.0
         self.consumed = False
 
     def deposit(self, g: torch.Tensor, scale: float = 1.0) -> bool:
+        """Two deposits ride into the kernel (a block's residual branch and a
+        decoder skip consumer of the same tensor); a third is folded in fp32."""
         if self.consumed:
             return False
         if self.g is None:
             self.g, self.scale = g, float(scale)
+        elif self.g2 is None:
+            self.g2, self.scale2 = g, float(scale)
         else:
             self.g, self.scale = (self.g.float() * self.scale + g.float() * scale).to(g.dtype), 1.0
         return True
 
     def take(self):
-        g, sc = self.g, self.scale
-        self.g, self.scale, self.consumed = None, 1.0, True
-        return g, sc
+        r = (self.g, self.scale, self.g2, self.scale2)
+        self.g = self.g2 = None
+        self.scale = self.scale2 = 1.0
+        self.consumed = True
+        return r
 
 
-def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None, dres=None, dres_scale=1.0):
+def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None, dres=None, dres_scale=1.0,
+            dres2=None, dres2_scale=1.0):
     N, H, W, C1 = x.shape
     C = C1 + (x2.shape[-1] if x2 is not None else 0)
     P = H * W
@@ -432,7 +439,7 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None,
                           b.data_ptr(), N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), dg.data_ptr(),
                           db.data_ptr(), cp.data_ptr(), gp.data_ptr(), coef.data_ptr(), int(direct), int(ssld),
                           _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), _ptr(dx2), C1, _ptr(dres),
-                          float(dres_scale), _st()),
+                          float(dres_scale), _ptr(dres2), float(dres2_scale), _st()),
          "gn_bwd")
     if x2 is not None:
         dx = (dx, dx2)
@@ -443,7 +450,8 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None,
     return dx, dss, dg, db
 
 
-def _gn_bwd_parts(mode, x, dy, stats, w, b, G, parts, x2=None, dres=None, dres_scale=1.0):
+def _gn_bwd_parts(mode, x, dy, stats, w, b, G, parts, x2=None, dres=None, dres_scale=1.0, dres2=None,
+                  dres2_scale=1.0):
     """GroupNorm backward apply over the consumer conv's epilogue partials
     (no reduce pass)."""
     _, grp, nparts, _ = parts
@@ -461,7 +469,7 @@ def _gn_bwd_parts(mode, x, dy, stats, w, b, G, parts, x2=None, dres=None, dres_s
     _chk(_lib.d3d_gn_bwd_apply_parts(mode, x.data_ptr(), dy.data_ptr(), stats.data_ptr(), w.data_ptr(), b.data_ptr(),
                                      N, H * W, C, G, dx.data_ptr(), dg.data_ptr(), db.data_ptr(), chan.data_ptr(),
                                      grp.data_ptr(), int(nparts), int(direct), _ptr(x2), _ptr(dx2), C1, _ptr(dres),
-                                     float(dres_scale), _st()), "gn_bwd_apply_parts")
+                                     float(dres_scale), _ptr(dres2), float(dres2_scale), _st()), "gn_bwd_apply_parts")
     if x2 is not None:
         dx = (dx, dx2)
     if direct:
@@ -492,15 +500,19 @@ class _GroupNorm(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, b, stats = ctx.saved_tensors
         G, mode = ctx.cfg
-        dres, rsc = ctx.slot.take() if ctx.slot is not None else (None, 1.0)
+        dres, rsc, dres2, rsc2 = ctx.slot.take() if ctx.slot is not None else (None, 1.0, None, 1.0)
         if dres is not None:
             dres = dres.reshape(x.shape).contiguous()
+        if dres2 is not None:
+            dres2 = dres2.reshape(x.shape).contiguous()
         dy = dy.contiguous()
         parts = ctx.gnb.take(dy) if ctx.gnb is not None else None
         if parts is not None:
-            dx, dg, db = _gn_bwd_parts(mode, x, dy, stats, w, b, G, parts, dres=dres, dres_scale=rsc)
+            dx, dg, db = _gn_bwd_parts(mode, x, dy, stats, w, b, G, parts, dres=dres, dres_scale=rsc, dres2=dres2,
+                                       dres2_scale=rsc2)
         else:
-            dx, _, dg, db = _gn_bwd(mode, x, dy, None, stats, w, b, G, 0.0, 0, dres=dres, dres_scale=rsc)
+            dx, _, dg, db = _gn_bwd(mode, x, dy, None, stats, w, b, G, 0.0, 0, dres=dres, dres_scale=rsc,
+                                    dres2=dres2, dres2_scale=rsc2)
         return dx, dg, db, None, None, None, None
 
 
@@ -537,6 +549,10 @@ class _CatGNDense(torch.autograd.Function):
         ctx.save_for_backward(a, b, gw, gb, stats, dw)
         ctx.cfg = (groups, db is not None)
         ctx.params = (dw, db)
+        # the skip's other consumer (the next encoder block's GroupNorm, whose
+        # backward runs after this one) takes b's gradient inside its apply
+        # kernel: no autograd bf16 add of the two gradients
+        ctx.bslot = getattr(b, "_d3d_res_slot", None)
         ctx.gnb = None
         if any(ctx.needs_input_grad[:4]):
             ctx.gnb = _GnbHolder(a, b, C1, stats, gw, gb, groups, 1)
@@ -609,6 +625,8 @@ class _CatGNDense(torch.autograd.Function):
             job()
             gW = dWt.view(dwp.shape)
             gB = dbt
+        if ctx.bslot is not None and ctx.bslot.deposit(db_in):
+            db_in = None
         return da, db_in, dgw, dgb, gW, gB, None, None
 
 
@@ -792,6 +810,9 @@ if os.environ.get("D3D_WGRAD_GROUP_WIDE"):             # A/B knob: 128 x 256 (1)
     _lib.d3d_wgrad_group_wide(int(os.environ["D3D_WGRAD_GROUP_WIDE"]))
 if os.environ.get("D3D_WGRAD_GROUP_NS"):               # A/B knob: LDS ring stages (2-4)
     _lib.d3d_wgrad_group_stages(int(os.environ["D3D_WGRAD_GROUP_NS"]))
+if os.environ.get("D3D_WGRAD_HALO"):                   # A/B knob "on[,blocks[,stages]]": all-taps halo tiles
+    _hv = [int(v) for v in os.environ["D3D_WGRAD_HALO"].split(",")] + [0, 0]
+    _lib.d3d_wgrad_group_halo(_hv[0], _hv[1], _hv[2])
 
 
 def wgrad_job(dy, x, OC, IC, N, H, W, taps, dw, db=None, scale=1.0, accumulate=True, x2=None, C1=0):

@@ -604,6 +604,9 @@ WG_JOBS = [
     (2048, 1, 1, 512, 1536, 1, 0, True),     # 1x1 projection
     (8192, 1, 1, 768, 256, 1, 256, True),    # 1x1 over the virtual concat [x | x2]
     (32, 32, 32, 256, 256, 9, 0, True),
+    (4, 16, 64, 192, 128, 9, 128, False),    # halo tiles over the virtual concat, non-square, 3 channel tiles
+    (1, 32, 32, 64, 256, 9, 0, True),        # halo tile, small: unsplit OIHW epilogue
+    (1, 128, 128, 128, 128, 9, 0, True),     # 128-wide image: four 32-pixel steps per row
 ]
 
 
@@ -617,17 +620,21 @@ def _wg_ref(g, x, taps):
     return dw.reshape(OC, IC, 9)
 
 
-@pytest.mark.parametrize("wide", [1, 0])
-@pytest.mark.parametrize("pk,blocks,minpix", [(32, 512, 512), (64, 512, 512), (32, 4096, 64)])
-def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide):
-    """Grouped weight gradients (wgrad_group.hip): one launch over a mixed
-    batch of 3x3 / 1x1 / virtual-concat jobs (+ the grouped slab reduce for
-    the split ones) == the fp32 torch weight gradients, accumulated onto the
-    existing gradient with the scale, bias sums included; bitwise equal on a
-    re-run.  The last case plans many more splits (small blocks)."""
+@pytest.mark.parametrize("pk,blocks,minpix,wide,halo,ns", [
+    (32, 512, 512, 0, 1, 2), (32, 512, 512, 0, 0, 2), (64, 512, 512, 0, 1, 2), (32, 4096, 64, 0, 1, 2),
+    (32, 4096, 64, 0, 0, 2), (32, 512, 512, 1, 0, 2), (32, 512, 512, 0, 1, 3), (32, 64, 512, 0, 1, 2)])
+def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
+    """Grouped weight gradients (wgrad_group.hip): the per-tap 128 x 128 tile
+    launch and the all-taps halo tile launch (3x3 jobs on W % 32 == 0 images)
+    over a mixed batch of 3x3 / 1x1 / virtual-concat jobs (+ the grouped slab
+    reduce for the split ones) == the fp32 torch weight gradients, accumulated
+    onto the existing gradient with the scale, bias sums included; bitwise
+    equal on a re-run.  blocks=4096 plans many more splits (small blocks),
+    blocks=64 leaves the big halo jobs nearly unsplit."""
     torch.manual_seed(5)
     H._lib.d3d_wgrad_group_cfg(blocks, pk, minpix)
     H._lib.d3d_wgrad_group_wide(wide)
+    H._lib.d3d_wgrad_group_halo(halo, blocks, ns)
     try:
         jobs, refs, outs = [], [], []
         for (N, Hh, W, IC, OC, taps, C1, bias) in WG_JOBS:
@@ -652,6 +659,10 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide):
         sp = (ctypes.c_int * len(jobs))()
         pp = (ctypes.c_int * len(jobs))()
         H._lib.d3d_wgrad_group_plan((H._WgJob * len(jobs))(*jobs), len(jobs), sp, pp, None)
+        eng = [H._lib.d3d_wgrad_group_engine(ctypes.byref(j)) for j in jobs]
+        want = [int(bool(halo) and t == 9 and W % 32 == 0 and OC % 128 == 0 and IC % 64 == 0)
+                for (N, Hh, W, IC, OC, t, C1, b) in WG_JOBS]
+        assert eng == want, (eng, want)
         H.wgrad_group_run(jobs)
         torch.cuda.synchronize()
         first = []
@@ -663,6 +674,9 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide):
         assert max(sp) > 1, list(sp)                          # split-K slabs + grouped reduce exercised
         if blocks <= 1024:
             assert min(sp) == 1, list(sp)                     # ... and the direct OIHW epilogue
+        if halo:
+            hs = [s_ for s_, e in zip(sp, eng) if e]
+            assert (blocks > 1024 or min(hs) == 1) and (blocks < 512 or max(hs) > 1), hs
         for (_, _, dw0, db0), (dw, db, _) in zip(refs, outs):  # re-run: bitwise
             dw.copy_(dw0)
             if db is not None:
@@ -676,6 +690,7 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide):
     finally:
         H._lib.d3d_wgrad_group_cfg(512, 32, 512)
         H._lib.d3d_wgrad_group_wide(0)
+        H._lib.d3d_wgrad_group_halo(1, 512, 2)
 
 
 @pytest.mark.parametrize("micro", [2, 0])
@@ -1031,10 +1046,12 @@ def test_graph_step_bitwise_deterministic():
             assert torch.equal(a, b), (a - b).abs().max().item()
 
 
-@pytest.mark.parametrize("kind", ["conv_res", "linear_res", "nin_input"])
+@pytest.mark.parametrize("kind", ["conv_res", "linear_res", "nin_input", "skip_concat"])
 def test_residual_grad_slot(H, kind):
     """ResGradSlot: the residual branch's gradient of x handed to the
-    GroupNorm backward kernel == autograd summing the two branches."""
+    GroupNorm backward kernel == autograd summing the two branches.
+    skip_concat: x also feeds a decoder-style virtual concat [y | x]
+    (cat_gn_silu_dense), whose gradient of x is the slot's second deposit."""
     torch.manual_seed(5)
     C, Co = 128, (256 if kind == "nin_input" else 128)
     x = torch.randn(4, 16, 16, C, device=DEV).to(BF).requires_grad_(True)
@@ -1044,9 +1061,16 @@ def test_residual_grad_slot(H, kind):
     wl = torch.randn(Co, C, device=DEV) / math.sqrt(C)
     bl = torch.randn(Co, device=DEV) * 0.1
     go = torch.randn(4, 16, 16, Co, device=DEV).to(BF)
+    gam2 = torch.rand(2 * C, device=DEV) + 0.5
+    bet2 = torch.randn(2 * C, device=DEV) * 0.1
+    wd = torch.randn(C, 2 * C, device=DEV) / math.sqrt(2 * C)
+    bd = torch.randn(C, device=DEV) * 0.1
+    go2 = torch.randn(4, 16, 16, 2 * C, device=DEV)
+    go3 = torch.randn(4, 16, 16, C, device=DEV)
 
     def run(use):
         x.grad = None
+        x.__dict__.pop("_d3d_res_slot", None)
         slot = H.ResGradSlot() if use else None
         if kind == "conv_res":
             h = H.group_norm(x, gam, bet, 32, 1e-5, True, slot)
@@ -1054,10 +1078,20 @@ def test_residual_grad_slot(H, kind):
         elif kind == "linear_res":
             h = H.group_norm(x, gam, bet, 32, 1e-5, False, slot)
             y = H.linear(h, wl, bl, residual=x, out_scale=1 / math.sqrt(2), res_slot=slot)
-        else:
+        elif kind == "nin_input":
             h = H.group_norm(x, gam, bet, 32, 1e-5, True, slot)
             s = H.linear(x, wl, bl, in_slot=slot)
             y = H.conv3x3(h, w, None, residual=s, out_scale=1 / math.sqrt(2))
+        else:
+            h = H.group_norm(x, gam, bet, 32, 1e-5, True, slot)
+            y1 = H.conv3x3(h, w, None, residual=x, out_scale=1 / math.sqrt(2), res_slot=slot)
+            if use:
+                x._d3d_res_slot = slot
+            hc, sk = H.cat_gn_silu_dense(y1, x, gam2, bet2, wd, bd, 32)
+            ((hc.float() * go2).sum() + (sk.float() * go3).sum()).backward()
+            if use:
+                assert slot.consumed and slot.g is None and slot.g2 is None
+            return x.grad.float().clone()
         y.backward(go)
         if use:
             assert slot.consumed and slot.g is None
