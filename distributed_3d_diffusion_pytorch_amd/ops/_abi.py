@@ -28,6 +28,7 @@ SIGNATURES = {
     "d3d_conv_s64_cfg": [I],
     "d3d_conv_res_cfg": [I],
     # elementwise.hip
+    "d3d_period_sum": [P, P, I, L, P],
     "d3d_silu": [P, P, L, P],
     "d3d_dsilu": [P, P, P, L, P],
     "d3d_avgpool2": [P, P, I, I, I, I, I, P],

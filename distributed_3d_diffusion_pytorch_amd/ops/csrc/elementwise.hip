@@ -387,6 +387,41 @@ __global__ void diff_loss_bwd_k(const bf16* __restrict__ y, const float* __restr
 }
 }  // namespace
 
+// Gradient of a batch-broadcast residual (the conditioning convs' learned
+// per-frame embedding, added to every example with period 2, models/xunet.py
+// levels()): out[q] = sum_r in[r][q] over R repeats of a QM-element block,
+// bf16 in / out, fp32 accumulation in a fixed order.  One 16-byte vector per
+// lane, four repeats in flight (replaces a torch reduction + cast).
+namespace {
+__global__ void __launch_bounds__(256) period_sum_k(const bf16* __restrict__ in, bf16* __restrict__ out, int R,
+                                                    long nvec) {
+  const long i = blockIdx.x * 256L + threadIdx.x;
+  if (i >= nvec) return;
+  const long stride = nvec * 8;
+  const bf16* p = in + i * 8;
+  f32x8 a = {};
+  int r = 0;
+  for (; r + 4 <= R; r += 4) {
+    const f32x8 v0 = ld8(p + r * stride), v1 = ld8(p + (r + 1) * stride), v2 = ld8(p + (r + 2) * stride),
+                v3 = ld8(p + (r + 3) * stride);
+    a += v0;
+    a += v1;
+    a += v2;
+    a += v3;
+  }
+  for (; r < R; ++r) a += ld8(p + r * stride);
+  st8(out + i * 8, a);
+}
+}  // namespace
+
+D3D_API int d3d_period_sum(const void* in, void* out, int R, long QM, hipStream_t st) {
+  if (R < 1 || QM % 8) return (int)hipErrorInvalidValue;
+  const long nvec = QM / 8;
+  hipLaunchKernelGGL(period_sum_k, dim3((unsigned)((nvec + 255) / 256)), dim3(256), 0, st, (const bf16*)in,
+                     (bf16*)out, R, nvec);
+  return (int)hipGetLastError();
+}
+
 D3D_API int d3d_silu(const void* x, void* y, long n, hipStream_t st) {
   hipLaunchKernelGGL(silu_k, dim3(ew_grid(n / 8)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, n / 8);
   return (int)hipGetLastError();

@@ -101,6 +101,7 @@ struct GrJob {
   float* db;
   int OC, IC, taps, splits, blk0, nblk_w, acc;
   float scale;
+  int flat, pad_;                 // flat: slabs already in OIHW order (halo tiles): a plain sum over splits
 };
 struct GrTable {
   int n, pad_;
@@ -589,20 +590,21 @@ __global__ void __launch_bounds__(256, 2) wgrad_grp2_k(GwTable tab) {
 }
 
 // ---------------------------------------------------------- halo tiles ----
-// 3x3 stride-1 jobs on images W % 32 == 0 (the 64x64 / 32x32 levels, ~80 % of
-// the weight-gradient FLOPs): one block = 128 output channels x 64 input
+// 3x3 stride-1 jobs (power-of-two images, W >= 8): one block = 128 output channels x 64 input
 // channels x ALL NINE taps of one pixel split.  Eight waves (two per SIMD);
 // wave (wm, wn) owns output channels 64wm.. +63 x input channels 16wn.. +15 x
 // the nine taps (4 x 9 = 36 MFMA 16x16x32 tiles, 144 accumulator registers).
-// A 32-pixel K-step (half or one image row) stages the dY rows [32][128 co]
-// and the input WINDOW [3 rows][34 px][64 ci] -- the step's pixels with the
-// one-pixel border around them, zero-filled outside the image -- so the B
-// fragment of tap (kh, kw) is window rows kh*34 + kw + k: one window feeds the
-// nine taps, and the step's dY fragments are read once for all nine.  Per MFMA
+// A 32-pixel K-step (half / one row at W >= 32, 2 / 4 rows at W = 16 / 8)
+// stages the dY rows [32][128 co] and the input WINDOW [RR + 2 rows][Wm + 2
+// px][64 ci] (Wm = min(W, 32), RR = 32 / Wm image rows per step) -- the step's
+// pixels with the one-pixel border around them, zero-filled outside the image
+// -- so the B fragment of tap (kh, kw) at step pixel k is window row
+// f(k) + kh*(Wm + 2) + kw, f(k) = (k / Wm)(Wm + 2) + k % Wm: one window feeds
+// the nine taps, and the step's dY fragments are read once for all nine.  Per MFMA
 // that is 0.72 transposed LDS reads and 0.07 KB of DMA, against 1.0 and 0.25 KB
 // for the per-tap 128 x 128 tile above (which re-reads dY and X once per tap).
 constexpr int GH_BM = 128, GH_BN = 64, GH_PK = 32, GH_WR = 34;
-constexpr int GH_BROWS = 128;                          // window rows, 3 x 34 = 102 padded to 16 DMAs of 8
+constexpr int GH_BROWS = 128;                          // window rows (<= 3 x 34 = 102) padded to 16 DMAs of 8
 constexpr int GH_STAGE = GH_PK * GH_BM + GH_BROWS * GH_BN;   // bf16: 4096 (dY) + 8192 (window) = 24 KB
 
 // 16-byte chunk swizzle of the 128-byte window rows: the 8 consecutive rows a
@@ -612,8 +614,8 @@ __device__ __forceinline__ int gh_swz(int row) { return 2 * ((row >> 1) & 3); }
 
 __device__ __forceinline__ void gh_issue(bf16* sA, bf16* sB, const bf16* __restrict__ dY, const bf16* __restrict__ I,
                                          long in_elems, long p0, long p_end, int OC, int IC, int OH, int OW, int lw,
-                                         int wave, const unsigned* aoff, const unsigned* boff, const unsigned* bfl,
-                                         bool on) {
+                                         int Wm, int RR, int wave, const unsigned* aoff, const unsigned* boff,
+                                         const unsigned* bfl, bool on) {
   typedef __attribute__((address_space(3))) void lds_void;
   const __amdgpu_buffer_rsrc_t rA = gw_rsrc(dY + p0 * OC, on ? (p_end - p0) * OC * 2 : 0);
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sA + wave * 4 * GH_BM), 16, aoff[0], 0, 0, 0);
@@ -622,8 +624,8 @@ __device__ __forceinline__ void gh_issue(bf16* sA, bf16* sB, const bf16* __restr
   const long pb = p0 - OW - 1;
   const __amdgpu_buffer_rsrc_t rB = gw_rsrc(I + pb * IC, on ? (in_elems - pb * IC) * 2 : 0);
   const int x0 = (int)(p0 & (OW - 1)), y = (int)((p0 >> lw) & (OH - 1));
-  const unsigned bad = 1u | (y == 0 ? 2u : 0u) | (y == OH - 1 ? 4u : 0u) | (x0 == 0 ? 8u : 0u) |
-                       (x0 + GH_PK == OW ? 16u : 0u);
+  const unsigned bad = 1u | (y == 0 ? 2u : 0u) | (y + RR == OH ? 4u : 0u) | (x0 == 0 ? 8u : 0u) |
+                       (x0 + Wm == OW ? 16u : 0u);
 #pragma unroll
   for (int j = 0; j < 2; ++j)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * 2 + j) * 8 * GH_BN), 16,
@@ -660,6 +662,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
   const long in_elems = P * IC;
   const long p_begin = (long)split * J.pps;
   const long p_end = p_begin + J.pps < P ? p_begin + J.pps : P;
+  const int Wm = OW < GH_PK ? OW : GH_PK, RR = GH_PK / Wm, WR = Wm + 2, NR = RR + 2;
 
   unsigned aoff[1], boff[2], bfl[2];
   {
@@ -672,31 +675,34 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int wr = (wave * 2 + j) * 8 + (lane >> 3);
-      const int kh = wr / GH_WR, px = wr - kh * GH_WR;
+      const int kh = wr / WR, px = wr - kh * WR;
       const int chunk = (lane & 7) ^ gh_swz(wr);
-      const bool valid = wr < 3 * GH_WR;
+      const bool valid = wr < NR * WR;
       boff[j] = valid ? (unsigned)(((kh * OW + px) * IC + ci0 + chunk * 8) * 2) : 0u;
-      bfl[j] = (valid ? 0u : 1u) | (kh == 0 ? 2u : 0u) | (kh == 2 ? 4u : 0u) | (px == 0 ? 8u : 0u) |
-               (px == GH_WR - 1 ? 16u : 0u);
+      bfl[j] = (valid ? 0u : 1u) | (kh == 0 ? 2u : 0u) | (kh == NR - 1 ? 4u : 0u) | (px == 0 ? 8u : 0u) |
+               (px == WR - 1 ? 16u : 0u);
     }
   }
   // transposed-read offsets (elements in a stage): lane (g, q, pc) reads K row
   // 4g + q (and + 16), 8-element chunk pc >> 1 of its 16 columns, half pc & 1
-  int la[4], lb[9];
+  int la[4], lb[9], lbh[9];
   {
     const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
     const int kr = 4 * g + q, x7 = 2 * (kr & 7);
 #pragma unroll
     for (int i = 0; i < 4; ++i) la[i] = kr * GH_BM + (((wm * 8 + 2 * i + (pc >> 1)) ^ x7) << 3) + (pc & 1) * 4;
+    const int f0 = (kr / Wm) * WR + kr % Wm, f1 = ((kr + 16) / Wm) * WR + (kr + 16) % Wm;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const int row = (t / 3) * GH_WR + (t % 3) + kr;
-      lb[t] = GH_PK * GH_BM + row * GH_BN + (((2 * wn + (pc >> 1)) ^ gh_swz(row)) << 3) + (pc & 1) * 4;
+      const int r0 = f0 + (t / 3) * WR + (t % 3), r1 = f1 + (t / 3) * WR + (t % 3);
+      lb[t] = GH_PK * GH_BM + r0 * GH_BN + (((2 * wn + (pc >> 1)) ^ gh_swz(r0)) << 3) + (pc & 1) * 4;
+      lbh[t] = GH_PK * GH_BM + r1 * GH_BN + (((2 * wn + (pc >> 1)) ^ gh_swz(r1)) << 3) + (pc & 1) * 4;
     }
   }
   auto issue = [&](long p0, int stage, bool on) {
     bf16* sA = smem + stage * GH_STAGE;
-    gh_issue(sA, sA + GH_PK * GH_BM, dY, I, in_elems, p0, p_end, OC, IC, OH, OW, lw, wave, aoff, boff, bfl, on);
+    gh_issue(sA, sA + GH_PK * GH_BM, dY, I, in_elems, p0, p_end, OC, IC, OH, OW, lw, Wm, RR, wave, aoff, boff, bfl,
+             on);
   };
 
   f32x4 acc[4][9];
@@ -714,7 +720,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
   // while tap t's eight MFMAs run (register budget: 288 accumulators)
   auto rd_b = [&](const bf16* s, int t) {
     gs16x4 lo = gw_tr_asm(s + lb[t]);
-    gs16x4 hi = gw_tr_asm(s + lb[t] + 16 * GH_BN);
+    gs16x4 hi = gw_tr_asm(s + lbh[t]);
     gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, v);
   };
@@ -805,15 +811,16 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
       J.bslab[((long)split * 2 + 1) * OC + cw + i * 16 + fr] = 0.f;
     }
   }
-  const long KW = 9L * ICt;
-  float* slab = J.slab + (long)split * OC * KW;
+  // slab in OIHW order ([split][co][ci][tap]): each lane's nine taps are
+  // contiguous, and the reduce is a plain coalesced sum over the splits
+  float* slab = J.slab + (long)split * OC * 9L * ICt;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float* d = slab + (long)(cw + i * 16 + fq * 4 + e) * KW + cig;
+      float* d = slab + ((long)(cw + i * 16 + fq * 4 + e) * ICt + cig) * 9;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) d[(long)t * ICt] = acc[i][t][e];
+      for (int t = 0; t < 9; ++t) d[t] = acc[i][t][e];
     }
 }
 
@@ -849,6 +856,17 @@ __global__ void __launch_bounds__(256) wgrad_grp_reduce_k(GrTable tab) {
       const float v = (((red[0][0][c] + red[1][0][c]) + red[2][0][c]) + red[3][0][c]) * J.scale;
       J.db[co] = J.acc ? J.db[co] + v : v;
     }
+    return;
+  }
+  if (J.flat) {                                    // OIHW slabs: 1024 consecutive floats per block
+    const long total = (long)OC * IC * taps;
+    const long e0 = (long)b * 1024 + tid * 4;
+    if (e0 >= total) return;
+    f32x4 a = *reinterpret_cast<const f32x4*>(J.slab + e0);
+    for (int sp = 1; sp < splits; ++sp) a += *reinterpret_cast<const f32x4*>(J.slab + (long)sp * total + e0);
+    a *= J.scale;
+    f32x4* d = reinterpret_cast<f32x4*>(J.dw + e0);
+    *d = J.acc ? *d + a : a;
     return;
   }
   const int ncg = (IC + 63) / 64;
@@ -902,7 +920,10 @@ static int g_gw_minpix = 512;      // lower bound of the pixels per block
 // waiting on the ring's DMAs (profiles/r4/kb_ns*.jsonl, b16_ns_blocks_ab.txt)
 static int g_gw_ns = 2;
 static int g_gw_wide = 0;          // 1: 128 x 256 chunk-pair tiles (wgrad_grp2_k; measured slower: profiles/r4/kb_w1_*), 0: 128 x 128
-static int g_gh_on = 1;            // 3x3 jobs on W % 32 == 0 images -> wgrad_halo_k
+// 3x3 jobs -> wgrad_halo_k: 0 never; 1 at W >= 32, and at W = 16 with >= 32768
+// pixels (the per-tap tile won on the small 16x16 / 8x8 jobs: fewer pixels per
+// all-taps block, profiles/r4/halo_wgrad/README.txt); 2 at any W >= 8 (tests)
+static int g_gh_on = 1;
 // target blocks per halo launch: one block per CU runs at a time, so the
 // planner fits the batch into at most this many blocks rounded DOWN to whole
 // rounds of the CU count -- 522 blocks on 256 CUs ran as three rounds, the last
@@ -927,7 +948,7 @@ D3D_API int d3d_wgrad_group_stages(int ns) {
 }
 // halo (all-taps) tiles for 3x3 jobs: on (0/1), target blocks, ring stages (2/3); < 0 keeps a value
 D3D_API int d3d_wgrad_group_halo(int on, int blocks, int ns) {
-  if (on >= 0) g_gh_on = on ? 1 : 0;
+  if (on >= 0) g_gh_on = on > 2 ? 2 : on;
   if (blocks > 0) g_gh_blocks = blocks;
   if (ns == 2 || ns == 3) g_gh_ns = ns;
   return 0;
@@ -961,8 +982,12 @@ struct GwPlan {
 
 // the all-taps halo tile takes the job (block-shape and alignment conditions)
 static bool gh_takes(const WgJobDesc& d) {
-  return g_gh_on && d.taps == 9 && d.W >= GH_PK && d.W % GH_PK == 0 && d.OC % GH_BM == 0 && d.IC % GH_BN == 0 &&
-         (!d.x2 || d.C1 % GH_BN == 0) && (long)(2 * d.W + GH_WR) * d.IC * 2 < (1L << 30);
+  const int Wm = d.W < GH_PK ? d.W : GH_PK;
+  const long P = (long)d.N * d.H * d.W;
+  if (g_gh_on == 1 && d.W < 32 && !(d.W == 16 && P >= 32768)) return false;
+  return g_gh_on && d.taps == 9 && d.W >= 8 && gw_lg2(d.W) >= 0 && gw_lg2(d.H) >= 0 && d.H >= GH_PK / Wm &&
+         d.OC % GH_BM == 0 && d.IC % GH_BN == 0 && (!d.x2 || d.C1 % GH_BN == 0) &&
+         (long)(GH_PK / Wm + 2) * d.W * d.IC * 2 < (1L << 30);
 }
 
 // halo: every job of d is a halo job (tiles = 128 x 64 x 9 taps)
@@ -1110,7 +1135,8 @@ static long gw_tables(const WgJobDesc* d, int n, const GwPlan& pl, float* ws, bo
       Rj.taps = D.taps;
       Rj.splits = pl.splits[i];
       Rj.blk0 = (int)rblk;
-      Rj.nblk_w = D.OC * cdiv(D.IC, 64);
+      Rj.flat = halo ? 1 : 0;
+      Rj.nblk_w = halo ? (int)cdiv((long)D.OC * D.IC * D.taps, 1024L) : D.OC * cdiv(D.IC, 64);
       Rj.acc = D.acc;
       Rj.scale = D.scale;
       rblk += Rj.nblk_w + (D.db ? cdiv(D.OC, 64) : 0);

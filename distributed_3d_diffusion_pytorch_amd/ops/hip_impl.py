@@ -971,7 +971,7 @@ class _Conv(torch.autograd.Function):
         dres = None
         if has_res and ctx.needs_input_grad[4]:
             if res_period:
-                dres = g.reshape(N // res_period, res_period, *g.shape[1:]).sum(0, dtype=F32).to(g.dtype)
+                dres = _period_sum(g, res_period)
             elif slot is None or not slot.deposit(g, ks):
                 assert ks == 1.0            # (lazy only when the slot takes it)
                 dres = g
@@ -1028,6 +1028,20 @@ def _tap_coef(IH, IW, OH, OW, stride, device):
         m = torch.tensor(rows, dtype=F32).to(device)
         _TAPCOEF[key] = m
     return m
+
+
+def _period_sum(g: torch.Tensor, period: int) -> torch.Tensor:
+    """Gradient of a residual broadcast over the batch with the given period:
+    [N, ...] -> [period, ...], summed over the N / period repeats (bf16, fp32
+    accumulation; elementwise.hip period_sum_k)."""
+    g = g.contiguous()
+    N = g.shape[0]
+    out = torch.empty((period,) + tuple(g.shape[1:]), dtype=g.dtype, device=g.device)
+    qm = out.numel()
+    if g.dtype != BF16 or qm % 8 or N % period:
+        return g.reshape(N // period, period, *g.shape[1:]).sum(0, dtype=F32).to(g.dtype)
+    _chk(_lib.d3d_period_sum(g.data_ptr(), out.data_ptr(), N // period, qm, _st()), "period_sum")
+    return out
 
 
 def _sgemm(A, B, C, M, N, K, batch, sa, sb, sc, alpha: float = 1.0, beta: float = 0.0) -> None:
@@ -1122,8 +1136,7 @@ class _CondConv(torch.autograd.Function):
         drb = per if has_rb else None
         dres = None
         if has_res:
-            dres = g if not res_period else \
-                g.reshape(N // res_period, res_period, *g.shape[1:]).sum(0, dtype=F32).to(g.dtype)
+            dres = g if not res_period else _period_sum(g, res_period)
         return None, None, dW, db, drb, dres, None, None, None
 
 

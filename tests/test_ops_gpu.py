@@ -599,7 +599,8 @@ def test_wgrad_tn_matches_fp32(H, P, M, N, ldy, splits):
 WG_JOBS = [
     (32, 64, 64, 128, 128, 9, 0, True),      # 64x64 level at 16 examples / GPU: split-K
     (32, 8, 8, 512, 512, 9, 0, True),        # 8x8 level: unsplit, direct OIHW epilogue
-    (4, 16, 16, 384, 256, 9, 0, False),
+    (4, 16, 16, 384, 256, 9, 0, False),      # halo tile at W = 16: two image rows per 32-pixel step
+    (2, 8, 8, 128, 128, 9, 0, True),         # halo tile at W = 8, four rows per step, unsplit
     (6, 8, 16, 72, 200, 9, 0, True),         # channel tails (partial tiles), non-square image
     (2048, 1, 1, 512, 1536, 1, 0, True),     # 1x1 projection
     (8192, 1, 1, 768, 256, 1, 256, True),    # 1x1 over the virtual concat [x | x2]
@@ -621,8 +622,9 @@ def _wg_ref(g, x, taps):
 
 
 @pytest.mark.parametrize("pk,blocks,minpix,wide,halo,ns", [
-    (32, 512, 512, 0, 1, 2), (32, 512, 512, 0, 0, 2), (64, 512, 512, 0, 1, 2), (32, 4096, 64, 0, 1, 2),
-    (32, 4096, 64, 0, 0, 2), (32, 512, 512, 1, 0, 2), (32, 512, 512, 0, 1, 3), (32, 64, 512, 0, 1, 2)])
+    (32, 512, 512, 0, 2, 2), (32, 512, 512, 0, 0, 2), (64, 512, 512, 0, 2, 2), (32, 4096, 64, 0, 2, 2),
+    (32, 4096, 64, 0, 0, 2), (32, 512, 512, 1, 0, 2), (32, 512, 512, 0, 2, 3), (32, 64, 512, 0, 2, 2),
+    (32, 512, 512, 0, 1, 2)])
 def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
     """Grouped weight gradients (wgrad_group.hip): the per-tap 128 x 128 tile
     launch and the all-taps halo tile launch (3x3 jobs on W % 32 == 0 images)
@@ -660,7 +662,8 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
         pp = (ctypes.c_int * len(jobs))()
         H._lib.d3d_wgrad_group_plan((H._WgJob * len(jobs))(*jobs), len(jobs), sp, pp, None)
         eng = [H._lib.d3d_wgrad_group_engine(ctypes.byref(j)) for j in jobs]
-        want = [int(bool(halo) and t == 9 and W % 32 == 0 and OC % 128 == 0 and IC % 64 == 0)
+        want = [int(bool(halo) and t == 9 and W >= 8 and Hh >= 32 // min(W, 32) and OC % 128 == 0 and IC % 64 == 0
+                    and (halo == 2 or W >= 32 or (W == 16 and N * Hh * W >= 32768)))
                 for (N, Hh, W, IC, OC, t, C1, b) in WG_JOBS]
         assert eng == want, (eng, want)
         H.wgrad_group_run(jobs)
@@ -1099,6 +1102,18 @@ def test_residual_grad_slot(H, kind):
 
     a, b = run(True), run(False)
     assert rel(a, b) < 1e-2, rel(a, b)
+
+
+@pytest.mark.parametrize("N,period", [(256, 2), (6, 2), (5, 1)])
+def test_period_sum_matches_fp32(H, N, period):
+    """period_sum_k (gradient of a batch-broadcast residual) == fp32 torch sum
+    over the repeats, cast to bf16."""
+    torch.manual_seed(2)
+    g = torch.randn(N, 8, 8, 40, device=DEV).to(BF)
+    out = H._period_sum(g, period)
+    ref = g.float().reshape(N // period, period, 8, 8, 40).sum(0)
+    assert out.shape == (period, 8, 8, 40) and out.dtype == BF
+    assert (out.float() - ref).abs().max().item() <= 0.01 * ref.abs().max().item() + 1e-2
 
 
 def test_diffusion_inputs_kernel_matches_torch(H):

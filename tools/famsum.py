@@ -3,10 +3,10 @@ ms/step and launches per family, the weight-gradient family total."""
 import re
 import sys
 
-FAM = ["wgrad_grp", "wgrad_tn", "conv_wgrad", "wgrad_reduce", "reduce9", "reduce2", "chansum", "gn_bwd_reduce",
+FAM = ["wgrad_halo", "wgrad_grp", "wgrad_tn", "conv_wgrad", "wgrad_reduce", "reduce9", "reduce2", "chansum", "gn_bwd_reduce",
        "gn_bwd_apply", "gn_apply", "gn_stats", "silu_k", "at::native", "halo", "conv_w8_k", "conv_bufl",
-       "conv_s64", "attn", "gemm_fw", "adam", "mlp", "sgemm", "border", "ray", "cond_prep", "diff", "pack"]
-WG = ("wgrad_grp", "wgrad_tn", "conv_wgrad", "wgrad_reduce", "reduce9", "reduce2")
+       "conv_s64", "attn", "gemm_fw", "adam", "mlp", "sgemm", "border", "ray", "cond_prep", "diff", "pack", "period_sum"]
+WG = ("wgrad_halo", "wgrad_grp", "wgrad_tn", "conv_wgrad", "wgrad_reduce", "reduce9", "reduce2")
 
 
 def main(path):

@@ -3,7 +3,7 @@
 # streams on); rpstats summaries (stats, grid, exposed/solo, gaps) on the box.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
-O=/root/repo/gpurun_out/prof5
+O=/root/repo/gpurun_out/${PROF_OUT:-prof5}
 mkdir -p $O
 timeout -k 10 600 rocprofv3 --kernel-trace -d $O/db128 -o run -- python3 /root/repo/bench.py --steps 8 --warmup 3 > $O/b128.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace -d $O/db16 -o run -- python3 /root/repo/bench.py --steps 20 --warmup 3 --global_batch 16 > $O/b16.log 2>&1 || exit $?
@@ -21,3 +21,4 @@ done
 tail -n1 $O/b128.log | cut -c1-150; tail -n1 $O/b16.log | cut -c1-150
 head -3 $O/stats128.txt; head -3 $O/stats16.txt; cat $O/busy16.txt | head -4; head -5 $O/gaps16.txt
 grep -c Cijk $O/stats128.txt $O/stats16.txt || true
+python3 /root/repo/tools/famsum.py $O/stats128.txt > $O/families.txt; python3 /root/repo/tools/famsum.py $O/stats16.txt >> $O/families.txt; cat $O/families.txt

@@ -1,0 +1,16 @@
+#!/bin/bash
+# halo wgrad at W = 8 / 16, period sum, full-model checks, flush batches, step A/B, kernel trace
+set -o pipefail
+O=gpurun_out/r4p
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_ops_gpu.py -x -q --timeout 120 --timeout-method thread -m gpu -k "wgrad_group or period_sum or full_model or model_hip_vs or graph_train_step or graph_step_bitwise or cond_conv or residual_grad_slot" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for ex in 128 16; do
+  timeout -k 10 120 python tools/kbench_wgrad_group.py --examples $ex --skip_old > $O/kb_e$ex.jsonl 2> $O/err.txt || { tail $O/err.txt; exit 1; }
+  echo "== e$ex"; cut -c1-100 $O/kb_e$ex.jsonl
+done
+for i in 1 2; do
+  timeout -k 10 300 python bench.py --global_batch 16 --steps 30 --warmup 5 > $O/b16_$i.json 2> $O/b16.err || { tail $O/b16.err; exit 1; }
+  timeout -k 10 300 python bench.py --steps 10 --warmup 3 > $O/b128_$i.json 2> $O/b128.err || { tail $O/b128.err; exit 1; }
+  python -c "import json;[print(f,json.load(open('$O/'+f+'_$i.json'))['value']) for f in ('b16','b128')]"
+done
