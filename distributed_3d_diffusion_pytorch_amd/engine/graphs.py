@@ -162,13 +162,13 @@ class GraphedTrainStep:
             # zeroing -- on the update stream behind one event that the
             # forward waits on right before it first reads those parameters
             o = tr.optim
-            self.H.adam_update_part(o.flat, o.exp_avg, o.exp_avg_sq, o.ema, self.hp, 0)
+            # (each part clears the gradients it consumes: no separate zeroing pass)
+            self.H.adam_update_part(o.flat, o.exp_avg, o.exp_avg_sq, o.ema, self.hp, 0, zero_g=True)
             S = self.upd_stream
             S.wait_stream(main)
             ev = torch.cuda.Event()
             with torch.cuda.stream(S):
-                self.H.adam_update_part(o.flat, o.exp_avg, o.exp_avg_sq, o.ema, self.hp, 1)
-                o.flat.grad.zero_()
+                self.H.adam_update_part(o.flat, o.exp_avg, o.exp_avg_sq, o.ema, self.hp, 1, zero_g=True)
                 ev.record(S)
             self.loss_acc.zero_()
             _xunet.PARAM_FENCE[0] = (self.fence_level, ev)
@@ -193,11 +193,11 @@ class GraphedTrainStep:
     def _update(self) -> None:
         o = self.tr.optim
         if _FUSED_UPDATE:
-            # Adam + operand repack fused (ops.hip_impl.adam_update_all)
-            self.H.adam_update_all(o.flat, o.exp_avg, o.exp_avg_sq, o.ema, self.hp)
+            # Adam + operand repack + gradient zeroing fused (ops.hip_impl.adam_update_all)
+            self.H.adam_update_all(o.flat, o.exp_avg, o.exp_avg_sq, o.ema, self.hp, zero_g=True)
         else:
             self.H.adam_flat_dev(o.flat.data, o.flat.grad, o.exp_avg, o.exp_avg_sq, o.ema, self.hp)
-        o.flat.grad.zero_()
+            o.flat.grad.zero_()
         self.loss_acc.zero_()
 
     def capture(self, nchunks: int = 1) -> None:

@@ -26,6 +26,7 @@ SIGNATURES = {
     "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, I, P, P],
     "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P, F, P, F, P],
     "d3d_conv_s64_cfg": [I],
+    "d3d_conv_halo_cfg": [I],
     "d3d_conv_res_cfg": [I],
     # elementwise.hip
     "d3d_period_sum": [P, P, I, L, P],
@@ -76,7 +77,7 @@ SIGNATURES = {
     "d3d_cond_prep": [P, P, P, I, C.c_double, C.c_double, P, P, P, P],
     # attention.hip
     "d3d_attn_fwd": [P, P, P, I, I, I, I, I, F, P],
-    "d3d_adam_fused": [P, P, P, P, P, P, P, P, I, P, P, I, P],
+    "d3d_adam_fused": [P, P, P, P, P, P, P, P, I, P, P, I, I, P],
     # mlp.hip
     "d3d_mlp_ws": [I, I, I],
     "d3d_mlp_pe": [P, I, I, F, P, P],

@@ -90,11 +90,13 @@ struct AdamRange {
   int blk0, pad;
 };
 
-__global__ void __launch_bounds__(256) adam_ranges_k(float* __restrict__ p, const float* __restrict__ g,
+// zero_g: the gradient is cleared as it is consumed (the graph step's
+// gradient zeroing folded into the update: one pass over the buffer fewer)
+__global__ void __launch_bounds__(256) adam_ranges_k(float* __restrict__ p, float* __restrict__ g,
                                                      float* __restrict__ m, float* __restrict__ v,
                                                      float* __restrict__ ema, const float* __restrict__ hp,
                                                      const AdamRange* __restrict__ ranges,
-                                                     const int* __restrict__ blk_range) {
+                                                     const int* __restrict__ blk_range, int zero_g) {
   const AdamRange r = ranges[blk_range[blockIdx.x]];
   const long base = r.start + (long)(blockIdx.x - r.blk0) * 4096;
   const long end = r.start + r.len;
@@ -106,6 +108,7 @@ __global__ void __launch_bounds__(256) adam_ranges_k(float* __restrict__ p, cons
     if (i >= end) break;
     f32x4 pp = *reinterpret_cast<f32x4*>(p + i);
     const f32x4 gg = *reinterpret_cast<const f32x4*>(g + i);
+    if (zero_g) *reinterpret_cast<f32x4*>(g + i) = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 mm = *reinterpret_cast<f32x4*>(m + i);
     f32x4 vv = *reinterpret_cast<f32x4*>(v + i);
 #pragma unroll
@@ -140,11 +143,11 @@ struct AdamTile {
   int OC, IC, taps, ICp0, OCp1, blk0;
 };
 
-__global__ void __launch_bounds__(256) adam_pack_tiles_k(float* __restrict__ p, const float* __restrict__ g,
+__global__ void __launch_bounds__(256) adam_pack_tiles_k(float* __restrict__ p, float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v,
                                                          float* __restrict__ ema, const float* __restrict__ hp,
                                                          const AdamTile* __restrict__ tiles,
-                                                         const int* __restrict__ blk_tile) {
+                                                         const int* __restrict__ blk_tile, int zero_g) {
   // rows padded by one float: the transposed reads below step through rows
   // (stride 16 * 9 = 144 floats = 16 mod 32 banks put every row of a lane
   // group on two banks -- 51 % LDS conflict cycles at bs16); 145 spreads them
@@ -169,6 +172,7 @@ __global__ void __launch_bounds__(256) adam_pack_tiles_k(float* __restrict__ p, 
       if (r >= nco) continue;
       const long i = d.off + ((long)(co0 + r) * d.IC + ci0) * T + q;
       f32x4 pp = *reinterpret_cast<const f32x4*>(p + i), gg = *reinterpret_cast<const f32x4*>(g + i);
+      if (zero_g) *reinterpret_cast<f32x4*>(g + i) = f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 mm = *reinterpret_cast<const f32x4*>(m + i), vv = *reinterpret_cast<const f32x4*>(v + i);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -196,6 +200,7 @@ __global__ void __launch_bounds__(256) adam_pack_tiles_k(float* __restrict__ p, 
       const long i = d.off + ((long)(co0 + r) * d.IC + ci0) * T + q;
       float mm = m[i], vv = v[i];
       const float pn = adam_elem(p[i], g[i], mm, vv, b1, b2, eps, wd, step_size, inv_bc2, grad_scale);
+      if (zero_g) g[i] = 0.f;
       p[i] = pn;
       m[i] = mm;
       v[i] = vv;
@@ -237,15 +242,15 @@ __global__ void __launch_bounds__(256) adam_pack_tiles_k(float* __restrict__ p, 
 // One optimizer step over the flat buffers, repacking the MFMA operands of
 // the tile-table weights on the way (the repack of every other cached
 // operand -- plain casts, channel slices -- follows as d3d_pack_all).
-D3D_API int d3d_adam_fused(float* p, const float* g, float* m, float* v, float* ema, const float* hp,
+D3D_API int d3d_adam_fused(float* p, float* g, float* m, float* v, float* ema, const float* hp,
                            const void* ranges, const int* blk_range, int range_blocks, const void* tiles,
-                           const int* blk_tile, int tile_blocks, hipStream_t st) {
+                           const int* blk_tile, int tile_blocks, int zero_g, hipStream_t st) {
   if (range_blocks > 0)
     hipLaunchKernelGGL(adam_ranges_k, dim3(range_blocks), dim3(256), 0, st, p, g, m, v, ema, hp,
-                       (const AdamRange*)ranges, blk_range);
+                       (const AdamRange*)ranges, blk_range, zero_g);
   if (tile_blocks > 0)
     hipLaunchKernelGGL(adam_pack_tiles_k, dim3(tile_blocks), dim3(256), 0, st, p, g, m, v, ema, hp,
-                       (const AdamTile*)tiles, blk_tile);
+                       (const AdamTile*)tiles, blk_tile, zero_g);
   return (int)hipGetLastError();
 }
 

@@ -958,7 +958,10 @@ constexpr int HALO_CH = 32;
 template <int OWT, int BNT = 512>
 struct HaloGeom {
   static constexpr int TR = BNT / OWT;                        // image rows per tile
-  static constexpr int HW2 = OWT + 2;                          // halo row length
+  // halo row length, padded to a multiple of 8 pixels: the fragment swizzle
+  // depends on pixel bits 1-2 only, so a kh shift of whole halo rows keeps it
+  // (the tap's B offsets are a constant per kh; the pad pixels are never loaded)
+  static constexpr int HW2 = (OWT + 2 + 7) / 8 * 8;
   static constexpr int HP = (TR + 2) * HW2;                    // halo pixels
   static constexpr int HPW = (HP + 127) / 128;                 // 1-KiB pieces per wave (16 pixels each)
   static constexpr int HBUF = HPW * 8 * 16 * HALO_CH;          // bf16 elements per halo buffer
@@ -982,7 +985,12 @@ __device__ __forceinline__ void halo_issue_b(bf16* sH, const bf16* I, int in_byt
                                              hoff[k] + (unsigned)cbyte, 0, 0, 0);
 }
 
-template <int OWT, bool TRANS, int BNT = 512, bool PF = false, bool RES = true>   // RES: see conv_w8_k
+// AU: the nine taps unrolled with every B-fragment LDS offset precomputed
+// (9 x TN registers): the swizzled address of a tap-shifted halo pixel is not
+// linear in the shift, and computing it per step cost ~48 VALU per 32 MFMAs
+// on the critical path between the barrier and the first MFMA.  (Without the
+// residual prefetch only: with it the register file overflows.)
+template <int OWT, bool TRANS, int BNT = 512, bool PF = false, bool RES = true, bool AU = false>
 __global__ void __launch_bounds__(512, 1)
 conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
@@ -1129,6 +1137,65 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
         for (int j = 0; j < TN; ++j) bfr[j] = bn[j];
       }
     }
+  } else if constexpr (AU) {
+  halo_issue_b<Gm::HPW>(sH, I, in_bytes, hoff, 0, wave);
+  halo_issue_a(sAr, Wp, w_bytes, aoff, a_soff(0), wave);
+  halo_issue_a(sAr + Gm::ABUF, Wp, w_bytes, aoff, a_soff(1), wave);
+  halo_issue_a(sAr + 2 * Gm::ABUF, Wp, w_bytes, aoff, a_soff(2), wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (RES) {
+    if (res) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(__builtin_bit_cast(unsigned long long, rres[i][j])));
+    }
+  }
+  int bo[3][TN], ao[TM];                       // per kw; the kh shift is a constant (HW2 % 8 == 0)
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int hp = hp0[j] + kw;
+      bo[kw][j] = hp * HALO_CH + ((fq ^ ((hp >> 1) & 2)) << 3);
+    }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int row = wm * WM + i * 16 + fr;
+    ao[i] = row * HALO_CH + ((fq ^ ((row >> 1) & 2)) << 3);
+  }
+  for (int c = 0; c < NCH; ++c) {
+    const bf16* hb = sH + (c & 1) * Gm::HBUF;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int s = c * 9 + t;
+      if (t >= 1 && t <= 3) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + Gm::HPW) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      halo_issue_a(sAr + ((s + 3) & 3) * Gm::ABUF, Wp, w_bytes, aoff, a_soff(s + 3), wave);
+      if (t == 0) {
+        const int cn = c + 1 < NCH ? c + 1 : NCH - 1;
+        halo_issue_b<Gm::HPW>(sH + ((c + 1) & 1) * Gm::HBUF, I, in_bytes, hoff, cn * HALO_CH * 2, wave);
+      }
+      const bf16* a = sAr + (s & 3) * Gm::ABUF;
+      __builtin_amdgcn_s_setprio(1);
+      bf16x8 af[TM], bfr[TN];
+      const int kh = TRANS ? 2 - t / 3 : t / 3, kw = TRANS ? 2 - t % 3 : t % 3;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(hb + kh * Gm::HW2 * HALO_CH + bo[kw][j]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a + ao[i]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
   } else {
   halo_issue_b<Gm::HPW>(sH, I, in_bytes, hoff, 0, wave);
   halo_issue_a(sAr, Wp, w_bytes, aoff, a_soff(0), wave);
@@ -2677,6 +2744,11 @@ static bool s64_wanted(long Mpix, int OC, int ICp, int taps) {
 // 1: the residual-free convs (dgrad, conv1) still run the residual-capable
 // kernel variants (round-3 behaviour; A/B switch for the RES template)
 static int g_conv_res_always = 0;
+static int g_halo_au = 1;          // conv_halo_k AU (unrolled taps, precomputed B offsets); 0: per-step addressing
+D3D_API int d3d_conv_halo_cfg(int au) {
+  g_halo_au = au;
+  return 0;
+}
 D3D_API int d3d_conv_res_cfg(int always) {
   g_conv_res_always = always;
   return 0;
@@ -2807,11 +2879,14 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
     auto nblk = [&](int bn) { return OH % (bn / OW) ? 0L : (long)N * (OH / (bn / OW)) * (OC / 128); };
     if (OW != 32 && nblk(512) >= 256) {
       dim3 gh((unsigned)(N * (OH / (512 / OW))), (unsigned)(OC / 128), 1);
+#define HALO2(OWv, TR, RS, AUv)                                                                                   \
+  hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512, false, RS, AUv>), gh, dim3(512), 0, st, (const bf16*)I,          \
+                     (const bf16*)Wp, bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, \
+                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, gb)
 #define HALO(OWv, TR, RS)                                                                                          \
-  hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512, false, RS>), gh, dim3(512), 0, st, (const bf16*)I, (const bf16*)Wp, \
-                     bias,                                                                                         \
-                     row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, IC, ICp, OC, scale,   \
-                     res_nmod, gnp, gn_groups, (bf16*)O2, gb)
+  do {                                                                                                            \
+    if (g_halo_au && OWv == 64 && !RS) HALO2(OWv, TR, RS, true); else HALO2(OWv, TR, RS, false);                  \
+  } while (0)
       if (OW == 64) {
         if (trans) { if (res || g_conv_res_always) HALO(64, true, true); else HALO(64, true, false); }
         else if (res || g_conv_res_always) HALO(64, false, true); else HALO(64, false, false);
@@ -2820,6 +2895,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
         else if (res || g_conv_res_always) HALO(128, false, true); else HALO(128, false, false);
       }
 #undef HALO
+#undef HALO2
       if (gn_done && gnp) *gn_done = 1;
       if (silu_done && O2) *silu_done = 1;
       if (gnb_done && gb.grp) *gnb_done = 1;

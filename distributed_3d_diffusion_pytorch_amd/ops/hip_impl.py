@@ -711,6 +711,8 @@ assert ctypes.sizeof(_GnbArgs) == 64
 # the epilogue costs the halo dgrad +25-40 % while the reduce pass it
 # replaces is a bandwidth-bound 30-160 us); kept for A/B and its tests.
 _GNB_EPI = os.environ.get("D3D_GNB_EPI", "0") != "0"
+if os.environ.get("D3D_HALO_AU"):        # A/B knob: halo conv with unrolled taps / precomputed offsets (1) or not (0)
+    _lib.d3d_conv_halo_cfg(int(os.environ["D3D_HALO_AU"]))
 if os.environ.get("D3D_GN_CFG"):        # A/B knob "blocks,red_u,app_u": GroupNorm launch shapes
     _lib.d3d_gn_cfg(*[int(v) for v in os.environ["D3D_GN_CFG"].split(",")])
 
@@ -1966,29 +1968,34 @@ def prepare_update_parts(flat, parts) -> None:
         _fused_tables(flat, set(only), key=(id(flat), "part", k), take_unowned=k == 0)
 
 
-def adam_update_part(flat, m, v, ema, hp, k) -> None:
-    """The fused Adam + operand repack of part ``k`` (:func:`prepare_update_parts`)."""
+def adam_update_part(flat, m, v, ema, hp, k, zero_g=False) -> None:
+    """The fused Adam + operand repack of part ``k`` (:func:`prepare_update_parts`).
+    ``zero_g``: clear the part's gradients as they are consumed (the parts
+    together cover every parameter; padding between parameters is never
+    written, so it stays zero)."""
     ent = _FUSED.get((id(flat), "part", k))
     if ent is None or ent["rev"] != _REV[0] or ent["flat"] is not flat:
         raise RuntimeError("update-part tables missing or stale (prepare_update_parts before the capture)")
-    _adam_fused_launch(flat, m, v, ema, hp, ent)
+    _adam_fused_launch(flat, m, v, ema, hp, ent, zero_g)
 
 
-def _adam_fused_launch(flat, m, v, ema, hp, ent) -> None:
+def _adam_fused_launch(flat, m, v, ema, hp, ent, zero_g=False) -> None:
     (tt, tb, tblk), (rt, rb, rblk), (rd, rm, rest_blk) = ent["tiles"], ent["ranges"], ent["rest"]
     if tblk or rblk:
         _chk(_lib.d3d_adam_fused(flat.data.data_ptr(), flat.grad.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(ema),
-                                 hp.data_ptr(), _ptr(rt), _ptr(rb), int(rblk), _ptr(tt), _ptr(tb), int(tblk), _st()),
+                                 hp.data_ptr(), _ptr(rt), _ptr(rb), int(rblk), _ptr(tt), _ptr(tb), int(tblk),
+                                 int(bool(zero_g)), _st()),
              "adam_fused")
     if rest_blk:
         _chk(_lib.d3d_pack_all(rd.data_ptr(), rm.data_ptr(), rest_blk, _st()), "pack_all")
 
 
-def adam_update_all(flat, m, v, ema, hp) -> None:
+def adam_update_all(flat, m, v, ema, hp, zero_g=False) -> None:
     """One optimizer step over the whole flat buffer with the cached bf16
     operands repacked from the updated weights (replaces adam_flat_dev +
     refresh_weights).  Inside a graph capture the tables must already exist
-    (:func:`prepare_fused_update`)."""
+    (:func:`prepare_fused_update`).  ``zero_g``: the gradient buffer is left
+    zeroed (the range table covers every element the tile table does not)."""
     capturing = torch.cuda.is_current_stream_capturing()
     ent = _FUSED.get(id(flat))
     if ent is None or ent["rev"] != _REV[0] or ent["flat"] is not flat:
@@ -1997,7 +2004,8 @@ def adam_update_all(flat, m, v, ema, hp) -> None:
         ent = _fused_tables(flat)
     (tt, tb, tblk), (rt, rb, rblk), (rd, rm, rest_blk) = ent["tiles"], ent["ranges"], ent["rest"]
     _chk(_lib.d3d_adam_fused(flat.data.data_ptr(), flat.grad.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(ema),
-                             hp.data_ptr(), _ptr(rt), _ptr(rb), int(rblk), _ptr(tt), _ptr(tb), int(tblk), _st()),
+                             hp.data_ptr(), _ptr(rt), _ptr(rb), int(rblk), _ptr(tt), _ptr(tb), int(tblk),
+                             int(bool(zero_g)), _st()),
          "adam_fused")
     if rest_blk:
         _chk(_lib.d3d_pack_all(rd.data_ptr(), rm.data_ptr(), rest_blk, _st()), "pack_all")

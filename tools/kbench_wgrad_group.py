@@ -71,7 +71,7 @@ def main():
     dev = torch.device("cuda")
     torch.manual_seed(0)
     for name, spec in batches(2 * a.examples):
-        if a.only and not any(name.startswith(o) for o in a.only.split(",")):
+        if a.only and not any(name.startswith(o.replace("_", " ")) for o in a.only.split(",")):
             continue
         tens = []
         flops = 0.0
