@@ -985,7 +985,7 @@ static bool gh_takes(const WgJobDesc& d) {
   const int Wm = d.W < GH_PK ? d.W : GH_PK;
   const long P = (long)d.N * d.H * d.W;
   if (g_gh_on == 1 && d.W < 32 && !(d.W == 16 && P >= 32768)) return false;
-  return g_gh_on && d.taps == 9 && d.W >= 8 && gw_lg2(d.W) >= 0 && gw_lg2(d.H) >= 0 && d.H >= GH_PK / Wm &&
+  return g_gh_on && d.taps == 9 && d.W >= 8 && gw_lg2(d.W) >= 0 && ((uintptr_t)d.dw & 15) == 0 && gw_lg2(d.H) >= 0 && d.H >= GH_PK / Wm &&
          d.OC % GH_BM == 0 && d.IC % GH_BN == 0 && (!d.x2 || d.C1 % GH_BN == 0) &&
          (long)(GH_PK / Wm + 2) * d.W * d.IC * 2 < (1L << 30);
 }
@@ -1135,8 +1135,9 @@ static long gw_tables(const WgJobDesc* d, int n, const GwPlan& pl, float* ws, bo
       Rj.taps = D.taps;
       Rj.splits = pl.splits[i];
       Rj.blk0 = (int)rblk;
-      Rj.flat = halo ? 1 : 0;
-      Rj.nblk_w = halo ? (int)cdiv((long)D.OC * D.IC * D.taps, 1024L) : D.OC * cdiv(D.IC, 64);
+      // flat: the halo tiles' OIHW slabs, and every 1x1 job's ([co][ci] is OIHW)
+      Rj.flat = (halo || D.taps == 1) && ((long)D.OC * D.IC * D.taps) % 4 == 0 && ((uintptr_t)D.dw & 15) == 0;
+      Rj.nblk_w = Rj.flat ? (int)cdiv((long)D.OC * D.IC * D.taps, 1024L) : D.OC * cdiv(D.IC, 64);
       Rj.acc = D.acc;
       Rj.scale = D.scale;
       rblk += Rj.nblk_w + (D.db ? cdiv(D.OC, 64) : 0);
