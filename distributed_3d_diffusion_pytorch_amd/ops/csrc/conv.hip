@@ -1063,7 +1063,11 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   // epilogue the 8-byte residual reads (16 pixels x 32 B per instruction)
   // were fully exposed -- one block per CU, nothing left to overlap them --
   // and cost +30 % on the level-0 conv (tools/kbench_conv_epi.py).
-  bf16x4 rres[RES ? TM : 1][RES ? TN : 1];
+  // AU: the residual goes straight into the accumulators instead (the
+  // epilogue computes (acc + bias + res) * scale either way), which frees
+  // the 64 prefetch registers the unrolled-tap offsets need
+  constexpr bool RPF = RES && !AU;
+  bf16x4 rres[RPF ? TM : 1][RPF ? TN : 1];
   if (RES && res) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -1072,7 +1076,13 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int co = m0 + wm * WM + i * 16 + fq * 4;
-        rres[i][j] = co < OC ? *reinterpret_cast<const bf16x4*>(res + rpix * OC + co) : bf16x4{};
+        const bf16x4 r4 = co < OC ? *reinterpret_cast<const bf16x4*>(res + rpix * OC + co) : bf16x4{};
+        if constexpr (RPF) {
+          rres[i][j] = r4;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] = (float)r4[e];
+        }
       }
     }
   }
@@ -1143,14 +1153,6 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
   halo_issue_a(sAr + Gm::ABUF, Wp, w_bytes, aoff, a_soff(1), wave);
   halo_issue_a(sAr + 2 * Gm::ABUF, Wp, w_bytes, aoff, a_soff(2), wave);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (RES) {
-    if (res) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(__builtin_bit_cast(unsigned long long, rres[i][j])));
-    }
-  }
   int bo[3][TN], ao[TM];                       // per kw; the kh shift is a constant (HW2 % 8 == 0)
 #pragma unroll
   for (int kw = 0; kw < 3; ++kw)
@@ -1286,7 +1288,7 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + cb[i][e];
-      if constexpr (RES) {
+      if constexpr (RPF) {
         if (res) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += (float)rres[i][j][e];
@@ -2744,7 +2746,8 @@ static bool s64_wanted(long Mpix, int OC, int ICp, int taps) {
 // 1: the residual-free convs (dgrad, conv1) still run the residual-capable
 // kernel variants (round-3 behaviour; A/B switch for the RES template)
 static int g_conv_res_always = 0;
-static int g_halo_au = 1;          // conv_halo_k AU (unrolled taps, precomputed B offsets); 0: per-step addressing
+// conv_halo_k AU (unrolled taps, precomputed B offsets, residual preloaded into the accumulators); 0 off
+static int g_halo_au = 1;
 D3D_API int d3d_conv_halo_cfg(int au) {
   g_halo_au = au;
   return 0;
@@ -2885,7 +2888,8 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
                      IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, gb)
 #define HALO(OWv, TR, RS)                                                                                          \
   do {                                                                                                            \
-    if (g_halo_au && OWv == 64 && !RS) HALO2(OWv, TR, RS, true); else HALO2(OWv, TR, RS, false);                  \
+    if (g_halo_au && OWv == 64) HALO2(OWv, TR, RS, true);                                                          \
+    else HALO2(OWv, TR, RS, false);                                                                                 \
   } while (0)
       if (OW == 64) {
         if (trans) { if (res || g_conv_res_always) HALO(64, true, true); else HALO(64, true, false); }

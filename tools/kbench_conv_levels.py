@@ -38,12 +38,16 @@ def main():
     H._ensure_impl()
     H._lib.d3d_conv_res_cfg(int(os.environ.get("D3D_CONV_RES_ALWAYS", "0")))
     for N in ns:
-        for Hh, C in ((64, 128), (32, 256), (16, 256), (8, 512)):
+        levels = [(64, 128, 128), (32, 256, 256), (16, 256, 256), (8, 512, 512)]
+        if os.environ.get("KB_CONV_EXTRA"):             # level-entry convs (channel change) and decoder concat widths
+            levels = [(32, 128, 256), (16, 256, 256), (8, 256, 512), (64, 384, 128), (64, 256, 128), (32, 512, 256),
+                      (32, 384, 256)]
+        for Hh, C, OC in levels:
             x = torch.randn(N, Hh, Hh, C, device="cuda").to(BF)
-            w = torch.randn(C, C, 3, 3, device="cuda") * 0.03
-            b = torch.randn(C, device="cuda") * 0.1
-            r = torch.randn(N, Hh, Hh, C, device="cuda").to(BF)
-            fl = 2.0 * N * Hh * Hh * C * C * 9
+            w = torch.randn(OC, C, 3, 3, device="cuda") * 0.03
+            b = torch.randn(OC, device="cuda") * 0.1
+            r = torch.randn(N, Hh, Hh, OC, device="cuda").to(BF)
+            fl = 2.0 * N * Hh * Hh * C * OC * 9
             with torch.no_grad():
                 f1 = timeit(lambda: H.conv3x3(x, w, b, gn_groups=32))
                 f2 = timeit(lambda: H.conv3x3(x, w, b, residual=r, out_scale=0.7071, gn_groups=32))
@@ -51,7 +55,7 @@ def main():
             y = H.conv3x3(xr, w, None)
             g = torch.randn_like(y)
             d = timeit(lambda: torch.autograd.grad(y, xr, g, retain_graph=True))
-            print(json.dumps({"res_always": os.environ.get("D3D_CONV_RES_ALWAYS", "0"), "N": N, "level": f"{Hh}x{Hh}x{C}", "fwd_us": round(f1, 1),
+            print(json.dumps({"res_always": os.environ.get("D3D_CONV_RES_ALWAYS", "0"), "N": N, "level": f"{Hh}x{Hh}x{C}->{OC}", "fwd_us": round(f1, 1),
                               "fwd_tfs": round(fl / f1 / 1e6, 1), "fwd_res_us": round(f2, 1),
                               "fwd_res_tfs": round(fl / f2 / 1e6, 1), "dgrad_us": round(d, 1),
                               "dgrad_tfs": round(fl / d / 1e6, 1)}), flush=True)
