@@ -2888,7 +2888,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
                      IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, gb)
 #define HALO(OWv, TR, RS)                                                                                          \
   do {                                                                                                            \
-    if (g_halo_au && OWv == 64) HALO2(OWv, TR, RS, true);                                                          \
+    if (g_halo_au) HALO2(OWv, TR, RS, true);                                                                        \
     else HALO2(OWv, TR, RS, false);                                                                                 \
   } while (0)
       if (OW == 64) {

@@ -42,6 +42,8 @@ def main():
         if os.environ.get("KB_CONV_EXTRA"):             # level-entry convs (channel change) and decoder concat widths
             levels = [(32, 128, 256), (16, 256, 256), (8, 256, 512), (64, 384, 128), (64, 256, 128), (32, 512, 256),
                       (32, 384, 256)]
+        if os.environ.get("KB_CONV_128"):               # 128x128 images (BASELINE config 4)
+            levels = [(128, 128, 128), (64, 256, 256)]
         for Hh, C, OC in levels:
             x = torch.randn(N, Hh, Hh, C, device="cuda").to(BF)
             w = torch.randn(OC, C, 3, 3, device="cuda") * 0.03
