@@ -775,6 +775,15 @@ def _wgrad(g, x, OC, IC, N, H, W, OH, OW, stride, taps=9, want_bias=False, dW=No
     """Split-K weight gradient (+ fused bias column sums).  Writes into the
     given dW/db (accumulating when asked) or into fresh fp32 tensors."""
     _ensure_impl()
+    if _WGRAD_DIRECT_HALO and stride == 1 and (OH, OW) == (H, W) and taps == 9 and x.dtype == BF16:
+        # the all-taps halo tile when it takes the shape (one grouped launch of one job)
+        dW_ = dW if dW is not None else torch.empty(OC, IC, taps, dtype=F32, device=x.device)
+        db_ = db if (db is not None or not want_bias) else torch.empty(OC, dtype=F32, device=x.device)
+        j = wgrad_job(g, x, OC, IC, N, H, W, taps, dW_, db_, scale, accumulate) if g.is_contiguous() and \
+            x.is_contiguous() else None
+        if j is not None and _lib.d3d_wgrad_group_engine(ctypes.byref(j)) == 1:
+            wgrad_group_run([j])
+            return dW_, db_
     s, pps = ctypes.c_int(), ctypes.c_int()
     _lib.d3d_conv_wgrad_plan3(N, H, W, OH, OW, OC, IC, taps, stride, ctypes.byref(s), ctypes.byref(pps))
     extra = 2 * s.value * OC if (want_bias or db is not None) else 0
@@ -806,6 +815,8 @@ assert ctypes.sizeof(_WgJob) == 80
 # 1: weight-gradient jobs deferred inside graph capture run grouped, one
 # launch (+ one slab reduce) per sink flush; 0: one launch pair per job
 _WGRAD_GROUP = os.environ.get("D3D_WGRAD_GROUP", "1") != "0"
+# direct (non-sink) weight gradients -- the conditioning conv's -- on the halo tile when it takes the shape
+_WGRAD_DIRECT_HALO = _WGRAD_GROUP and os.environ.get("D3D_WGRAD_DIRECT_HALO", "1") != "0"
 if os.environ.get("D3D_WGRAD_GROUP_BLOCKS"):           # planner target (A/B knob): blocks per grouped launch
     _lib.d3d_wgrad_group_cfg(int(os.environ["D3D_WGRAD_GROUP_BLOCKS"]), 0, 0)
 if os.environ.get("D3D_WGRAD_GROUP_WIDE"):             # A/B knob: 128 x 256 (1) or 128 x 128 (0) tiles
