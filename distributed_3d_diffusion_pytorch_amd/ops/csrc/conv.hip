@@ -2748,8 +2748,14 @@ static bool s64_wanted(long Mpix, int OC, int ICp, int taps) {
 static int g_conv_res_always = 0;
 // conv_halo_k AU (unrolled taps, precomputed B offsets, residual preloaded into the accumulators); 0 off
 static int g_halo_au = 1;
+// 32-wide images on the halo kernel (16-row tiles) when the grid fills the chip:
+// the 32x32 level at bs128 903 -> 1020 TF/s fwd, 892 -> 979 dgrad against
+// conv_w8_k (profiles/r4/halo_w32/)
+static int g_halo_w32 = 1;
+// knob: bits 0-1 AU (0 off / 1 on), bit 2 the 32-wide halo (D3D_HALO_AU=5: both, the default)
 D3D_API int d3d_conv_halo_cfg(int au) {
-  g_halo_au = au;
+  g_halo_au = au & 3;
+  g_halo_w32 = (au >> 2) & 1;
   return 0;
 }
 D3D_API int d3d_conv_res_cfg(int always) {
@@ -2880,7 +2886,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
       OC % 128 == 0 && (OW == 32 || OW == 64 || OW == 128) && in_bytes < (1L << 31) && w_bytes < (1L << 31)) {
     // 512-pixel tiles where they fill the chip (64/128-wide images)
     auto nblk = [&](int bn) { return OH % (bn / OW) ? 0L : (long)N * (OH / (bn / OW)) * (OC / 128); };
-    if (OW != 32 && nblk(512) >= 256) {
+    if ((OW != 32 || g_halo_w32) && nblk(512) >= 256) {
       dim3 gh((unsigned)(N * (OH / (512 / OW))), (unsigned)(OC / 128), 1);
 #define HALO2(OWv, TR, RS, AUv)                                                                                   \
   hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512, false, RS, AUv>), gh, dim3(512), 0, st, (const bf16*)I,          \
@@ -2894,6 +2900,9 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
       if (OW == 64) {
         if (trans) { if (res || g_conv_res_always) HALO(64, true, true); else HALO(64, true, false); }
         else if (res || g_conv_res_always) HALO(64, false, true); else HALO(64, false, false);
+      } else if (OW == 32) {
+        if (trans) { if (res || g_conv_res_always) HALO(32, true, true); else HALO(32, true, false); }
+        else if (res || g_conv_res_always) HALO(32, false, true); else HALO(32, false, false);
       } else {
         if (trans) { if (res || g_conv_res_always) HALO(128, true, true); else HALO(128, true, false); }
         else if (res || g_conv_res_always) HALO(128, false, true); else HALO(128, false, false);
