@@ -2752,10 +2752,19 @@ static int g_halo_au = 1;
 // the 32x32 level at bs128 903 -> 1020 TF/s fwd, 892 -> 979 dgrad against
 // conv_w8_k (profiles/r4/halo_w32/)
 static int g_halo_w32 = 1;
-// knob: bits 0-1 AU (0 off / 1 on), bit 2 the 32-wide halo (D3D_HALO_AU=5: both, the default)
+// 16-wide images (one image per 256-pixel tile) when the grid fills the chip
+// (bs128: 16x16x256 dgrad 155 -> 106 us), and 32-wide images in 8-row tiles
+// where 16-row ones would not fill it (bs16: 32x32x256 dgrad 139 -> 71 us);
+// bench +0.6 % bs128, +1.5 % bs16 (profiles/r4/halo_small/)
+static int g_halo_w16 = 1;
+static int g_halo_w32s = 1;
+// knob: bits 0-1 AU (0 off / 1 on), bit 2 the 32-wide halo, bit 3 the 16-wide halo, bit 4 the 8-row
+// 32-wide tiles (D3D_HALO_AU=29: all, the default)
 D3D_API int d3d_conv_halo_cfg(int au) {
   g_halo_au = au & 3;
   g_halo_w32 = (au >> 2) & 1;
+  g_halo_w16 = (au >> 3) & 1;
+  g_halo_w32s = (au >> 4) & 1;
   return 0;
 }
 D3D_API int d3d_conv_res_cfg(int always) {
@@ -2883,7 +2892,8 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
   dim3 grid((unsigned)((Mpix + BN - 1) / BN), (unsigned)((OC + BM - 1) / BM), (unsigned)nsplit);
   const long in_bytes = (long)N * IH * IW * IC * 2, w_bytes = (long)((OC + 127) / 128 * 128) * taps * ICp * 2;
   if (g_conv_impl == 8 && taps == 9 && stride == 1 && IW == OW && IH == OH && ldo == OC && IC % HALO_CH == 0 &&
-      OC % 128 == 0 && (OW == 32 || OW == 64 || OW == 128) && in_bytes < (1L << 31) && w_bytes < (1L << 31)) {
+      OC % 128 == 0 && (OW == 16 || OW == 32 || OW == 64 || OW == 128) && in_bytes < (1L << 31) &&
+      w_bytes < (1L << 31)) {
     // 512-pixel tiles where they fill the chip (64/128-wide images)
     auto nblk = [&](int bn) { return OH % (bn / OW) ? 0L : (long)N * (OH / (bn / OW)) * (OC / 128); };
     if ((OW != 32 || g_halo_w32) && nblk(512) >= 256) {
@@ -2909,6 +2919,27 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
       }
 #undef HALO
 #undef HALO2
+      if (gn_done && gnp) *gn_done = 1;
+      if (silu_done && O2) *silu_done = 1;
+      if (gnb_done && gb.grp) *gnb_done = 1;
+      return (int)hipGetLastError();
+    }
+    if (((OW == 16 && g_halo_w16) || (OW == 32 && g_halo_w32s)) && nblk(256) >= 256) {
+      // 256-pixel tiles (waves of 64 x 64): a whole 16-wide image, or 8 rows of a
+      // 32-wide one where the 16-row tiles would not fill the chip (bs16)
+      dim3 gh((unsigned)(N * (OH / (256 / OW))), (unsigned)(OC / 128), 1);
+#define HALOS(OWv, TR, RS)                                                                                         \
+  hipLaunchKernelGGL((conv_halo_k<OWv, TR, 256, false, RS, true>), gh, dim3(512), 0, st, (const bf16*)I,           \
+                     (const bf16*)Wp, bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, \
+                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, gb)
+      if (OW == 16) {
+        if (trans) { if (res || g_conv_res_always) HALOS(16, true, true); else HALOS(16, true, false); }
+        else if (res || g_conv_res_always) HALOS(16, false, true); else HALOS(16, false, false);
+      } else {
+        if (trans) { if (res || g_conv_res_always) HALOS(32, true, true); else HALOS(32, true, false); }
+        else if (res || g_conv_res_always) HALOS(32, false, true); else HALOS(32, false, false);
+      }
+#undef HALOS
       if (gn_done && gnp) *gn_done = 1;
       if (silu_done && O2) *silu_done = 1;
       if (gnb_done && gb.grp) *gnb_done = 1;

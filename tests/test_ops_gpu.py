@@ -195,7 +195,9 @@ W8_SHAPES = [
     (16, 32, 32, 512, 512, 1, False, True, 0.5),                  # w8n: 2 x 128 tiles of 256 x 128
     (32, 64, 64, 384, 128, 1, True, True, 1 / math.sqrt(2)),      # halo: 8-row tiles, 12 channel chunks
     (8, 128, 128, 128, 256, 1, False, False, 1.0),                # halo: 4-row tiles of 128-wide images
-    (64, 32, 32, 128, 256, 1, False, False, 1.0),                 # 32-wide: conv_w8_k
+    (64, 32, 32, 128, 256, 1, False, False, 1.0),                 # 32-wide: halo (16-row tiles), else conv_w8_k
+    (128, 16, 16, 256, 256, 1, True, False, 1 / math.sqrt(2)),    # 16-wide: halo 1-image tiles when enabled
+    (32, 32, 32, 256, 256, 1, False, False, 1.0),                 # 32-wide at bs16: halo 8-row tiles when enabled
 ]
 
 
