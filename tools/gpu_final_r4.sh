@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-4 end-of-round evidence: full GPU suite, smoke, benches (bs128, bs16, bs32, sampling), 128px
 set -o pipefail
-O=gpurun_out/final_r4
+O=gpurun_out/${FINAL_OUT:-final_r4}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
