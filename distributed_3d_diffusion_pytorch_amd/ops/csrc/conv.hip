@@ -2931,7 +2931,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
 #define HALOS(OWv, TR, RS)                                                                                         \
   hipLaunchKernelGGL((conv_halo_k<OWv, TR, 256, false, RS, true>), gh, dim3(512), 0, st, (const bf16*)I,           \
                      (const bf16*)Wp, bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, \
-                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, gb)
+                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, GnbArgs{})
       if (OW == 16) {
         if (trans) { if (res || g_conv_res_always) HALOS(16, true, true); else HALOS(16, true, false); }
         else if (res || g_conv_res_always) HALOS(16, false, true); else HALOS(16, false, false);
@@ -2942,7 +2942,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
 #undef HALOS
       if (gn_done && gnp) *gn_done = 1;
       if (silu_done && O2) *silu_done = 1;
-      if (gnb_done && gb.grp) *gnb_done = 1;
+      // (no GroupNorm-backward epilogue on the 256-pixel tiles: gnb_done stays 0, the caller runs the reduce)
       return (int)hipGetLastError();
     }
   }

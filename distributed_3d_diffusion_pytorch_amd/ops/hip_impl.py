@@ -711,6 +711,8 @@ assert ctypes.sizeof(_GnbArgs) == 64
 # the epilogue costs the halo dgrad +25-40 % while the reduce pass it
 # replaces is a bandwidth-bound 30-160 us); kept for A/B and its tests.
 _GNB_EPI = os.environ.get("D3D_GNB_EPI", "0") != "0"
+if os.environ.get("D3D_GEMM_TUNE"):     # A/B knob "cfg,gm,grid" (gemm.hip d3d_gemm_tune; 0 keeps a value)
+    _lib.d3d_gemm_tune(*[int(v) for v in os.environ["D3D_GEMM_TUNE"].split(",")])
 if os.environ.get("D3D_HALO_AU"):        # A/B knob: halo conv with unrolled taps / precomputed offsets (1) or not (0)
     _lib.d3d_conv_halo_cfg(int(os.environ["D3D_HALO_AU"]))
 if os.environ.get("D3D_GN_CFG"):        # A/B knob "blocks,red_u,app_u": GroupNorm launch shapes
