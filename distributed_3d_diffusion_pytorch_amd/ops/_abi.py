@@ -101,6 +101,7 @@ SIGNATURES = {
     "d3d_wgrad_group_wide": [I],
     "d3d_wgrad_group_stages": [I],
     "d3d_wgrad_group_halo": [I, I, I],
+    "d3d_wgrad_group_halo_pk": [I],
     "d3d_wgrad_group_engine": [P],
     "d3d_wgrad_group": [P, I, P, L, P],
     "d3d_wgrad_group_plan": [P, I, IP, IP, C.POINTER(C.c_long)],

@@ -604,21 +604,31 @@ __global__ void __launch_bounds__(256, 2) wgrad_grp2_k(GwTable tab) {
 // that is 0.72 transposed LDS reads and 0.07 KB of DMA, against 1.0 and 0.25 KB
 // for the per-tap 128 x 128 tile above (which re-reads dY and X once per tap).
 constexpr int GH_BM = 128, GH_BN = 64, GH_PK = 32, GH_WR = 34;
-constexpr int GH_BROWS = 128;                          // window rows (<= 3 x 34 = 102) padded to 16 DMAs of 8
-constexpr int GH_STAGE = GH_PK * GH_BM + GH_BROWS * GH_BN;   // bf16: 4096 (dY) + 8192 (window) = 24 KB
+// K-step of PK pixels (32 or 64): window rows padded to whole 8-row DMAs
+// (<= 3 x 34 = 102 -> 128 at PK = 32, <= 3 x 66 = 198 -> 256 at PK = 64)
+template <int PK> struct GhGeom {
+  static constexpr int BROWS = PK == 64 ? 256 : 128;
+  static constexpr int STAGE = PK * GH_BM + BROWS * GH_BN;    // bf16 elements: 24 KB (PK 32) / 48 KB (PK 64)
+  static constexpr int PER_A = PK / 32, PER_B = BROWS / 64;   // DMA instructions per wave per stage
+};
 
 // 16-byte chunk swizzle of the 128-byte window rows: the 8 consecutive rows a
 // transposed read's 32-lane group touches (any tap offset) land on 64 distinct
 // banks
 __device__ __forceinline__ int gh_swz(int row) { return 2 * ((row >> 1) & 3); }
 
+template <int PK>
 __device__ __forceinline__ void gh_issue(bf16* sA, bf16* sB, const bf16* __restrict__ dY, const bf16* __restrict__ I,
                                          long in_elems, long p0, long p_end, int OC, int IC, int OH, int OW, int lw,
                                          int Wm, int RR, int wave, const unsigned* aoff, const unsigned* boff,
                                          const unsigned* bfl, bool on) {
   typedef __attribute__((address_space(3))) void lds_void;
+  typedef GhGeom<PK> Gg;
   const __amdgpu_buffer_rsrc_t rA = gw_rsrc(dY + p0 * OC, on ? (p_end - p0) * OC * 2 : 0);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sA + wave * 4 * GH_BM), 16, aoff[0], 0, 0, 0);
+#pragma unroll
+  for (int i = 0; i < Gg::PER_A; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sA + (wave * Gg::PER_A + i) * 4 * GH_BM), 16, aoff[i], 0,
+                                             0, 0);
   // window origin: pixel (y - 1, x0 - 1); it may lie before the tensor, and
   // only masked lanes (top row, left column) ever address below the tensor
   const long pb = p0 - OW - 1;
@@ -627,15 +637,17 @@ __device__ __forceinline__ void gh_issue(bf16* sA, bf16* sB, const bf16* __restr
   const unsigned bad = 1u | (y == 0 ? 2u : 0u) | (y + RR == OH ? 4u : 0u) | (x0 == 0 ? 8u : 0u) |
                        (x0 + Wm == OW ? 16u : 0u);
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * 2 + j) * 8 * GH_BN), 16,
+  for (int j = 0; j < Gg::PER_B; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * Gg::PER_B + j) * 8 * GH_BN), 16,
                                              (bfl[j] & bad) ? 0x80000000u : boff[j], 0, 0, 0);
 }
 
-template <int NS>
+template <int NS, int PK>
 __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
-  constexpr int PER = 1 + 2;                     // DMA instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) bf16 smem[NS * GH_STAGE];
+  typedef GhGeom<PK> Gg;
+  constexpr int PER = Gg::PER_A + Gg::PER_B;     // DMA instructions per wave per stage
+  constexpr int KK = PK / 32;                    // MFMA K slices per step
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * Gg::STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -662,19 +674,20 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
   const long in_elems = P * IC;
   const long p_begin = (long)split * J.pps;
   const long p_end = p_begin + J.pps < P ? p_begin + J.pps : P;
-  const int Wm = OW < GH_PK ? OW : GH_PK, RR = GH_PK / Wm, WR = Wm + 2, NR = RR + 2;
+  const int Wm = OW < PK ? OW : PK, RR = PK / Wm, WR = Wm + 2, NR = RR + 2;
 
-  unsigned aoff[1], boff[2], bfl[2];
+  unsigned aoff[Gg::PER_A], boff[Gg::PER_B], bfl[Gg::PER_B];
   {
     const int lrow = lane >> 4, pch = lane & 15;
-    {
-      const int trow = wave * 4 + lrow;
+#pragma unroll
+    for (int i = 0; i < Gg::PER_A; ++i) {
+      const int trow = (wave * Gg::PER_A + i) * 4 + lrow;
       const int lc = pch ^ (2 * (trow & 7));
-      aoff[0] = (unsigned)((trow * OC + m0 + lc * 8) * 2);
+      aoff[i] = (unsigned)((trow * OC + m0 + lc * 8) * 2);
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int wr = (wave * 2 + j) * 8 + (lane >> 3);
+    for (int j = 0; j < Gg::PER_B; ++j) {
+      const int wr = (wave * Gg::PER_B + j) * 8 + (lane >> 3);
       const int kh = wr / WR, px = wr - kh * WR;
       const int chunk = (lane & 7) ^ gh_swz(wr);
       const bool valid = wr < NR * WR;
@@ -685,6 +698,9 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
   }
   // transposed-read offsets (elements in a stage): lane (g, q, pc) reads K row
   // 4g + q (and + 16), 8-element chunk pc >> 1 of its 16 columns, half pc & 1
+  // (PK = 64 only on images W >= 64: a step is one row segment, so K slice
+  // kk is the slice-0 rows + 32 kk -- the swizzle's period divides 32 -- and
+  // the offsets of slice 0 serve every slice through the immediate)
   int la[4], lb[9], lbh[9];
   {
     const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
@@ -695,14 +711,14 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int r0 = f0 + (t / 3) * WR + (t % 3), r1 = f1 + (t / 3) * WR + (t % 3);
-      lb[t] = GH_PK * GH_BM + r0 * GH_BN + (((2 * wn + (pc >> 1)) ^ gh_swz(r0)) << 3) + (pc & 1) * 4;
-      lbh[t] = GH_PK * GH_BM + r1 * GH_BN + (((2 * wn + (pc >> 1)) ^ gh_swz(r1)) << 3) + (pc & 1) * 4;
+      lb[t] = PK * GH_BM + r0 * GH_BN + (((2 * wn + (pc >> 1)) ^ gh_swz(r0)) << 3) + (pc & 1) * 4;
+      lbh[t] = PK * GH_BM + r1 * GH_BN + (((2 * wn + (pc >> 1)) ^ gh_swz(r1)) << 3) + (pc & 1) * 4;
     }
   }
   auto issue = [&](long p0, int stage, bool on) {
-    bf16* sA = smem + stage * GH_STAGE;
-    gh_issue(sA, sA + GH_PK * GH_BM, dY, I, in_elems, p0, p_end, OC, IC, OH, OW, lw, Wm, RR, wave, aoff, boff, bfl,
-             on);
+    bf16* sA = smem + stage * Gg::STAGE;
+    gh_issue<PK>(sA, sA + PK * GH_BM, dY, I, in_elems, p0, p_end, OC, IC, OH, OW, lw, Wm, RR, wave, aoff, boff, bfl,
+                 on);
   };
 
   f32x4 acc[4][9];
@@ -710,7 +726,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const long nsteps = (p_end - p_begin) / GH_PK;          // (the planner keeps splits on 64-pixel bounds)
+  const long nsteps = (p_end - p_begin) / PK;             // (the planner keeps splits on 64-pixel bounds)
   const bool bias_wave = J.db != nullptr && bx == 0 && wn == 0;
   float bsum[4];
 #pragma unroll
@@ -718,53 +734,57 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
   const unsigned ones = 0x3F803F80u;
   // the dY fragments once per step; the window fragment of tap t + 1 is read
   // while tap t's eight MFMAs run (register budget: 288 accumulators)
-  auto rd_b = [&](const bf16* s, int t) {
-    gs16x4 lo = gw_tr_asm(s + lb[t]);
-    gs16x4 hi = gw_tr_asm(s + lbh[t]);
+  auto rd_b = [&](const bf16* s, int kk, int t) {
+    gs16x4 lo = gw_tr_asm(s + lb[t] + kk * 32 * GH_BN);
+    gs16x4 hi = gw_tr_asm(s + lbh[t] + kk * 32 * GH_BN);
     gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, v);
   };
   auto compute = [&](const bf16* s) {
-    bf16x8 af[4], bcur[1], bnext[1];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      gs16x4 lo = gw_tr_asm(s + la[i]);
-      gs16x4 hi = gw_tr_asm(s + la[i] + 16 * GH_BM);
-      gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      af[i] = __builtin_bit_cast(bf16x8, v);
-    }
-    bcur[0] = rd_b(s, 0);
-    gw_tr_wait<4, 1>(af, bcur);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if (t < 8) bnext[0] = rd_b(s, t + 1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[0], acc[i][t], 0, 0, 0);
-      if (t < 8) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        asm volatile("" : "+v"(bnext[0]));
-        bcur[0] = bnext[0];
-      }
-    }
-    if (bias_wave) {
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8 af[4], bcur[1], bnext[1];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const auto u = __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, af[i]);
+        gs16x4 lo = gw_tr_asm(s + la[i] + kk * 32 * GH_BM);
+        gs16x4 hi = gw_tr_asm(s + la[i] + kk * 32 * GH_BM + 16 * GH_BM);
+        gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+      bcur[0] = rd_b(s, kk, 0);
+      gw_tr_wait<4, 1>(af, bcur);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) bsum[i] = gw_dot2(u[w], ones, bsum[i]);
+      for (int t = 0; t < 9; ++t) {
+        if (t < 8) bnext[0] = rd_b(s, kk, t + 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[0], acc[i][t], 0, 0, 0);
+        if (t < 8) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          asm volatile("" : "+v"(bnext[0]));
+          bcur[0] = bnext[0];
+        }
+      }
+      if (bias_wave) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const auto u = __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, af[i]);
+#pragma unroll
+          for (int w = 0; w < 4; ++w) bsum[i] = gw_dot2(u[w], ones, bsum[i]);
+        }
       }
     }
   };
 #pragma unroll
-  for (int t = 0; t < NS - 1; ++t) issue(p_begin + t * GH_PK, t, t < nsteps);
+  for (int t = 0; t < NS - 1; ++t) issue(p_begin + t * PK, t, t < nsteps);
   for (long s = 0; s < nsteps; ++s) {
     const int st = (int)(s % NS);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PER) : "memory");
     __builtin_amdgcn_s_barrier();
     const long nx = s + NS - 1;
-    issue(p_begin + (nx < nsteps ? nx : s) * GH_PK, (int)(nx % NS), nx < nsteps);
+    issue(p_begin + (nx < nsteps ? nx : s) * PK, (int)(nx % NS), nx < nsteps);
     __builtin_amdgcn_s_setprio(1);
-    compute(smem + st * GH_STAGE);
+    compute(smem + st * Gg::STAGE);
     __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
@@ -931,6 +951,9 @@ static int g_gh_on = 1;
 // profiles/r4/halo_wgrad/)
 static int g_gh_blocks = 256;
 static int g_gh_ns = 2;            // LDS ring stages of wgrad_halo_k (2 or 3)
+// pixels per K-step of wgrad_halo_k on W >= 64 jobs (64: half the barriers per MFMA; L0 flush
+// 945 -> 1051 TF/s at bs128, profiles/r4/halo_pk64/); 32 elsewhere
+static int g_gh_pk = 64;
 
 D3D_API int d3d_wgrad_group_cfg(int blocks, int pk, int minpix) {
   if (blocks > 0) g_gw_blocks = blocks;
@@ -951,6 +974,10 @@ D3D_API int d3d_wgrad_group_halo(int on, int blocks, int ns) {
   if (on >= 0) g_gh_on = on > 2 ? 2 : on;
   if (blocks > 0) g_gh_blocks = blocks;
   if (ns == 2 || ns == 3) g_gh_ns = ns;
+  return 0;
+}
+D3D_API int d3d_wgrad_group_halo_pk(int pk) {
+  if (pk == 32 || pk == 64) g_gh_pk = pk;
   return 0;
 }
 
@@ -1062,16 +1089,19 @@ static void gw_plan(const WgJobDesc* d, int n, GwPlan& pl, bool halo = false) {
 // the per-tap 128 x 128 tile (everything else); one launch each, planned
 // separately (each fills the GPU on its own), one reduce for both.
 struct GwSplit {
-  WgJobDesc hd[GW_MAX], od[GW_MAX];
-  int hidx[GW_MAX], oidx[GW_MAX];
-  int hn = 0, on = 0;
-  GwPlan hp, op;
+  WgJobDesc hd[GW_MAX], qd[GW_MAX], od[GW_MAX];
+  int hidx[GW_MAX], qidx[GW_MAX], oidx[GW_MAX];
+  int hn = 0, qn = 0, on = 0;
+  GwPlan hp, qp, op;          // halo 32-pixel steps, halo 64-pixel steps (W >= 64), per-tap tile
   long ws_floats;
 };
 
 static void gw_split_plan(const WgJobDesc* d, int n, GwSplit& S) {
   for (int i = 0; i < n; ++i) {
-    if (gh_takes(d[i])) {
+    if (gh_takes(d[i]) && g_gh_pk == 64 && d[i].W >= 64) {
+      S.qidx[S.qn] = i;
+      S.qd[S.qn++] = d[i];
+    } else if (gh_takes(d[i])) {
       S.hidx[S.hn] = i;
       S.hd[S.hn++] = d[i];
     } else {
@@ -1079,11 +1109,12 @@ static void gw_split_plan(const WgJobDesc* d, int n, GwSplit& S) {
       S.od[S.on++] = d[i];
     }
   }
-  S.hp.ws_floats = S.op.ws_floats = 0;
-  S.hp.blocks = S.op.blocks = 0;
+  S.hp.ws_floats = S.qp.ws_floats = S.op.ws_floats = 0;
+  S.hp.blocks = S.qp.blocks = S.op.blocks = 0;
   if (S.hn) gw_plan(S.hd, S.hn, S.hp, true);
+  if (S.qn) gw_plan(S.qd, S.qn, S.qp, true);
   if (S.on) gw_plan(S.od, S.on, S.op, false);
-  S.ws_floats = S.hp.ws_floats + S.op.ws_floats;
+  S.ws_floats = S.hp.ws_floats + S.qp.ws_floats + S.op.ws_floats;
 }
 
 // fills tab (and appends the split jobs to rt) for the jobs of one engine
@@ -1157,20 +1188,27 @@ D3D_API long d3d_wgrad_group(const WgJobDesc* d, int n, float* ws, long ws_float
   GwSplit S;
   gw_split_plan(d, n, S);
   if (!ws) return S.ws_floats;
-  if (ws_floats < S.ws_floats || S.hp.blocks >= (1L << 31) || S.op.blocks >= (1L << 31)) return -3;
+  if (ws_floats < S.ws_floats || S.hp.blocks >= (1L << 31) || S.qp.blocks >= (1L << 31) ||
+      S.op.blocks >= (1L << 31))
+    return -3;
   GrTable rt{};
   long rblk = 0;
+  if (S.qn) {
+    GwTable tab;
+    const long blk = gw_tables(S.qd, S.qn, S.qp, ws + S.hp.ws_floats, true, tab, rt, rblk);
+    hipLaunchKernelGGL((wgrad_halo_k<2, 64>), dim3((unsigned)blk), dim3(512), 0, st, tab);
+  }
   if (S.hn) {
     GwTable tab;
     const long blk = gw_tables(S.hd, S.hn, S.hp, ws, true, tab, rt, rblk);
     if (g_gh_ns == 3)
-      hipLaunchKernelGGL(wgrad_halo_k<3>, dim3((unsigned)blk), dim3(512), 0, st, tab);
+      hipLaunchKernelGGL((wgrad_halo_k<3, 32>), dim3((unsigned)blk), dim3(512), 0, st, tab);
     else
-      hipLaunchKernelGGL(wgrad_halo_k<2>, dim3((unsigned)blk), dim3(512), 0, st, tab);
+      hipLaunchKernelGGL((wgrad_halo_k<2, 32>), dim3((unsigned)blk), dim3(512), 0, st, tab);
   }
   if (S.on) {
     GwTable tab;
-    const long blk = gw_tables(S.od, S.on, S.op, ws + S.hp.ws_floats, false, tab, rt, rblk);
+    const long blk = gw_tables(S.od, S.on, S.op, ws + S.hp.ws_floats + S.qp.ws_floats, false, tab, rt, rblk);
     if (g_gw_wide) {
       if (g_gw_pk == 64)
         hipLaunchKernelGGL(wgrad_grp2_k<64>, dim3((unsigned)blk), dim3(256), 0, st, tab);
@@ -1201,11 +1239,15 @@ D3D_API int d3d_wgrad_group_plan(const WgJobDesc* d, int n, int* splits, int* pp
     splits[S.hidx[i]] = S.hp.splits[i];
     pps[S.hidx[i]] = S.hp.pps[i];
   }
+  for (int i = 0; i < S.qn; ++i) {
+    splits[S.qidx[i]] = S.qp.splits[i];
+    pps[S.qidx[i]] = S.qp.pps[i];
+  }
   for (int i = 0; i < S.on; ++i) {
     splits[S.oidx[i]] = S.op.splits[i];
     pps[S.oidx[i]] = S.op.pps[i];
   }
-  if (blocks) *blocks = S.hp.blocks + S.op.blocks;
+  if (blocks) *blocks = S.hp.blocks + S.qp.blocks + S.op.blocks;
   return 0;
 }
 D3D_API int d3d_wgrad_group_engine(const WgJobDesc* d) { return gh_takes(*d) ? 1 : 0; }

@@ -626,7 +626,7 @@ def _wg_ref(g, x, taps):
 @pytest.mark.parametrize("pk,blocks,minpix,wide,halo,ns", [
     (32, 512, 512, 0, 2, 2), (32, 512, 512, 0, 0, 2), (64, 512, 512, 0, 2, 2), (32, 4096, 64, 0, 2, 2),
     (32, 4096, 64, 0, 0, 2), (32, 512, 512, 1, 0, 2), (32, 512, 512, 0, 2, 3), (32, 64, 512, 0, 2, 2),
-    (32, 512, 512, 0, 1, 2)])
+    (32, 512, 512, 0, 1, 2), (32, 512, 512, 0, 3, 2), (32, 4096, 64, 0, 3, 2)])
 def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
     """Grouped weight gradients (wgrad_group.hip): the per-tap 128 x 128 tile
     launch and the all-taps halo tile launch (3x3 jobs on W % 32 == 0 images)
@@ -638,7 +638,9 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
     torch.manual_seed(5)
     H._lib.d3d_wgrad_group_cfg(blocks, pk, minpix)
     H._lib.d3d_wgrad_group_wide(wide)
-    H._lib.d3d_wgrad_group_halo(halo, blocks, ns)
+    # halo 3: the 64-pixel K-step halo kernel for the W >= 64 jobs (the rest as halo 1)
+    H._lib.d3d_wgrad_group_halo(1 if halo == 3 else halo, blocks, ns)
+    H._lib.d3d_wgrad_group_halo_pk(64 if halo == 3 else 32)       # (restored to the default 64 below)
     try:
         jobs, refs, outs = [], [], []
         for (N, Hh, W, IC, OC, taps, C1, bias) in WG_JOBS:
@@ -681,7 +683,8 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
             assert min(sp) == 1, list(sp)                     # ... and the direct OIHW epilogue
         if halo:
             hs = [s_ for s_, e in zip(sp, eng) if e]
-            assert (blocks > 1024 or min(hs) == 1) and (blocks < 512 or max(hs) > 1), hs
+            # (halo 3 plans the W >= 64 jobs in a launch of their own: the small job may split)
+            assert (blocks > 1024 or halo == 3 or min(hs) == 1) and (blocks < 512 or max(hs) > 1), hs
         for (_, _, dw0, db0), (dw, db, _) in zip(refs, outs):  # re-run: bitwise
             dw.copy_(dw0)
             if db is not None:
@@ -696,6 +699,7 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
         H._lib.d3d_wgrad_group_cfg(512, 32, 512)
         H._lib.d3d_wgrad_group_wide(0)
         H._lib.d3d_wgrad_group_halo(1, 512, 2)
+        H._lib.d3d_wgrad_group_halo_pk(64)
 
 
 @pytest.mark.parametrize("micro", [2, 0])
