@@ -990,7 +990,10 @@ __device__ __forceinline__ void halo_issue_b(bf16* sH, const bf16* I, int in_byt
 // linear in the shift, and computing it per step cost ~48 VALU per 32 MFMAs
 // on the critical path between the barrier and the first MFMA.  (Without the
 // residual prefetch only: with it the register file overflows.)
-template <int OWT, bool TRANS, int BNT = 512, bool PF = false, bool RES = true, bool AU = false>
+// P2 (with AU): one barrier per PAIR of taps over an 8-slot weight ring (the
+// LDS budget of the 64-wide tile: 2 x 48 KB halo + 64 KB ring = all 160 KB);
+// halves the per-MFMA barrier / wait cost.  Needs an even chunk count.
+template <int OWT, bool TRANS, int BNT = 512, bool PF = false, bool RES = true, bool AU = false, bool P2 = false>
 __global__ void __launch_bounds__(512, 1)
 conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
@@ -998,9 +1001,9 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
             float* __restrict__ gnp, int gn_groups, bf16* __restrict__ O2, GnbArgs gb) {
   typedef HaloGeom<OWT, BNT> Gm;
   constexpr int BM = 128, BN = BNT, WM = 64, WN = BN / 4, TM = 4, TN = WN / 16;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * Gm::HBUF + 4 * Gm::ABUF];
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * Gm::HBUF + (P2 ? 8 : 4) * Gm::ABUF];
   bf16* const sH = smem;                       // [2][HBUF]
-  bf16* const sAr = smem + 2 * Gm::HBUF;       // [4][ABUF]
+  bf16* const sAr = smem + 2 * Gm::HBUF;       // [4 or 8][ABUF]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1147,6 +1150,67 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
         for (int j = 0; j < TN; ++j) bfr[j] = bn[j];
       }
     }
+  } else if constexpr (AU && P2) {
+  // prologue: halo of chunk 0, weights of steps 0..3
+  halo_issue_b<Gm::HPW>(sH, I, in_bytes, hoff, 0, wave);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) halo_issue_a(sAr + k * Gm::ABUF, Wp, w_bytes, aoff, a_soff(k), wave);
+  int bo[3][TN], ao[TM];
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int hp = hp0[j] + kw;
+      bo[kw][j] = hp * HALO_CH + ((fq ^ ((hp >> 1) & 2)) << 3);
+    }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int row = wm * WM + i * 16 + fr;
+    ao[i] = row * HALO_CH + ((fq ^ ((row >> 1) & 2)) << 3);
+  }
+  auto step = [&](int s, int t, const bf16* hb) {
+    const bf16* a = sAr + (s & 7) * Gm::ABUF;
+    const int kh = TRANS ? 2 - t / 3 : t / 3, kw = TRANS ? 2 - t % 3 : t % 3;
+    bf16x8 af[TM], bfr[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(hb + kh * Gm::HW2 * HALO_CH + bo[kw][j]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a + ao[i]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  };
+  // chunks in pairs (18 steps = 9 tap pairs per iteration); step s: chunk s / 9,
+  // tap s % 9, weights in ring slot s & 7, issued 4 steps ahead.  Halo of the
+  // next chunk issued at the first pair after the previous chunk's last step
+  // (pairs 0 and 5 of an iteration); waits allow the newer halo pieces in
+  // flight at the two pairs after its issue.
+  for (int c2 = 0; c2 < NCH; c2 += 2) {
+    const int S0 = c2 * 9;
+#pragma unroll
+    for (int pp = 0; pp < 9; ++pp) {
+      if (pp == 1 || pp == 2 || pp == 6 || pp == 7) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + Gm::HPW) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      const int s0 = S0 + 2 * pp;
+      halo_issue_a(sAr + ((s0 + 4) & 7) * Gm::ABUF, Wp, w_bytes, aoff, a_soff(s0 + 4), wave);
+      halo_issue_a(sAr + ((s0 + 5) & 7) * Gm::ABUF, Wp, w_bytes, aoff, a_soff(s0 + 5), wave);
+      if (pp == 0 || pp == 5) {
+        const int cn0 = c2 + (pp == 0 ? 1 : 2), cn = cn0 < NCH ? cn0 : NCH - 1;
+        halo_issue_b<Gm::HPW>(sH + (cn0 & 1) * Gm::HBUF, I, in_bytes, hoff, cn * HALO_CH * 2, wave);
+      }
+      __builtin_amdgcn_s_setprio(1);
+      const int sr0 = 2 * pp, sr1 = 2 * pp + 1;            // steps within the chunk pair
+      step(S0 + sr0, sr0 % 9, sH + (sr0 / 9) * Gm::HBUF);
+      step(S0 + sr1, sr1 % 9, sH + (sr1 / 9) * Gm::HBUF);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
   } else if constexpr (AU) {
   halo_issue_b<Gm::HPW>(sH, I, in_bytes, hoff, 0, wave);
   halo_issue_a(sAr, Wp, w_bytes, aoff, a_soff(0), wave);
@@ -2758,13 +2822,16 @@ static int g_halo_w32 = 1;
 // bench +0.6 % bs128, +1.5 % bs16 (profiles/r4/halo_small/)
 static int g_halo_w16 = 1;
 static int g_halo_w32s = 1;
+static int g_halo_p2 = 1;          // tap pairs per barrier (8-slot weight ring) on the 512-pixel tiles
 // knob: bits 0-1 AU (0 off / 1 on), bit 2 the 32-wide halo, bit 3 the 16-wide halo, bit 4 the 8-row
-// 32-wide tiles (D3D_HALO_AU=29: all, the default)
+// 32-wide tiles, bit 5 tap pairs per barrier (D3D_HALO_AU=61: all, the default; 29: all but
+// the tap pairs -- profiles/r4/halo_p2: fwd -2..4 % on the N=256 levels, bs128 +0.7 %, bs16 +0.3 %)
 D3D_API int d3d_conv_halo_cfg(int au) {
   g_halo_au = au & 3;
   g_halo_w32 = (au >> 2) & 1;
   g_halo_w16 = (au >> 3) & 1;
   g_halo_w32s = (au >> 4) & 1;
+  g_halo_p2 = (au >> 5) & 1;
   return 0;
 }
 D3D_API int d3d_conv_res_cfg(int always) {
@@ -2898,13 +2965,15 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
     auto nblk = [&](int bn) { return OH % (bn / OW) ? 0L : (long)N * (OH / (bn / OW)) * (OC / 128); };
     if ((OW != 32 || g_halo_w32) && nblk(512) >= 256) {
       dim3 gh((unsigned)(N * (OH / (512 / OW))), (unsigned)(OC / 128), 1);
-#define HALO2(OWv, TR, RS, AUv)                                                                                   \
-  hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512, false, RS, AUv>), gh, dim3(512), 0, st, (const bf16*)I,          \
+#define HALO3(OWv, TR, RS, AUv, P2v)                                                                              \
+  hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512, false, RS, AUv, (P2v && OWv != 128)>), gh, dim3(512), 0, st, (const bf16*)I,     \
                      (const bf16*)Wp, bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, \
                      IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, gb)
+#define HALO2(OWv, TR, RS, AUv) HALO3(OWv, TR, RS, AUv, false)
 #define HALO(OWv, TR, RS)                                                                                          \
   do {                                                                                                            \
-    if (g_halo_au) HALO2(OWv, TR, RS, true);                                                                        \
+    if (g_halo_au && g_halo_p2 && OWv != 128 && (IC / HALO_CH) % 2 == 0) HALO3(OWv, TR, RS, true, true);          \
+    else if (g_halo_au) HALO2(OWv, TR, RS, true);                                                                   \
     else HALO2(OWv, TR, RS, false);                                                                                 \
   } while (0)
       if (OW == 64) {
@@ -2919,6 +2988,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
       }
 #undef HALO
 #undef HALO2
+#undef HALO3
       if (gn_done && gnp) *gn_done = 1;
       if (silu_done && O2) *silu_done = 1;
       if (gnb_done && gb.grp) *gnb_done = 1;
