@@ -56,11 +56,11 @@ constexpr int G_PK = 64;         // K per LDS stage (two steps): 128-byte rows, 
 // ds_read_b128 lane groups read 16 rows at one chunk: conflict-free)
 __device__ __forceinline__ int g_swz(int row, int chunk) { return row * G_PK + ((chunk ^ (row & 7)) << 3); }
 
-template <int WI, int WJ>
+template <int WI, int WJ, int NST = 2>
 struct GCfg {
   static constexpr int BM = 32 * WI, BN = 32 * WJ;       // 2 x 2 waves of 16*WI x 16*WJ
   static constexpr int STAGE = (BM + BN) * G_PK;         // bf16 per stage (two K-steps)
-  static constexpr int BIAS = 2 * STAGE;                 // 4 slots of 256 fp32
+  static constexpr int BIAS = NST * STAGE;               // 4 slots of 256 fp32
   static constexpr int LDS = BIAS + 4 * 512;
   static constexpr int DA = BM / 32, DB = BN / 32;       // DMA pieces (8 rows x 128 B) per wave and stage
   static constexpr int ND = DA + DB;
@@ -158,13 +158,18 @@ __device__ __forceinline__ void g_epi_pair(const f32x4 (&acc)[WI][WJ], const GEp
   __builtin_amdgcn_sched_barrier(0);       // one pair at a time: bounded live registers
 }
 
-template <int WI, int WJ, int F>
+// NST: LDS stages in the ring (NST - 1 DMAs in flight).  The small problems
+// (one or two tiles per CU, K <= 1024: attention / NIN projections and their
+// input gradients at 8x8 .. 32x32) are latency-bound with two stages -- each
+// stage waits a whole HBM round trip for 8 MFMAs -- so they take 4.
+template <int WI, int WJ, int F, int NST = 2>
 __global__ void __launch_bounds__(256, 1)
 gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ O, const float* __restrict__ bias,
           const bf16* __restrict__ R, int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha,
           float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw) {
   constexpr bool BIAS = (F & (F_B32 | F_B16)) != 0, BBF = (F & F_B16) != 0;
-  using C = GCfg<WI, WJ>;
+  using C = GCfg<WI, WJ, NST>;
+  static_assert(NST == 2 || NST == 4, "stage ring of 2 or 4 (4 bias slots: <= 3 tiles ahead at K >= 128)");
   __shared__ __attribute__((aligned(16))) bf16 smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -273,12 +278,16 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   tile_mn(tile, mb, nb);
   bias_dma();
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {              // stages 0 and 1: K-steps 0..3
+  for (int k = 0; k < NST; ++k) {            // stages 0 .. NST-1 (may run into the next tiles)
 #pragma unroll
     for (int d = 0; d < C::ND; ++d) dma(k, d);
     advance();
+    // the cursor entered the next tile: its bias (K = 128 crosses inside the
+    // prologue; without this the second tile of a block read a stale slot)
+    if (lkb == 0) bias_dma();
   }
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::ND) : "memory");
+  // stage 0 landed (a bias DMA between stages only makes the count stricter)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 1) * C::ND) : "memory");
   G_BAR();
 #pragma unroll
   for (int j = 0; j < WJ; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + fb0 + j * 16 * G_PK);
@@ -305,14 +314,16 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
       // whenever an LDS-heavy kernel shared the CU (the per-pixel weight
       // gradients on the side stream): wrong GEMM outputs under co-residency
       // (tools/stress_concurrent.py, profiles/race_graph_wgrad_flush_r3.txt).
-      if (after_epi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(C::NS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      // stage p + 1 landed; stages p + 2 .. p + NST - 1 (and the epilogue's
+      // stores) may stay in flight
+      if (after_epi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * C::ND + C::NS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * C::ND) : "memory");
       G_BAR();
     }
     // next K-step's fragments: second half of this stage, or first half of the next
-    const bf16* sn = smem + (ODD ? (((s >> 1) + 1) & 1) : ((s >> 1) & 1)) * C::STAGE;
+    const bf16* sn = smem + (ODD ? (((s >> 1) + 1) & (NST - 1)) : ((s >> 1) & (NST - 1))) * C::STAGE;
     const int ra = ODD ? fa0 : fa1, rbo = ODD ? fb0 : fb1;
-    const int ls = (s >> 1) & 1;
+    const int ls = (s >> 1) & (NST - 1);        // stage p's slot: refilled with stage p + NST
     g_for(std::make_integer_sequence<int, C::NM>{}, [&](auto kc) {
       constexpr int k = decltype(kc)::value;
       if constexpr (decltype(first)::value) g_mma0(acc[k / WJ][k % WJ], ca[k / WJ], cb[k % WJ]);
@@ -417,8 +428,8 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
     if (tile >= ntiles) break;
     ++ti;
     tile_mn(tile, mb, nb);
-    {   // first fragments of the next tile: stage (s / 2) & 1, published by the last body's barrier
-      const bf16* sn = smem + ((s >> 1) & 1) * C::STAGE;
+    {   // first fragments of the next tile: stage s / 2, published by the last body's barrier
+      const bf16* sn = smem + ((s >> 1) & (NST - 1)) * C::STAGE;
 #pragma unroll
       for (int j = 0; j < WJ; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(sn + fb0 + j * 16 * G_PK);
 #pragma unroll
@@ -432,6 +443,7 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
 static int g_cfg_force = 0;     // 0: by problem size; 8 / 4 / 2: force the WI = WJ tile
 static int g_gm = 8;
 static int g_grid = 0;          // 0: resident blocks on every CU
+static int g_deep = 1;          // 4-stage ring for the 64 / 128 tiles of small problems
 static int g_cus() {
   static int n = 0;
   if (!n) {
@@ -443,12 +455,15 @@ static int g_cus() {
 }
 
 // Tuning switches for in-process A/B (forced tile config, tile-group width,
-// grid); a value <= 0 leaves the setting unchanged (cfg 1 restores the size rule).
+// grid); 0 leaves a setting unchanged (cfg 1 restores the size rule, cfg -1 / -2
+// turn the deep stage ring on / off, grid -1 restores the resident grid).
 D3D_API void d3d_gemm_tune(int cfg, int gm, int grid) {
-  if (cfg == 1) g_cfg_force = 0;
+  if (cfg == -1 || cfg == -2) g_deep = cfg == -1;       // -1 / -2: deep stage ring on / off
+  else if (cfg == 1) g_cfg_force = 0;
   else if (cfg > 0) g_cfg_force = cfg;
   if (gm > 0) g_gm = gm;
   if (grid > 0) g_grid = grid;
+  else if (grid < 0) g_grid = 0;                        // back to resident blocks on every CU
 }
 
 // Tile configuration for a problem: the 256 x 256 tile when it gives the chip
@@ -473,13 +488,13 @@ D3D_API int d3d_gemm_nt_ok(int M, int N, int K, int lda, int ldb) {
   return 1;
 }
 
-template <int W, int F>
+template <int W, int F, int NST = 2>
 static void g_launch(int G_, hipStream_t st, const void* A, const void* B, void* O, const void* bias, const void* R,
                      int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, int mt, int nt,
                      int gm, float* gnp, int G, int hw) {
-  hipLaunchKernelGGL((gemm_fw_k<W, W, F>), dim3(G_), dim3(256), 0, st, (const bf16*)A, (const bf16*)B, (bf16*)O,
-                     (const float*)bias, (const bf16*)R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G,
-                     hw);
+  hipLaunchKernelGGL((gemm_fw_k<W, W, F, NST>), dim3(G_), dim3(256), 0, st, (const bf16*)A, (const bf16*)B,
+                     (bf16*)O, (const float*)bias, (const bf16*)R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt,
+                     gm, gnp, G, hw);
 }
 
 // epi 0: O = (alpha * A.B^T + bias + R) * scale (+ GroupNorm partials gnp:
@@ -505,6 +520,9 @@ D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, i
   const int mt = cdiv(M, BT), nt = cdiv(N, BT);
   const long tiles = (long)mt * nt;
   if (tiles >= (1L << 31)) return -1;
+  // deep ring (68 KB / 130 KB of LDS: 2 / 1 blocks per CU) when those
+  // resident blocks hold every tile -- the latency-bound small problems
+  const bool deep = g_deep && W != 8 && tiles <= (long)g_cus() * (W == 4 ? 1 : 2);
   const int per_cu = W == 8 ? 1 : W == 4 ? 2 : 4;
   const int G_ = (int)std::min<long>(tiles, g_grid > 0 ? g_grid : (long)g_cus() * per_cu);
   const int gm = std::max(1, std::min(mt, g_gm));
@@ -512,7 +530,11 @@ D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, i
                           : (bias_ ? (bias_bf16 ? F_B16 : F_B32) : 0) | (R ? F_RES : 0) | (gnp ? F_GN : 0);
 #define G_CASE(W_, F_)                                                                                          \
   if (W == W_ && F == (F_)) {                                                                                   \
-    g_launch<W_, F_>(G_, st, A, B, O, bias_, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, hw); \
+    if (W_ != 8 && deep)                                                                                        \
+      g_launch<W_, F_, (W_ != 8 ? 4 : 2)>(G_, st, A, B, O, bias_, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, \
+                                          nt, gm, gnp, G, hw);                                                  \
+    else                                                                                                        \
+      g_launch<W_, F_>(G_, st, A, B, O, bias_, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, hw); \
     return (int)hipGetLastError();                                                                              \
   }
 #define G_CASES(W_)                                                                                             \

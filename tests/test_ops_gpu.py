@@ -298,6 +298,39 @@ def test_gemm_nt(H, cfg, M, N, K, lda, ldb, ldo, bias, res, alpha, scale):
 
 
 @pytest.mark.parametrize("cfg", [8, 4, 2])
+@pytest.mark.parametrize("grid", [0, 7])
+@pytest.mark.parametrize("K", [128, 192, 512])
+def test_gemm_deep_ring(H, cfg, grid, K):
+    """4-stage LDS ring of the small-problem GEMM (gemm.hip NST): equals the
+    2-stage ring bit for bit and the fp32 product -- one tile per block, and a
+    forced 7-block grid where each block walks many tiles with the loader up to
+    two tiles ahead (bias slots, K = 128: two stages per tile).  cfg 8 (2-stage
+    only) pins the K = 128 multi-tile bias: the prologue crossed into a block's
+    second tile without loading its bias (the bs128 128->256 skip projection)."""
+    torch.manual_seed(17)
+    M, N = 200, 1000
+    a = torch.randn(M, K, device=DEV).to(BF)
+    b = torch.randn(N, K, device=DEV).to(BF)
+    bb = torch.randn(M, device=DEV)
+    r = torch.randn(N, M, device=DEV).to(BF)
+    outs = []
+    try:
+        for deep in (-1, -2):
+            H._lib.d3d_gemm_tune(deep, 0, 0)
+            H._lib.d3d_gemm_tune(cfg, 0, grid if grid else 0)
+            out = torch.empty(N, M, device=DEV, dtype=BF)
+            H.gemm_nt(a, b, out, M, N, K, K, K, M, bias=bb, res=r, alpha=0.5, scale=0.75)
+            outs.append(out)
+    finally:
+        H._lib.d3d_gemm_tune(-1, 0, 0)
+        H._lib.d3d_gemm_tune(1, 0, 0)
+        H._lib.d3d_gemm_tune(0, 0, -1)
+    ref = ((b.float() @ a.float().t()) * 0.5 + bb + r.float()) * 0.75
+    assert rel(outs[0], ref) < 1e-2
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("cfg", [8, 4, 2])
 def test_gemm_bf16_bias_and_dsilu_epilogue(H, cfg):
     """bf16 bias, the in-place residual (out == res) of the virtual-concat
     skip, and the dsilu epilogue (FiLM input gradient) against fp32."""

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Deep (4-stage) LDS ring for the small-problem GEMM: numerics, kernel A/B, step A/B
+set -o pipefail
+O=gpurun_out/r4ac
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_ops_gpu.py -x -q --timeout 120 --timeout-method thread -m gpu -k "gemm or linear or full_model or attn" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 200 python tools/kbench_gemm_small.py > $O/kg.jsonl 2> $O/err.txt || { tail $O/err.txt; exit 1; }
+cat $O/kg.jsonl
+for i in 1 2; do for g in -1 -2; do
+  D3D_GEMM_TUNE=$g,0,0 timeout -k 10 300 python bench.py --global_batch 16 --steps 30 --warmup 5 > $O/b16_${g}_$i.json 2> $O/b16.err || { tail $O/b16.err; exit 1; }
+  D3D_GEMM_TUNE=$g,0,0 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > $O/b128_${g}_$i.json 2> $O/b128.err || { tail $O/b128.err; exit 1; }
+  python -c "import json;[print('g$g',f,json.load(open('$O/'+f+'_${g}_$i.json'))['value']) for f in ('b128','b16')]"
+done; done
