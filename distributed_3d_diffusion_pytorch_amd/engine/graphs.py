@@ -39,11 +39,31 @@ added to every mask kernel's baked seed) and the Adam block ``hp``.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import os
 from typing import Optional
 
 import torch
 import torch.distributed as dist
+
+
+@contextlib.contextmanager
+def _gc_paused():
+    """No Python garbage collection while a stream is being captured: a dead
+    reference cycle (e.g. a previous Trainer and its CUDAGraphs) finalised by
+    a collection that happens to run mid-capture destroys a graph / releases a
+    graph memory pool inside the capture -- an illegal call that aborts the
+    process (torch >= 2.9 no longer collects before capture by default).  The
+    cycles are collected here, before the capture begins."""
+    was = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def probe_graph_collective(device: torch.device) -> bool:
@@ -63,7 +83,7 @@ def probe_graph_collective(device: torch.device) -> bool:
         torch.cuda.current_stream(device).wait_stream(s)
         torch.cuda.synchronize(device)      # the warm-up has completed (see _capture on the watchdog)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        with _gc_paused(), torch.cuda.graph(g, capture_error_mode="thread_local"):
             w = dist.all_reduce(x, async_op=True)
             w.wait()
             x.mul_(2.0)
@@ -260,18 +280,19 @@ class GraphedTrainStep:
         mode = "thread_local" if comm else "global"     # RCCL's watchdog thread keeps querying events
         # graphs sharing a memory pool are captured in their replay order
         # (leading micro-batches first)
-        if comm and nchunks > 1:
-            self.gA0 = torch.cuda.CUDAGraph()
-            self.gA0.register_generator_state(tr.gen)
-            with torch.cuda.graph(self.gA0, pool=self.pool, capture_error_mode=mode):
-                self._body(False)
-        self.gA = torch.cuda.CUDAGraph()
-        self.gA.register_generator_state(tr.gen)
-        with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
-            self._body(comm, defer=self.defer)
-        self.gB = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.gB, pool=self.pool, capture_error_mode=mode):
-            self._update()
+        with _gc_paused():
+            if comm and nchunks > 1:
+                self.gA0 = torch.cuda.CUDAGraph()
+                self.gA0.register_generator_state(tr.gen)
+                with torch.cuda.graph(self.gA0, pool=self.pool, capture_error_mode=mode):
+                    self._body(False)
+            self.gA = torch.cuda.CUDAGraph()
+            self.gA.register_generator_state(tr.gen)
+            with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
+                self._body(comm, defer=self.defer)
+            self.gB = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.gB, pool=self.pool, capture_error_mode=mode):
+                self._update()
         torch.cuda.synchronize()
         tr.gen.set_state(gstate)
         # scope the device seed word to the replays (an eager forward after

@@ -230,7 +230,8 @@ class DiffusionSampler:
         hip_impl.refresh_weights()
         torch.cuda.synchronize(dev)
         graph = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(graph):
+        from .graphs import _gc_paused            # (no collection finalising old graphs mid-capture)
+        with torch.no_grad(), _gc_paused(), torch.cuda.graph(graph):
             body()
         torch.cuda.synchronize(dev)
         g["z"].copy_(z_keep)
