@@ -711,6 +711,9 @@ assert ctypes.sizeof(_GnbArgs) == 64
 # the epilogue costs the halo dgrad +25-40 % while the reduce pass it
 # replaces is a bandwidth-bound 30-160 us); kept for A/B and its tests.
 _GNB_EPI = os.environ.get("D3D_GNB_EPI", "0") != "0"
+_GEMM_DEEP8 = os.environ.get("D3D_GEMM_DEEP8", "0") == "1"   # 8-stage LDS ring, one 64-tile block per CU
+if os.environ.get("D3D_GEMM_DEEP8"):
+    _lib.d3d_gemm_tune(-3 if _GEMM_DEEP8 else -4, 0, 0)
 if os.environ.get("D3D_GEMM_TUNE"):     # A/B knob "cfg,gm,grid" (gemm.hip d3d_gemm_tune; 0 keeps a value)
     _lib.d3d_gemm_tune(*[int(v) for v in os.environ["D3D_GEMM_TUNE"].split(",")])
 if os.environ.get("D3D_HALO_AU"):        # A/B knob: halo conv with unrolled taps / precomputed offsets (1) or not (0)

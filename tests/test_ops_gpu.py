@@ -299,7 +299,7 @@ def test_gemm_nt(H, cfg, M, N, K, lda, ldb, ldo, bias, res, alpha, scale):
 
 @pytest.mark.parametrize("cfg", [8, 4, 2])
 @pytest.mark.parametrize("grid", [0, 7])
-@pytest.mark.parametrize("K", [128, 192, 512])
+@pytest.mark.parametrize("K", [128, 192, 512, 1536])
 def test_gemm_deep_ring(H, cfg, grid, K):
     """4-stage LDS ring of the small-problem GEMM (gemm.hip NST): equals the
     2-stage ring bit for bit and the fp32 product -- one tile per block, and a
@@ -315,8 +315,9 @@ def test_gemm_deep_ring(H, cfg, grid, K):
     r = torch.randn(N, M, device=DEV).to(BF)
     outs = []
     try:
-        for deep in (-1, -2):
+        for deep, deep8 in ((-1, -3), (-1, -4), (-2, -4)):      # 8-, 4-, 2-stage rings
             H._lib.d3d_gemm_tune(deep, 0, 0)
+            H._lib.d3d_gemm_tune(deep8, 0, 0)
             H._lib.d3d_gemm_tune(cfg, 0, grid if grid else 0)
             out = torch.empty(N, M, device=DEV, dtype=BF)
             H.gemm_nt(a, b, out, M, N, K, K, K, M, bias=bb, res=r, alpha=0.5, scale=0.75)
@@ -325,9 +326,10 @@ def test_gemm_deep_ring(H, cfg, grid, K):
         H._lib.d3d_gemm_tune(-1, 0, 0)
         H._lib.d3d_gemm_tune(1, 0, 0)
         H._lib.d3d_gemm_tune(0, 0, -1)
+        H._lib.d3d_gemm_tune(-3 if H._GEMM_DEEP8 else -4, 0, 0)
     ref = ((b.float() @ a.float().t()) * 0.5 + bb + r.float()) * 0.75
     assert rel(outs[0], ref) < 1e-2
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 @pytest.mark.parametrize("cfg", [8, 4, 2])
