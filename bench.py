@@ -163,6 +163,9 @@ def main() -> None:
     sync()
     dt = time.perf_counter() - t0
     trainer.sync()          # (a deferred update of the last timed step; outside the timed region)
+    # memory record of the benchmark itself (the comm diagnostics below capture / run extra steps)
+    hbm_peak = round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if ctx.device.type == "cuda" else None
+    retries = torch.cuda.memory_stats().get("num_alloc_retries", 0) if ctx.device.type == "cuda" else None
     comm = comm_diagnostics(trainer, pool, ctx) if (trainer.reducer is not None and trainer.reducer.active) else None
     if prof is not None:
         prof.__exit__(None, None, None)
@@ -200,14 +203,24 @@ def main() -> None:
             "final_loss": lv,
             # N > 1: what the gradient communication did (measured after the timed steps)
             "comm": comm,
-            "hbm_peak_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if ctx.device.type == "cuda" else None,
+            "hbm_peak_gib": hbm_peak,
             # caching-allocator retries (a full cache flush + device sync each): non-zero means the step
             # ran at the HBM limit and paid for it
-            "alloc_retries": torch.cuda.memory_stats().get("num_alloc_retries", 0) if ctx.device.type == "cuda"
-            else None,
+            "alloc_retries": retries,
+            # (op, shape) pairs that left the HIP kernels for the torch composition (only possible with
+            # D3D_ALLOW_TORCH_FALLBACK=1; otherwise such a shape is an error)
+            "fallbacks": _fallback_count(),
         }
         print(json.dumps(out), flush=True)
     cleanup()
+
+
+def _fallback_count() -> int:
+    try:
+        from distributed_3d_diffusion_pytorch_amd.ops import hip_impl
+    except Exception:           # noqa: BLE001 -- no native library (CPU plumbing run)
+        return 0
+    return len(hip_impl.FALLBACKS)
 
 
 def comm_diagnostics(trainer, pool, ctx) -> dict:
@@ -254,6 +267,7 @@ def bench_sample(args) -> None:
     sampler and stochastic conditioning (sampling.py:129-155) for a batch of
     `sample_batch` chains on one GPU (random-init weights, synthetic poses)."""
     from distributed_3d_diffusion_pytorch_amd.models import XUNet
+    from distributed_3d_diffusion_pytorch_amd.models.flops import forward_flops
     from distributed_3d_diffusion_pytorch_amd.engine import DiffusionSampler, RecordEntry
     from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
     from distributed_3d_diffusion_pytorch_amd import ops
@@ -289,9 +303,10 @@ def bench_sample(args) -> None:
            "vs_baseline": None, "dtype": "bf16", "data": "synthetic poses/images, random-init weights",
            "config": {"model": "XUNet ch128 136.7M", "global_batch": b, "cfg_batch": 2 * b, "image_size": S,
                       "parallelism": "single", "shared_conditioning": share},
-           # FLOPs of the plain per-example 2b forward / time (the shared
-           # conditioning path executes ~38 % fewer, so this is an equivalent rate)
-           "per_example_equiv_tflops": round(2 * b * 235.9e9 * (S / 64.0) ** 2 * args.timesteps / dt / 1e12, 1),
+           # FLOPs the step actually executes (models/flops.py: the 2b-example
+           # trunk, the conditioning part on the 2 CFG classes when shared)
+           "executed_tflops": round(forward_flops(model, 2 * b, 2 if share else None) * args.timesteps / dt / 1e12,
+                                    1),
            "finite": bool(torch.isfinite(out).all())}
     print(json.dumps(res), flush=True)
 

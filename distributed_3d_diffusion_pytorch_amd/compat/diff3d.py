@@ -20,6 +20,8 @@ reference's version uses un-imported ``tqdm``/``time``, D13).
 """
 from __future__ import annotations
 
+import operator
+
 from typing import Optional
 
 import torch
@@ -159,11 +161,18 @@ class Diff3D(nn.Module):
         included).  Note the return type: the per-step list by default (as
         the reference), the final tensor only with ``return_all=False``."""
         if isinstance(model, torch.Tensor):
+            if K is None:
+                # sample(img, R, T, K, w=...): the keyword w lands in the wrong slot of the shifted form
+                raise TypeError("sample(img, R, T, K, w, timesteps): in the model-less form pass w (and "
+                                "timesteps) positionally, or call sample(None, img, R, T, K, w=..., timesteps=...)")
             if w is not None:
-                if not isinstance(w, int) or isinstance(w, bool):
-                    raise TypeError("sample(img, R, T, K, w, timesteps): timesteps must be an int, "
-                                    f"got {type(w).__name__}")
-                timesteps = w
+                if isinstance(w, bool):
+                    raise TypeError("sample(img, R, T, K, w, timesteps): timesteps must be an integer, got bool")
+                try:
+                    timesteps = operator.index(w)      # int, numpy integers, 0-d integer tensors
+                except TypeError:
+                    raise TypeError("sample(img, R, T, K, w, timesteps): timesteps must be an integer, "
+                                    f"got {type(w).__name__}") from None
             model, img, R, T, K, w = None, model, img, R, T, K
         net = model if model is not None else self.xunet_denoiser
         dev = next(net.parameters()).device

@@ -406,7 +406,10 @@ class GraphedTrainStep:
         self.H.set_device_seed(self.seed)
         try:
             torch.cuda.synchronize()
-            with torch.cuda.graph(g0, pool=torch.cuda.graph_pool_handle(), capture_error_mode="thread_local"):
+            # (GC paused like every other capture: a collection finalising an
+            # old graph mid-capture aborts the process, uncatchably)
+            with _gc_paused(), torch.cuda.graph(g0, pool=torch.cuda.graph_pool_handle(),
+                                                capture_error_mode="thread_local"):
                 self._body(False, defer=self.defer)
         finally:
             self.H.set_device_seed(None)

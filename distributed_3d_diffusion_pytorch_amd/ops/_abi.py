@@ -56,8 +56,7 @@ SIGNATURES = {
     "d3d_pack_conv_weight": [P, P, I, I, I, I, I, P],
     "d3d_conv": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P],
     "d3d_conv2": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P],
-    "d3d_conv3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P, IP, P, IP, P],
-    "d3d_gn_bwd_apply_parts": [I, P, P, P, P, P, I, I, I, I, P, P, P, P, P, I, I, P, P, I, P, F, P, F, P],
+    "d3d_conv3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P, IP, P],
     "d3d_conv_plan": [I, I, I, I, I, I],
     "d3d_set_conv_korder": [I],
     "d3d_set_wgrad_impl": [I],
@@ -98,7 +97,6 @@ SIGNATURES = {
     # wgrad_group.hip (job tables: arrays of hip_impl._WgJob)
     "d3d_wgrad_group_cfg": [I, I, I],
     "d3d_wgrad_group_ok": [P],
-    "d3d_wgrad_group_wide": [I],
     "d3d_wgrad_group_stages": [I],
     "d3d_wgrad_group_halo": [I, I, I],
     "d3d_wgrad_group_halo_pk": [I],

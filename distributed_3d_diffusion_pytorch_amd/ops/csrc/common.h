@@ -39,7 +39,16 @@ __device__ __forceinline__ f32x8 ld8f(const float* p) {
 __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
 
+// sigmoid through the hardware reciprocal (v_rcp_f32, 1 ulp) instead of the
+// IEEE division sequence (~10 VALU: scale, rcp, Newton steps, fixup): every
+// SiLU / dSiLU user -- the GroupNorm passes, the FiLM dgrad epilogue, the conv
+// SiLU epilogues -- is VALU-heavy.  exp(-x) = inf gives rcp(inf) = 0.
+// (D3D_SIGMOID_IEEE: the division form, for the same-box A/B build only.)
+#ifdef D3D_SIGMOID_IEEE
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+#else
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+#endif
 __device__ __forceinline__ float siluf_(float x) { return x * sigmoidf_(x); }
 // d/dx silu(x) = s * (1 + x * (1 - s))
 __device__ __forceinline__ float dsiluf_(float x) {
@@ -121,6 +130,22 @@ __device__ __forceinline__ void silu_store4(bf16* __restrict__ O2, long off, bf1
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Compute units of the CURRENT device (launch planners size grids in whole
+// waves of blocks per CU), cached per device ordinal: a process that drives
+// several GPUs -- or one whose current device is not 0 -- gets each device's
+// own count.  (Every MI355X has 256; the cache only avoids the query per launch.)
+static inline int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int n = cache[dev];
+  if (n <= 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return n;
+}
+
 // ----------------------------------------- fused GroupNorm statistics -----
 // GroupNorm partial statistics of a conv output, produced by the conv's
 // epilogue so the GroupNorm that consumes the output skips its statistics
@@ -182,107 +207,6 @@ __device__ __forceinline__ void gn_part_store(float (&s)[TM][NH], float (&q)[TM]
       float* d = gnp + ((n * G + g) * nparts + t) * 2;
       d[0] = a;
       d[1] = b;
-    }
-  }
-}
-
-// --------------------------------- GroupNorm-backward partials in a dgrad ----
-// The input gradient of a conv whose input is a GroupNorm(+SiLU) output
-// (ResnetBlock conv1 after GN0, `xunet.py:139-140`; the head conv after the
-// last GN) IS the GroupNorm's output gradient dy.  The conv's epilogue holds dy
-// in registers, so it also forms the backward's per-(image, group)
-// reductions -- sum dA*gamma and sum dA*gamma*xhat, dA = dy *
-// [dsilu(gamma*xhat + beta)] -- from the GroupNorm input x and its statistics,
-// instead of a separate pass that re-reads x and dy (gn_bwd_reduce_k).  The
-// per-channel dgamma / dbeta sums come out of the apply pass, which forms dA
-// anyway.  Granularity: 64 pixels of one image x one 4-channel quad (the
-// lane's channels; any group width that is a multiple of 4 works -- the
-// decoder's concat GroupNorms have 12 / 24 channels per group); every slot is
-// written by exactly one lane after a fixed shuffle order: deterministic, no
-// atomics.   grp [N][C/4][nparts][2]
-struct GnbArgs {
-  const bf16* x;          // GroupNorm input [N, HW, C1] (or all C channels when x2 is null)
-  const bf16* x2;         // channels [C1, C) of a virtual concat, [N, HW, C - C1]
-  const float* stats;     // [N][G] (mean, rstd)
-  const float* gamma;
-  const float* beta;
-  float* grp;
-  int C1, G, mode, pad_;  // mode 1: GroupNorm + SiLU, 0: GroupNorm
-};
-
-// acc: the wave's fp32 tile (TM row tiles of 16 channels x TN fragments of 16
-// pixels), dy = bf16(acc * scale) as stored; co_base / pix_base: the wave's
-// first channel / pixel (TN % 4 == 0: whole 64-pixel parts).  The caller
-// guarantees co_base + 16 TM <= C and that the wave's channels lie in one
-// concat source (C1 % 64 == 0): every load is unconditional with a
-// wave-uniform base (per-lane conditional loads became one exec-masked branch
-// and a vmcnt(0) per load).  Loads go through restrict-qualified locals, so no
-// load waits behind the partial stores; the SiLU derivative uses the hardware
-// reciprocal.
-template <int TM, int TN>
-__device__ __forceinline__ void gnb_tile(const f32x4 (&acc)[TM][TN], float scale, const GnbArgs& a, int lane,
-                                         int co_base, long pix_base, int C, int HW, long Mpix) {
-  const int fr = lane & 15, fq = lane >> 4;
-  const int Cg = C / a.G, nparts = HW / 64;
-  const bool second = a.x2 != nullptr && co_base >= a.C1;       // wave-uniform
-  const bf16* __restrict__ xs = second ? a.x2 + (co_base - a.C1) : a.x + co_base;
-  const int ld = a.x2 == nullptr ? C : (second ? C - a.C1 : a.C1);
-  const float* __restrict__ stats = a.stats;
-  const float* __restrict__ gam = a.gamma + co_base + fq * 4;
-  const float* __restrict__ bet = a.beta + co_base + fq * 4;
-  float* __restrict__ grp = a.grp;
-#pragma unroll
-  for (int h = 0; h < TN / 4; ++h) {
-    const long p0 = pix_base + h * 64;
-    if (p0 >= Mpix) continue;                      // (wave-uniform)
-    const int n = (int)(p0 / HW);
-    const int t = (int)(p0 - (long)n * HW) / 64;
-    bf16x4 xr[TM][4];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        xr[i][jj] = *reinterpret_cast<const bf16x4*>(xs + (p0 + jj * 16 + fr) * ld + i * 16 + fq * 4);
-    float ga[TM], gb[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const f32x4 gm = *reinterpret_cast<const f32x4*>(gam + i * 16);
-      const f32x4 bt = *reinterpret_cast<const f32x4*>(bet + i * 16);
-      const int g = (co_base + i * 16 + fq * 4) / Cg;
-      const float mean = stats[(n * a.G + g) * 2], rstd = stats[(n * a.G + g) * 2 + 1];
-      ga[i] = gb[i] = 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float sg = 0.f, sb = 0.f;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const float dy = (float)(bf16)(acc[i][h * 4 + jj][e] * scale);
-          const float xhat = ((float)xr[i][jj][e] - mean) * rstd;
-          float dA = dy;
-          if (a.mode) {
-            const float z = xhat * gm[e] + bt[e];
-            const float sgm = __builtin_amdgcn_rcpf(1.0f + __expf(-z));
-            dA = dy * sgm * (1.0f + z * (1.0f - sgm));
-          }
-          sg += dA * xhat;
-          sb += dA;
-        }
-        ga[i] += sb * gm[e];                       // sum dA*gamma over the lane's pixels
-        gb[i] += sg * gm[e];                       // sum dA*gamma*xhat
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) {           // the 16 pixels of a fragment column
-        ga[i] += __shfl_xor(ga[i], m, 64);
-        gb[i] += __shfl_xor(gb[i], m, 64);
-      }
-      if (fr == 0) {
-        float* d = grp + (((long)n * (C / 4) + (co_base + i * 16 + fq * 4) / 4) * nparts + t) * 2;
-        d[0] = ga[i];
-        d[1] = gb[i];
-      }
     }
   }
 }

@@ -998,7 +998,7 @@ __global__ void __launch_bounds__(512, 1)
 conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
             int w_bytes, int Nimg, int OH, int IC, int ICp, int OC, float scale, int res_nmod,
-            float* __restrict__ gnp, int gn_groups, bf16* __restrict__ O2, GnbArgs gb) {
+            float* __restrict__ gnp, int gn_groups, bf16* __restrict__ O2) {
   typedef HaloGeom<OWT, BNT> Gm;
   constexpr int BM = 128, BN = BNT, WM = 64, WN = BN / 4, TM = 4, TN = WN / 16;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * Gm::HBUF + (P2 ? 8 : 4) * Gm::ABUF];
@@ -1371,9 +1371,6 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     }
   }
   if (gnp) gn_part_store<TM, NH>(gs, gq, lane, m0 + wm * WM, n0 + wn * WN, OC, gn_groups, OHW, Mpix, gnp);
-  // the output is a GroupNorm's output gradient (input gradient of the conv
-  // after GN0 / the last GN): its backward partials (common.h gnb_tile)
-  if (gb.grp) gnb_tile<TM, TN>(acc, scale, gb, lane, m0 + wm * WM, n0 + wn * WN, OC, OHW, Mpix);
 }
 
 // split-K epilogue: O[pix][co] = (sum_s part[s][pix][co] + bias + row_bias
@@ -2885,25 +2882,14 @@ D3D_API int d3d_conv_plan(int N, int OH, int OW, int OC, int ICp, int taps) {
 // O2 != nullptr: also write silu(output) to O2 (same layout) when the chosen
 // kernel can; *silu_done reports whether it did (the caller runs the SiLU
 // pass otherwise).
-// gnb != nullptr: the output is a GroupNorm's output gradient -- also produce
-// the GroupNorm backward's partials (common.h GnbArgs / gnb_tile) when the
-// chosen kernel can (*gnb_done = 1; the caller runs the reduce pass otherwise).
 D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,
                       void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW, int OC, int ldo, int stride,
                       int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, float* gnp,
-                      int gn_groups, int* gn_done, void* O2, int* silu_done, const GnbArgs* gnb, int* gnb_done,
-                      hipStream_t st) {
+                      int gn_groups, int* gn_done, void* O2, int* silu_done, hipStream_t st) {
   long Mpix = (long)N * OH * OW;
   if (gn_done) *gn_done = 0;
   if (silu_done) *silu_done = 0;
-  if (gnb_done) *gnb_done = 0;
   if (!silu_done) O2 = nullptr;
-  GnbArgs gb{};
-  // (gnb_tile wants whole 64-channel wave slices in one concat source)
-  if (gnb && gnb_done && gnb->grp && !bias && !row_bias && !res && ldo == OC && gnb->G > 0 && OC % 64 == 0 &&
-      OC % gnb->G == 0 && (OC / gnb->G) % 4 == 0 && (OH * OW) % 64 == 0 && (gnb->mode == 0 || gnb->mode == 1) &&
-      (gnb->x2 == nullptr || gnb->C1 % 64 == 0))
-    gb = *gnb;
   // Operands beyond the kernels' 32-bit buffer offsets (2 GiB: e.g. the
   // 256-channel decoder concat of 128x128 images at one micro-batch of 128):
   // run the conv over image chunks that fit, each at full speed, instead of
@@ -2931,7 +2917,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
                                    res_nmod, taps, ws, nsplit,
                                    gnp ? gnp + (long)n0 * gn_groups * parts_per_img * 2 : nullptr, gn_groups,
                                    gn_done ? &d : nullptr, O2 ? (char*)O2 + n0 * img_out : nullptr,
-                                   O2 ? &ds : nullptr, nullptr, nullptr, st);
+                                   O2 ? &ds : nullptr, st);
           if (rc) return rc;
           all_gn &= d;
           all_silu &= ds;
@@ -2968,7 +2954,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
 #define HALO3(OWv, TR, RS, AUv, P2v)                                                                              \
   hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512, false, RS, AUv, (P2v && OWv != 128)>), gh, dim3(512), 0, st, (const bf16*)I,     \
                      (const bf16*)Wp, bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, \
-                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, gb)
+                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2)
 #define HALO2(OWv, TR, RS, AUv) HALO3(OWv, TR, RS, AUv, false)
 #define HALO(OWv, TR, RS)                                                                                          \
   do {                                                                                                            \
@@ -2991,7 +2977,6 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
 #undef HALO3
       if (gn_done && gnp) *gn_done = 1;
       if (silu_done && O2) *silu_done = 1;
-      if (gnb_done && gb.grp) *gnb_done = 1;
       return (int)hipGetLastError();
     }
     if (((OW == 16 && g_halo_w16) || (OW == 32 && g_halo_w32s)) && nblk(256) >= 256) {
@@ -3001,7 +2986,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
 #define HALOS(OWv, TR, RS)                                                                                         \
   hipLaunchKernelGGL((conv_halo_k<OWv, TR, 256, false, RS, true>), gh, dim3(512), 0, st, (const bf16*)I,           \
                      (const bf16*)Wp, bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, \
-                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, GnbArgs{})
+                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2)
       if (OW == 16) {
         if (trans) { if (res || g_conv_res_always) HALOS(16, true, true); else HALOS(16, true, false); }
         else if (res || g_conv_res_always) HALOS(16, false, true); else HALOS(16, false, false);
@@ -3012,7 +2997,6 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
 #undef HALOS
       if (gn_done && gnp) *gn_done = 1;
       if (silu_done && O2) *silu_done = 1;
-      // (no GroupNorm-backward epilogue on the 256-pixel tiles: gnb_done stays 0, the caller runs the reduce)
       return (int)hipGetLastError();
     }
   }
@@ -3146,7 +3130,7 @@ D3D_API int d3d_conv2(const void* I, const void* Wp, const float* bias, const fl
                       int trans, float scale, int res_nmod, int taps, float* ws, int nsplit, float* gnp,
                       int gn_groups, int* gn_done, hipStream_t st) {
   return d3d_conv3(I, Wp, bias, row_bias, res, O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans, scale,
-                   res_nmod, taps, ws, nsplit, gnp, gn_groups, gn_done, nullptr, nullptr, nullptr, nullptr, st);
+                   res_nmod, taps, ws, nsplit, gnp, gn_groups, gn_done, nullptr, nullptr, st);
 }
 
 D3D_API int d3d_conv(const void* I, const void* Wp, const float* bias, const float* row_bias, const void* res,

@@ -169,8 +169,8 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
           float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw) {
   constexpr bool BIAS = (F & (F_B32 | F_B16)) != 0, BBF = (F & F_B16) != 0;
   using C = GCfg<WI, WJ, NST>;
-  // 4 bias slots: the loader may run at most 3 tiles ahead -- NST 4 needs K >= 128, NST 8 K >= 256 (host)
-  static_assert(NST == 2 || NST == 4 || NST == 8, "stage ring of 2, 4 or 8");
+  // 4 bias slots: the loader may run at most 3 tiles ahead -- NST 4 needs K >= 128 (host)
+  static_assert(NST == 2 || NST == 4, "stage ring of 2 or 4");
   __shared__ __attribute__((aligned(16))) bf16 smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -445,23 +445,13 @@ static int g_cfg_force = 0;     // 0: by problem size; 8 / 4 / 2: force the WI =
 static int g_gm = 8;
 static int g_grid = 0;          // 0: resident blocks on every CU
 static int g_deep = 1;          // 4-stage ring for the 64 / 128 tiles of small problems
-static int g_deep8 = 0;         // 8-stage ring for one 64-tile block per CU
-static int g_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
-}
+static int g_cus() { return device_cus(); }
 
 // Tuning switches for in-process A/B (forced tile config, tile-group width,
 // grid); 0 leaves a setting unchanged (cfg 1 restores the size rule, cfg -1 / -2
 // turn the deep stage ring on / off, grid -1 restores the resident grid).
 D3D_API void d3d_gemm_tune(int cfg, int gm, int grid) {
   if (cfg == -1 || cfg == -2) g_deep = cfg == -1;       // -1 / -2: deep stage ring on / off
-  else if (cfg == -3 || cfg == -4) g_deep8 = cfg == -3;  // -3 / -4: 8-stage ring on / off
   else if (cfg == 1) g_cfg_force = 0;
   else if (cfg > 0) g_cfg_force = cfg;
   if (gm > 0) g_gm = gm;
@@ -526,10 +516,7 @@ D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, i
   // deep ring (68 KB / 130 KB of LDS: 2 / 1 blocks per CU) when those
   // resident blocks hold every tile -- the latency-bound small problems
   const bool deep = g_deep && W != 8 && tiles <= (long)g_cus() * (W == 4 ? 1 : 2);
-  // one 64-tile block per CU: an 8-stage ring (128 KB) -- at one block of four
-  // waves per CU a long reduction (the K = 1536 qkv input gradient) still
-  // waited on the round trips with 3 stages in flight
-  const bool deep8 = deep && g_deep8 && W == 2 && K >= 256 && tiles <= (long)g_cus();
+  // (an 8-stage ring for one 64-tile block per CU measured no gain, profiles/r4/gemm_deep8/: removed)
   const int per_cu = W == 8 ? 1 : W == 4 ? 2 : 4;
   const int G_ = (int)std::min<long>(tiles, g_grid > 0 ? g_grid : (long)g_cus() * per_cu);
   const int gm = std::max(1, std::min(mt, g_gm));
@@ -537,10 +524,7 @@ D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, i
                           : (bias_ ? (bias_bf16 ? F_B16 : F_B32) : 0) | (R ? F_RES : 0) | (gnp ? F_GN : 0);
 #define G_CASE(W_, F_)                                                                                          \
   if (W == W_ && F == (F_)) {                                                                                   \
-    if (W_ == 2 && deep8)                                                                                       \
-      g_launch<W_, F_, (W_ == 2 ? 8 : 2)>(G_, st, A, B, O, bias_, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, \
-                                          nt, gm, gnp, G, hw);                                                  \
-    else if (W_ != 8 && deep)                                                                                   \
+    if (W_ != 8 && deep)                                                                                   \
       g_launch<W_, F_, (W_ != 8 ? 4 : 2)>(G_, st, A, B, O, bias_, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, \
                                           nt, gm, gnp, G, hw);                                                  \
     else                                                                                                        \

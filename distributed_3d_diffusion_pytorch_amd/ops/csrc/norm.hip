@@ -14,8 +14,6 @@
 #include "common.h"
 #include <stdlib.h>
 
-D3D_API int d3d_colsum(const float* in, long R, int Cc, float* part, float* out, float* out_odd, int accumulate,
-                       hipStream_t st);
 
 namespace {
 
@@ -412,41 +410,6 @@ __device__ __forceinline__ void sum_group_parts(const float* __restrict__ grp_pa
   __syncthreads();
 }
 
-// Group sums of image n from the dgrad-epilogue partials (common.h gnb_tile:
-// [N][C/4][nparts][2], quads of a group contiguous): NT / G threads per group
-// each sum a strided share of the group's Cg/4 x nparts pairs, merged in a
-// fixed order through LDS.
-__device__ __forceinline__ void sum_group_parts_epi(const float* __restrict__ grp, int n, int G, int C, int nparts,
-                                                    float* s_out) {
-  __shared__ float s_sub[2 * NT];
-  const int tpg = G <= NT ? NT / G : 1;
-  const int cnt = (C / G / 4) * nparts;            // pairs per group
-  for (int g0 = 0; g0 < G; g0 += NT / tpg) {
-    const int g = g0 + threadIdx.x / tpg, sub = threadIdx.x % tpg;
-    float a = 0.f, b = 0.f;
-    if (g < G) {
-      const float* pp = grp + ((long)n * (C / 4) + (long)g * (C / G / 4)) * nparts * 2;
-      for (int t = sub; t < cnt; t += tpg) {
-        a += pp[2 * t];
-        b += pp[2 * t + 1];
-      }
-    }
-    s_sub[threadIdx.x * 2] = a;
-    s_sub[threadIdx.x * 2 + 1] = b;
-    __syncthreads();
-    if (sub == 0 && g < G) {
-      float x = 0.f, y = 0.f;
-      for (int k = 0; k < tpg; ++k) {
-        x += s_sub[(threadIdx.x + k) * 2];
-        y += s_sub[(threadIdx.x + k) * 2 + 1];
-      }
-      s_out[g * 2] = x;
-      s_out[g * 2 + 1] = y;
-    }
-    __syncthreads();
-  }
-}
-
 // MODE 0: GN, 1: GN+SiLU, 2: GN+FiLM(+dropout)
 template <int MODE>
 __global__ void __launch_bounds__(NT) gn_apply2_k(const bf16* __restrict__ x, const float* __restrict__ part,
@@ -758,12 +721,9 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
                                                       const float* __restrict__ chan_part,
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                       int accumulate, int trows, const bf16* __restrict__ dres,
-                                                      float dres_scale, long chan_R, int gparts,
-                                                      float* __restrict__ chan_out, const bf16* __restrict__ dres2,
+                                                      float dres_scale, long chan_R, const bf16* __restrict__ dres2,
                                                       float dres2_scale) {
-  // chan_R: rows of chan_part; gparts > 0: grp_part holds the consumer conv's
-  // dgrad-epilogue partials ([N][G][gparts][2], common.h gnb_tile) instead of
-  // the reduce pass's [N][nchunks][G][2]
+  // chan_R: rows of chan_part (the reduce pass's per-block dgamma / dbeta partials)
   if ((int)blockIdx.y < trows) {        // leading grid rows: dgamma / dbeta, 4 rows (waves) per block
     const int blk = blockIdx.y * nchunks + blockIdx.x;
     dgb_rowsum(chan_part, chan_R, 2 * C, blk * (NT / 64) + (threadIdx.x >> 6), dgamma, dbeta, accumulate);
@@ -774,10 +734,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
   const int Cg = C / G;
   const float inv = 1.f / (float)((long)P * Cg);
   __shared__ float s_ab[2 * 1024];
-  if (gparts > 0)
-    sum_group_parts_epi(grp_part, n, G, C, gparts, s_ab);
-  else
-    sum_group_parts(grp_part, n, nchunks, G, s_ab);
+  sum_group_parts(grp_part, n, nchunks, G, s_ab);
   for (int g = threadIdx.x; g < G; g += NT) {
     s_c[g * 4 + 0] = stats[(n * G + g) * 2];
     s_c[g * 4 + 1] = stats[(n * G + g) * 2 + 1];
@@ -790,11 +747,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
   const uint32_t dkey = drop_key(seed), dthr = drop_threshold(p_drop);
   const int cv = C / 8, rpi = NT / cv;
   const int tid = threadIdx.x, roff = tid / cv;
-  // chan_out: this block's per-channel dgamma / dbeta partials (the reduce
-  // pass that made them is gone when the consumer conv's epilogue supplied
-  // the group sums): row (n, chunk) of [N * nchunks][C][2], summed by colsum
-  if (roff >= rpi && chan_out == nullptr) return;
-  const bool act = roff < rpi;
+  if (roff >= rpi) return;
   const int c0 = (tid % cv) * 8;
   float mean[8], rstd[8], c1[8], c2[8], gm[8], bt[8];
   {
@@ -817,10 +770,7 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
   else if (c0 < cat.C1) { dst = dx + c0; dld = cat.C1; }
   else { dst = cat.dx2 + (c0 - cat.C1); dld = C - cat.C1; }
   const long pix0 = (long)n * P;
-  const int r1 = act ? min(P, chunk * rows + rows) : 0;
-  float pg[8], pb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) pg[j] = pb[j] = 0.f;
+  const int r1 = min(P, chunk * rows + rows);
   for (int r = chunk * rows + roff; r < r1; r += U * rpi) {
     f32x8 xv[U], dv[U], sc[U], rv[U], rv2[U];
 #pragma unroll
@@ -851,39 +801,10 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
                        dsc, dsh, keepmul);
         const float dxh = dA * gm[j];
         o[j] = rstd[j] * (dxh - c1[j] - xhat * c2[j]);
-        pg[j] += dA * xhat;
-        pb[j] += dA;
       }
       if (dres) o += rv[u] * dres_scale;    // the residual branch's gradient of the same input
       if (dres2) o += rv2[u] * dres2_scale;  // ... and a second consumer's (a decoder skip, models/xunet.py)
       st8(dst + pix * dld, o);
-    }
-  }
-  if (chan_out) {
-    // fold the rpi row lanes of each channel in a fixed order (structure of
-    // arrays: each thread's 8 channels are two 16-byte stores)
-    // (reuses the group-coefficient array: every thread copied its
-    // coefficients to registers before its row loop; the barrier below makes
-    // sure all of them have before any lane overwrites it)
-    float* s_red = s_c;
-    __syncthreads();
-    float* o = s_red + roff * C + c0;
-    if (act) {
-      *reinterpret_cast<f32x4*>(o) = f32x4{pg[0], pg[1], pg[2], pg[3]};
-      *reinterpret_cast<f32x4*>(o + 4) = f32x4{pg[4], pg[5], pg[6], pg[7]};
-      *reinterpret_cast<f32x4*>(o + rpi * C) = f32x4{pb[0], pb[1], pb[2], pb[3]};
-      *reinterpret_cast<f32x4*>(o + rpi * C + 4) = f32x4{pb[4], pb[5], pb[6], pb[7]};
-    }
-    __syncthreads();
-    float* row = chan_out + ((long)n * nchunks + chunk) * 2 * C;
-    for (int c = tid; c < C; c += NT) {
-      float a = 0.f, b = 0.f;
-      for (int k = 0; k < rpi; ++k) {
-        a += s_red[k * C + c];
-        b += s_red[rpi * C + k * C + c];
-      }
-      row[2 * c] = a;
-      row[2 * c + 1] = b;
     }
   }
 }
@@ -1008,7 +929,7 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
   hipLaunchKernelGGL((gn_bwd_apply2_k<M, U>), dim3(p.nchunks, N + trows), dim3(NT), 0, st, (const bf16*)x,             \
                      (const bf16*)dy, (const bf16*)ss, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows,    \
                      p.nchunks, p_drop, (uint64_t)seed, ssld, (const uint64_t*)seed_dev, cat, chan_part, dgamma,    \
-                     dbeta, accumulate, trows, (const bf16*)dres, dres_scale, (long)N * p.nchunks, 0, nullptr,        \
+                     dbeta, accumulate, trows, (const bf16*)dres, dres_scale, (long)N * p.nchunks,                  \
                      (const bf16*)dres2, dres2_scale)
 #define APP(M) if (g_gn_app_u == 4) APP1(M, 4); else if (g_gn_app_u == 1) APP1(M, 1); else APP1(M, 2)
   if (mode == 0) APP(0);
@@ -1017,35 +938,6 @@ D3D_API int d3d_gn_bwd2(int mode, const void* x, const void* dy, const void* ss,
 #undef APP
 #undef APP1
   return (int)hipGetLastError();
-}
-
-// Backward apply over partials the consumer conv's dgrad epilogue produced
-// (conv.hip, GnbArgs): chan_part [2C][N * nparts], grp_part [N][C/4][nparts][2];
-// no reduce pass.  mode 0 / 1 (GroupNorm [+ SiLU]).
-// chan_ws: workspace of N * nchunks * 2C + 64 * 2C floats (d3d_gn_plan's
-// nchunks) for the per-block dgamma / dbeta partials and their column sum.
-D3D_API int d3d_gn_bwd_apply_parts(int mode, const void* x, const void* dy, const float* stats, const float* gamma,
-                                   const float* beta, int N, int P, int C, int G, void* dx, float* dgamma,
-                                   float* dbeta, float* chan_ws, const float* grp_part, int nparts,
-                                   int accumulate, const void* x2, void* dx2, int C1, const void* dres,
-                                   float dres_scale, const void* dres2, float dres2_scale, hipStream_t st) {
-  if (mode != 0 && mode != 1) return (int)hipErrorInvalidValue;
-  if (G > 1024 || nparts < 1 || C % G || (C / G) % 4 || C > 2048) return (int)hipErrorInvalidValue;
-  Plan p = make_plan(N, P, C);
-  if (p.rpi * C > 2048) return (int)hipErrorInvalidValue;
-  Cat cat{(const bf16*)x2, (bf16*)dx2, C1};
-  if (x2) dres = dres2 = nullptr;
-#define APP(M)                                                                                                    \
-  hipLaunchKernelGGL((gn_bwd_apply2_k<M, 2>), dim3(p.nchunks, N), dim3(NT), 0, st, (const bf16*)x, (const bf16*)dy,   \
-                     (const bf16*)nullptr, stats, grp_part, gamma, beta, (bf16*)dx, P, C, G, p.rows, p.nchunks,    \
-                     0.f, (uint64_t)0, 2 * C, (const uint64_t*)nullptr, cat, (const float*)nullptr, dgamma, dbeta,  \
-                     accumulate, 0, (const bf16*)dres, dres_scale, 0L, nparts, chan_ws, (const bf16*)dres2,       \
-                     dres2_scale)
-  if (mode == 0) APP(0);
-  else APP(1);
-#undef APP
-  const long R = (long)N * p.nchunks;
-  return d3d_colsum(chan_ws, R, 2 * C, chan_ws + R * 2 * C, dgamma, dbeta, accumulate, st);
 }
 
 D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, const float* stats,

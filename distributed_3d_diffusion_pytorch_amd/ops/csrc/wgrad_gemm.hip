@@ -273,15 +273,7 @@ wgrad_tn_k(const bf16* __restrict__ Y, const bf16* __restrict__ X, float* __rest
 static int t_var = 0;
 D3D_API void d3d_wgrad_tn_tune(int v) { t_var = v; }
 
-static int t_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
-}
+static int t_cus() { return device_cus(); }
 
 // Pixel rows per split for `splits` splits: whole 128-row units.
 static long t_rps(long P, int splits) { return ((P / 128 + splits - 1) / splits) * 128; }

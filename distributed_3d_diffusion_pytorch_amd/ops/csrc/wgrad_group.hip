@@ -141,27 +141,6 @@ __device__ __forceinline__ void gw_issue(bf16* sA, bf16* sB, const bf16* __restr
   }
 }
 
-// the input (B) half of gw_issue alone: the second chunk of a wide tile
-template <int PK>
-__device__ __forceinline__ void gw_issue_b(bf16* sB, const bf16* __restrict__ I, long in_elems, long p0, int IC,
-                                           int OH, int OW, int kh, int kw, int dpix, int lw, int wave,
-                                           const int* trow, const unsigned* boff, const bool* bok) {
-  typedef __attribute__((address_space(3))) void lds_void;
-  constexpr int PPW = PK / 16;
-  const long pb = p0 + dpix;
-  const __amdgpu_buffer_rsrc_t rB = gw_rsrc(I + pb * IC, (in_elems - pb * IC) * 2);
-  const int wedge = kw == 0 ? 0 : OW - 1, hedge = kh == 0 ? 0 : OH - 1;
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int pp = (int)p0 + trow[i];
-    bool bad = !bok[i];
-    if (kw != 1) bad |= (pp & (OW - 1)) == wedge;
-    if (kh != 1) bad |= ((pp >> lw) & (OH - 1)) == hedge;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(sB + (wave * PPW + i) * 4 * GW_BN), 16,
-                                             bad ? 0x80000000u : boff[i], 0, 0, 0);
-  }
-}
-
 }  // namespace
 
 // One 128 (output channels) x 128 (input channels of one tap) tile of one
@@ -385,212 +364,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_grp_k(GwTable tab) {
   }
 }
 
-// Wide tile: 128 output channels x TWO 128-column chunks of the (tap, input
-// channel) axis -- chunk c of a job is (tap c / ncb, channels (c % ncb) * 128
-// ...), so at 128 input channels a block covers two taps, at >= 256 two
-// channel slices of one tap.  Waves 2 (M) x 2 (chunk), 64 x 128 each (4 x 8
-// MFMA 16x16x32 tiles): twice the MFMAs per transposed LDS read of the 64 x 64
-// wave tile above -- that tile's per-K-step LDS traffic (fragment reads +
-// DMA) outran its 16 MFMAs per wave.
-template <int PK>
-__global__ void __launch_bounds__(256, 2) wgrad_grp2_k(GwTable tab) {
-  constexpr int BM = 128, NS = 2;
-  constexpr int WM = 64, TM = 4, TN = 8;
-  constexpr int STAGE = PK * 3 * 128;              // A | B chunk 0 | B chunk 1
-  constexpr int PPW = PK / 16;
-  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
-  __shared__ float bred[BM];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  int R;
-  {
-    const int T = gridDim.x, L = blockIdx.x;
-    const int q = T / 8, r = T % 8, xcd = L % 8;
-    R = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
-  }
-  int k = 0;
-  while (k + 1 < tab.n && R >= tab.j[k + 1].blk0) ++k;
-  const GwJob& J = tab.j[k];
-  const bf16* dY = J.dy;
-  const int OC = J.OC, ICt = J.IC, C1 = J.C1, taps = J.taps, OH = J.H, OW = J.W, lw = J.lw;
-  const int ncb = J.ncb, nmb = J.nmb, splits = J.splits;
-  const long P = J.P;
-  const int nch = taps * ncb, npair = (nch + 1) / 2;
-  const int b = R - J.blk0;
-  const int bx = b % npair, by = (b / npair) % nmb, split = b / (npair * nmb);
-  const int m0 = by * BM;
-  const long p_begin = (long)split * J.pps;
-  const long p_end = p_begin + J.pps < P ? p_begin + J.pps : P;
-  // the two chunks of this block (chunk 1 may not exist: odd chunk count)
-  int tapc[2], ci0c[2], ci0gc[2], ICc[2], dpixc[2], khc[2], kwc[2];
-  bool validc[2];
-  const bf16* Ic[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int ch = 2 * bx + c;
-    validc[c] = ch < nch;
-    const int chv = validc[c] ? ch : 2 * bx;
-    tapc[c] = chv / ncb;
-    ci0gc[c] = (chv % ncb) * 128;
-    const bool second = J.x2 != nullptr && ci0gc[c] >= C1;
-    Ic[c] = second ? J.x2 : J.x;
-    ICc[c] = J.x2 == nullptr ? ICt : (second ? ICt - C1 : C1);
-    ci0c[c] = second ? ci0gc[c] - C1 : ci0gc[c];
-    khc[c] = taps == 9 ? tapc[c] / 3 : 1;
-    kwc[c] = taps == 9 ? tapc[c] % 3 : 1;
-    dpixc[c] = (khc[c] - 1) * OW + (kwc[c] - 1);
-  }
-
-  const int lrow = lane >> 4, pch = lane & 15;
-  int trow[PPW];
-  unsigned aoff[PPW], boff[2][PPW];
-  bool bok[2][PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    trow[i] = (wave * PPW + i) * 4 + lrow;
-    const int lc = pch ^ (2 * (trow[i] & 7));
-    const int co = m0 + lc * 8;
-    aoff[i] = co < OC ? (unsigned)((trow[i] * OC + co) * 2) : 0x80000000u;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int ci = ci0c[c] + lc * 8;
-      boff[c][i] = (unsigned)((trow[i] * ICc[c] + ci) * 2);
-      bok[c][i] = ci < ICc[c];
-    }
-  }
-  const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
-  const int x7 = 2 * ((4 * g + q) & 7);
-  int la[TM], lb[TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) la[i] = (4 * g + q) * 128 + ((((wm * 8 + 2 * i + (pc >> 1)) ^ x7)) << 3) + (pc & 1) * 4;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) lb[j] = (4 * g + q) * 128 + ((((2 * j + (pc >> 1)) ^ x7)) << 3) + (pc & 1) * 4;
-
-  // (a __device__ function, not a lambda body: buffer-resource values must
-  // not appear in host-visible code, or the host pass drops the kernel stub)
-  auto issue = [&](long p0, int stage) {
-    bf16* sA = smem + stage * STAGE;
-    gw_issue<PK>(sA, sA + PK * 128, dY, Ic[0], P * ICc[0], p0, p_end, OC, ICc[0], OH, OW, khc[0], kwc[0], dpixc[0],
-                 lw, wave, trow, aoff, boff[0], bok[0]);
-    if (validc[1])                                 // (block-uniform)
-      gw_issue_b<PK>(sA + 2 * PK * 128, Ic[1], P * ICc[1], p0, ICc[1], OH, OW, khc[1], kwc[1], dpixc[1], lw, wave,
-                     trow, boff[1], bok[1]);
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const long nsteps = (p_end - p_begin + PK - 1) / PK;
-  const bool do_bias = J.db != nullptr && bx == 0;
-  const bool mine = validc[wn];                   // this wave's chunk exists (wave-uniform)
-  float bacc = 0.f;
-  const int bcol = tid & 127, bhalf = tid >> 7;
-  auto compute = [&](const bf16* a) {
-    const bf16* bb = a + (1 + wn) * PK * 128;
-    if (do_bias) {
-#pragma unroll
-      for (int r = 0; r < PK / 2; ++r) {
-        const int row = bhalf * (PK / 2) + r;
-        bacc += (float)a[row * 128 + ((((bcol >> 3) ^ (2 * (row & 7)))) << 3) + (bcol & 7)];
-      }
-    }
-    if (!mine) return;
-#pragma unroll
-    for (int kk = 0; kk < PK / 32; ++kk) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        gs16x4 lo = gw_tr(bb + lb[j] + kk * 32 * 128);
-        gs16x4 hi = gw_tr(bb + lb[j] + kk * 32 * 128 + 16 * 128);
-        gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        gs16x4 lo = gw_tr(a + la[i] + kk * 32 * 128);
-        gs16x4 hi = gw_tr(a + la[i] + kk * 32 * 128 + 16 * 128);
-        gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  };
-  if (nsteps > 0) issue(p_begin, 0);
-  for (long s = 0; s < nsteps; ++s) {
-    const int st = (int)(s & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (s + 1 < nsteps) issue(p_begin + (s + 1) * PK, st ^ 1);
-    __builtin_amdgcn_s_setprio(1);
-    compute(smem + st * STAGE);
-    __builtin_amdgcn_s_setprio(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-
-  const int fr = lane & 15, fq = lane >> 4;
-  const long KW = (long)taps * ICt;
-  const int tap = tapc[wn], ci0 = ci0c[wn], ci0g = ci0gc[wn], IC = ICc[wn];
-  if (splits == 1) {
-    const float sc = J.scale;
-    float* dw = J.dw;
-    const int acc_in = J.acc;
-    if (do_bias) {                                  // block-uniform: the barrier is safe
-      if (bhalf) bred[bcol] = bacc;
-      __syncthreads();
-      if (!bhalf && m0 + bcol < OC) {
-        const float v = (bacc + bred[bcol]) * sc;
-        float* d = J.db + m0 + bcol;
-        *d = acc_in ? *d + v : v;
-      }
-    }
-    if (!mine) return;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int cl = ci0 + j * 16 + fr;
-      if (cl >= IC || cl >= ci0 + 128) continue;
-      const int ci = ci0g - ci0 + cl;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int co = m0 + wm * WM + i * 16 + fq * 4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (co + e < OC) {
-            float* d = dw + ((long)(co + e) * ICt + ci) * taps + tap;
-            const float v = acc[i][j][e] * sc;
-            *d = acc_in ? *d + v : v;
-          }
-      }
-    }
-    return;
-  }
-  if (do_bias && m0 + bcol < OC) J.bslab[((long)split * 2 + bhalf) * OC + m0 + bcol] = bacc;
-  if (!mine) return;
-  float* slab = J.slab + (long)split * OC * KW;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int cl = ci0 + j * 16 + fr;
-    if (cl >= IC || cl >= ci0 + 128) continue;
-    const int ci = ci0g - ci0 + cl;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int co = m0 + wm * WM + i * 16 + fq * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (co + e < OC) slab[(long)(co + e) * KW + tap * ICt + ci] = acc[i][j][e];
-    }
-  }
-}
-
 // ---------------------------------------------------------- halo tiles ----
-// 3x3 stride-1 jobs (power-of-two images, W >= 8): one block = 128 output channels x 64 input
+// 3x3 stride-1 jobs (power-of-two images, W >= 16): one block = 128 output channels x 64 input
 // channels x ALL NINE taps of one pixel split.  Eight waves (two per SIMD);
 // wave (wm, wn) owns output channels 64wm.. +63 x input channels 16wn.. +15 x
 // the nine taps (4 x 9 = 36 MFMA 16x16x32 tiles, 144 accumulator registers).
@@ -939,10 +714,9 @@ static int g_gw_minpix = 512;      // lower bound of the pixels per block
 // CU) beat the deeper rings (64 KB, two blocks) once the fragment reads stopped
 // waiting on the ring's DMAs (profiles/r4/kb_ns*.jsonl, b16_ns_blocks_ab.txt)
 static int g_gw_ns = 2;
-static int g_gw_wide = 0;          // 1: 128 x 256 chunk-pair tiles (wgrad_grp2_k; measured slower: profiles/r4/kb_w1_*), 0: 128 x 128
 // 3x3 jobs -> wgrad_halo_k: 0 never; 1 at W >= 32, and at W = 16 with >= 32768
 // pixels (the per-tap tile won on the small 16x16 / 8x8 jobs: fewer pixels per
-// all-taps block, profiles/r4/halo_wgrad/README.txt); 2 at any W >= 8 (tests)
+// all-taps block, profiles/r4/halo_wgrad/README.txt)
 static int g_gh_on = 1;
 // target blocks per halo launch: one block per CU runs at a time, so the
 // planner fits the batch into at most this many blocks rounded DOWN to whole
@@ -961,17 +735,13 @@ D3D_API int d3d_wgrad_group_cfg(int blocks, int pk, int minpix) {
   if (minpix > 0) g_gw_minpix = minpix;
   return 0;
 }
-D3D_API int d3d_wgrad_group_wide(int wide) {
-  g_gw_wide = wide ? 1 : 0;
-  return 0;
-}
 D3D_API int d3d_wgrad_group_stages(int ns) {
   if (ns >= 2 && ns <= 4) g_gw_ns = ns;
   return 0;
 }
 // halo (all-taps) tiles for 3x3 jobs: on (0/1), target blocks, ring stages (2/3); < 0 keeps a value
 D3D_API int d3d_wgrad_group_halo(int on, int blocks, int ns) {
-  if (on >= 0) g_gh_on = on > 2 ? 2 : on;
+  if (on >= 0) g_gh_on = on ? 1 : 0;
   if (blocks > 0) g_gh_blocks = blocks;
   if (ns == 2 || ns == 3) g_gh_ns = ns;
   return 0;
@@ -1011,8 +781,8 @@ struct GwPlan {
 static bool gh_takes(const WgJobDesc& d) {
   const int Wm = d.W < GH_PK ? d.W : GH_PK;
   const long P = (long)d.N * d.H * d.W;
-  if (g_gh_on == 1 && d.W < 32 && !(d.W == 16 && P >= 32768)) return false;
-  return g_gh_on && d.taps == 9 && d.W >= 8 && gw_lg2(d.W) >= 0 && ((uintptr_t)d.dw & 15) == 0 && gw_lg2(d.H) >= 0 && d.H >= GH_PK / Wm &&
+  if (d.W < 32 && !(d.W == 16 && P >= 32768)) return false;
+  return g_gh_on && d.taps == 9 && gw_lg2(d.W) >= 0 && ((uintptr_t)d.dw & 15) == 0 && gw_lg2(d.H) >= 0 && d.H >= GH_PK / Wm &&
          d.OC % GH_BM == 0 && d.IC % GH_BN == 0 && (!d.x2 || d.C1 % GH_BN == 0) &&
          (long)(GH_PK / Wm + 2) * d.W * d.IC * 2 < (1L << 30);
 }
@@ -1026,7 +796,7 @@ static void gw_plan(const WgJobDesc* d, int n, GwPlan& pl, bool halo = false) {
       pl.tiles[i] = (d[i].OC / GH_BM) * (d[i].IC / GH_BN);
     } else {
       const int nch = d[i].taps * cdiv(d[i].IC, GW_BN);
-      pl.tiles[i] = (g_gw_wide ? (nch + 1) / 2 : nch) * cdiv(d[i].OC, GW_BM);
+      pl.tiles[i] = nch * cdiv(d[i].OC, GW_BM);
     }
     work += (double)pl.tiles[i] * P;
   }
@@ -1036,9 +806,7 @@ static void gw_plan(const WgJobDesc* d, int n, GwPlan& pl, bool halo = false) {
   Q = (Q + 63) / 64 * 64;
   if (halo) {
     // whole rounds: the smallest Q whose block count fits the round-down target
-    static int cus = 0;
-    if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0))
-      cus = 256;
+    const int cus = device_cus();
     const long T = std::max<long>(cus, (long)g_gh_blocks / cus * cus);
     auto nblk = [&](long q) {
       long t = 0;
@@ -1209,12 +977,7 @@ D3D_API long d3d_wgrad_group(const WgJobDesc* d, int n, float* ws, long ws_float
   if (S.on) {
     GwTable tab;
     const long blk = gw_tables(S.od, S.on, S.op, ws + S.hp.ws_floats + S.qp.ws_floats, false, tab, rt, rblk);
-    if (g_gw_wide) {
-      if (g_gw_pk == 64)
-        hipLaunchKernelGGL(wgrad_grp2_k<64>, dim3((unsigned)blk), dim3(256), 0, st, tab);
-      else
-        hipLaunchKernelGGL(wgrad_grp2_k<32>, dim3((unsigned)blk), dim3(256), 0, st, tab);
-    } else if (g_gw_pk == 64) {
+    if (g_gw_pk == 64) {
       hipLaunchKernelGGL((wgrad_grp_k<64, 2>), dim3((unsigned)blk), dim3(256), 0, st, tab);
     } else if (g_gw_ns == 4) {
       hipLaunchKernelGGL((wgrad_grp_k<32, 4>), dim3((unsigned)blk), dim3(256), 0, st, tab);

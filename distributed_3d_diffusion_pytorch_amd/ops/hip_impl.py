@@ -115,14 +115,28 @@ def _need_bf16(*ts):
             raise TypeError(f"HIP kernels take bf16 activations, got {t.dtype}")
 
 
-# Shapes a HIP kernel does not cover run the torch composition instead; each
-# such (op, shape) is reported once on stderr and counted here so tests and
-# benchmarks can assert that the hot path never falls back.
+# Shapes a HIP kernel does not cover run the torch composition instead -- only
+# with D3D_ALLOW_TORCH_FALLBACK=1 (the same switch that guards the library
+# load, ops/_backend.py): otherwise such a shape is an error, so a GPU run can
+# never silently leave the native path.  Each allowed (op, shape) is reported
+# once on stderr and counted here; bench.py reports the count and the
+# full-model / graph-step tests assert it stays empty.
 FALLBACKS: Dict[str, int] = {}
+
+
+class NativeFallbackError(RuntimeError):
+    """A shape outside the HIP kernels' coverage while fallbacks are not allowed."""
+
+
+def fallbacks_allowed() -> bool:
+    return os.environ.get("D3D_ALLOW_TORCH_FALLBACK", "0") == "1"
 
 
 def _fallback(op: str, why: str) -> None:
     key = f"{op}: {why}"
+    if not fallbacks_allowed():
+        raise NativeFallbackError(f"HIP {op} does not cover this shape ({why}); set D3D_ALLOW_TORCH_FALLBACK=1 "
+                                  "to run the torch composition instead")
     if key not in FALLBACKS:
         import sys
         print(f"[d3d] HIP {op} falls back to the torch composition ({why})", file=sys.stderr, flush=True)
@@ -450,35 +464,6 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None,
     return dx, dss, dg, db
 
 
-def _gn_bwd_parts(mode, x, dy, stats, w, b, G, parts, x2=None, dres=None, dres_scale=1.0, dres2=None,
-                  dres2_scale=1.0):
-    """GroupNorm backward apply over the consumer conv's epilogue partials
-    (no reduce pass)."""
-    _, grp, nparts, _ = parts
-    N, H, W, C1 = x.shape
-    C = C1 + (x2.shape[-1] if x2 is not None else 0)
-    dev = x.device
-    nch, _ = _gn_plan(N, H * W, C)
-    chan = torch.empty(N * nch * 2 * C + 64 * 2 * C, dtype=F32, device=dev)
-    dx = torch.empty_like(x)
-    dx2 = torch.empty_like(x2) if x2 is not None else None
-    tg, tb = SINK.target(w), SINK.target(b)
-    direct = tg is not None and tb is not None
-    dg = tg if direct else torch.empty(C, dtype=F32, device=dev)
-    db = tb if direct else torch.empty(C, dtype=F32, device=dev)
-    _chk(_lib.d3d_gn_bwd_apply_parts(mode, x.data_ptr(), dy.data_ptr(), stats.data_ptr(), w.data_ptr(), b.data_ptr(),
-                                     N, H * W, C, G, dx.data_ptr(), dg.data_ptr(), db.data_ptr(), chan.data_ptr(),
-                                     grp.data_ptr(), int(nparts), int(direct), _ptr(x2), _ptr(dx2), C1, _ptr(dres),
-                                     float(dres_scale), _ptr(dres2), float(dres2_scale), _st()), "gn_bwd_apply_parts")
-    if x2 is not None:
-        dx = (dx, dx2)
-    if direct:
-        SINK.done(w)
-        SINK.done(b)
-        return dx, None, None
-    return dx, dg, db
-
-
 class _GroupNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, groups, eps, silu, slot=None):
@@ -488,10 +473,6 @@ class _GroupNorm(torch.autograd.Function):
         ctx.save_for_backward(x, weight, bias, stats)
         ctx.cfg = (groups, 1 if silu else 0)
         ctx.slot = slot
-        ctx.gnb = None
-        if silu and any(ctx.needs_input_grad[:3]):
-            ctx.gnb = _GnbHolder(x, None, C, stats, weight, bias, groups, 1)
-            y._d3d_gnb = ctx.gnb
         SINK.use(weight, ctx.needs_input_grad[1])
         SINK.use(bias, ctx.needs_input_grad[2])
         return y
@@ -506,13 +487,8 @@ class _GroupNorm(torch.autograd.Function):
         if dres2 is not None:
             dres2 = dres2.reshape(x.shape).contiguous()
         dy = dy.contiguous()
-        parts = ctx.gnb.take(dy) if ctx.gnb is not None else None
-        if parts is not None:
-            dx, dg, db = _gn_bwd_parts(mode, x, dy, stats, w, b, G, parts, dres=dres, dres_scale=rsc, dres2=dres2,
-                                       dres2_scale=rsc2)
-        else:
-            dx, _, dg, db = _gn_bwd(mode, x, dy, None, stats, w, b, G, 0.0, 0, dres=dres, dres_scale=rsc,
-                                    dres2=dres2, dres2_scale=rsc2)
+        dx, _, dg, db = _gn_bwd(mode, x, dy, None, stats, w, b, G, 0.0, 0, dres=dres, dres_scale=rsc,
+                                dres2=dres2, dres2_scale=rsc2)
         return dx, dg, db, None, None, None, None
 
 
@@ -553,10 +529,6 @@ class _CatGNDense(torch.autograd.Function):
         # backward runs after this one) takes b's gradient inside its apply
         # kernel: no autograd bf16 add of the two gradients
         ctx.bslot = getattr(b, "_d3d_res_slot", None)
-        ctx.gnb = None
-        if any(ctx.needs_input_grad[:4]):
-            ctx.gnb = _GnbHolder(a, b, C1, stats, gw, gb, groups, 1)
-            y._d3d_gnb = ctx.gnb
         SINK.use(gw, ctx.needs_input_grad[2])
         SINK.use(gb, ctx.needs_input_grad[3])
         SINK.use(dw, ctx.needs_input_grad[4])
@@ -570,11 +542,7 @@ class _CatGNDense(torch.autograd.Function):
         N, H, W, C1 = a.shape
         C2 = b.shape[-1]
         dy = dy.contiguous()
-        parts = ctx.gnb.take(dy) if ctx.gnb is not None else None
-        if parts is not None:
-            (da, db_in), dgw, dgb = _gn_bwd_parts(1, a, dy, stats, gw, gb, G, parts, x2=b)
-        else:
-            (da, db_in), _, dgw, dgb = _gn_bwd(1, a, dy, None, stats, gw, gb, G, 0.0, 0, x2=b)
+        (da, db_in), _, dgw, dgb = _gn_bwd(1, a, dy, None, stats, gw, gb, G, 0.0, 0, x2=b)
         g = dskip.contiguous()
         OC = g.shape[-1]
         g2 = g.reshape(-1, OC)
@@ -699,21 +667,6 @@ def gn_film(x, weight, bias, ss, groups=32, eps=1e-5, dropout_p=0.0, training=Fa
 
 
 # ----------------------------------------------------------------- conv ----
-class _GnbArgs(ctypes.Structure):
-    """common.h GnbArgs: GroupNorm-backward partials from a dgrad epilogue."""
-    _fields_ = [("x", ctypes.c_void_p), ("x2", ctypes.c_void_p), ("stats", ctypes.c_void_p),
-                ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("grp", ctypes.c_void_p),
-                ("C1", ctypes.c_int), ("G", ctypes.c_int), ("mode", ctypes.c_int), ("pad_", ctypes.c_int)]
-
-
-assert ctypes.sizeof(_GnbArgs) == 64
-# Off by default: measured slower end to end (profiles/r4/gnb_epi_ab.txt --
-# the epilogue costs the halo dgrad +25-40 % while the reduce pass it
-# replaces is a bandwidth-bound 30-160 us); kept for A/B and its tests.
-_GNB_EPI = os.environ.get("D3D_GNB_EPI", "0") != "0"
-_GEMM_DEEP8 = os.environ.get("D3D_GEMM_DEEP8", "0") == "1"   # 8-stage LDS ring, one 64-tile block per CU
-if os.environ.get("D3D_GEMM_DEEP8"):
-    _lib.d3d_gemm_tune(-3 if _GEMM_DEEP8 else -4, 0, 0)
 if os.environ.get("D3D_GEMM_TUNE"):     # A/B knob "cfg,gm,grid" (gemm.hip d3d_gemm_tune; 0 keeps a value)
     _lib.d3d_gemm_tune(*[int(v) for v in os.environ["D3D_GEMM_TUNE"].split(",")])
 if os.environ.get("D3D_HALO_AU"):        # A/B knob: halo conv with unrolled taps / precomputed offsets (1) or not (0)
@@ -722,27 +675,8 @@ if os.environ.get("D3D_GN_CFG"):        # A/B knob "blocks,red_u,app_u": GroupNo
     _lib.d3d_gn_cfg(*[int(v) for v in os.environ["D3D_GN_CFG"].split(",")])
 
 
-class _GnbHolder:
-    """Links a GroupNorm(+SiLU) output to the conv that consumes it: the conv's
-    input-gradient launch may produce the GroupNorm backward's partial sums
-    in its epilogue (``parts``), which the GroupNorm backward then uses
-    instead of its reduce pass (`xunet.py:139-140` GN0 -> conv1)."""
-    __slots__ = ("x", "x2", "C1", "stats", "w", "b", "G", "mode", "parts")
-
-    def __init__(self, x, x2, C1, stats, w, b, G, mode):
-        self.x, self.x2, self.C1, self.stats, self.w, self.b, self.G, self.mode = x, x2, C1, stats, w, b, G, mode
-        self.parts = None
-
-    def take(self, dy):
-        """The partials, when they were made from exactly this gradient."""
-        p, self.parts = self.parts, None
-        if p is None or p[3] != dy.data_ptr():
-            return None
-        return p
-
-
 def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale, res_nmod=0,
-              taps=9, gn_groups=0, silu_out=None, gnb=None):
+              taps=9, gn_groups=0, silu_out=None):
     """Launch the conv; with gn_groups > 0 the epilogue may also emit the
     GroupNorm partial statistics of ``out``: returns (part, nparts) when it
     did (the consuming GroupNorm then skips its statistics pass), else None.
@@ -756,22 +690,12 @@ def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo
         gnp = torch.empty(N * gn_groups * (OH * OW // 64) * 2, dtype=F32, device=x.device)
     done = ctypes.c_int(0)
     sdone = ctypes.c_int(0)
-    bdone = ctypes.c_int(0)
-    ga = None
-    if gnb is not None and _GNB_EPI and (OH * OW) % 64 == 0 and ldo == OC:
-        nparts = OH * OW // 64
-        grp = torch.empty(N * (OC // 4) * nparts * 2, dtype=F32, device=x.device)
-        ga = _GnbArgs(gnb.x.data_ptr(), _ptr(gnb.x2), gnb.stats.data_ptr(), gnb.w.data_ptr(), gnb.b.data_ptr(),
-                      grp.data_ptr(), int(gnb.C1), int(gnb.G), int(gnb.mode), 0)
     _chk(_lib.d3d_conv3(x.data_ptr(), wp.data_ptr(), _ptr(bias), _ptr(row_bias), _ptr(res), out.data_ptr(), N, H, W,
                         IC, ICp, OH, OW, OC, ldo, stride, int(trans), float(scale), int(res_nmod), taps, _ptr(ws), ns,
-                        _ptr(gnp), int(gn_groups), ctypes.byref(done), _ptr(silu_out), ctypes.byref(sdone),
-                        ctypes.byref(ga) if ga is not None else None, ctypes.byref(bdone), _st()),
+                        _ptr(gnp), int(gn_groups), ctypes.byref(done), _ptr(silu_out), ctypes.byref(sdone), _st()),
          "conv")
     if silu_out is not None and not sdone.value:
         _chk(_lib.d3d_silu(out.data_ptr(), silu_out.data_ptr(), out.numel(), _st()), "silu")
-    if ga is not None and bdone.value:
-        gnb.parts = (None, grp, nparts, out.data_ptr())
     return (gnp, OH * OW // 64) if done.value else None
 
 
@@ -824,8 +748,6 @@ _WGRAD_GROUP = os.environ.get("D3D_WGRAD_GROUP", "1") != "0"
 _WGRAD_DIRECT_HALO = _WGRAD_GROUP and os.environ.get("D3D_WGRAD_DIRECT_HALO", "1") != "0"
 if os.environ.get("D3D_WGRAD_GROUP_BLOCKS"):           # planner target (A/B knob): blocks per grouped launch
     _lib.d3d_wgrad_group_cfg(int(os.environ["D3D_WGRAD_GROUP_BLOCKS"]), 0, 0)
-if os.environ.get("D3D_WGRAD_GROUP_WIDE"):             # A/B knob: 128 x 256 (1) or 128 x 128 (0) tiles
-    _lib.d3d_wgrad_group_wide(int(os.environ["D3D_WGRAD_GROUP_WIDE"]))
 if os.environ.get("D3D_WGRAD_GROUP_NS"):               # A/B knob: LDS ring stages (2-4)
     _lib.d3d_wgrad_group_stages(int(os.environ["D3D_WGRAD_GROUP_NS"]))
 if os.environ.get("D3D_WGRAD_HALO"):                   # A/B knob "on[,blocks[,stages]]": all-taps halo tiles
@@ -901,7 +823,6 @@ class _Conv(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, residual, out_scale, row_bias, res_period, taps, gn=None, res_slot=None):
-        gnb = getattr(x, "_d3d_gnb", None)          # x is a GroupNorm(+SiLU) output (see _GnbHolder)
         x = x.contiguous()
         N, H, W, IC = x.shape
         OC = weight.shape[0]
@@ -923,7 +844,6 @@ class _Conv(torch.autograd.Function):
         ctx.cfg = (stride, out_scale, residual is not None, row_bias is not None, bias is not None, res_period, taps)
         ctx.bias_param = bias
         ctx.res_slot = res_slot
-        ctx.gnb = gnb if stride == 1 else None
         SINK.use(weight, ctx.needs_input_grad[1])
         SINK.use(bias, ctx.needs_input_grad[2])
         return out
@@ -956,7 +876,7 @@ class _Conv(torch.autograd.Function):
             wt = packed_weight(weight, True, taps)
             dx = torch.empty_like(x)
             _conv_fwd(g, wt, None, None, None, dx, N, OH, OW, OC, _up(OC, 64), H, W, IC, IC, stride, True, ks, 0,
-                      taps, gnb=ctx.gnb)
+                      taps)
         dW = db = drb = None
         tw = SINK.target(weight) if need_w else None
         tb = SINK.target(bias) if need_b else None

@@ -67,3 +67,11 @@ def test_diff3d_api(srn):
     assert len(imgs3) == 3
     with pytest.raises(TypeError):
         m.sample(batch[0][:, 0], batch[1].float(), batch[2].float(), batch[3][0].float(), 2.0, 2.5)
+    # integer-like step counts (numpy / 0-d tensors) are accepted
+    assert len(m.sample(batch[0][:, 0], batch[1].float(), batch[2].float(), batch[3][0].float(), 2.0,
+                        np.int64(2))) == 2
+    assert len(m.sample(batch[0][:, 0], batch[1].float(), batch[2].float(), batch[3][0].float(), 2.0,
+                        torch.tensor(1))) == 1
+    # a keyword w in the model-less form gets its own message (not "timesteps must be ...")
+    with pytest.raises(TypeError, match="positionally"):
+        m.sample(batch[0][:, 0], batch[1].float(), batch[2].float(), batch[3][0].float(), w=2.0)

@@ -42,6 +42,20 @@ def test_param_count_128():
     assert count_params(XUNet(H=128, W=128, ch=128)) == 138_440_099
 
 
+def test_analytic_flops_match_survey():
+    """models/flops.py reproduces SURVEY Appendix C's measured forward FLOPs
+    per example (235.9 G at 64x64, 969.3 G at 128x128) and splits off the
+    conditioning part the shared-conditioning sampler runs per CFG class."""
+    from distributed_3d_diffusion_pytorch_amd.models.flops import (forward_flops, image_flops,
+                                                                   reference_example_flops)
+    m = XUNet(H=64, W=64, ch=128)
+    assert abs(reference_example_flops(m) / 1e9 - 235.9) < 0.05
+    assert abs(reference_example_flops(XUNet(H=128, W=128, ch=128)) / 1e9 - 969.3) < 0.05
+    f = image_flops(m)
+    full, shared = forward_flops(m, 128), forward_flops(m, 128, cond_examples=2)
+    assert abs(full - shared - 2 * 126 * f["cond"]) < 1e3 and shared < 0.7 * full
+
+
 def test_zero_init():
     m = XUNet(H=16, W=16, ch=32, emb_ch=64)
     sd = m.state_dict()

@@ -315,9 +315,8 @@ def test_gemm_deep_ring(H, cfg, grid, K):
     r = torch.randn(N, M, device=DEV).to(BF)
     outs = []
     try:
-        for deep, deep8 in ((-1, -3), (-1, -4), (-2, -4)):      # 8-, 4-, 2-stage rings
+        for deep in (-1, -2):      # 4-, 2-stage rings
             H._lib.d3d_gemm_tune(deep, 0, 0)
-            H._lib.d3d_gemm_tune(deep8, 0, 0)
             H._lib.d3d_gemm_tune(cfg, 0, grid if grid else 0)
             out = torch.empty(N, M, device=DEV, dtype=BF)
             H.gemm_nt(a, b, out, M, N, K, K, K, M, bias=bb, res=r, alpha=0.5, scale=0.75)
@@ -326,10 +325,9 @@ def test_gemm_deep_ring(H, cfg, grid, K):
         H._lib.d3d_gemm_tune(-1, 0, 0)
         H._lib.d3d_gemm_tune(1, 0, 0)
         H._lib.d3d_gemm_tune(0, 0, -1)
-        H._lib.d3d_gemm_tune(-3 if H._GEMM_DEEP8 else -4, 0, 0)
     ref = ((b.float() @ a.float().t()) * 0.5 + bb + r.float()) * 0.75
     assert rel(outs[0], ref) < 1e-2
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("cfg", [8, 4, 2])
@@ -636,8 +634,8 @@ def test_wgrad_tn_matches_fp32(H, P, M, N, ldy, splits):
 WG_JOBS = [
     (32, 64, 64, 128, 128, 9, 0, True),      # 64x64 level at 16 examples / GPU: split-K
     (32, 8, 8, 512, 512, 9, 0, True),        # 8x8 level: unsplit, direct OIHW epilogue
-    (4, 16, 16, 384, 256, 9, 0, False),      # halo tile at W = 16: two image rows per 32-pixel step
-    (2, 8, 8, 128, 128, 9, 0, True),         # halo tile at W = 8, four rows per step, unsplit
+    (128, 16, 16, 384, 256, 9, 0, False),    # halo tile at W = 16 (>= 32768 pixels): two image rows per 32-pixel step
+    (2, 8, 8, 128, 128, 9, 0, True),         # W = 8: per-tap tile, unsplit
     (6, 8, 16, 72, 200, 9, 0, True),         # channel tails (partial tiles), non-square image
     (2048, 1, 1, 512, 1536, 1, 0, True),     # 1x1 projection
     (8192, 1, 1, 768, 256, 1, 256, True),    # 1x1 over the virtual concat [x | x2]
@@ -658,11 +656,11 @@ def _wg_ref(g, x, taps):
     return dw.reshape(OC, IC, 9)
 
 
-@pytest.mark.parametrize("pk,blocks,minpix,wide,halo,ns", [
-    (32, 512, 512, 0, 2, 2), (32, 512, 512, 0, 0, 2), (64, 512, 512, 0, 2, 2), (32, 4096, 64, 0, 2, 2),
-    (32, 4096, 64, 0, 0, 2), (32, 512, 512, 1, 0, 2), (32, 512, 512, 0, 2, 3), (32, 64, 512, 0, 2, 2),
-    (32, 512, 512, 0, 1, 2), (32, 512, 512, 0, 3, 2), (32, 4096, 64, 0, 3, 2)])
-def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
+@pytest.mark.parametrize("pk,blocks,minpix,halo,ns", [
+    (32, 512, 512, 1, 2), (32, 512, 512, 0, 2), (64, 512, 512, 1, 2), (32, 4096, 64, 1, 2),
+    (32, 4096, 64, 0, 2), (64, 512, 512, 0, 2), (32, 512, 512, 1, 3), (32, 64, 512, 1, 2),
+    (32, 512, 512, 3, 2), (32, 4096, 64, 3, 2)])
+def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, halo, ns):
     """Grouped weight gradients (wgrad_group.hip): the per-tap 128 x 128 tile
     launch and the all-taps halo tile launch (3x3 jobs on W % 32 == 0 images)
     over a mixed batch of 3x3 / 1x1 / virtual-concat jobs (+ the grouped slab
@@ -672,7 +670,6 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
     blocks=64 leaves the big halo jobs nearly unsplit."""
     torch.manual_seed(5)
     H._lib.d3d_wgrad_group_cfg(blocks, pk, minpix)
-    H._lib.d3d_wgrad_group_wide(wide)
     # halo 3: the 64-pixel K-step halo kernel for the W >= 64 jobs (the rest as halo 1)
     H._lib.d3d_wgrad_group_halo(1 if halo == 3 else halo, blocks, ns)
     H._lib.d3d_wgrad_group_halo_pk(64 if halo == 3 else 32)       # (restored to the default 64 below)
@@ -701,8 +698,8 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
         pp = (ctypes.c_int * len(jobs))()
         H._lib.d3d_wgrad_group_plan((H._WgJob * len(jobs))(*jobs), len(jobs), sp, pp, None)
         eng = [H._lib.d3d_wgrad_group_engine(ctypes.byref(j)) for j in jobs]
-        want = [int(bool(halo) and t == 9 and W >= 8 and Hh >= 32 // min(W, 32) and OC % 128 == 0 and IC % 64 == 0
-                    and (halo == 2 or W >= 32 or (W == 16 and N * Hh * W >= 32768)))
+        want = [int(bool(halo) and t == 9 and Hh >= 32 // min(W, 32) and OC % 128 == 0 and IC % 64 == 0
+                    and (W >= 32 or (W == 16 and N * Hh * W >= 32768)))
                 for (N, Hh, W, IC, OC, t, C1, b) in WG_JOBS]
         assert eng == want, (eng, want)
         H.wgrad_group_run(jobs)
@@ -732,7 +729,6 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, wide, halo, ns):
                 assert torch.equal(db, b1)
     finally:
         H._lib.d3d_wgrad_group_cfg(512, 32, 512)
-        H._lib.d3d_wgrad_group_wide(0)
         H._lib.d3d_wgrad_group_halo(1, 512, 2)
         H._lib.d3d_wgrad_group_halo_pk(64)
 
@@ -777,11 +773,9 @@ def test_graph_train_step_matches_eager(micro):
 
 
 @pytest.mark.parametrize("N,Hh,C1,C2,OC", [(32, 64, 128, 0, 128), (12, 64, 256, 128, 128), (8, 128, 128, 0, 128)])
-def test_gn_silu_conv_backward_partials_from_dgrad(H, N, Hh, C1, C2, OC):
+def test_gn_silu_conv_composition(H, N, Hh, C1, C2, OC):
     """GN0 + SiLU -> conv1 (`xunet.py:139-140`; C2 > 0: the decoder's virtual
-    concat): the conv's input-gradient epilogue forms the GroupNorm backward's
-    partial sums (halo dgrad), the GroupNorm backward skips its reduce pass --
-    against the fp32 composition, and against the unfused HIP path."""
+    concat) forward and backward against the fp32 composition."""
     torch.manual_seed(9)
     C = C1 + C2
     xa = (torch.randn(N, Hh, Hh, C1, device=DEV) * 1.5 + 0.3).to(BF)
@@ -806,22 +800,10 @@ def test_gn_silu_conv_backward_partials_from_dgrad(H, N, Hh, C1, C2, OC):
     ins = [xa, xb, gw, gb, w] if C2 else [xa, gw, gb, w]
     fh = hip if C2 else (lambda xa, gw, gb, w: hip(xa, None, gw, gb, w))
     fr = ref if C2 else (lambda xa, gw, gb, w: ref(xa, None, gw, gb, w))
-    calls = []
-    orig, saved = H._gn_bwd_parts, H._GNB_EPI
-    H._gn_bwd_parts = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
-    try:
-        H._GNB_EPI = True                    # (off by default: measured slower end to end)
-        yh, yr, gh, gr = run_both(fh, fr, ins, go)
-        H._GNB_EPI = False
-        _, _, gu, _ = run_both(fh, fr, ins, go)
-    finally:
-        H._GNB_EPI = saved
-        H._gn_bwd_parts = orig
-    assert calls, "the fused GroupNorm-backward path did not run"
+    yh, yr, gh, gr = run_both(fh, fr, ins, go)
     assert rel(yh, yr) < 2e-2
-    for a, b, c in zip(gh, gr, gu):
+    for a, b in zip(gh, gr):
         assert rel(a, b) < 3e-2, rel(a, b)
-        assert rel(a, c) < 2e-2, rel(a, c)
 
 
 @pytest.mark.parametrize("s", [1, 2, 4, 8])
@@ -1084,6 +1066,7 @@ def test_graph_step_bitwise_deterministic():
         SINK.stream_enabled = prev
         hip_impl.set_device_seed(None)
     ref = runs[0]
+    assert hip_impl.FALLBACKS == {}, hip_impl.FALLBACKS     # every op of the replayed step ran natively
     assert all(math.isfinite(v) for v in ref[0]), ref[0]
     for r in runs[1:]:
         assert ref[0] == r[0], (ref[0], r[0])
@@ -1466,6 +1449,8 @@ def test_full_model_64px_matches_fp32_oracle():
         res[be] = (r2(out, ref), {n: r2(p.grad, sd[n].grad) for n, p in m.named_parameters()
                                   if p.grad is not None and sd[n].grad.norm() > 0})
     (oh, gh), (ot, gt) = res["hip"], res["torch"]
+    from distributed_3d_diffusion_pytorch_amd.ops import hip_impl
+    assert hip_impl.FALLBACKS == {}, hip_impl.FALLBACKS     # the HIP run never left the native kernels
     odir = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out")
     os.makedirs(odir, exist_ok=True)
     with open(os.path.join(odir, "oracle64_errors.txt"), "w") as f:

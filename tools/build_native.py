@@ -47,6 +47,7 @@ def build(force: bool = False, jobs: int = 8, debug: bool = False, verbose: bool
     hdr_mtime = max((os.path.getmtime(h) for h in hdrs), default=0)
     flags = ["-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
     flags += ["-O0", "-g"] if debug else ["-O3"]
+    flags += os.environ.get("D3D_EXTRA_FLAGS", "").split()      # A/B builds (e.g. -DD3D_SIGMOID_IEEE)
 
     def compile_one(src: str) -> str:
         obj = os.path.join(OBJ_, os.path.basename(src)[:-4] + ".o")
@@ -90,7 +91,15 @@ def main() -> None:
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--rev", default="", help="build ops/csrc as of this git revision into build/ab/<rev>/ "
                                               "(load it with D3D_LIB_PATH for an in-process A/B)")
+    ap.add_argument("--variant", default="", help="build the CURRENT sources (with D3D_EXTRA_FLAGS) into "
+                                                  "ablib/<name>/libd3d_hip.so for a same-box A/B (D3D_LIB_PATH)")
     a = ap.parse_args()
+    if a.variant:
+        d = os.path.join(ROOT, "ablib", a.variant)
+        os.makedirs(d, exist_ok=True)
+        print(build(a.force, a.jobs, a.debug, out=os.path.join(d, "libd3d_hip.so"),
+                    obj=os.path.join(ROOT, "build", "ab", "variant_" + a.variant)))
+        return
     if a.rev:
         d = os.path.join(ROOT, "build", "ab", a.rev)
         src = os.path.join(d, "csrc")

@@ -66,8 +66,6 @@ def main():
     a = ap.parse_args()
     H._ensure_impl()
     H._lib.d3d_wgrad_group_cfg(a.blocks, a.pk, a.minpix)
-    if os.environ.get("D3D_WGRAD_GROUP_WIDE"):
-        H._lib.d3d_wgrad_group_wide(int(os.environ["D3D_WGRAD_GROUP_WIDE"]))
     dev = torch.device("cuda")
     torch.manual_seed(0)
     for name, spec in batches(2 * a.examples):
