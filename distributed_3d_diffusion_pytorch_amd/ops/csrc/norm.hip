@@ -809,6 +809,298 @@ __global__ void __launch_bounds__(NT) gn_bwd_apply2_k(const bf16* __restrict__ x
   }
 }
 
+// ------------------------------------------------ whole-image kernels ----
+// The 16x16 / 8x8 levels (and 32x32 on request): a block owns ONE image x a
+// slab of CS channels (whole groups; CS / 8 threads per pixel row, rpi rows
+// per pass, U rows per thread) and holds the slab in registers, so every
+// statistic the pass needs is reduced inside the block and the pass is ONE
+// launch that reads its inputs once, all loads issued up front:
+//   forward : statistics (two-pass mean / M2 over the registers) + apply
+//             [+ SiLU | + FiLM + dropout] -- no statistics pass, no partials
+//             merge, and mean / rstd published for the backward;
+//   backward: the group reductions (sum dA*gamma, sum dA*gamma*xhat) AND the
+//             apply -- one launch instead of the reduce + apply pair -- plus
+//             per-image dgamma / dbeta rows that a column sum (off the
+//             critical path, on the weight-gradient stream) folds over images.
+// At 32 images of 16x16x256 the chunked pair ran at 0.4-1.2 TB/s, latency
+// bound: 128 blocks with a few rows each, three dependent round trips
+// (partials -> statistics -> data) per pass.  Reductions are fixed-order
+// (column sums over the row lanes, then the group's columns): deterministic.
+struct ImgGeom {
+  int cv, rpi, tid, roff, v, c0, lg, gs;   // lanes per row, rows per pass, thread, row lane, column, channel, group
+  bool act;
+};
+
+__device__ __forceinline__ ImgGeom img_geom(int NTI, int CS, int Cg) {
+  ImgGeom g;
+  g.cv = CS / 8;
+  g.rpi = NTI / g.cv;
+  g.tid = threadIdx.x;
+  g.roff = g.tid / g.cv;
+  g.v = g.tid - g.roff * g.cv;
+  g.act = g.roff < g.rpi;
+  g.c0 = blockIdx.x * CS + g.v * 8;
+  g.lg = g.v * 8 / Cg;                     // group within the slab (Cg % 8 == 0: one per thread)
+  g.gs = CS / Cg;
+  return g;
+}
+
+// K values per thread -> per-group block sums (every thread gets its group's
+// K totals).  red: LDS [K][NTI] + [K][cv]; fixed order.
+template <int K>
+__device__ __forceinline__ void img_group_sum(float (&val)[K], float* red, const ImgGeom& g, int NTI, int Cg) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) red[k * NTI + g.tid] = g.act ? val[k] : 0.f;
+  __syncthreads();
+  float* col = red + K * NTI;
+  if (g.tid < K * g.cv) {                  // column sums over the row lanes
+    const int k = g.tid / g.cv, c = g.tid - k * g.cv;
+    float a = 0.f;
+    for (int r = 0; r < g.rpi; ++r) a += red[k * NTI + r * g.cv + c];
+    col[k * g.cv + c] = a;
+  }
+  __syncthreads();
+  const int c8 = Cg / 8;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float a = 0.f;
+    for (int j = 0; j < c8; ++j) a += col[k * g.cv + g.lg * c8 + j];
+    val[k] = a;
+  }
+  __syncthreads();                         // red / col may be reused right after
+}
+
+template <int NTI, int U, int MODE>
+__global__ void __launch_bounds__(NTI) gn_img_fwd_k(const bf16* __restrict__ x, float* __restrict__ stats_out,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    const bf16* __restrict__ ss, bf16* __restrict__ y, int P, int C,
+                                                    int G, int CS, float eps, float p_drop, uint64_t seed, int ssld,
+                                                    const uint64_t* __restrict__ seed_dev, Cat cat,
+                                                    const int* __restrict__ ss_map) {
+  __shared__ float red[2 * NTI + 2 * 64];
+  const int Cg = C / G, n = blockIdx.y;
+  const ImgGeom g = img_geom(NTI, CS, Cg);
+  const RowSrc src = row_src(x, cat, g.act ? g.c0 : 0, C);
+  const long pix0 = (long)n * P;
+  const long spix0 = (MODE == 2 && ss_map) ? (long)ss_map[n] * P : pix0;
+  bf16x8 a[U], sc[U], sf[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {            // every load of the slab issued up front
+    const int r = g.roff + u * g.rpi;
+    if (g.act && r < P) {
+      a[u] = *reinterpret_cast<const bf16x8*>(src.p + (pix0 + r) * src.ld);
+      if (MODE == 2) {
+        sc[u] = *reinterpret_cast<const bf16x8*>(ss + (spix0 + r) * ssld + g.c0);
+        sf[u] = *reinterpret_cast<const bf16x8*>(ss + (spix0 + r) * ssld + C + g.c0);
+      }
+    }
+  }
+  const float inv = 1.f / (float)((long)P * Cg);
+  float m[1] = {0.f};
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (g.act && g.roff + u * g.rpi < P)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[0] += (float)a[u][j];
+  img_group_sum<1>(m, red, g, NTI, Cg);
+  const float mean = m[0] * inv;
+  float q[1] = {0.f};
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (g.act && g.roff + u * g.rpi < P)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (float)a[u][j] - mean;
+        q[0] += d * d;
+      }
+  img_group_sum<1>(q, red, g, NTI, Cg);
+  const float rstd = rsqrtf(fmaxf(q[0] * inv, 0.f) + eps);
+  if (!g.act) return;
+  if (g.roff == 0 && (g.v * 8) % Cg == 0) {   // one thread per group publishes mean / rstd
+    const int gg = g.c0 / Cg;
+    stats_out[((long)n * G + gg) * 2 + 0] = mean;
+    stats_out[((long)n * G + gg) * 2 + 1] = rstd;
+  }
+  if (MODE == 2 && seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
+  const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const uint32_t dkey = drop_key(seed), dthr = drop_threshold(p_drop);
+  float A[8], Bc[8];
+  {
+    const f32x8 gm = ld8f(gamma + g.c0), bt = ld8f(beta + g.c0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      A[j] = rstd * gm[j];
+      Bc[j] = bt[j] - mean * A[j];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int r = g.roff + u * g.rpi;
+    if (r >= P) break;
+    const long pix = pix0 + r;
+    const uint64_t e = (uint64_t)pix * C + g.c0;
+    f32x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float h = (float)a[u][j] * A[j] + Bc[j];
+      if (MODE == 1) h = siluf_(h);
+      if (MODE == 2) {
+        h = h * (1.f + (float)sc[u][j]) + (float)sf[u][j];
+        if (p_drop > 0.f) h = drop_elem(dkey, e + j, dthr) ? 0.f : h * keep_scale;
+      }
+      o[j] = h;
+    }
+    st8(y + pix * C + g.c0, o);
+  }
+}
+
+template <int NTI, int U, int MODE>
+__global__ void __launch_bounds__(NTI) gn_img_bwd_k(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                    const bf16* __restrict__ ss, const float* __restrict__ stats,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    bf16* __restrict__ dx, bf16* __restrict__ dss,
+                                                    float* __restrict__ chan_out, int P, int C, int G, int CS,
+                                                    float p_drop, uint64_t seed, int ssld,
+                                                    const uint64_t* __restrict__ seed_dev, Cat cat,
+                                                    const bf16* __restrict__ dres, float dres_scale,
+                                                    const bf16* __restrict__ dres2, float dres2_scale) {
+  // red: [2][NTI] group partials + columns; later [2][rpi][CS] channel partials (<= 2 * NTI * 8)
+  __shared__ __attribute__((aligned(16))) float red[16 * NTI];
+  const int Cg = C / G, n = blockIdx.y;
+  const ImgGeom g = img_geom(NTI, CS, Cg);
+  const int c0 = g.act ? g.c0 : 0;
+  const RowSrc src = row_src(x, cat, c0, C);
+  const long pix0 = (long)n * P;
+  bf16x8 xv[U], dv[U], sc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int r = g.roff + u * g.rpi;
+    if (g.act && r < P) {
+      xv[u] = *reinterpret_cast<const bf16x8*>(src.p + (pix0 + r) * src.ld);
+      dv[u] = *reinterpret_cast<const bf16x8*>(dy + (pix0 + r) * C + c0);
+      if (MODE == 2) sc[u] = *reinterpret_cast<const bf16x8*>(ss + (pix0 + r) * ssld + c0);
+    }
+  }
+  const int gg = c0 / Cg;
+  const float mean = stats[((long)n * G + gg) * 2], rstd = stats[((long)n * G + gg) * 2 + 1];
+  if (MODE == 2 && seed_dev) seed += *seed_dev * 0x9E3779B97F4A7C15ull;
+  const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const uint32_t dkey = drop_key(seed), dthr = drop_threshold(p_drop);
+  const f32x8 gm = ld8f(gamma + c0), bt = ld8f(beta + c0);
+  float dg[8], db[8], gsum[2] = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dg[j] = db[j] = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int r = g.roff + u * g.rpi;
+    if (!g.act || r >= P) break;
+    const long pix = pix0 + r;
+    const uint64_t e = (uint64_t)pix * C + c0;
+    f32x8 o_s, o_t;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float keepmul = 1.f;
+      if (MODE == 2 && p_drop > 0.f) keepmul = drop_elem(dkey, e + j, dthr) ? 0.f : keep_scale;
+      float xhat, dA, dsc = 0.f, dsh = 0.f;
+      bwd_elem<MODE>((float)xv[u][j], (float)dv[u][j], mean, rstd, gm[j], bt[j], MODE == 2 ? (float)sc[u][j] : 0.f,
+                     xhat, dA, dsc, dsh, keepmul);
+      o_s[j] = dsc;
+      o_t[j] = dsh;
+      dg[j] += dA * xhat;
+      db[j] += dA;
+      const float dxh = dA * gm[j];
+      gsum[0] += dxh;
+      gsum[1] += dxh * xhat;
+    }
+    if (MODE == 2) {
+      st8(dss + pix * ssld + c0, o_s);
+      st8(dss + pix * ssld + C + c0, o_t);
+    }
+  }
+  img_group_sum<2>(gsum, red, g, NTI, Cg);
+  const float inv = 1.f / (float)((long)P * Cg);
+  const float c1 = gsum[0] * inv, c2 = gsum[1] * inv;
+  // per-image dgamma / dbeta of the slab's channels: [rpi][CS] x 2 in LDS,
+  // column sums over the row lanes -> chan_out row n ([N][C] pairs (dg, db))
+  {
+    const int SL = g.rpi * CS;
+    if (g.act) {
+      float* o = red + g.roff * CS + g.v * 8;
+      *reinterpret_cast<f32x4*>(o) = f32x4{dg[0], dg[1], dg[2], dg[3]};
+      *reinterpret_cast<f32x4*>(o + 4) = f32x4{dg[4], dg[5], dg[6], dg[7]};
+      *reinterpret_cast<f32x4*>(o + SL) = f32x4{db[0], db[1], db[2], db[3]};
+      *reinterpret_cast<f32x4*>(o + SL + 4) = f32x4{db[4], db[5], db[6], db[7]};
+    }
+    __syncthreads();
+    for (int t = g.tid; t < 2 * CS; t += NTI) {
+      const int k = t / CS, c = t - k * CS;
+      float a = 0.f;
+      for (int r = 0; r < g.rpi; ++r) a += red[k * SL + r * CS + c];
+      chan_out[((long)n * C + blockIdx.x * CS + c) * 2 + k] = a;
+    }
+  }
+  if (!g.act) return;
+  bf16* dst;
+  long dld;
+  if (cat.x2 == nullptr) { dst = dx + c0; dld = C; }
+  else if (c0 < cat.C1) { dst = dx + c0; dld = cat.C1; }
+  else { dst = cat.dx2 + (c0 - cat.C1); dld = C - cat.C1; }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int r = g.roff + u * g.rpi;
+    if (r >= P) break;
+    const long pix = pix0 + r;
+    const uint64_t e = (uint64_t)pix * C + c0;
+    f32x8 rv = {}, rv2 = {};
+    if (dres) rv = ld8(dres + pix * C + c0);
+    if (dres2) rv2 = ld8(dres2 + pix * C + c0);
+    f32x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float keepmul = 1.f;
+      if (MODE == 2 && p_drop > 0.f) keepmul = drop_elem(dkey, e + j, dthr) ? 0.f : keep_scale;
+      float xhat, dA, dsc, dsh;
+      bwd_elem<MODE>((float)xv[u][j], (float)dv[u][j], mean, rstd, gm[j], bt[j], MODE == 2 ? (float)sc[u][j] : 0.f,
+                     xhat, dA, dsc, dsh, keepmul);
+      o[j] = rstd * (dA * gm[j] - c1 - xhat * c2);
+    }
+    if (dres) o += rv * dres_scale;
+    if (dres2) o += rv2 * dres2_scale;
+    st8(dst + pix * dld, o);
+  }
+}
+
+// Launch geometry of the whole-image kernels, or ok = 0 when the shape is
+// outside them: groups of whole 8-channel vectors, the slab's rows in <= 8
+// registers per thread of a 256 / 512-thread block, images up to max_p pixels.
+struct ImgPlan {
+  int ok, CS, NTI, U;
+};
+static int g_gn_img_maxp = 256;            // 0: whole-image kernels off (A/B knob, d3d_gn_img_cfg)
+
+ImgPlan img_plan(int P, int C, int G) {
+  ImgPlan p{0, 0, 0, 0};
+  if (G <= 0 || C % G || C > 4096 || P < 1 || P > g_gn_img_maxp) return p;
+  const int Cg = C / G;
+  if (Cg % 8) return p;
+  int CS = C;
+  for (int k = Cg; k < C; k += Cg)
+    if (C % k == 0 && k >= 32) { CS = k; break; }
+  const int cv = CS / 8;
+  for (int nt = 256; nt <= 512; nt *= 2) {
+    if (cv > nt) continue;
+    const int rpi = nt / cv;
+    const int u = (P + rpi - 1) / rpi;
+    if (u > 8) continue;
+    p.U = u <= 1 ? 1 : u <= 2 ? 2 : u <= 4 ? 4 : 8;
+    p.NTI = nt;
+    p.CS = CS;
+    p.ok = 1;
+    return p;
+  }
+  return p;
+}
+
 inline int ew_grid(long nvec) {
   long g = (nvec + 255) / 256;
   if (g > 256L * 16) g = 256L * 16;
@@ -946,4 +1238,72 @@ D3D_API int d3d_gn_bwd(int mode, const void* x, const void* dy, const void* ss, 
                        float* grp_part, float* coef, hipStream_t st) {
   return d3d_gn_bwd2(mode, x, dy, ss, stats, gamma, beta, N, P, C, G, p_drop, seed, dx, dss, dgamma, dbeta,
                      chan_part, grp_part, coef, 0, 0, nullptr, nullptr, nullptr, 0, nullptr, 1.f, nullptr, 1.f, st);
+}
+
+// ------------------------------------------------ whole-image C ABI ----
+D3D_API int d3d_gn_img_cfg(int max_p) {
+  if (max_p >= 0) g_gn_img_maxp = max_p;
+  return g_gn_img_maxp;
+}
+
+D3D_API int d3d_gn_img_ok(int P, int C, int G) { return img_plan(P, C, G).ok; }
+
+// Forward in one launch (statistics from the registers + apply); stats_out
+// [N][G] (mean, rstd).  mode 0 GN, 1 GN+SiLU, 2 GN+FiLM(+dropout).
+D3D_API int d3d_gn_img_fwd(int mode, const void* x, float* stats_out, const float* gamma, const float* beta,
+                           const void* ss, void* y, int N, int P, int C, int G, float eps, float p_drop,
+                           unsigned long long seed, int ssld, const void* seed_dev, const void* x2, int C1,
+                           const int* ss_map, hipStream_t st) {
+  const ImgPlan p = img_plan(P, C, G);
+  if (!p.ok) return (int)hipErrorInvalidValue;
+  Cat cat{(const bf16*)x2, nullptr, C1};
+  if (ssld == 0) ssld = 2 * C;
+  const dim3 grid(C / p.CS, N);
+#define IF1(NT_, U_, M_)                                                                                            \
+  hipLaunchKernelGGL((gn_img_fwd_k<NT_, U_, M_>), grid, dim3(NT_), 0, st, (const bf16*)x, stats_out, gamma, beta,  \
+                     (const bf16*)ss, (bf16*)y, P, C, G, p.CS, eps, p_drop, (uint64_t)seed, ssld,                 \
+                     (const uint64_t*)seed_dev, cat, ss_map)
+#define IFU(NT_, M_)                                                                                                \
+  if (p.U == 1) IF1(NT_, 1, M_); else if (p.U == 2) IF1(NT_, 2, M_); else if (p.U == 4) IF1(NT_, 4, M_);        \
+  else IF1(NT_, 8, M_)
+#define IFM(M_) if (p.NTI == 256) { IFU(256, M_); } else { IFU(512, M_); }
+  if (mode == 0) { IFM(0); }
+  else if (mode == 1) { IFM(1); }
+  else { IFM(2); }
+#undef IFM
+#undef IFU
+#undef IF1
+  return (int)hipGetLastError();
+}
+
+// Backward in one launch: dx (+ dss for mode 2) and per-image dgamma / dbeta
+// rows chan_out [N][C][2] (fold them over images with d3d_colsum(chan_out, N,
+// 2C, ...) -> dgamma, dbeta).
+D3D_API int d3d_gn_img_bwd(int mode, const void* x, const void* dy, const void* ss, const float* stats,
+                           const float* gamma, const float* beta, int N, int P, int C, int G, float p_drop,
+                           unsigned long long seed, void* dx, void* dss, float* chan_out, int ssld,
+                           const void* seed_dev, const void* x2, void* dx2, int C1, const void* dres,
+                           float dres_scale, const void* dres2, float dres2_scale, hipStream_t st) {
+  const ImgPlan p = img_plan(P, C, G);
+  if (!p.ok) return (int)hipErrorInvalidValue;
+  Cat cat{(const bf16*)x2, (bf16*)dx2, C1};
+  if (ssld == 0) ssld = 2 * C;
+  if (x2) dres = dres2 = nullptr;
+  const dim3 grid(C / p.CS, N);
+#define IB1(NT_, U_, M_)                                                                                            \
+  hipLaunchKernelGGL((gn_img_bwd_k<NT_, U_, M_>), grid, dim3(NT_), 0, st, (const bf16*)x, (const bf16*)dy,         \
+                     (const bf16*)ss, stats, gamma, beta, (bf16*)dx, (bf16*)dss, chan_out, P, C, G, p.CS, p_drop,  \
+                     (uint64_t)seed, ssld, (const uint64_t*)seed_dev, cat, (const bf16*)dres, dres_scale,          \
+                     (const bf16*)dres2, dres2_scale)
+#define IBU(NT_, M_)                                                                                                \
+  if (p.U == 1) IB1(NT_, 1, M_); else if (p.U == 2) IB1(NT_, 2, M_); else if (p.U == 4) IB1(NT_, 4, M_);        \
+  else IB1(NT_, 8, M_)
+#define IBM(M_) if (p.NTI == 256) { IBU(256, M_); } else { IBU(512, M_); }
+  if (mode == 0) { IBM(0); }
+  else if (mode == 1) { IBM(1); }
+  else { IBM(2); }
+#undef IBM
+#undef IBU
+#undef IB1
+  return (int)hipGetLastError();
 }

@@ -365,14 +365,40 @@ def _gn_stats(x, G, eps):
     return stats
 
 
+# Whole-image GroupNorm kernels (norm.hip gn_img_*): images of at most this
+# many pixels (the 16x16 / 8x8 levels) run each GroupNorm pass as ONE launch
+# that keeps an (image, channel slab) in registers -- statistics and backward
+# reductions inside the block.  D3D_GN_IMG=<max pixels> (0: off).
+if os.environ.get("D3D_GN_IMG"):
+    _lib.d3d_gn_img_cfg(int(os.environ["D3D_GN_IMG"]))
+_GN_IMG_OK: Dict[Tuple[int, int, int, int], bool] = {}
+
+
+def gn_img_ok(P: int, C: int, G: int) -> bool:
+    key = (P, C, G, _lib.d3d_gn_img_cfg(-1))
+    v = _GN_IMG_OK.get(key)
+    if v is None:
+        v = _GN_IMG_OK[key] = bool(_lib.d3d_gn_img_ok(P, C, G))
+    return v
+
+
 def _gn_fwd(mode, x, w, b, G, eps, ss=None, ssld=0, p=0.0, seed=0, x2=None, ss_map=None):
     """Statistics pass + fused finalize/apply (mode 0 GN, 1 GN+SiLU, 2 GN+FiLM):
-    two launches; returns (y, stats) with stats = per-(image, group) mean/rstd.
-    With x2, the input is the virtual channel concat [x | x2]."""
+    two launches (one when the producing epilogue made the statistics, or for
+    small images: the whole-image kernel); returns (y, stats) with stats =
+    per-(image, group) mean/rstd.  With x2, the input is the virtual channel
+    concat [x | x2]."""
     N, H, W, C1 = x.shape
     C = C1 + (x2.shape[-1] if x2 is not None else 0)
     P = H * W
     stats = torch.empty(N * G * 2, dtype=F32, device=x.device)
+    if gn_img_ok(P, C, G):
+        y = torch.empty(N, H, W, C, dtype=x.dtype, device=x.device)
+        _chk(_lib.d3d_gn_img_fwd(mode, x.data_ptr(), stats.data_ptr(), w.data_ptr(), b.data_ptr(), _ptr(ss),
+                                 y.data_ptr(), N, P, C, G, float(eps), float(p), int(seed), int(ssld),
+                                 _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), C1, _ptr(ss_map), _st()),
+             "gn_img_fwd")
+        return y, stats
     fused = getattr(x, "_d3d_gnpart", None) if x2 is None else None
     if fused is not None and fused[1] == G:
         part, conv_parts = fused[0], fused[2]       # statistics came out of the producing conv's epilogue
@@ -436,6 +462,9 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None,
     N, H, W, C1 = x.shape
     C = C1 + (x2.shape[-1] if x2 is not None else 0)
     P = H * W
+    if gn_img_ok(P, C, G):
+        return _gn_bwd_img(mode, x, dy, ss, stats, w, b, G, p, seed, dss, ssld, x2, dres, dres_scale, dres2,
+                           dres2_scale)
     nch, _ = _gn_plan(N, P, C)
     dev = x.device
     dx = torch.empty_like(x)
@@ -461,6 +490,42 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None,
         SINK.done(w)
         SINK.done(b)
         return dx, dss, None, None
+    return dx, dss, dg, db
+
+
+def _gn_bwd_img(mode, x, dy, ss, stats, w, b, G, p, seed, dss, ssld, x2, dres, dres_scale, dres2, dres2_scale):
+    """Whole-image GroupNorm backward: ONE launch on the compute stream (dx,
+    dss) plus the fold of its per-image dgamma / dbeta rows -- a parameter
+    gradient nothing downstream waits for, so it runs as a sink job on the
+    weight-gradient stream when the parameters are sink-managed."""
+    N, H, W, C1 = x.shape
+    C = C1 + (x2.shape[-1] if x2 is not None else 0)
+    P = H * W
+    dev = x.device
+    dx = torch.empty_like(x)
+    dx2 = torch.empty_like(x2) if x2 is not None else None
+    if dss is None and ss is not None:
+        dss = torch.empty_like(ss)
+    chan = torch.empty(N * 2 * C + 64 * 2 * C, dtype=F32, device=dev)     # [N][C][2] rows + colsum workspace
+    _chk(_lib.d3d_gn_img_bwd(mode, x.data_ptr(), dy.data_ptr(), _ptr(ss), stats.data_ptr(), w.data_ptr(),
+                             b.data_ptr(), N, P, C, G, float(p), int(seed), dx.data_ptr(), _ptr(dss), chan.data_ptr(),
+                             int(ssld), _ptr(_SEED_DEV[0]) if mode == 2 else None, _ptr(x2), _ptr(dx2), C1,
+                             _ptr(dres), float(dres_scale), _ptr(dres2), float(dres2_scale), _st()),
+         "gn_img_bwd")
+    if x2 is not None:
+        dx = (dx, dx2)
+    tg, tb = SINK.target(w), SINK.target(b)
+    ws = chan[N * 2 * C:]
+    if tg is not None and tb is not None:
+        def job():
+            _chk(_lib.d3d_colsum(chan.data_ptr(), N, 2 * C, ws.data_ptr(), tg.data_ptr(), tb.data_ptr(), 1, _st()),
+                 "gn_img_dgb")
+        SINK.submit(dev, job, (chan,), (w, b))
+        return dx, dss, None, None
+    dg = torch.empty(C, dtype=F32, device=dev)
+    db = torch.empty(C, dtype=F32, device=dev)
+    _chk(_lib.d3d_colsum(chan.data_ptr(), N, 2 * C, ws.data_ptr(), dg.data_ptr(), db.data_ptr(), 0, _st()),
+         "gn_img_dgb")
     return dx, dss, dg, db
 
 
@@ -927,6 +992,10 @@ def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=No
     _need_bf16(x, residual)
     OC, IC = weight.shape[0], weight.shape[1]
     if IC % 8 == 0 and OC % 8 == 0:
+        if gn_groups:
+            OH, OW = (x.shape[1] - 1) // stride + 1, (x.shape[2] - 1) // stride + 1
+            if gn_img_ok(OH * OW, OC, int(gn_groups)):
+                gn_groups = 0           # the consumer's whole-image kernel makes its own statistics
         gn = {"groups": int(gn_groups)} if gn_groups else None
         y = _Conv.apply(x, weight, bias, stride, residual, out_scale, row_bias, res_period, 9, gn, res_slot)
         if gn is not None and "part" in gn:
@@ -1523,6 +1592,8 @@ def linear(x, weight, bias, residual=None, out_scale=1.0, res_slot=None, in_slot
     statistics of the GroupNorm that reads the output (attached as
     ``_d3d_gnpart``; see :func:`carry_gn_stats` across reshapes)."""
     _need_bf16(x, residual)
+    if gn_groups and x.dim() == 3 and gn_img_ok(x.shape[1], weight.shape[0], int(gn_groups)):
+        gn_groups = 0                   # the consumer's whole-image kernel makes its own statistics
     gn = {"groups": int(gn_groups)} if (gn_groups and _EPI_GN_STATS) else None
     y = _Linear.apply(x, weight, bias, residual, out_scale, res_slot, in_slot, gn)
     if gn is not None and "part" in gn:

@@ -138,6 +138,68 @@ def test_gn_film_dropout(H):
     assert torch.equal(dshift == 0, dropped)
 
 
+@pytest.mark.parametrize("N,Hh,C,C1,mode,maxp", [
+    (32, 8, 512, 0, 1, 256), (32, 16, 256, 0, 2, 256), (32, 8, 512, 0, 0, 256), (5, 16, 768, 512, 1, 256),
+    (4, 8, 1024, 512, 1, 256), (3, 8, 768, 256, 1, 256), (6, 4, 256, 0, 2, 256), (4, 32, 256, 0, 1, 1024),
+    (3, 32, 256, 0, 2, 1024)])
+def test_gn_whole_image(H, N, Hh, C, C1, mode, maxp):
+    """Whole-image GroupNorm kernels (norm.hip gn_img_*: statistics and the
+    backward reductions inside one block per (image, channel slab), one
+    launch per pass): forward and every gradient against the fp32 torch
+    composition and against the chunked kernels on the same inputs; with a
+    virtual concat [a | b] (C1 > 0, 24-channel groups at C = 768), dropout
+    (mode 2), and the 512-thread form (32x32, maxp 1024)."""
+    torch.manual_seed(31)
+    x = (torch.randn(N, Hh, Hh, C, device=DEV) * 1.7 + 0.4).to(BF)
+    w = torch.randn(C, device=DEV) * 0.5 + 1
+    b = torch.randn(C, device=DEV) * 0.1
+    ss = (torch.randn(N, Hh, Hh, 2 * C, device=DEV) * 0.5).to(BF)
+    go = torch.randn(N, Hh, Hh, C, device=DEV)
+    p = 0.1 if mode == 2 else 0.0
+
+    def hip(*ins):
+        if C1:
+            return H.cat_gn_silu_dense(ins[0][..., :C1].contiguous(), ins[0][..., C1:].contiguous(), ins[1], ins[2],
+                                       wd, None)[0]
+        if mode == 2:
+            return H.gn_film(ins[0], ins[1], ins[2], ins[3], 32, 1e-5, p, True, 77)
+        return H.group_norm(ins[0], ins[1], ins[2], 32, 1e-5, mode == 1)
+
+    wd = torch.randn(64, C, device=DEV) / 30
+    ins = [x, w, b] + ([ss] if mode == 2 else [])
+    prev = H._lib.d3d_gn_img_cfg(-1)
+    try:
+        H._lib.d3d_gn_img_cfg(maxp)
+        assert H.gn_img_ok(Hh * Hh, C, 32)
+        xi = [leaf(t) for t in ins]
+        yi = hip(*xi)
+        yi.backward(go.to(yi.dtype))
+        H._lib.d3d_gn_img_cfg(0)                       # the chunked kernels, same inputs
+        assert not H.gn_img_ok(Hh * Hh, C, 32)
+        xc = [leaf(t) for t in ins]
+        yc = hip(*xc)
+        yc.backward(go.to(yc.dtype))
+    finally:
+        H._lib.d3d_gn_img_cfg(prev)
+    torch.cuda.synchronize()
+    assert rel(yi, yc) < 1e-2, rel(yi, yc)
+    for a, c in zip(xi, xc):
+        assert rel(a.grad, c.grad) < 2e-2, rel(a.grad, c.grad)
+    if not C1:
+        xr = [leaf(t, torch.float32) if t.dtype == BF else leaf(t) for t in ins]
+        if mode == 2:
+            # the fp32 composition with the kernel's own dropout mask (identity when p = 0)
+            keep = (H.gn_film(x, torch.ones_like(w), torch.zeros_like(b), torch.zeros_like(ss) , 32, 1e-5, p, True, 77)
+                    != 0).float()
+            yr = T.gn_film(*xr, 32, 1e-5, 0.0, False, 0) * keep / (1 - p)
+        else:
+            yr = T.group_norm(*xr, 32, 1e-5, mode == 1)
+        yr.backward(go)
+        assert rel(yi, yr) < 2e-2, rel(yi, yr)
+        for a, c in zip(xi, xr):
+            assert rel(a.grad, c.grad) < 3e-2, rel(a.grad, c.grad)
+
+
 CONV_SHAPES = [
     # N, H, W, Cin, Cout, stride, residual, row_bias, scale
     (4, 16, 16, 128, 128, 1, True, False, 1 / math.sqrt(2)),
