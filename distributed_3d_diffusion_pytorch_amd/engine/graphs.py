@@ -24,10 +24,19 @@ Layout of one step (MI355X, one process per GPU):
       payload (dist.grad_dtype) narrows each bucket into a persistent bf16
       mirror on the collective's stream and widens it back inside the graph.
       ``dist.force_comm`` runs this topology on a 1-rank RCCL group (tests).
-  [world > 1, comm_mode "post"] fallback when a probe capture of an RCCL
-      collective fails (or D3D_GRAPH_COMM=0, or gloo): eager all-reduce of the
-      flat gradient after graph A in 4 async chunks,
-      each chunk's Adam launched as soon as its collective lands.
+  [world > 1, comm_mode "event"] when a probe capture of an RCCL collective
+      fails (or D3D_GRAPH_COMM=0): graph A is captured WITHOUT collectives but
+      with one EXTERNAL event-record node per bucket, placed where the bucket's
+      last gradient is deposited (the same hooks / sink notifications).  After
+      each replay the host issues every bucket's all-reduce eagerly on a comm
+      stream behind its event, so the reduction of bucket k still overlaps the
+      backward kernels the replay runs for the layers below it -- the
+      in-graph overlap without capturing RCCL -- and the deferred update
+      stays on.  An external-event probe gates it.
+  [world > 1, comm_mode "post"] last resort (the event probe failed too, or
+      D3D_GRAPH_COMM=post, or gloo): eager all-reduce of the flat gradient
+      after graph A in 4 async chunks, each chunk's Adam launched as soon as
+      its collective lands.
   graph B: fused Adam reading its per-step hyper-parameters from a device
       block (lr warmup / bias correction change every step; the 1/world
       gradient average is folded in) -> batched weight repack -> gradient /
@@ -102,6 +111,52 @@ def probe_graph_collective(device: torch.device) -> bool:
     return bool(flag.item() > 0.5)
 
 
+def probe_external_events(device: torch.device) -> bool:
+    """True when an EXTERNAL event recorded inside a captured graph orders
+    work on another stream behind the replay's progress (comm_mode "event"):
+    the graph runs ~3 ms of matmuls, then bumps a device counter and records
+    the event; a second stream waits on the event and copies the counter.
+    Reading a stale counter means the wait did not hold.  Agreed over the
+    group (MIN) when a process group exists."""
+    ok = 1.0
+    try:
+        a = torch.randn(4096, 4096, device=device) * 1e-3
+        cnt = torch.zeros(1, device=device)
+        seen = torch.zeros(1, device=device)
+        ev = torch.cuda.Event(external=True)
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(device)
+        with _gc_paused(), torch.cuda.graph(g, capture_error_mode="thread_local"):
+            b = a
+            for _ in range(16):
+                b = b @ a
+            cnt.add_(1.0 + 0.0 * b[0, :1])
+            ev.record()
+            for _ in range(4):
+                b = b @ a
+        s = torch.cuda.Stream(device=device)
+        for rep in range(3):
+            g.replay()
+            s.wait_event(ev)
+            with torch.cuda.stream(s):
+                seen.copy_(cnt)
+            torch.cuda.current_stream(device).wait_stream(s)
+            torch.cuda.synchronize(device)
+            if float(seen.item()) != float(rep + 1):
+                print(f"[graphs] external-event probe: replay {rep} saw counter {float(seen.item())}", flush=True)
+                ok = 0.0
+                break
+        del g
+    except Exception as e:                   # noqa: BLE001 -- any failure means "do not use external events"
+        print(f"[graphs] external-event probe failed ({type(e).__name__}: {e})", flush=True)
+        ok = 0.0
+    if dist.is_available() and dist.is_initialized():
+        flag = torch.tensor([ok], device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = float(flag.item())
+    return ok > 0.5
+
+
 _FUSED_UPDATE = True
 # Deferred optimizer step: the Adam update of step t runs inside the replay of
 # step t+1's graph A, the bulk of it on a side stream overlapped with the
@@ -143,12 +198,21 @@ class GraphedTrainStep:
         self.gA0: Optional[torch.cuda.CUDAGraph] = None     # fwd+bwd without comm (leading micro-batches)
         self.gB: Optional[torch.cuda.CUDAGraph] = None
         self.comm_mode = None
+        self.events = None
         red = trainer.reducer
         if red is not None and red.active:
             # fp32 and bf16 payloads alike (the bf16 mirror is persistent, see
-            # parallel/ddp.py): the collectives are captured inside graph A
-            want = os.environ.get("D3D_GRAPH_COMM", "1") != "0"
-            self.comm_mode = "graph" if (want and probe_graph_collective(dev)) else "post"
+            # parallel/ddp.py): the collectives are captured inside graph A;
+            # failing that, issued behind external events of the replay
+            want = os.environ.get("D3D_GRAPH_COMM", "1")
+            if want == "1" and probe_graph_collective(dev):
+                self.comm_mode = "graph"
+            elif want != "post" and dist.get_backend() == "nccl" and probe_external_events(dev):
+                self.comm_mode = "event"
+                self.events = [torch.cuda.Event(external=True) for _ in red.buckets]
+                self.comm_stream = torch.cuda.Stream(device=dev)
+            else:
+                self.comm_mode = "post"
         # Deferred, overlapped optimizer step (see step()): needs the fused
         # update, the in-graph (or no) reduction and one micro-batch per step.
         split = trainer.model.update_parts() if hasattr(trainer.model, "update_parts") else None
@@ -165,13 +229,17 @@ class GraphedTrainStep:
             self.H.set_words(self.hp, _NOOP_HP)
 
     # ------------------------------------------------------------------
-    def _body(self, comm: bool = False, defer: bool = False) -> None:
+    def _body(self, comm: bool = False, defer: bool = False, events: bool = False) -> None:
+        """One micro-batch forward + backward.  ``comm``: the bucket
+        all-reduces are issued (captured) from the gradient hooks; ``events``
+        (capture only): the hooks record the buckets' external events instead."""
         tr = self.tr
         if tr.sink is not None:
             tr.sink.reset()
         red = tr.reducer
         if red is not None:
-            red.enabled = comm
+            red.enabled = comm or events
+            red.events = self.events if events else None
             red.reset()
         from ..models import xunet as _xunet
         main = torch.cuda.current_stream()
@@ -205,10 +273,11 @@ class GraphedTrainStep:
         loss = ops.diff_loss_nhwc(y, eps, tr.cfg.diffusion.loss_type)
         (loss * self.frac).backward()
         self.loss_acc.add_(loss.detach() * self.frac)
-        if red is not None and comm:
+        if red is not None and (comm or events):
             red.finish()            # remaining buckets + the join of RCCL's stream (captured edges)
         if red is not None:
             red.enabled = False
+            red.events = None
 
     def _update(self) -> None:
         o = self.tr.optim
@@ -249,6 +318,7 @@ class GraphedTrainStep:
         tr.model.set_dropout_seed(0)             # baked; the per-step part is self.seed
         self.H.set_device_seed(self.seed)
         comm = self.comm_mode == "graph"
+        events = self.comm_mode == "event"
         self.img.normal_()
         self.R.copy_(torch.eye(3, device=self.R.device).expand_as(self.R))
         self.K.copy_(torch.eye(3, device=self.K.device).expand_as(self.K))
@@ -277,11 +347,12 @@ class GraphedTrainStep:
         if self.defer:
             self.H.prepare_update_parts(tr.flat, self.parts)
         torch.cuda.synchronize()
-        mode = "thread_local" if comm else "global"     # RCCL's watchdog thread keeps querying events
+        # RCCL's watchdog thread keeps querying the events of eager collectives
+        mode = "thread_local" if self.comm_mode is not None else "global"
         # graphs sharing a memory pool are captured in their replay order
         # (leading micro-batches first)
         with _gc_paused():
-            if comm and nchunks > 1:
+            if (comm or events) and nchunks > 1:
                 self.gA0 = torch.cuda.CUDAGraph()
                 self.gA0.register_generator_state(tr.gen)
                 with torch.cuda.graph(self.gA0, pool=self.pool, capture_error_mode=mode):
@@ -289,7 +360,7 @@ class GraphedTrainStep:
             self.gA = torch.cuda.CUDAGraph()
             self.gA.register_generator_state(tr.gen)
             with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
-                self._body(comm, defer=self.defer)
+                self._body(comm, defer=self.defer, events=events)
             self.gB = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.gB, pool=self.pool, capture_error_mode=mode):
                 self._update()
@@ -343,6 +414,9 @@ class GraphedTrainStep:
             self.K.copy_(K[s:s + mb])
             last = ci == nchunks - 1
             (self.gA if (last or self.gA0 is None) else self.gA0).replay()
+        if self.comm_mode == "event":
+            # the bucket all-reduces behind the replay's external events (overlapping its backward)
+            tr.reducer.issue_after_events(self.comm_stream)
         loss = self.loss_acc.clone()
         world = tr.ctx.world
         o = tr.optim
@@ -400,6 +474,13 @@ class GraphedTrainStep:
         if self.comm_mode == "post":
             with_comm = dev_ms(lambda: (self.gA.replay(), self._reduce_update_chunked()))
             without = dev_ms(lambda: (self.gA.replay(), self._update()))
+            return max(0.0, with_comm - without)
+        if self.comm_mode == "event":
+            with_comm = dev_ms(lambda: (self.gA.replay(), self.tr.reducer.issue_after_events(self.comm_stream)))
+            without = dev_ms(self.gA.replay)
+            with_comm = min(with_comm, dev_ms(lambda: (self.gA.replay(),
+                                                       self.tr.reducer.issue_after_events(self.comm_stream))))
+            tr.flat.zero_grad()
             return max(0.0, with_comm - without)
         g0 = torch.cuda.CUDAGraph()
         g0.register_generator_state(tr.gen)

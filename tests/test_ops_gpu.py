@@ -1334,7 +1334,9 @@ def _graph_comm_1rank_worker(out_dir):
     # (payload, micro-batch): one micro-batch (deferred update) for both
     # payloads, and two micro-batches, where the leading one's graph gA0 is
     # captured next to the comm graph (thread_local, no watchdog wait)
-    for gd, mb in (("fp32", 0), ("bf16", 0), ("fp32", 2)):
+    for gd, mb, gc in (("fp32", 0, "1"), ("bf16", 0, "1"), ("fp32", 2, "1"), ("fp32", 0, "0"), ("bf16", 0, "0"),
+                       ("fp32", 2, "0")):
+        os.environ["D3D_GRAPH_COMM"] = gc        # "0": no RCCL capture -> external-event comm mode
         res = []
         for graph in (False, True):
             cfg = make_config(None, {"model.H": 32, "model.W": 32, "data.imgsize": 32, "global_batch": 4,
@@ -1348,9 +1350,14 @@ def _graph_comm_1rank_worker(out_dir):
             mode = f"{g.comm_mode}/{int(g.defer)}/{int(g.gA0 is not None)}" if g is not None else "eager"
             tr.sync()
             res.append((losses, tr.flat.data.clone(), mode))
+            exposed = g.measure_comm(2) if g is not None else 0.0      # (changes the training state)
+            if g is not None and g.comm_mode == "event":
+                mode += f"/{len(g.events)}=={len(tr.reducer.buckets)}/{exposed is not None and exposed >= 0}"
             del tr
         (le, pe, _), (lg, pg, mode) = res
-        lines.append(f"{gd}/{mb} {(pe - pg).abs().max().item()} {max(abs(a - b) for a, b in zip(le, lg))} {mode}")
+        lines.append(f"{gd}/{mb}/{gc} {(pe - pg).abs().max().item()} {max(abs(a - b) for a, b in zip(le, lg))} "
+                     f"{mode}")
+    os.environ.pop("D3D_GRAPH_COMM", None)
     with open(os.path.join(out_dir, "gc1.txt"), "w") as f:
         f.write("\n".join(lines))
     cleanup()
@@ -1360,17 +1367,26 @@ def test_graph_step_captured_collectives_one_rank(tmp_path):
     """Graph A captured with the real bucketed RCCL all-reduces (1-rank
     group), deferred update on, fp32 and bf16 payloads, and a two-micro-batch
     step (leading graph gA0 captured too): comm_mode "graph", parameters equal
-    to the eager bucketed step within 5e-4.  No sleep before any capture."""
+    to the eager bucketed step within 5e-4.  No sleep before any capture.
+    The same three with D3D_GRAPH_COMM=0: comm_mode "event" (one external
+    event per bucket in graph A, the all-reduces issued behind them after each
+    replay), same parameters; measure_comm works in both modes."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from distributed_3d_diffusion_pytorch_amd.parallel import spawn
     import test_ops_gpu as me
     spawn(me._graph_comm_1rank_worker, 1, (str(tmp_path),))
     rows = open(tmp_path / "gc1.txt").read().split("\n")
-    assert [r.split()[0] for r in rows] == ["fp32/0", "bf16/0", "fp32/2"]
+    assert [r.split()[0] for r in rows] == ["fp32/0/1", "bf16/0/1", "fp32/2/1", "fp32/0/0", "bf16/0/0", "fp32/2/0"]
     for r in rows:
         gd, d, dl, mode = r.split()
-        assert mode == ("graph/0/1" if gd == "fp32/2" else "graph/1/0"), r
+        if gd.endswith("/1"):
+            assert mode == ("graph/0/1" if gd == "fp32/2/1" else "graph/1/0"), r
+        else:
+            # external-event mode: deferred update kept (one micro-batch), one event per bucket
+            nb = mode.split("/")[3].split("==")
+            assert mode.startswith("event/0/1" if gd == "fp32/2/0" else "event/1/0"), r
+            assert nb[0] == nb[1] and int(nb[0]) >= 2 and mode.endswith("/True"), r
         assert float(d) < 5e-4 and float(dl) < 2e-3, r
 
 

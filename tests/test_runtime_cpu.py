@@ -20,11 +20,11 @@ TINY_OV = {"model.ch": 32, "model.emb_ch": 64, "model.H": 16, "model.W": 16, "da
            "data.num_workers": 0, "data.synthetic": True}
 
 
-def _tiny_bench(gpus, extra=()):
+def _tiny_bench(gpus, extra=(), omp=2):
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     env.pop("RANK", None)
-    env["OMP_NUM_THREADS"] = "2"
+    env["OMP_NUM_THREADS"] = str(omp)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--device", "cpu", "--ch", "32",
            "--emb_ch", "64", "--imgsize", "16", "--global_batch", "4", "--steps", "2", "--warmup", "1",
            "--dtype", "fp32", "--backend", "torch", *extra]
@@ -59,6 +59,21 @@ def test_bench_reports_comm_diagnostics_four_ranks():
     assert c["buckets"] == len(c["bucket_mib"]) >= 1 and abs(sum(c["bucket_mib"]) - c["total_mib"]) < 0.1
     assert c["payload"] == "bf16"
     assert c["exposed_allreduce_ms"] >= 0.0
+
+
+def test_bench_eight_ranks_full_node_layout():
+    """The 8-GPU launch shape of the scaling run, rehearsed with 8 gloo ranks
+    on the host: `bench.py --gpus 8` self-spawns 8 ranks, the global batch is
+    split 8 ways, every rank's process group has world size 8, and the comm
+    record carries the bucket layout (sizes summing to the flat gradient, the
+    small first bucket first) and an exposed all-reduce time."""
+    r = _tiny_bench(8, ("--global_batch", "8", "--bucket_mb", "0.25"), omp=1)
+    assert r["n_gpus"] == 8 and r["config"]["parallelism"] == "dp8" and r["config"]["per_gpu_batch"] == 1
+    c = r["comm"]
+    assert c["world_pg"] == 8 and c["backend_pg"] == "gloo" and c["active"] and "error" not in c, c
+    assert c["buckets"] == len(c["bucket_mib"]) >= 2, c
+    assert abs(sum(c["bucket_mib"]) - c["total_mib"]) < 0.05
+    assert c["exposed_allreduce_ms"] >= 0.0 and r["value"] > 0
 
 
 def test_bench_launcher_fails_when_a_rank_dies():
