@@ -120,20 +120,22 @@ def probe_external_events(device: torch.device) -> bool:
     group (MIN) when a process group exists."""
     ok = 1.0
     try:
-        a = torch.randn(4096, 4096, device=device) * 1e-3
+        # (elementwise passes over 256 MiB, no library calls: a library's lazy
+        # initialisation inside the capture would invalidate it)
+        a = torch.zeros(64 << 20, device=device)
         cnt = torch.zeros(1, device=device)
         seen = torch.zeros(1, device=device)
         ev = torch.cuda.Event(external=True)
         g = torch.cuda.CUDAGraph()
+        a.mul_(0.5).add_(1.0)                # (warm the elementwise kernels outside the capture)
         torch.cuda.synchronize(device)
         with _gc_paused(), torch.cuda.graph(g, capture_error_mode="thread_local"):
-            b = a
-            for _ in range(16):
-                b = b @ a
-            cnt.add_(1.0 + 0.0 * b[0, :1])
+            for _ in range(16):              # ~2 ms of HBM-bound work ahead of the event
+                a.mul_(0.5).add_(1.0)
+            cnt.add_(1.0 + 0.0 * a[:1])
             ev.record()
             for _ in range(4):
-                b = b @ a
+                a.mul_(0.5).add_(1.0)
         s = torch.cuda.Stream(device=device)
         for rep in range(3):
             g.replay()
