@@ -112,8 +112,9 @@ def probe_graph_collective(device: torch.device) -> bool:
 
 
 def probe_external_events(device: torch.device) -> bool:
-    """True when an EXTERNAL event recorded inside a captured graph orders
-    work on another stream behind the replay's progress (comm_mode "event"):
+    """True when an EXTERNAL event recorded inside a captured graph
+    (ops.hip_impl.ExternalEvent) orders work on another stream behind the
+    replay's progress (comm_mode "event"):
     the graph runs ~3 ms of matmuls, then bumps a device counter and records
     the event; a second stream waits on the event and copies the counter.
     Reading a stale counter means the wait did not hold.  Agreed over the
@@ -125,7 +126,8 @@ def probe_external_events(device: torch.device) -> bool:
         a = torch.zeros(64 << 20, device=device)
         cnt = torch.zeros(1, device=device)
         seen = torch.zeros(1, device=device)
-        ev = torch.cuda.Event(external=True)
+        from ..ops.hip_impl import ExternalEvent
+        ev = ExternalEvent()                 # (torch refuses Event(external=True) on ROCm)
         g = torch.cuda.CUDAGraph()
         a.mul_(0.5).add_(1.0)                # (warm the elementwise kernels outside the capture)
         torch.cuda.synchronize(device)
@@ -139,7 +141,7 @@ def probe_external_events(device: torch.device) -> bool:
         s = torch.cuda.Stream(device=device)
         for rep in range(3):
             g.replay()
-            s.wait_event(ev)
+            ev.wait_on(s)
             with torch.cuda.stream(s):
                 seen.copy_(cnt)
             torch.cuda.current_stream(device).wait_stream(s)
@@ -211,7 +213,8 @@ class GraphedTrainStep:
                 self.comm_mode = "graph"
             elif want != "post" and dist.get_backend() == "nccl" and probe_external_events(dev):
                 self.comm_mode = "event"
-                self.events = [torch.cuda.Event(external=True) for _ in red.buckets]
+                from ..ops.hip_impl import ExternalEvent
+                self.events = [ExternalEvent() for _ in red.buckets]
                 self.comm_stream = torch.cuda.Stream(device=dev)
             else:
                 self.comm_mode = "post"

@@ -159,7 +159,7 @@ class GradReducer:
         prev = self.enabled
         self.enabled = True
         for b, ev in enumerate(self.events):
-            stream.wait_event(ev)
+            ev.wait_on(stream)
             with torch.cuda.stream(stream):
                 self._launched[b] = True
                 self._collective(b)

@@ -1392,11 +1392,14 @@ def test_graph_step_captured_collectives_one_rank(tmp_path):
         gd, d, dl, mode = r.split()
         if gd.endswith("/1"):
             assert mode == ("graph/0/1" if gd == "fp32/2/1" else "graph/1/0"), r
-        else:
+        elif mode.startswith("event"):
             # external-event mode: deferred update kept (one micro-batch), one event per bucket
             nb = mode.split("/")[3].split("==")
             assert mode.startswith("event/0/1" if gd == "fp32/2/0" else "event/1/0"), r
             assert nb[0] == nb[1] and int(nb[0]) >= 2 and mode.endswith("/True"), r
+        else:
+            # the event probe refused this stack: the chunked post-graph reduction
+            assert mode.startswith("post/0/"), r
         assert float(d) < 5e-4 and float(dl) < 2e-3, r
 
 

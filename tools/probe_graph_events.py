@@ -23,7 +23,9 @@ def external():
     a = torch.zeros(64 << 20, device=dev)
     cnt = torch.zeros(1, device=dev)
     seen = torch.zeros(1, device=dev)
-    ev = torch.cuda.Event(external=True)
+    sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+    from distributed_3d_diffusion_pytorch_amd.ops.hip_impl import ExternalEvent
+    ev = ExternalEvent()
     g = torch.cuda.CUDAGraph()
     a.mul_(0.5).add_(1.0)
     torch.cuda.synchronize()
@@ -36,7 +38,7 @@ def external():
     s = torch.cuda.Stream()
     for rep in range(3):
         g.replay()
-        s.wait_event(ev)
+        ev.wait_on(s)
         with torch.cuda.stream(s):
             seen.copy_(cnt)
         torch.cuda.current_stream().wait_stream(s)
