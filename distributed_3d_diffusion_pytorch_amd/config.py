@@ -80,6 +80,10 @@ class DistConfig:
     bucket_mb: float = 64.0          # gradient bucket size (xGMI: see SURVEY 5.8)
     first_bucket_mb: float = 4.0
     grad_dtype: str = "fp32"         # fp32 | bf16 all-reduce payload
+    # payload of the graph step's post-graph fallback (comm_mode "post": the
+    # RCCL capture probe failed, so the reduction cannot overlap backward and
+    # runs exposed after the replay -- half the bytes there): bf16 | fp32
+    post_grad_dtype: str = "bf16"
     timeout_s: float = 600.0
     checksum_every: int = 0          # cross-rank parameter checksum cadence
     force_comm: bool = False         # test switch: bucketed reducer + its collectives even at world 1

@@ -24,19 +24,16 @@ Layout of one step (MI355X, one process per GPU):
       payload (dist.grad_dtype) narrows each bucket into a persistent bf16
       mirror on the collective's stream and widens it back inside the graph.
       ``dist.force_comm`` runs this topology on a 1-rank RCCL group (tests).
-  [world > 1, comm_mode "event"] when a probe capture of an RCCL collective
-      fails (or D3D_GRAPH_COMM=0): graph A is captured WITHOUT collectives but
-      with one EXTERNAL event-record node per bucket, placed where the bucket's
-      last gradient is deposited (the same hooks / sink notifications).  After
-      each replay the host issues every bucket's all-reduce eagerly on a comm
-      stream behind its event, so the reduction of bucket k still overlaps the
-      backward kernels the replay runs for the layers below it -- the
-      in-graph overlap without capturing RCCL -- and the deferred update
-      stays on.  An external-event probe gates it.
-  [world > 1, comm_mode "post"] last resort (the event probe failed too, or
-      D3D_GRAPH_COMM=post, or gloo): eager all-reduce of the flat gradient
-      after graph A in 4 async chunks, each chunk's Adam launched as soon as
-      its collective lands.
+  [world > 1, comm_mode "post"] fallback when a probe capture of an RCCL
+      collective fails (or D3D_GRAPH_COMM=0, or gloo): eager all-reduce of the
+      flat gradient after graph A in 4 async chunks, each chunk's Adam
+      launched as soon as its collective lands; bf16 payload by default
+      (dist.post_grad_dtype: the reduction is exposed here, so half the bytes
+      is half the exposed time).  (Overlapping it with the replay's backward
+      would need a signal out of the running graph: external event-record
+      nodes are refused by this stack -- torch's Event(external=True) on ROCm
+      and hipEventRecordWithFlags(hipEventRecordExternal) inside a capture,
+      hipErrorInvalidValue on the box, which also invalidates the capture.)
   graph B: fused Adam reading its per-step hyper-parameters from a device
       block (lr warmup / bias correction change every step; the 1/world
       gradient average is folded in) -> batched weight repack -> gradient /
@@ -111,56 +108,6 @@ def probe_graph_collective(device: torch.device) -> bool:
     return bool(flag.item() > 0.5)
 
 
-def probe_external_events(device: torch.device) -> bool:
-    """True when an EXTERNAL event recorded inside a captured graph
-    (ops.hip_impl.ExternalEvent) orders work on another stream behind the
-    replay's progress (comm_mode "event"):
-    the graph runs ~3 ms of matmuls, then bumps a device counter and records
-    the event; a second stream waits on the event and copies the counter.
-    Reading a stale counter means the wait did not hold.  Agreed over the
-    group (MIN) when a process group exists."""
-    ok = 1.0
-    try:
-        # (elementwise passes over 256 MiB, no library calls: a library's lazy
-        # initialisation inside the capture would invalidate it)
-        a = torch.zeros(64 << 20, device=device)
-        cnt = torch.zeros(1, device=device)
-        seen = torch.zeros(1, device=device)
-        from ..ops.hip_impl import ExternalEvent
-        ev = ExternalEvent()                 # (torch refuses Event(external=True) on ROCm)
-        g = torch.cuda.CUDAGraph()
-        a.mul_(0.5).add_(1.0)                # (warm the elementwise kernels outside the capture)
-        torch.cuda.synchronize(device)
-        with _gc_paused(), torch.cuda.graph(g, capture_error_mode="thread_local"):
-            for _ in range(16):              # ~2 ms of HBM-bound work ahead of the event
-                a.mul_(0.5).add_(1.0)
-            cnt.add_(1.0 + 0.0 * a[:1])
-            ev.record()
-            for _ in range(4):
-                a.mul_(0.5).add_(1.0)
-        s = torch.cuda.Stream(device=device)
-        for rep in range(3):
-            g.replay()
-            ev.wait_on(s)
-            with torch.cuda.stream(s):
-                seen.copy_(cnt)
-            torch.cuda.current_stream(device).wait_stream(s)
-            torch.cuda.synchronize(device)
-            if float(seen.item()) != float(rep + 1):
-                print(f"[graphs] external-event probe: replay {rep} saw counter {float(seen.item())}", flush=True)
-                ok = 0.0
-                break
-        del g
-    except Exception as e:                   # noqa: BLE001 -- any failure means "do not use external events"
-        print(f"[graphs] external-event probe failed ({type(e).__name__}: {e})", flush=True)
-        ok = 0.0
-    if dist.is_available() and dist.is_initialized():
-        flag = torch.tensor([ok], device=device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        ok = float(flag.item())
-    return ok > 0.5
-
-
 _FUSED_UPDATE = True
 # Deferred optimizer step: the Adam update of step t runs inside the replay of
 # step t+1's graph A, the bulk of it on a side stream overlapped with the
@@ -202,22 +149,16 @@ class GraphedTrainStep:
         self.gA0: Optional[torch.cuda.CUDAGraph] = None     # fwd+bwd without comm (leading micro-batches)
         self.gB: Optional[torch.cuda.CUDAGraph] = None
         self.comm_mode = None
-        self.events = None
         red = trainer.reducer
         if red is not None and red.active:
             # fp32 and bf16 payloads alike (the bf16 mirror is persistent, see
-            # parallel/ddp.py): the collectives are captured inside graph A;
-            # failing that, issued behind external events of the replay
-            want = os.environ.get("D3D_GRAPH_COMM", "1")
-            if want == "1" and probe_graph_collective(dev):
-                self.comm_mode = "graph"
-            elif want != "post" and dist.get_backend() == "nccl" and probe_external_events(dev):
-                self.comm_mode = "event"
-                from ..ops.hip_impl import ExternalEvent
-                self.events = [ExternalEvent() for _ in red.buckets]
-                self.comm_stream = torch.cuda.Stream(device=dev)
-            else:
-                self.comm_mode = "post"
+            # parallel/ddp.py): the collectives are captured inside graph A
+            want = os.environ.get("D3D_GRAPH_COMM", "1") != "0"
+            self.comm_mode = "graph" if (want and probe_graph_collective(dev)) else "post"
+        # post mode: a persistent narrow mirror of the flat gradient (bf16 payload)
+        self.post_mirror = None
+        if self.comm_mode == "post" and trainer.cfg.dist.post_grad_dtype == "bf16":
+            self.post_mirror = torch.empty(trainer.flat.grad.numel(), dtype=torch.bfloat16, device=dev)
         # Deferred, overlapped optimizer step (see step()): needs the fused
         # update, the in-graph (or no) reduction and one micro-batch per step.
         split = trainer.model.update_parts() if hasattr(trainer.model, "update_parts") else None
@@ -234,17 +175,13 @@ class GraphedTrainStep:
             self.H.set_words(self.hp, _NOOP_HP)
 
     # ------------------------------------------------------------------
-    def _body(self, comm: bool = False, defer: bool = False, events: bool = False) -> None:
-        """One micro-batch forward + backward.  ``comm``: the bucket
-        all-reduces are issued (captured) from the gradient hooks; ``events``
-        (capture only): the hooks record the buckets' external events instead."""
+    def _body(self, comm: bool = False, defer: bool = False) -> None:
         tr = self.tr
         if tr.sink is not None:
             tr.sink.reset()
         red = tr.reducer
         if red is not None:
-            red.enabled = comm or events
-            red.events = self.events if events else None
+            red.enabled = comm
             red.reset()
         from ..models import xunet as _xunet
         main = torch.cuda.current_stream()
@@ -278,11 +215,10 @@ class GraphedTrainStep:
         loss = ops.diff_loss_nhwc(y, eps, tr.cfg.diffusion.loss_type)
         (loss * self.frac).backward()
         self.loss_acc.add_(loss.detach() * self.frac)
-        if red is not None and (comm or events):
+        if red is not None and comm:
             red.finish()            # remaining buckets + the join of RCCL's stream (captured edges)
         if red is not None:
             red.enabled = False
-            red.events = None
 
     def _update(self) -> None:
         o = self.tr.optim
@@ -323,7 +259,6 @@ class GraphedTrainStep:
         tr.model.set_dropout_seed(0)             # baked; the per-step part is self.seed
         self.H.set_device_seed(self.seed)
         comm = self.comm_mode == "graph"
-        events = self.comm_mode == "event"
         self.img.normal_()
         self.R.copy_(torch.eye(3, device=self.R.device).expand_as(self.R))
         self.K.copy_(torch.eye(3, device=self.K.device).expand_as(self.K))
@@ -352,12 +287,11 @@ class GraphedTrainStep:
         if self.defer:
             self.H.prepare_update_parts(tr.flat, self.parts)
         torch.cuda.synchronize()
-        # RCCL's watchdog thread keeps querying the events of eager collectives
-        mode = "thread_local" if self.comm_mode is not None else "global"
+        mode = "thread_local" if comm else "global"     # RCCL's watchdog thread keeps querying events
         # graphs sharing a memory pool are captured in their replay order
         # (leading micro-batches first)
         with _gc_paused():
-            if (comm or events) and nchunks > 1:
+            if comm and nchunks > 1:
                 self.gA0 = torch.cuda.CUDAGraph()
                 self.gA0.register_generator_state(tr.gen)
                 with torch.cuda.graph(self.gA0, pool=self.pool, capture_error_mode=mode):
@@ -365,7 +299,7 @@ class GraphedTrainStep:
             self.gA = torch.cuda.CUDAGraph()
             self.gA.register_generator_state(tr.gen)
             with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
-                self._body(comm, defer=self.defer, events=events)
+                self._body(comm, defer=self.defer)
             self.gB = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.gB, pool=self.pool, capture_error_mode=mode):
                 self._update()
@@ -380,17 +314,27 @@ class GraphedTrainStep:
 
     # ------------------------------------------------------------------
     def _reduce_update_chunked(self) -> None:
-        """fp32 all-reduce in chunks, each chunk's Adam behind its own
-        collective (overlaps the optimizer with the remaining reduction)."""
+        """All-reduce in chunks (bf16 payload through a persistent mirror by
+        default), each chunk's Adam behind its own collective (overlaps the
+        optimizer with the remaining reduction)."""
         o = self.tr.optim
         p, g, m, v, ema = o.flat.data, o.flat.grad, o.exp_avg, o.exp_avg_sq, o.ema
         n = g.numel()
         k = 4
         cuts = [0] + [min(n, (n * i // k + 255) // 256 * 256) for i in range(1, k)] + [n]
         spans = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
-        works = [dist.all_reduce(g[a:b], async_op=True) for a, b in spans]
+        mir = self.post_mirror
+        works = []
+        for a, b in spans:
+            if mir is None:
+                works.append(dist.all_reduce(g[a:b], async_op=True))
+            else:
+                mir[a:b].copy_(g[a:b])
+                works.append(dist.all_reduce(mir[a:b], async_op=True))
         for (a, b), w in zip(spans, works):
             w.wait()
+            if mir is not None:
+                g[a:b].copy_(mir[a:b])
             self.H.adam_flat_dev(p[a:b], g[a:b], m[a:b], v[a:b], ema[a:b] if ema is not None else None, self.hp,
                                  refresh=False)
         self.H.refresh_weights()
@@ -419,21 +363,19 @@ class GraphedTrainStep:
             self.K.copy_(K[s:s + mb])
             last = ci == nchunks - 1
             (self.gA if (last or self.gA0 is None) else self.gA0).replay()
-        if self.comm_mode == "event":
-            # the bucket all-reduces behind the replay's external events (overlapping its backward)
-            tr.reducer.issue_after_events(self.comm_stream)
         loss = self.loss_acc.clone()
         world = tr.ctx.world
         o = tr.optim
         clip = tr.cfg.optim.grad_clip
         o.hparams_to(self.hp, 1.0 / world)        # kernel-argument write: no host wait
         post = self.comm_mode == "post"
-        if post and (clip > 0 or want_norm or tr.cfg.dist.grad_dtype == "bf16"):
+        if post and (clip > 0 or want_norm):
+            # the norm needs the whole reduced gradient first: one reduction, no chunking
             g = tr.flat.grad
-            if tr.cfg.dist.grad_dtype == "bf16":
-                gb = g.to(torch.bfloat16)
-                dist.all_reduce(gb)
-                g.copy_(gb)
+            if self.post_mirror is not None:
+                self.post_mirror.copy_(g)
+                dist.all_reduce(self.post_mirror)
+                g.copy_(self.post_mirror)
             else:
                 dist.all_reduce(g)
             post = False
@@ -479,13 +421,6 @@ class GraphedTrainStep:
         if self.comm_mode == "post":
             with_comm = dev_ms(lambda: (self.gA.replay(), self._reduce_update_chunked()))
             without = dev_ms(lambda: (self.gA.replay(), self._update()))
-            return max(0.0, with_comm - without)
-        if self.comm_mode == "event":
-            with_comm = dev_ms(lambda: (self.gA.replay(), self.tr.reducer.issue_after_events(self.comm_stream)))
-            without = dev_ms(self.gA.replay)
-            with_comm = min(with_comm, dev_ms(lambda: (self.gA.replay(),
-                                                       self.tr.reducer.issue_after_events(self.comm_stream))))
-            tr.flat.zero_grad()
             return max(0.0, with_comm - without)
         g0 = torch.cuda.CUDAGraph()
         g0.register_generator_state(tr.gen)

@@ -24,10 +24,6 @@ SIGNATURES = {
     "d3d_border_fix": [P, P, I, I, I, I, I, I, I, P, P],
     "d3d_border_sums": [P, P, I, I, I, I, P],
     "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, I, P, P],
-    "d3d_event_create": [],
-    "d3d_event_destroy": [P],
-    "d3d_event_record_external": [P, P],
-    "d3d_stream_wait_event": [P, P],
     "d3d_gn_img_cfg": [I],
     "d3d_gn_img_ok": [I, I, I],
     "d3d_gn_img_fwd": [I, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, P, P],
@@ -120,8 +116,7 @@ def declare(lib: C.CDLL) -> None:
         if fn is None:          # an older build (A/B runs via D3D_LIB_PATH): calls fail when made
             continue
         fn.argtypes = args
-        fn.restype = C.c_long if name in RET_LONG else (C.c_void_p if name in RET_PTR else C.c_int)
+        fn.restype = C.c_long if name in RET_LONG else C.c_int
 
 
 RET_LONG = {"d3d_mlp_ws", "d3d_wgrad_group"}
-RET_PTR = {"d3d_event_create"}

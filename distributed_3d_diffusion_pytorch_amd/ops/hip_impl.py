@@ -347,35 +347,6 @@ def set_device_seed(t: Optional[torch.Tensor]) -> None:
     _SEED_DEV[0] = t
 
 
-class ExternalEvent:
-    """A HIP event whose record INSIDE a stream capture becomes an external
-    event-record node of the graph (csrc/streamsig.hip): each replay records
-    it when it reaches that point, so a stream outside the graph can wait on
-    the replay's progress (engine/graphs.py comm_mode "event").  Outside a
-    capture, ``record`` is a plain event record."""
-
-    def __init__(self):
-        self.h = _lib.d3d_event_create()
-        if not self.h:
-            raise RuntimeError("hipEventCreateWithFlags failed")
-
-    def record(self, stream=None) -> None:
-        st = stream if stream is not None else torch.cuda.current_stream()
-        _chk(_lib.d3d_event_record_external(self.h, st.cuda_stream), "event_record_external")
-
-    def wait_on(self, stream) -> None:
-        """Make ``stream`` wait for the most recent record of this event."""
-        _chk(_lib.d3d_stream_wait_event(stream.cuda_stream, self.h), "stream_wait_event")
-
-    def __del__(self):
-        h, self.h = getattr(self, "h", None), None
-        if h and _lib is not None:
-            try:
-                _lib.d3d_event_destroy(h)
-            except Exception:       # noqa: BLE001 -- interpreter shutdown
-                pass
-
-
 # ------------------------------------------------------------ GroupNorm ----
 def _gn_plan(N, P, C):
     a, b = ctypes.c_int(), ctypes.c_int()

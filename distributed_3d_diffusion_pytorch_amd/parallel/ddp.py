@@ -71,11 +71,6 @@ class GradReducer:
             for i in bk["params"]:
                 self.param_bucket[i] = b
         self.sink = None            # ops.gradsink.GradSink delivering kernel-deposited grads
-        # graph step, comm_mode "event" (engine/graphs.py): while graph A is
-        # captured, a completed bucket records its EXTERNAL event here instead
-        # of issuing the collective; the collectives are issued eagerly behind
-        # those events after each replay (issue_after_events)
-        self.events: Optional[list] = None
         self._pending = [0] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
         self._works: List = []
@@ -114,22 +109,16 @@ class GradReducer:
         if self._launched[b]:
             return
         self._launched[b] = True
-        ctx = self.sink.collective() if self.sink is not None else contextlib.nullcontext()
-        with ctx:       # behind the sink's weight-gradient stream (ops/gradsink.py)
-            if self.events is not None:
-                self.events[b].record()         # (graph capture: an external event-record node)
-                return
-            self._collective(b)
-
-    def _collective(self, b: int) -> None:
         bk = self.buckets[b]
         view = self.flat.grad[bk["start"]: bk["end"]]
-        if self.mirror is None:
-            self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
-        else:
-            tmp = self.mirror[bk["start"]: bk["end"]]
-            tmp.copy_(view)                                         # narrow on the collective's stream
-            self._works.append((dist.all_reduce(tmp, group=self.group, async_op=True), tmp, view))
+        ctx = self.sink.collective() if self.sink is not None else contextlib.nullcontext()
+        with ctx:       # behind the sink's weight-gradient stream (ops/gradsink.py)
+            if self.mirror is None:
+                self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+            else:
+                tmp = self.mirror[bk["start"]: bk["end"]]
+                tmp.copy_(view)                                     # narrow on the collective's stream
+                self._works.append((dist.all_reduce(tmp, group=self.group, async_op=True), tmp, view))
 
     def finish(self) -> None:
         """Launch any bucket whose gradients never arrived (unused params) and
@@ -147,24 +136,6 @@ class GradReducer:
             if tmp is not None:
                 view.copy_(tmp)                                     # widen (persistent mirror: no recycling)
         self.reset()
-
-    def issue_after_events(self, stream) -> None:
-        """comm_mode "event": after a replay of graph A, issue every bucket's
-        all-reduce on ``stream`` behind that bucket's external event (recorded
-        by the replay when the bucket's gradients are complete), so the
-        reduction of bucket k overlaps the backward kernels the graph still
-        runs for the layers below it; then make the current stream wait for
-        all of them (finish())."""
-        assert self.events is not None and len(self.events) == len(self.buckets)
-        prev = self.enabled
-        self.enabled = True
-        for b, ev in enumerate(self.events):
-            ev.wait_on(stream)
-            with torch.cuda.stream(stream):
-                self._launched[b] = True
-                self._collective(b)
-        self.finish()
-        self.enabled = prev
 
     def describe(self) -> dict:
         """Bucket layout and payload, for benchmark / metrics records."""
