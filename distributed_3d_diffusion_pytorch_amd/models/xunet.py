@@ -36,11 +36,6 @@ INV_SQRT2 = 1.0 / math.sqrt(2.0)
 
 
 _COND_STREAM = os.environ.get("D3D_COND_STREAM", "1") != "0"
-# Level-batched FiLM as part GEMMs (ops.film_batch(parts=)): 0 one GEMM per
-# level; 1 level 0 as [first encoder block] [rest of the encoder] [decoder]
-# -- its backward then starts per part as the trunk's backward completes
-# each part instead of forming the tail of the step; 2 every level.
-_FILM_PARTS = int(os.environ.get("D3D_FILM_PARTS", "1"))
 # conditioning stream: one FiLM GEMM + ready event per block instead of one per level
 FILM_BLOCK_EVENTS = False        # measured -1.2 % at bs16 and bs128 (profiles/r3/ab_film_events_s64.txt)
 _COND_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
@@ -394,24 +389,6 @@ class XUNet(nn.Module):
             self.__dict__["_fg"] = groups
         return self.__dict__["_fg"]
 
-    def _film_parts(self, level: int):
-        """Part GEMMs of a level's FiLM projections (indices into
-        ``_film_groups()[level]``) or None for one GEMM: the first encoder
-        block (needed first in forward, its backward completes last), the
-        rest of the encoder (+ the middle block at the last level), the
-        decoder blocks (their backward completes first)."""
-        if _FILM_PARTS == 0 or (_FILM_PARTS == 1 and level != 0):
-            return None
-        n = len(self._film_groups()[level])
-        nd = len(self.xunetblocks[level])
-        dec = list(range(nd, n))
-        if level == self.num_resolutions - 1:            # the middle block is the group's last entry
-            dec, mid = dec[:-1], [n - 1]
-        else:
-            mid = []
-        parts = [[0], list(range(1, nd)) + mid, dec]
-        return [p for p in parts if p]
-
     # -- dropout seeding: every forward gets a fresh base seed (set by the
     # trainer from its step counter) so HIP dropout masks are reproducible and
     # regenerated (not stored) in backward.
@@ -567,8 +544,7 @@ class XUNet(nn.Module):
                     if fence is not None and i == fence[0]:
                         cs.wait_event(fence[1])
                     outs = ops.film_batch(semb, [b.film.dense.weight for b in blocks],
-                                          [b.film.dense.bias for b in blocks], block_events=FILM_BLOCK_EVENTS,
-                                          parts=self._film_parts(i))
+                                          [b.film.dense.bias for b in blocks], block_events=FILM_BLOCK_EVENTS)
                     for o in outs:
                         o.record_stream(main)       # read by the trunk's GN-FiLM kernels
                     ev = torch.cuda.Event()
@@ -589,8 +565,7 @@ class XUNet(nn.Module):
                 if fence is not None and i == fence[0]:
                     torch.cuda.current_stream().wait_event(fence[1])
                 outs = ops.film_batch(sembs[i], [b.film.dense.weight for b in blocks],
-                                      [b.film.dense.bias for b in blocks],
-                                      parts=self._film_parts(i) if ss_map is None else None)
+                                      [b.film.dense.bias for b in blocks])
                 for b, o in zip(blocks, outs):
                     b.__dict__["_ss"] = o
         xz = batch.get("xz")

@@ -112,13 +112,11 @@ def cat_gn_silu_dense(a, b, gw, gb, dw, db, groups: int = 32, eps: float = 1e-5)
     return _t.cat_gn_silu_dense(a, b, gw, gb, dw, db, groups, eps)
 
 
-def film_batch(emb, weights, biases, block_events: bool = False, parts=None):
+def film_batch(emb, weights, biases, block_events: bool = False):
     """``dense_i(silu(emb))`` for every FiLM projection of one level
-    (``block_events``, HIP path: one GEMM and ready event per block;
-    ``parts``: index lists, one GEMM + ready event per part, see
-    hip_impl.film_batch)."""
+    (``block_events``, HIP path: one GEMM and ready event per block)."""
     if use_hip(emb):
-        return _h().film_batch(emb, weights, biases, block_events, parts)
+        return _h().film_batch(emb, weights, biases, block_events)
     return _t.film_batch(emb, weights, biases)
 
 

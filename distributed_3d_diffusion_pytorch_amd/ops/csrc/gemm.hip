@@ -10,8 +10,7 @@
 // with an fp32 (F_B32) or bf16 (F_B16) bias, a residual (F_RES) and the
 // GroupNorm partial statistics of O (F_GN); or F_DSILU: alpha * acc *
 // dsilu(R[n][m]) -- the FiLM input gradient through the SiLU of the
-// conditioning embedding -- plus R2[n][m] with F_DSILU | F_RES (the level's
-// FiLM input gradient accumulated over its part GEMMs, in place).
+// conditioning embedding.
 //
 // Schedule ("fat waves"): a 256-thread block = 2 x 2 waves, one per SIMD, each
 // owning WI x WJ MFMA 16x16x32 tiles (8 x 8 = 128 x 128 outputs and 256 fp32
@@ -75,10 +74,9 @@ enum : int { F_B32 = 1, F_B16 = 2, F_RES = 4, F_GN = 8, F_DSILU = 16 };
 // Epilogue parameters of one tile (32-bit offsets from the tile's row base).
 struct GEpi {
   const bf16* R;                 // residual / pre-activation rows n0.. of this tile
-  const bf16* R2;                // F_DSILU | F_RES: the residual rows (R is the pre-activation)
   bf16* obase;                   // output rows n0.. (buffer descriptor base / size: descriptors stay out of
-  int orec, rrec, r2rec;         // structs and lambda signatures, which the host pass also type-checks)
-  int M, ldo, ldr, ldr2;
+  int orec, rrec;                // structs and lambda signatures, which the host pass also type-checks)
+  int M, ldo, ldr;
   float as, bs, rs;              // acc, bias and residual factors
   int m0;
   int wm, wn, lane;
@@ -115,17 +113,7 @@ __device__ __forceinline__ void g_epi_pair(const f32x4 (&acc)[WI][WJ], const GEp
     const int oy = cok ? ((px + 16) * e.ldr + cl) * 2 : (int)0x80000000;
     const u2l rx2 = g_load8(e.R, e.rrec, ox), ry2 = g_load8(e.R, e.rrec, oy);
     const bf16x4 rx = __builtin_bit_cast(bf16x4, rx2), ry = __builtin_bit_cast(bf16x4, ry2);
-    if constexpr ((F & F_DSILU) && (F & F_RES)) {
-      const int qx = cok ? (px * e.ldr2 + cl) * 2 : (int)0x80000000;
-      const int qy = cok ? ((px + 16) * e.ldr2 + cl) * 2 : (int)0x80000000;
-      const bf16x4 sx = __builtin_bit_cast(bf16x4, g_load8(e.R2, e.r2rec, qx));
-      const bf16x4 sy = __builtin_bit_cast(bf16x4, g_load8(e.R2, e.r2rec, qy));
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        vx[k] = __builtin_fmaf(x[k] * e.as, dsiluf_((float)rx[k]), (float)sx[k]);
-        vy[k] = __builtin_fmaf(y[k] * e.as, dsiluf_((float)ry[k]), (float)sy[k]);
-      }
-    } else if constexpr (F & F_DSILU) {
+    if constexpr (F & F_DSILU) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         vx[k] = x[k] * e.as * dsiluf_((float)rx[k]);
@@ -178,8 +166,7 @@ template <int WI, int WJ, int F, int NST = 2>
 __global__ void __launch_bounds__(256, 1)
 gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ O, const float* __restrict__ bias,
           const bf16* __restrict__ R, int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha,
-          float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw,
-          const bf16* __restrict__ R2, int ldr2) {
+          float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw) {
   constexpr bool BIAS = (F & (F_B32 | F_B16)) != 0, BBF = (F & F_B16) != 0;
   using C = GCfg<WI, WJ, NST>;
   // 4 bias slots: the loader may run at most 3 tiles ahead -- NST 4 needs K >= 128 (host)
@@ -389,13 +376,9 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
       e.orec = (int)(rows * ldo * 2);
       e.R = (F & (F_RES | F_DSILU)) ? R + n0 * ldr : nullptr;
       e.rrec = (F & (F_RES | F_DSILU)) ? (int)(rows * ldr * 2) : 0;
-      constexpr bool R2ON = (F & F_DSILU) && (F & F_RES);
-      e.R2 = R2ON ? R2 + n0 * ldr2 : nullptr;
-      e.r2rec = R2ON ? (int)(rows * ldr2 * 2) : 0;
       e.M = M;
       e.ldo = ldo;
       e.ldr = ldr;
-      e.ldr2 = ldr2;
       e.as = (F & F_DSILU) ? alpha : alpha * scale;
       e.bs = scale;
       e.rs = scale;
@@ -501,25 +484,23 @@ D3D_API int d3d_gemm_nt_ok(int M, int N, int K, int lda, int ldb) {
 template <int W, int F, int NST = 2>
 static void g_launch(int G_, hipStream_t st, const void* A, const void* B, void* O, const void* bias, const void* R,
                      int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, int mt, int nt,
-                     int gm, float* gnp, int G, int hw, const void* R2 = nullptr, int ldr2 = 0) {
+                     int gm, float* gnp, int G, int hw) {
   hipLaunchKernelGGL((gemm_fw_k<W, W, F, NST>), dim3(G_), dim3(256), 0, st, (const bf16*)A, (const bf16*)B,
                      (bf16*)O, (const float*)bias, (const bf16*)R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt,
-                     gm, gnp, G, hw, (const bf16*)R2, ldr2);
+                     gm, gnp, G, hw);
 }
 
 // epi 0: O = (alpha * A.B^T + bias + R) * scale (+ GroupNorm partials gnp:
 // [N / hw][G][hw / 64] x (sum, sumsq), gn_part_store layout; needs hw % 64 ==
 // 0 and M / G in {4, 8, 16, 32}); epi 1: O = alpha * A.B^T * dsilu(R).
 // bias_bf16: the bias vector is bf16 (else fp32).
-// epi 2: O = alpha * A.B^T * dsilu(R) + R2 (R2 may alias O: in-place accumulation).
-D3D_API int d3d_gemm2(const void* A, const void* B, void* O, const void* bias_, int bias_bf16, const void* R, int M,
-                      int N, int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, float* gnp, int G,
-                      int hw, int epi, const void* R2, int ldr2, hipStream_t st) {
+D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, int bias_bf16, const void* R, int M,
+                     int N, int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, float* gnp, int G,
+                     int hw, int epi, hipStream_t st) {
   if (!d3d_gemm_nt_ok(M, N, K, lda, ldb)) return -1;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)O) & 15) return -1;
   if (ldo % 8 || ldo < M || (R && (ldr % 4 || ldr < M || ((uintptr_t)R & 7)))) return -1;
-  if ((epi == 1 || epi == 2) && (!R || bias_ || gnp)) return -1;
-  if (epi == 2 && (!R2 || ldr2 % 4 || ldr2 < M || ((uintptr_t)R2 & 7) || 256L * ldr2 * 2 >= (1L << 31))) return -1;
+  if (epi == 1 && (!R || bias_ || gnp)) return -1;
   if (gnp && bias_ && bias_bf16) return -1;
   int W = g_cfg(M, N);
   if (gnp) {
@@ -539,35 +520,26 @@ D3D_API int d3d_gemm2(const void* A, const void* B, void* O, const void* bias_, 
   const int per_cu = W == 8 ? 1 : W == 4 ? 2 : 4;
   const int G_ = (int)std::min<long>(tiles, g_grid > 0 ? g_grid : (long)g_cus() * per_cu);
   const int gm = std::max(1, std::min(mt, g_gm));
-  const int F = epi == 2 ? (F_DSILU | F_RES) : epi == 1 ? F_DSILU
+  const int F = epi == 1 ? F_DSILU
                           : (bias_ ? (bias_bf16 ? F_B16 : F_B32) : 0) | (R ? F_RES : 0) | (gnp ? F_GN : 0);
 #define G_CASE(W_, F_)                                                                                          \
   if (W == W_ && F == (F_)) {                                                                                   \
-    if (W_ != 8 && deep)                                                                                        \
+    if (W_ != 8 && deep)                                                                                   \
       g_launch<W_, F_, (W_ != 8 ? 4 : 2)>(G_, st, A, B, O, bias_, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, \
-                                          nt, gm, gnp, G, hw, R2, ldr2);                                        \
+                                          nt, gm, gnp, G, hw);                                                  \
     else                                                                                                        \
-      g_launch<W_, F_>(G_, st, A, B, O, bias_, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, hw, \
-                       R2, ldr2);                                                                               \
+      g_launch<W_, F_>(G_, st, A, B, O, bias_, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt, gm, gnp, G, hw); \
     return (int)hipGetLastError();                                                                              \
   }
 #define G_CASES(W_)                                                                                             \
   G_CASE(W_, 0) G_CASE(W_, F_B32) G_CASE(W_, F_B16) G_CASE(W_, F_RES) G_CASE(W_, F_B32 | F_RES)                 \
-  G_CASE(W_, F_B16 | F_RES) G_CASE(W_, F_DSILU) G_CASE(W_, F_DSILU | F_RES)
+  G_CASE(W_, F_B16 | F_RES) G_CASE(W_, F_DSILU)
   G_CASES(8) G_CASES(4) G_CASES(2)
   G_CASE(8, F_GN) G_CASE(8, F_B32 | F_GN) G_CASE(8, F_RES | F_GN) G_CASE(8, F_B32 | F_RES | F_GN)
   G_CASE(4, F_GN) G_CASE(4, F_B32 | F_GN) G_CASE(4, F_RES | F_GN) G_CASE(4, F_B32 | F_RES | F_GN)
 #undef G_CASES
 #undef G_CASE
   return -1;
-}
-
-D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, int bias_bf16, const void* R, int M,
-                     int N, int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, float* gnp, int G,
-                     int hw, int epi, hipStream_t st) {
-  if (epi == 2) return -1;
-  return d3d_gemm2(A, B, O, bias_, bias_bf16, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, gnp, G, hw, epi, nullptr,
-                   0, st);
 }
 
 D3D_API int d3d_gemm_nt_gn(const void* A, const void* B, void* O, const float* bias, const void* R, int M, int N,

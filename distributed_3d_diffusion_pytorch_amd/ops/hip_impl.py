@@ -1228,16 +1228,9 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, M: int, N: int,
     ``gnp``: the output's GroupNorm partial statistics (groups ``gn_groups``
     over images of ``gn_hw`` rows) from the same epilogue.  ``dsilu_of``
     (row stride ``ldr``): instead out = alpha * acc * dsilu(dsilu_of[n][m]) --
-    an input gradient through a SiLU whose pre-activation is dsilu_of -- plus
-    ``res`` (row stride ``ldo``; may be ``out`` itself: accumulation in place)
-    when both are given."""
+    an input gradient through a SiLU whose pre-activation is dsilu_of."""
     if bias is not None:
         assert bias.dtype in (F32, BF16) and bias.is_contiguous()
-    if dsilu_of is not None and res is not None:
-        _chk(_lib.d3d_gemm2(a.data_ptr(), b.data_ptr(), out.data_ptr(), None, 0, dsilu_of.data_ptr(), M, N, K, lda,
-                            ldb, ldo, ldr or ldo, float(alpha), float(scale), None, 0, 0, 2, res.data_ptr(), ldo,
-                            _st()), "gemm_dsilu_res")
-        return out
     epi = 0 if dsilu_of is None else 1
     r = res if dsilu_of is None else dsilu_of
     _chk(_lib.d3d_gemm(a.data_ptr(), b.data_ptr(), out.data_ptr(), _ptr(bias),
@@ -1416,26 +1409,6 @@ class _FiLMSlot:
         return self.buf[..., off: off + 2 * C]
 
 
-class _FiLMDeAcc:
-    """The input gradient d(e) of a level whose FiLM projections run as
-    several part GEMMs (film_batch(parts=)): each part's dgrad GEMM adds its
-    contribution into ONE buffer through its epilogue (dsilu + residual, in
-    place) and hands nothing to autograd; the part whose backward runs last
-    returns the total -- no autograd adds of [P, emb_ch] gradients.  An
-    end-of-backward check makes a partial backward (some part never ran)
-    an error instead of a silently missing gradient."""
-    __slots__ = ("n", "done", "buf")
-
-    def __init__(self, n: int):
-        self.n, self.done, self.buf = n, 0, None
-
-    def _check(self):
-        if self.done != 0:
-            n, self.done, self.buf = self.done, 0, None
-            raise RuntimeError(f"film_batch(parts=): only {n} of {self.n} part backwards ran; the level's "
-                               "embedding gradient was not returned")
-
-
 class _FiLMBatch(torch.autograd.Function):
     """All FiLM projections that read one level's conditioning embedding
     (`xunet.py:74-87`, ``dense(silu(emb))`` per ResnetBlock) as ONE GEMM
@@ -1447,7 +1420,7 @@ class _FiLMBatch(torch.autograd.Function):
     reduction scatters rows into each block's parameter gradient."""
 
     @staticmethod
-    def forward(ctx, e, slot, n, se, deacc, *wb):
+    def forward(ctx, e, slot, n, se, *wb):
         Ws, Bs = wb[:n], wb[n:]
         shp = e.shape
         K = shp[-1]
@@ -1481,12 +1454,12 @@ class _FiLMBatch(torch.autograd.Function):
             _fallback("film_batch", f"P={P} K={K} S={S} (library GEMM)")
             torch.addmm(bcat, x2, wcat.t(), out=y)
         ctx.save_for_backward(x2, e2)
-        ctx.n, ctx.slot, ctx.shp, ctx.deacc = n, slot, shp, deacc
+        ctx.n, ctx.slot, ctx.shp = n, slot, shp
         ctx.params = (Ws, Bs)
         ctx.widths = [w.shape[0] for w in Ws]
         for i, (w, b) in enumerate(zip(Ws, Bs)):
-            SINK.use(w, ctx.needs_input_grad[5 + i])
-            SINK.use(b, ctx.needs_input_grad[5 + n + i])
+            SINK.use(w, ctx.needs_input_grad[4 + i])
+            SINK.use(b, ctx.needs_input_grad[4 + n + i])
         y = y.view(*shp[:-1], S)
         outs, off = [], 0
         for wd in ctx.widths:
@@ -1524,31 +1497,17 @@ class _FiLMBatch(torch.autograd.Function):
         rows, K = x2.shape
         dx = None
         if ctx.needs_input_grad[0]:
-            acc = ctx.deacc
-            prev = acc.buf if acc is not None else None
-            dx = prev if prev is not None else torch.empty(rows, K, dtype=BF16, device=x2.device)
+            dx = torch.empty(rows, K, dtype=BF16, device=x2.device)
             if _gemm_ok(K, rows, S, S, S, dy, e2):
-                # d e = (dy @ Wcat) * dsilu(e) [+ the other parts' share, in place]: the SiLU derivative
-                # and the accumulation in the epilogue
-                gemm_nt(bf16_catT(Ws, "filmWT"), dy, dx, K, rows, S, S, S, K, dsilu_of=e2, ldr=K, res=prev)
+                # d e = (dy @ Wcat) * dsilu(e), the SiLU derivative in the epilogue
+                gemm_nt(bf16_catT(Ws, "filmWT"), dy, dx, K, rows, S, S, S, K, dsilu_of=e2, ldr=K)
             else:
                 _fallback("film_batch dgrad", f"P={rows} K={K} S={S} (library GEMM)")
                 ds = torch.mm(dy, bf16_cat(Ws, "filmW"))
-                d1 = torch.empty(rows, K, dtype=BF16, device=x2.device)
-                _chk(_lib.d3d_dsilu(e2.data_ptr(), ds.data_ptr(), d1.data_ptr(), d1.numel(), _st()), "dsilu")
-                dx = d1 if prev is None else prev.add_(d1)
-            if acc is not None:
-                acc.done += 1
-                if acc.done < acc.n:
-                    if acc.done == 1:
-                        torch.autograd.Variable._execution_engine.queue_callback(acc._check)
-                    acc.buf, dx = dx, None          # deposited: the part that runs last returns the sum
-                else:
-                    acc.buf, acc.done = None, 0
-            if dx is not None:
-                dx = dx.view(shp)
+                _chk(_lib.d3d_dsilu(e2.data_ptr(), ds.data_ptr(), dx.data_ptr(), dx.numel(), _st()), "dsilu")
+            dx = dx.view(shp)
         grads_w, grads_b = [None] * n, [None] * n
-        need_w = any(ctx.needs_input_grad[5: 5 + n])
+        need_w = any(ctx.needs_input_grad[4: 4 + n])
         if need_w:
             tw = [SINK.target(w) for w in Ws]
             tb = [SINK.target(b) for b in Bs]
@@ -1591,23 +1550,15 @@ class _FiLMBatch(torch.autograd.Function):
                 job()
                 grads_w = [t.view(w.shape) for t, w in zip(tw, Ws)]
                 grads_b = tb
-        return (dx, None, None, None, None, *grads_w, *grads_b)
+        return (dx, None, None, None, *grads_w, *grads_b)
 
 
-def film_batch(emb, weights, biases, block_events=False, parts=None):
+def film_batch(emb, weights, biases, block_events=False):
     """Level-batched FiLM projections ``dense_i(silu(emb))`` of the per-level
     pre-activation embedding -> tuple of ``[N,H,W,2C_i]`` modulations (column
     slices of one GEMM output; GN-FiLM reads them strided).  ``block_events``:
     one GEMM per block with a ready event attached to each output as
-    ``_d3d_ready`` (consumers on another stream wait per block).
-
-    ``parts`` (lists of block indices covering every block once): one GEMM
-    per part, in the given order, each output carrying its part's ready
-    event.  Backward: each part's input-gradient and weight-gradient GEMMs
-    start as soon as ITS blocks' d(scale|shift) are complete, instead of
-    after the level's last block -- at level 0 that is the tail of backward,
-    where the whole level's FiLM backward otherwise ran alone (bs16 trace) --
-    and the d(e) contributions accumulate in one buffer (_FiLMDeAcc)."""
+    ``_d3d_ready`` (consumers on another stream wait per block)."""
     _need_bf16(emb)
     K = emb.shape[-1]
     widths = [w.shape[0] for w in weights]
@@ -1615,32 +1566,11 @@ def film_batch(emb, weights, biases, block_events=False, parts=None):
         _fallback("film_batch", f"K={K} widths={widths}")
         se = silu(emb)
         return tuple(linear(se, w, b) for w, b in zip(weights, biases))
+    slot = _FiLMSlot(emb.shape[:-1], sum(widths), emb.device, want_events=bool(block_events))
     se = getattr(emb, "_d3d_silu", None)          # silu(emb) written by the conditioning conv (cond_conv)
     if se is not None and (se.shape != emb.shape or not se.is_contiguous() or not emb.is_contiguous()):
         se = None
-    if parts is not None and len(parts) > 1:
-        assert sorted(i for p_ in parts for i in p_) == list(range(len(weights))), parts
-        emb = emb.contiguous()
-        if se is None:
-            se = torch.empty_like(emb)             # silu(e) once for every part GEMM
-            _chk(_lib.d3d_silu(emb.data_ptr(), se.data_ptr(), emb.numel(), _st()), "silu")
-        acc = _FiLMDeAcc(len(parts))
-        outs = [None] * len(weights)
-        for p_ in parts:
-            ws_, bs_ = [weights[i] for i in p_], [biases[i] for i in p_]
-            slot = _FiLMSlot(emb.shape[:-1], sum(widths[i] for i in p_), emb.device)
-            po = _FiLMBatch.apply(emb, slot, len(ws_), se, acc, *ws_, *bs_)
-            ev = torch.cuda.Event()
-            ev.record()
-            off = 0
-            for i, o in zip(p_, po):
-                o._d3d_slot = (slot, off)
-                o._d3d_ready = ev
-                outs[i] = o
-                off += widths[i]
-        return tuple(outs)
-    slot = _FiLMSlot(emb.shape[:-1], sum(widths), emb.device, want_events=bool(block_events))
-    outs = _FiLMBatch.apply(emb.contiguous(), slot, len(weights), se, None, *weights, *biases)
+    outs = _FiLMBatch.apply(emb.contiguous(), slot, len(weights), se, *weights, *biases)
     off = 0
     for i, (o, wd) in enumerate(zip(outs, widths)):
         o._d3d_slot = (slot, off)

@@ -636,55 +636,6 @@ def test_sampler_step_matches_posterior(H):
     assert abs(nz.mean().item()) < 0.05 and abs(nz.std().item() - 1) < 0.05
 
 
-@pytest.mark.parametrize("parts", [[[0], [1, 2], [3]], [[2, 3], [0, 1]], [[1], [0], [3], [2]]])
-def test_film_batch_parts(H, parts):
-    """film_batch(parts=): one GEMM + ready event per part, each part's
-    backward accumulating its d(e) share in place through the dgrad
-    epilogue (dsilu + residual) and the last one returning the total ==
-    the single level GEMM and the fp32
-    per-block linears; a backward through only some parts is an error."""
-    torch.manual_seed(9)
-    K, chans, N, Hh = 1024, [128, 256, 128, 256], 8, 16
-    semb = (torch.randn(N, Hh, Hh, K, device=DEV) * 2).to(BF)
-    Ws = [torch.randn(2 * c, K, device=DEV) / 32 for c in chans]
-    Bs = [torch.randn(2 * c, device=DEV) * 0.1 for c in chans]
-    xs = [torch.randn(N, Hh, Hh, c, device=DEV).to(BF) for c in chans]
-    gam = [torch.rand(c, device=DEV) + 0.5 for c in chans]
-    bet = [torch.randn(c, device=DEV) * 0.1 for c in chans]
-    gos = [torch.randn(N, Hh, Hh, c, device=DEV) for c in chans]
-
-    def run(kind):
-        s = leaf(semb) if kind != "ref" else leaf(semb, torch.float32)
-        ws = [leaf(w) for w in Ws]
-        bs = [leaf(b) for b in Bs]
-        if kind == "ref":
-            sss = [T.linear(torch.nn.functional.silu(s), w, b) for w, b in zip(ws, bs)]
-        else:
-            sss = H.film_batch(s, ws, bs, parts=parts if kind == "parts" else None)
-        loss = 0
-        for x, g, b, ss, go in zip(xs, gam, bet, sss, gos):
-            xx = x if kind != "ref" else x.float()
-            y = (T if kind == "ref" else H).gn_film(xx, g, b, ss, 32, 1e-5, 0.0, False, 0)
-            loss = loss + (y.float() * go).sum()
-        loss.backward()
-        return [t.detach().clone() for t in sss], [s.grad] + [w.grad for w in ws] + [b.grad for b in bs]
-
-    fp, gp = run("parts")
-    f1, g1 = run("one")
-    _, gr = run("ref")
-    for a, b in zip(fp, f1):
-        assert rel(a, b) < 2e-3, rel(a, b)
-    for a, b, c in zip(gp, g1, gr):
-        assert rel(a, c) < 3e-2, rel(a, c)
-        assert rel(a, b) < 1e-2, rel(a, b)
-    # a backward that reaches only the first part's outputs: the accumulator refuses
-    s = leaf(semb)
-    ws, bs = [leaf(w) for w in Ws], [leaf(b) for b in Bs]
-    sss = H.film_batch(s, ws, bs, parts=[[0, 1], [2, 3]])
-    with pytest.raises(RuntimeError):
-        (sss[0].float().sum() + sss[1].float().sum()).backward()
-
-
 @pytest.mark.parametrize("mode", ["tn", "blas", "seg"])
 @pytest.mark.parametrize("chans,N,Hh", [([128, 128, 256], 4, 8), ([512, 512], 4, 8),
                                         ([128, 256, 384], 32, 32),    # 32768 rows: 8-wave 1x1 wgrad
