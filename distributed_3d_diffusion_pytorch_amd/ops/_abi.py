@@ -103,6 +103,7 @@ SIGNATURES = {
     "d3d_wgrad_group_ok": [P],
     "d3d_wgrad_group_stages": [I],
     "d3d_wgrad_group_halo": [I, I, I],
+    "d3d_wgrad_group_halo_big": [I, I],
     "d3d_wgrad_group_halo_pk": [I],
     "d3d_wgrad_group_engine": [P],
     "d3d_wgrad_group": [P, I, P, L, P],

@@ -724,6 +724,13 @@ static int g_gh_on = 1;
 // one 2 % full (the mixed decoder batch at 622 instead of ~990 TF/s,
 // profiles/r4/halo_wgrad/)
 static int g_gh_blocks = 256;
+// ... and for flushes of >= 2^g_gh_big_lg2 (tile x pixel) work -- the
+// bs128 steps, several 1M-pixel jobs per flush -- half that: twice the
+// pixels per block halves the split slabs (written by the blocks, re-read by
+// the reduce); the chip is busy with the input-gradient convs there anyway.
+// bs128 +2.0 %, bs16 (256 kept by the rule) unchanged, profiles/r5/ab_wgrad_halo_blocks.txt
+static int g_gh_blocks_big = 128;
+static int g_gh_big_lg2 = 22;
 static int g_gh_ns = 2;            // LDS ring stages of wgrad_halo_k (2 or 3)
 // pixels per K-step of wgrad_halo_k on W >= 64 jobs (64: half the barriers per MFMA; L0 flush
 // 945 -> 1051 TF/s at bs128, profiles/r4/halo_pk64/); 32 elsewhere
@@ -744,6 +751,12 @@ D3D_API int d3d_wgrad_group_halo(int on, int blocks, int ns) {
   if (on >= 0) g_gh_on = on ? 1 : 0;
   if (blocks > 0) g_gh_blocks = blocks;
   if (ns == 2 || ns == 3) g_gh_ns = ns;
+  return 0;
+}
+// big-flush target blocks and the work threshold (log2 of tile x pixel work); <= 0 keeps a value
+D3D_API int d3d_wgrad_group_halo_big(int blocks, int lg2) {
+  if (blocks > 0) g_gh_blocks_big = blocks;
+  if (lg2 > 0) g_gh_big_lg2 = lg2;
   return 0;
 }
 D3D_API int d3d_wgrad_group_halo_pk(int pk) {
@@ -801,7 +814,8 @@ static void gw_plan(const WgJobDesc* d, int n, GwPlan& pl, bool halo = false) {
     work += (double)pl.tiles[i] * P;
   }
   // one pixel count per block across the batch: ~g_gw_blocks equal blocks
-  long Q = (long)(work / (halo ? g_gh_blocks : g_gw_blocks));
+  const int gh_target = work >= (double)(1L << g_gh_big_lg2) ? g_gh_blocks_big : g_gh_blocks;
+  long Q = (long)(work / (halo ? gh_target : g_gw_blocks));
   Q = std::max<long>(Q, g_gw_minpix);
   Q = (Q + 63) / 64 * 64;
   if (halo) {

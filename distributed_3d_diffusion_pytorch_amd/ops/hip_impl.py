@@ -818,6 +818,8 @@ if os.environ.get("D3D_WGRAD_GROUP_NS"):               # A/B knob: LDS ring stag
 if os.environ.get("D3D_WGRAD_HALO"):                   # A/B knob "on[,blocks[,stages]]": all-taps halo tiles
     _hv = [int(v) for v in os.environ["D3D_WGRAD_HALO"].split(",")] + [0, 0]
     _lib.d3d_wgrad_group_halo(_hv[0], _hv[1], _hv[2])
+if os.environ.get("D3D_WGRAD_HALO_BIG"):               # A/B knob "blocks,lg2": halo target of the big flushes
+    _lib.d3d_wgrad_group_halo_big(*[int(v) for v in os.environ["D3D_WGRAD_HALO_BIG"].split(",")])
 if os.environ.get("D3D_WGRAD_HALO_PK"):                # A/B knob: pixels per halo K-step (32 / 64, the latter at W >= 64)
     _lib.d3d_wgrad_group_halo_pk(int(os.environ["D3D_WGRAD_HALO_PK"]))
 

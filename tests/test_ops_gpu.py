@@ -731,7 +731,7 @@ def _wg_ref(g, x, taps):
 @pytest.mark.parametrize("pk,blocks,minpix,halo,ns", [
     (32, 512, 512, 1, 2), (32, 512, 512, 0, 2), (64, 512, 512, 1, 2), (32, 4096, 64, 1, 2),
     (32, 4096, 64, 0, 2), (64, 512, 512, 0, 2), (32, 512, 512, 1, 3), (32, 64, 512, 1, 2),
-    (32, 512, 512, 3, 2), (32, 4096, 64, 3, 2)])
+    (32, 512, 512, 3, 2), (32, 4096, 64, 3, 2), (32, 256, 512, 4, 2)])
 def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, halo, ns):
     """Grouped weight gradients (wgrad_group.hip): the per-tap 128 x 128 tile
     launch and the all-taps halo tile launch (3x3 jobs on W % 32 == 0 images)
@@ -742,8 +742,11 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, halo, ns):
     blocks=64 leaves the big halo jobs nearly unsplit."""
     torch.manual_seed(5)
     H._lib.d3d_wgrad_group_cfg(blocks, pk, minpix)
-    # halo 3: the 64-pixel K-step halo kernel for the W >= 64 jobs (the rest as halo 1)
-    H._lib.d3d_wgrad_group_halo(1 if halo == 3 else halo, blocks, ns)
+    # halo 3: the 64-pixel K-step halo kernel for the W >= 64 jobs (the rest as halo 1);
+    # halo 4: halo 1 with the big-flush block target forced (2^10 work threshold, 64 blocks)
+    H._lib.d3d_wgrad_group_halo(1 if halo in (3, 4) else halo, blocks, ns)
+    if halo == 4:
+        H._lib.d3d_wgrad_group_halo_big(64, 10)
     H._lib.d3d_wgrad_group_halo_pk(64 if halo == 3 else 32)       # (restored to the default 64 below)
     try:
         jobs, refs, outs = [], [], []
@@ -801,7 +804,8 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, halo, ns):
                 assert torch.equal(db, b1)
     finally:
         H._lib.d3d_wgrad_group_cfg(512, 32, 512)
-        H._lib.d3d_wgrad_group_halo(1, 512, 2)
+        H._lib.d3d_wgrad_group_halo(1, 256, 2)             # (the library defaults)
+        H._lib.d3d_wgrad_group_halo_big(128, 22)
         H._lib.d3d_wgrad_group_halo_pk(64)
 
 
