@@ -141,6 +141,7 @@ class GraphedTrainStep:
         self.T = torch.zeros((micro_batch,) + tuple(T.shape[1:]), dtype=T.dtype, device=dev)
         self.K = torch.zeros((micro_batch,) + tuple(K.shape[1:]), dtype=K.dtype, device=dev)
         self.frac = torch.ones((), device=dev)
+        self._frac = 1                          # chunk count frac holds (1 / _frac)
         self.loss_acc = torch.zeros((), device=dev)
         self.seed = torch.zeros(3, dtype=torch.int64, device=dev)    # [dropout word, draw word, example offset]
         self.hp = torch.zeros(8, device=dev)
@@ -352,11 +353,13 @@ class GraphedTrainStep:
         # same seeds as the eager step (Trainer.train_step): the captured
         # kernels carry the base seeds and add these device words
         word = tr.step * tr.ctx.world + tr.ctx.rank
-        self.frac.fill_(1.0 / nchunks)
+        if self._frac != nchunks:
+            self.frac.fill_(1.0 / nchunks)
+            self._frac = nchunks
+        from .trainer import dropout_word
         for ci, s in enumerate(range(0, B, mb)):
-            from .trainer import dropout_word
-            for j, v in enumerate((dropout_word(word, ci), word, s)):     # kernel-argument fills, no H2D copy
-                self.seed[j].fill_(v)
+            # one kernel-argument write (no H2D copy, no host wait): fewer host launches at the step boundary
+            self.H.set_words64(self.seed, (dropout_word(word, ci), word, s))
             self.img.copy_(img[s:s + mb])
             self.R.copy_(R[s:s + mb])
             self.T.copy_(T[s:s + mb])

@@ -36,6 +36,8 @@ INV_SQRT2 = 1.0 / math.sqrt(2.0)
 
 
 _COND_STREAM = os.environ.get("D3D_COND_STREAM", "1") != "0"
+# AttnBlock: out_proj + the 1x1 `linear` as one merged map (ops.attn_out); 0: two layers
+_ATTN_MERGE = os.environ.get("D3D_ATTN_MERGE", "1") != "0"
 # conditioning stream: one FiLM GEMM + ready event per block instead of one per level
 FILM_BLOCK_EVENTS = False        # measured -1.2 % at bs16 and bs128 (profiles/r3/ab_film_events_s64.txt)
 _COND_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
@@ -161,11 +163,13 @@ class AttnLayer(nn.Module):
         self.attn_heads = attn_heads
         self.attn = nn.MultiheadAttention(in_channels, attn_heads, batch_first=True)
 
-    def forward(self, hn: torch.Tensor, cross: bool) -> torch.Tensor:
-        N, L, C = hn.shape
+    def core(self, hn: torch.Tensor, cross: bool) -> torch.Tensor:
+        """q/k/v projection + multi-head attention, before out_proj."""
         qkv = ops.linear(hn, self.attn.in_proj_weight, self.attn.in_proj_bias)
-        a = ops.attention(qkv, self.attn_heads, cross)
-        return ops.linear(a, self.attn.out_proj.weight, self.attn.out_proj.bias)
+        return ops.attention(qkv, self.attn_heads, cross)
+
+    def forward(self, hn: torch.Tensor, cross: bool) -> torch.Tensor:
+        return ops.linear(self.core(hn, cross), self.attn.out_proj.weight, self.attn.out_proj.bias)
 
 
 class AttnBlock(nn.Module):
@@ -189,11 +193,19 @@ class AttnBlock(nn.Module):
         assert C == self.in_channels
         slot = ops.res_slot(x) if torch.is_grad_enabled() and x.requires_grad else None
         hn = self.groupnorm(x, res_slot=slot).reshape(N, H * W, C)
-        o = self.attn_layer(hn, cross=(self.attn_type == "cross"))
         # the output feeds the next GroupNorm (the cross-attention block's, or
         # the next ResnetBlock's GN0): its statistics come out of this epilogue
-        y = ops.linear(o, self.linear.weight, self.linear.bias, residual=x.reshape(N, H * W, C),
-                       out_scale=INV_SQRT2, res_slot=slot, gn_groups=self.groupnorm.gn.num_groups)
+        if _ATTN_MERGE:
+            # out_proj and the 1x1 `linear` (no nonlinearity between them) as ONE map
+            a = self.attn_layer.core(hn, cross=(self.attn_type == "cross"))
+            op = self.attn_layer.attn.out_proj
+            y = ops.attn_out(a, op.weight, op.bias, self.linear.weight, self.linear.bias,
+                             residual=x.reshape(N, H * W, C), out_scale=INV_SQRT2, res_slot=slot,
+                             gn_groups=self.groupnorm.gn.num_groups)
+        else:
+            o = self.attn_layer(hn, cross=(self.attn_type == "cross"))
+            y = ops.linear(o, self.linear.weight, self.linear.bias, residual=x.reshape(N, H * W, C),
+                           out_scale=INV_SQRT2, res_slot=slot, gn_groups=self.groupnorm.gn.num_groups)
         return ops.carry_gn_stats(y, y.reshape(N, H, W, C))
 
 

@@ -67,6 +67,16 @@ def linear(x, weight, bias, residual: Optional[torch.Tensor] = None, out_scale: 
     return _t.linear(x, weight, bias, residual, out_scale)
 
 
+def attn_out(a, W_out, b_out, W_lin, b_lin, residual: Optional[torch.Tensor] = None, out_scale: float = 1.0,
+             res_slot=None, gn_groups: int = 0):
+    """The attention block's output map ``linear(out_proj(a))`` + residual,
+    x out_scale (`xunet.py:175,217-220`).  HIP: one merged GEMM forward and
+    backward (hip_impl.attn_out); torch: the two layers as written."""
+    if use_hip(a):
+        return _h().attn_out(a, W_out, b_out, W_lin, b_lin, residual, out_scale, res_slot, gn_groups)
+    return _t.linear(_t.linear(a, W_out, b_out), W_lin, b_lin, residual, out_scale)
+
+
 def carry_gn_stats(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
     """A reshaped view keeps the fused GroupNorm statistics of its source."""
     part = getattr(src, "_d3d_gnpart", None)

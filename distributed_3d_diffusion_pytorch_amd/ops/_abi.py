@@ -24,6 +24,8 @@ SIGNATURES = {
     "d3d_border_fix": [P, P, I, I, I, I, I, I, I, P, P],
     "d3d_border_sums": [P, P, I, I, I, I, P],
     "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, I, P, P],
+    "d3d_set_words64": [P, I, C.c_longlong, C.c_longlong, C.c_longlong, P],
+    "d3d_sgemm_jobs": [P, I, I, P],
     "d3d_gn_img_cfg": [I],
     "d3d_gn_img_ok": [I, I, I],
     "d3d_gn_img_fwd": [I, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, P, P],

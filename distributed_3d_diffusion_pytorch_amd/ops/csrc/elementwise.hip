@@ -537,3 +537,20 @@ D3D_API int d3d_set_words(float* dst, int n, float a0, float a1, float a2, float
   hipLaunchKernelGGL(set_words_k, dim3(1), dim3(64), 0, st, dst, n, w);
   return (int)hipGetLastError();
 }
+
+// The per-step seed block of the graph-replayed step (int64 [dropout word,
+// input-draw word, example offset]) in one launch instead of three fills.
+struct Words3L {
+  long long v[3];
+};
+
+__global__ void set_words64_k(long long* __restrict__ dst, int n, Words3L w) {
+  if ((int)threadIdx.x < n) dst[threadIdx.x] = w.v[threadIdx.x];
+}
+
+D3D_API int d3d_set_words64(long long* dst, int n, long long a0, long long a1, long long a2, hipStream_t st) {
+  if (n < 0 || n > 3) return (int)hipErrorInvalidValue;
+  Words3L w{{a0, a1, a2}};
+  hipLaunchKernelGGL(set_words64_k, dim3(1), dim3(64), 0, st, dst, n, w);
+  return (int)hipGetLastError();
+}

@@ -730,7 +730,7 @@ static int g_gh_blocks = 256;
 // the reduce); the chip is busy with the input-gradient convs there anyway.
 // bs128 +2.0 %, bs16 (256 kept by the rule) unchanged, profiles/r5/ab_wgrad_halo_blocks.txt
 static int g_gh_blocks_big = 128;
-static int g_gh_big_lg2 = 22;
+static int g_gh_big_lg2 = 21;
 static int g_gh_ns = 2;            // LDS ring stages of wgrad_halo_k (2 or 3)
 // pixels per K-step of wgrad_halo_k on W >= 64 jobs (64: half the barriers per MFMA; L0 flush
 // 945 -> 1051 TF/s at bs128, profiles/r4/halo_pk64/); 32 elsewhere

@@ -209,6 +209,7 @@ def refresh_weights() -> None:
     every cached operand; cache tokens advance to the new epoch."""
     _EPOCH[0] += 1
     if not _WCACHE:
+        _attn_refresh()
         return
     if _DESC_TABLE[2] != _REV[0]:
         rows = []
@@ -229,6 +230,7 @@ def refresh_weights() -> None:
     for ent in _WCACHE.values():
         p = ent[2][0]
         ent[0] = (p._version, _EPOCH[0])
+    _attn_refresh()
 
 
 def packed_weight(w: torch.Tensor, trans: bool, taps: int = 9) -> torch.Tensor:
@@ -1603,6 +1605,234 @@ def linear(x, weight, bias, residual=None, out_scale=1.0, res_slot=None, in_slot
     return y
 
 
+# ------------------------------------- attention output map (merged) ----
+# AttnBlock: out_proj (inside nn.MultiheadAttention, `xunet.py:175`) is
+# followed by the zero-init 1x1 `linear` (`xunet.py:190,217`) with nothing in
+# between: y = (a W_out^T + b_out) W_lin^T + b_lin = a W^T + b with
+# W = W_lin W_out, b = W_lin b_out + b_lin.  The forward runs ONE GEMM with the
+# merged operand; the input gradient is ONE GEMM against W^T; the weight
+# gradients come from ONE reduction M = dy^T a (+ colsum dy) over the pixels,
+# split back onto the two layers by C x C products:
+#     dW_out = W_lin^T M,   db_out = W_lin^T colsum,
+#     dW_lin = M W_out^T + colsum b_out^T,   db_lin = colsum.
+# W / W^T / b are derived operands: recomputed for every registered block by
+# one table launch (small_gemm.hip sgemm_jobs_k) after each optimizer update
+# (captured into the update graphs like the operand repack) or lazily when a
+# parameter changed.
+class _SgJob(ctypes.Structure):
+    _fields_ = [("A", ctypes.c_void_p), ("B", ctypes.c_void_p), ("C", ctypes.c_void_p), ("Cb", ctypes.c_void_p),
+                ("CbT", ctypes.c_void_p), ("u", ctypes.c_void_p), ("v", ctypes.c_void_p),
+                ("sam", ctypes.c_long), ("sak", ctypes.c_long), ("sbk", ctypes.c_long), ("sbn", ctypes.c_long),
+                ("scm", ctypes.c_long), ("scn", ctypes.c_long), ("M", ctypes.c_int), ("N", ctypes.c_int),
+                ("K", ctypes.c_int), ("ldb", ctypes.c_int), ("ldbt", ctypes.c_int), ("tile0", ctypes.c_int),
+                ("alpha", ctypes.c_float), ("beta", ctypes.c_float)]
+
+
+assert ctypes.sizeof(_SgJob) == 136
+
+
+def _sg(A=None, B=None, C=None, Cb=None, CbT=None, u=None, v=None, sam=0, sak=0, sbk=0, sbn=0, scm=0, scn=0,
+        M=1, N=1, K=1, ldb=0, ldbt=0, alpha=1.0, beta=0.0) -> dict:
+    return dict(A=A, B=B, C=C, Cb=Cb, CbT=CbT, u=u, v=v, sam=sam, sak=sak, sbk=sbk, sbn=sbn, scm=scm, scn=scn, M=M,
+                N=N, K=K, ldb=ldb, ldbt=ldbt, alpha=alpha, beta=beta)
+
+
+class _SgTable:
+    """A device-resident job table for d3d_sgemm_jobs (built eagerly, before
+    any capture; the tensors it points at must outlive it)."""
+
+    def __init__(self, jobs):
+        arr = (_SgJob * len(jobs))()
+        tile = 0
+        for i, j in enumerate(jobs):
+            r = arr[i]
+            for k, val in j.items():
+                if k in ("A", "B", "C", "Cb", "CbT", "u", "v"):
+                    setattr(r, k, val.data_ptr() if val is not None else None)
+                else:
+                    setattr(r, k, val)
+            r.tile0 = tile
+            tile += ((j["M"] + 63) // 64) * ((j["N"] + 63) // 64)
+        host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        self.dev = host.to("cuda")
+        self.n, self.tiles = len(jobs), tile
+
+    def run(self):
+        _chk(_lib.d3d_sgemm_jobs(self.dev.data_ptr(), self.n, self.tiles, _st()), "sgemm_jobs")
+
+
+class _AttnPair:
+    """Derived operands and gradient scratch of one AttnBlock's merged map."""
+
+    def __init__(self, W_out, b_out, W_lin, b_lin):
+        C = W_out.shape[0]
+        dev = W_out.device
+        self.params = (W_out, b_out, W_lin, b_lin)
+        self.C = C
+        self.Wm = torch.empty(C, C, dtype=BF16, device=dev)       # merged weight (forward A operand)
+        self.WmT = torch.empty(C, C, dtype=BF16, device=dev)      # its transpose (input-gradient A operand)
+        self.bm = torch.empty(C, dtype=F32, device=dev)
+        self.M = torch.empty(C, C, dtype=F32, device=dev)          # dy^T a of the backward
+        self.dcol = torch.empty(C, dtype=F32, device=dev)
+        self.tok = None
+        self.bwd = {}                                                # (grad target ptrs) -> _SgTable
+
+    def token(self):
+        return (_EPOCH[0],) + tuple(p._version for p in self.params)
+
+    def fwd_jobs(self):
+        W_out, b_out, W_lin, b_lin = self.params
+        C = self.C
+        wl = W_lin.detach().reshape(C, C)
+        return [_sg(A=wl, B=W_out.detach(), Cb=self.Wm, CbT=self.WmT, sam=C, sak=1, sbk=C, sbn=1, M=C, N=C, K=C,
+                    ldb=C, ldbt=C),
+                _sg(A=wl, B=b_out.detach(), C=self.bm, u=b_lin.detach(), sam=C, sak=1, sbk=1, sbn=0, scm=1, scn=0,
+                    M=C, N=1, K=C)]
+
+    def bwd_table(self, tw_out, tb_out, tw_lin, tb_lin, cache=True):
+        key = (tw_out.data_ptr(), tb_out.data_ptr(), tw_lin.data_ptr(), tb_lin.data_ptr())
+        t = self.bwd.get(key) if cache else None
+        if t is None:
+            W_out, b_out, W_lin, b_lin = self.params
+            C = self.C
+            wl = W_lin.detach().reshape(C, C)
+            t = _SgTable([
+                # dW_out += W_lin^T M ; db_out += W_lin^T colsum
+                _sg(A=wl, B=self.M, C=tw_out, sam=1, sak=C, sbk=C, sbn=1, scm=C, scn=1, M=C, N=C, K=C, beta=1.0),
+                _sg(A=wl, B=self.dcol, C=tb_out, sam=1, sak=C, sbk=1, sbn=0, scm=1, scn=0, M=C, N=1, K=C, beta=1.0),
+                # dW_lin += M W_out^T + colsum b_out^T ; db_lin += colsum
+                _sg(A=self.M, B=W_out.detach(), C=tw_lin, u=self.dcol, v=b_out.detach(), sam=C, sak=1, sbk=1, sbn=C,
+                    scm=C, scn=1, M=C, N=C, K=C, beta=1.0),
+                _sg(C=tb_lin, u=self.dcol, scm=1, scn=0, M=C, N=1, K=0, beta=1.0)])
+            if cache:
+                self.bwd[key] = t
+        return t
+
+
+_ATTN_PAIRS: Dict[Tuple[int, int], _AttnPair] = {}
+_ATTN_TABLE = [None, -1]         # forward-refresh table over every registered pair, its registry size
+
+
+def _attn_refresh() -> None:
+    """Recompute every registered block's merged operands (one launch)."""
+    if not _ATTN_PAIRS:
+        return
+    if _ATTN_TABLE[1] != len(_ATTN_PAIRS):
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("attention merge table built inside a graph capture")
+        _ATTN_TABLE[0] = _SgTable([j for pr in _ATTN_PAIRS.values() for j in pr.fwd_jobs()])
+        _ATTN_TABLE[1] = len(_ATTN_PAIRS)
+    _ATTN_TABLE[0].run()
+    for pr in _ATTN_PAIRS.values():
+        pr.tok = pr.token()
+
+
+def _attn_pair(W_out, b_out, W_lin, b_lin) -> _AttnPair:
+    key = (W_out.data_ptr(), W_lin.data_ptr())
+    pr = _ATTN_PAIRS.get(key)
+    if pr is None or pr.params[0] is not W_out or pr.params[2] is not W_lin:
+        pr = _ATTN_PAIRS[key] = _AttnPair(W_out, b_out, W_lin, b_lin)
+    if pr.tok != pr.token() and not torch.cuda.is_current_stream_capturing():
+        _attn_refresh()
+    return pr
+
+
+class _AttnOut(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, W_out, b_out, W_lin, b_lin, residual, out_scale, res_slot, gn):
+        pr = _attn_pair(W_out, b_out, W_lin, b_lin)
+        N_, L, C = a.shape
+        a2 = a.reshape(-1, C)
+        P = a2.shape[0]
+        r = residual.reshape(P, C).contiguous() if residual is not None else None
+        gnp = None
+        if gn is not None and L % 64 == 0 and C % gn["groups"] == 0 and C // gn["groups"] in (4, 8, 16, 32):
+            gnp = torch.empty((P // L) * gn["groups"] * (L // 64) * 2, dtype=F32, device=a.device)
+        y = torch.empty(P, C, dtype=BF16, device=a.device)
+        gemm_nt(pr.Wm, a2, y, C, P, C, C, C, C, bias=pr.bm, res=r, scale=float(out_scale), gnp=gnp,
+                gn_groups=gn["groups"] if gnp is not None else 0, gn_hw=L)
+        if gnp is not None:
+            gn["part"] = (gnp, L // 64)
+        ctx.save_for_backward(a2)
+        ctx.pr, ctx.scale, ctx.has_res, ctx.res_slot, ctx.shp = pr, float(out_scale), residual is not None, \
+            res_slot, a.shape
+        for i, p_ in enumerate((W_out, b_out, W_lin, b_lin)):
+            SINK.use(p_, ctx.needs_input_grad[1 + i])
+        return y.view(N_, L, C)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (a2,) = ctx.saved_tensors
+        pr, scale, slot = ctx.pr, ctx.scale, ctx.res_slot
+        C = pr.C
+        g = dy.reshape(-1, C).contiguous()
+        rows = g.shape[0]
+        # the scale of out = scale * (...) rides on the GEMM alpha, the reduction
+        # and the residual hand-off (as _Linear); a scaled copy only when the
+        # residual's gradient must be returned to autograd
+        lazy = not ctx.has_res or not ctx.needs_input_grad[5] or (slot is not None and not slot.consumed)
+        if scale != 1.0 and not lazy:
+            gs = torch.empty_like(g)
+            _chk(_lib.d3d_add_scale(g.data_ptr(), None, gs.data_ptr(), scale, g.numel(), _st()), "scale")
+            g, ks = gs, 1.0
+        else:
+            ks = scale
+        da = None
+        if ctx.needs_input_grad[0]:
+            da = torch.empty(rows, C, dtype=BF16, device=g.device)
+            gemm_nt(pr.WmT, g, da, C, rows, C, C, C, C, alpha=ks)
+            da = da.view(ctx.shp)
+        grads = [None] * 4
+        if any(ctx.needs_input_grad[1:5]):
+            W_out, b_out, W_lin, b_lin = pr.params
+            tgt = [SINK.target(p_) for p_ in (W_out, b_out, W_lin, b_lin)]
+            direct = all(t is not None for t in tgt)
+            if not direct:
+                tgt = [torch.zeros(p_.shape, dtype=F32, device=g.device).reshape(p_.shape[0], -1).squeeze(-1)
+                       for p_ in (W_out, b_out, W_lin, b_lin)]
+            tab = pr.bwd_table(tgt[0].reshape(C, C), tgt[1], tgt[2].reshape(C, C), tgt[3], cache=direct)
+            g4, x4 = g.reshape(rows, 1, 1, C), a2.contiguous().reshape(rows, 1, 1, C)
+            spec = wgrad_job(g4, x4, C, C, rows, 1, 1, 1, pr.M.view(C, C, 1), pr.dcol, ks, accumulate=False)
+
+            def reduce_job(g4=g4, x4=x4, ks=ks):
+                _wgrad(g4, x4, C, C, rows, 1, 1, 1, 1, 1, 1, dW=pr.M.view(C, C, 1), db=pr.dcol, accumulate=False,
+                       scale=ks)
+
+            if direct:
+                # M = ks dy^T a (+ colsum) as a grouped weight-gradient job, then the C x C split
+                # onto the two layers' gradients -- both on the weight-gradient stream, in order
+                SINK.submit(g.device, reduce_job, (g4, x4), (), spec=spec)
+                SINK.submit(g.device, tab.run, (), (W_out, b_out, W_lin, b_lin))
+            else:
+                reduce_job()
+                tab.run()
+                grads = [t.view(p_.shape) for t, p_ in zip(tgt, (W_out, b_out, W_lin, b_lin))]
+        dres = None
+        if ctx.has_res and ctx.needs_input_grad[5] and (slot is None or not slot.deposit(g, ks)):
+            assert ks == 1.0
+            dres = g.view(ctx.shp)
+        return (da, *grads, dres, None, None, None)
+
+
+def attn_out(a, W_out, b_out, W_lin, b_lin, residual=None, out_scale=1.0, res_slot=None, gn_groups=0):
+    """The attention block's output map ``linear(out_proj(a))`` (+ residual,
+    x out_scale, + fused GroupNorm statistics) as ONE merged GEMM forward and
+    backward (see _AttnPair).  ``a`` [N, L, C]."""
+    _need_bf16(a, residual)
+    C = a.shape[-1]
+    if C % 64 or W_lin.reshape(W_lin.shape[0], -1).shape != (C, C) or tuple(W_out.shape) != (C, C) or \
+            b_out is None or b_lin is None:
+        o = linear(a, W_out, b_out)
+        return linear(o, W_lin, b_lin, residual, out_scale, res_slot, None, gn_groups)
+    if gn_groups and gn_img_ok(a.shape[1], C, int(gn_groups)):
+        gn_groups = 0                   # the consumer's whole-image kernel makes its own statistics
+    gn = {"groups": int(gn_groups)} if (gn_groups and _EPI_GN_STATS) else None
+    y = _AttnOut.apply(a.contiguous(), W_out, b_out, W_lin, b_lin, residual, out_scale, res_slot, gn)
+    if gn is not None and "part" in gn:
+        y._d3d_gnpart = (gn["part"][0], int(gn_groups), gn["part"][1])
+    return y
+
+
 def carry_gn_stats(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
     """Keep fused GroupNorm partials on a reshaped view of the same data."""
     part = getattr(src, "_d3d_gnpart", None)
@@ -1975,8 +2205,10 @@ def prepare_update_parts(flat, parts) -> None:
     """Build the fused-update tables of a split update: ``parts`` is a list of
     parameter-index sets covering ``flat.params`` (host work; before a
     capture).  :func:`adam_update_part` then updates one part."""
+    attn = {id(p_) for pr in _ATTN_PAIRS.values() for p_ in pr.params}
     for k, only in enumerate(parts):
-        _fused_tables(flat, set(only), key=(id(flat), "part", k), take_unowned=k == 0)
+        ent = _fused_tables(flat, set(only), key=(id(flat), "part", k), take_unowned=k == 0)
+        ent["attn"] = any(id(flat.params[i]) in attn for i in only)
 
 
 def adam_update_part(flat, m, v, ema, hp, k, zero_g=False) -> None:
@@ -1988,6 +2220,8 @@ def adam_update_part(flat, m, v, ema, hp, k, zero_g=False) -> None:
     if ent is None or ent["rev"] != _REV[0] or ent["flat"] is not flat:
         raise RuntimeError("update-part tables missing or stale (prepare_update_parts before the capture)")
     _adam_fused_launch(flat, m, v, ema, hp, ent, zero_g)
+    if ent.get("attn"):
+        _attn_refresh()                     # this part updates attention output maps: re-derive the merged operands
 
 
 def _adam_fused_launch(flat, m, v, ema, hp, ent, zero_g=False) -> None:
@@ -2023,6 +2257,7 @@ def adam_update_all(flat, m, v, ema, hp, zero_g=False) -> None:
     _EPOCH[0] += 1
     for e in _WCACHE.values():
         e[0] = (e[2][0]._version, _EPOCH[0])
+    _attn_refresh()                         # the merged attention operands of the updated weights
 
 
 def set_words(dst: torch.Tensor, vals) -> torch.Tensor:
@@ -2032,6 +2267,16 @@ def set_words(dst: torch.Tensor, vals) -> torch.Tensor:
     vals = [float(v) for v in vals]
     assert dst.dtype == F32 and dst.is_cuda and dst.is_contiguous() and len(vals) <= min(8, dst.numel())
     _chk(_lib.d3d_set_words(dst.data_ptr(), len(vals), *(vals + [0.0] * (8 - len(vals))), _st()), "set_words")
+    return dst
+
+
+def set_words64(dst: torch.Tensor, vals) -> torch.Tensor:
+    """dst[:len(vals)] = vals (int64, <= 3) by one kernel whose arguments
+    carry the values (the graph step's per-step seed block)."""
+    vals = [int(v) for v in vals]
+    assert dst.dtype == torch.int64 and dst.is_cuda and dst.is_contiguous() and len(vals) <= min(3, dst.numel())
+    vals = [v - (1 << 64) if v >= (1 << 63) else v for v in vals]       # (two's complement for the ABI)
+    _chk(_lib.d3d_set_words64(dst.data_ptr(), len(vals), *(vals + [0] * (3 - len(vals))), _st()), "set_words64")
     return dst
 
 

@@ -210,6 +210,38 @@ def test_gn_whole_image(H, N, Hh, C, C1, mode, maxp):
             assert rel(a.grad, c.grad) < 3e-2, rel(a.grad, c.grad)
 
 
+@pytest.mark.parametrize("N,L,C", [(8, 256, 256), (16, 64, 512), (3, 100, 256)])
+def test_attn_out_merged(H, N, L, C):
+    """AttnBlock output map out_proj -> 1x1 linear as ONE merged GEMM
+    (hip_impl.attn_out: W = W_lin W_out, b = W_lin b_out + b_lin; input
+    gradient against W^T; weight gradients split from one dy^T a reduction)
+    against the fp32 two-layer composition: output and the gradients of a,
+    the residual and all four parameters; the merged operands follow an
+    in-place parameter update (version bump)."""
+    torch.manual_seed(23)
+    a = torch.randn(N, L, C, device=DEV).to(BF)
+    x = torch.randn(N, L, C, device=DEV).to(BF)
+    Wo = torch.randn(C, C, device=DEV) / math.sqrt(C)
+    bo = torch.randn(C, device=DEV) * 0.1
+    Wl = torch.randn(C, C, 1, 1, device=DEV) / math.sqrt(C)
+    bl = torch.randn(C, device=DEV) * 0.1
+    go = torch.randn(N, L, C, device=DEV)
+    s = 1 / math.sqrt(2)
+
+    def ref(a, x, Wo, bo, Wl, bl):
+        return T.linear(T.linear(a, Wo, bo), Wl, bl, x, s)
+
+    for rep in range(2):
+        yh, yr, gh, gr = run_both(lambda a, x, Wo, bo, Wl, bl: H.attn_out(a, Wo, bo, Wl, bl, residual=x, out_scale=s),
+                                  ref, [a, x, Wo, bo, Wl, bl], go)
+        assert rel(yh, yr) < 2e-2, (rep, rel(yh, yr))
+        for i, (u, v) in enumerate(zip(gh, gr)):
+            assert rel(u, v) < 3e-2, (rep, i, rel(u, v))
+        with torch.no_grad():              # a parameter update: the next forward re-derives W and b
+            Wl.mul_(-0.5)
+            bo.add_(0.3)
+
+
 CONV_SHAPES = [
     # N, H, W, Cin, Cout, stride, residual, row_bias, scale
     (4, 16, 16, 128, 128, 1, True, False, 1 / math.sqrt(2)),
@@ -805,7 +837,7 @@ def test_wgrad_group_matches_fp32(H, pk, blocks, minpix, halo, ns):
     finally:
         H._lib.d3d_wgrad_group_cfg(512, 32, 512)
         H._lib.d3d_wgrad_group_halo(1, 256, 2)             # (the library defaults)
-        H._lib.d3d_wgrad_group_halo_big(128, 22)
+        H._lib.d3d_wgrad_group_halo_big(128, 21)
         H._lib.d3d_wgrad_group_halo_pk(64)
 
 
