@@ -106,9 +106,11 @@ struct SgJob {
 };
 static_assert(sizeof(SgJob) == 136, "SgJob must match hip_impl._SgJob");
 
+constexpr int SJ_K = 32;          // K per LDS stage of the job-table form
+
 __global__ void __launch_bounds__(256) sgemm_jobs_k(const SgJob* __restrict__ jobs, int njobs) {
-  __shared__ float As[SG_K][SG_T + 1];
-  __shared__ float Bs[SG_K][SG_T + 1];
+  __shared__ float As[SJ_K][SG_T + 1];
+  __shared__ float Bs[SJ_K][SG_T + 1];
   int j = 0;
   while (j + 1 < njobs && (int)blockIdx.x >= jobs[j + 1].tile0) ++j;
   const SgJob& J = jobs[j];
@@ -117,17 +119,24 @@ __global__ void __launch_bounds__(256) sgemm_jobs_k(const SgJob* __restrict__ jo
   const int m0 = (t / ntn) * SG_T, n0 = (t % ntn) * SG_T;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   float acc[4][4] = {};
+  // loads walk the operand's contiguous axis across consecutive lanes
+  // (k-major when the k stride is 1, else m / n-major): coalesced either way
+  const bool a_k = J.sak == 1, b_k = J.sbk == 1;
   if (J.A) {
-    for (int k0 = 0; k0 < J.K; k0 += SG_K) {
-      for (int e = threadIdx.x; e < SG_K * SG_T; e += 256) {
-        const int kk = e / SG_T, mm = e % SG_T;
-        const int gm = m0 + mm, gk = k0 + kk, gn = n0 + mm;
+    for (int k0 = 0; k0 < J.K; k0 += SJ_K) {
+      for (int e = threadIdx.x; e < SJ_K * SG_T; e += 256) {
+        int kk = e / SG_T, mm = e % SG_T;
+        if (a_k) { kk = e % SJ_K; mm = e / SJ_K; }
+        const int gm = m0 + mm, gk = k0 + kk;
         As[kk][mm] = (gm < J.M && gk < J.K) ? J.A[gm * J.sam + gk * J.sak] : 0.f;
-        Bs[kk][mm] = (gn < J.N && gk < J.K) ? J.B[gk * J.sbk + gn * J.sbn] : 0.f;
+        int kb = e / SG_T, nn = e % SG_T;
+        if (b_k) { kb = e % SJ_K; nn = e / SJ_K; }
+        const int gn = n0 + nn, gkb = k0 + kb;
+        Bs[kb][nn] = (gn < J.N && gkb < J.K) ? J.B[gkb * J.sbk + gn * J.sbn] : 0.f;
       }
       __syncthreads();
-#pragma unroll
-      for (int kk = 0; kk < SG_K; ++kk) {
+#pragma unroll 8
+      for (int kk = 0; kk < SJ_K; ++kk) {
         float av[4], bv[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) av[i] = As[kk][ty + 16 * i];
