@@ -18,6 +18,7 @@
 #   env:<VAR=val>:<bs,bs..>    same-box A/B of an environment knob against the default
 #   prof:<bs>                  rocprofv3 kernel trace of the step + rpstats (stats, grid, busy, gaps,
 #                              solo, families)
+#   envprof:<VAR=val>:<bs>     the same trace with an environment knob set
 #   pmc:<bs>                   step-level hardware counters (three --pmc passes) -> table_bs<bs>.txt
 #   kbench:<tool.py>[:args]    a tools/ kernel micro-benchmark (args: comma-separated)
 set -o pipefail
@@ -113,6 +114,12 @@ for step in "$@"; do
         done
       done ;;
     prof) prof "$a" ;;
+    envprof)                     # envprof:<VAR=val>:<bs>: a trace with the knob set (files get a _<VAR> suffix)
+      var=${a%%=*}
+      export "${a?}"
+      prof "$b"
+      for f in stats grid busy gaps solo families; do mv "$O/$f$b.txt" "$O/${f}${b}_$var.txt"; done
+      unset "$var" ;;
     pmc) pmc "$a" ;;
     kbench)
       args=()
