@@ -1610,9 +1610,15 @@ def linear(x, weight, bias, residual=None, out_scale=1.0, res_slot=None, in_slot
 # followed by the zero-init 1x1 `linear` (`xunet.py:190,217`) with nothing in
 # between: y = (a W_out^T + b_out) W_lin^T + b_lin = a W^T + b with
 # W = W_lin W_out, b = W_lin b_out + b_lin.  The forward runs ONE GEMM with the
-# merged operand; the input gradient is ONE GEMM against W^T; the weight
-# gradients come from ONE reduction M = dy^T a (+ colsum dy) over the pixels,
-# split back onto the two layers by C x C products:
+# merged operand and the input gradient ONE GEMM against W^T: the trunk's
+# critical path loses one GEMM each way per attention block.  The weight
+# gradients need the layers' own intermediates: o = a W_out^T + b_out and
+# do = dy W_lin are recomputed by two GEMMs inside the weight-gradient job,
+# i.e. on the weight-gradient stream, off the critical path -- or, when the
+# pixel count is large against C (rows >= D3D_ATTN_SPLIT x C, bs128's 16x16
+# level), from ONE reduction M = dy^T a (+ colsum dy) split back onto the two
+# layers by C x C products (cheaper than two rows x C x C GEMMs there; at bs16
+# the fp32 products, latency-bound at ~125 us per block, measured -5..-7 %):
 #     dW_out = W_lin^T M,   db_out = W_lin^T colsum,
 #     dW_lin = M W_out^T + colsum b_out^T,   db_lin = colsum.
 # W / W^T / b are derived operands: recomputed for every registered block by
@@ -1672,8 +1678,7 @@ class _AttnPair:
         self.Wm = torch.empty(C, C, dtype=BF16, device=dev)       # merged weight (forward A operand)
         self.WmT = torch.empty(C, C, dtype=BF16, device=dev)      # its transpose (input-gradient A operand)
         self.bm = torch.empty(C, dtype=F32, device=dev)
-        self.M = torch.empty(C, C, dtype=F32, device=dev)          # dy^T a of the backward
-        self.dcol = torch.empty(C, dtype=F32, device=dev)
+        self.M = self.dcol = None                                    # dy^T a, colsum dy (split backward)
         self.tok = None
         self.bwd = {}                                                # (grad target ptrs) -> _SgTable
 
@@ -1695,6 +1700,9 @@ class _AttnPair:
         if t is None:
             W_out, b_out, W_lin, b_lin = self.params
             C = self.C
+            if self.M is None:
+                self.M = torch.empty(C, C, dtype=F32, device=W_out.device)
+                self.dcol = torch.empty(C, dtype=F32, device=W_out.device)
             wl = W_lin.detach().reshape(C, C)
             t = _SgTable([
                 # dW_out += W_lin^T M ; db_out += W_lin^T colsum
@@ -1709,6 +1717,12 @@ class _AttnPair:
         return t
 
 
+
+# split backward (one dy^T a reduction + C x C products) when rows >= this x C
+_ATTN_SPLIT = int(os.environ.get("D3D_ATTN_SPLIT", "64"))
+# below that, merge with the recomputing backward (measured neutral at bs16) or
+# keep the two layers (default)
+_ATTN_SMALL = os.environ.get("D3D_ATTN_MERGE_SMALL", "0") == "1"
 _ATTN_PAIRS: Dict[Tuple[int, int], _AttnPair] = {}
 _ATTN_TABLE = [None, -1]         # forward-refresh table over every registered pair, its registry size
 
@@ -1785,28 +1799,51 @@ class _AttnOut(torch.autograd.Function):
         grads = [None] * 4
         if any(ctx.needs_input_grad[1:5]):
             W_out, b_out, W_lin, b_lin = pr.params
-            tgt = [SINK.target(p_) for p_ in (W_out, b_out, W_lin, b_lin)]
+            ps = (W_out, b_out, W_lin, b_lin)
+            tgt = [SINK.target(p_) for p_ in ps]
             direct = all(t is not None for t in tgt)
             if not direct:
-                tgt = [torch.zeros(p_.shape, dtype=F32, device=g.device).reshape(p_.shape[0], -1).squeeze(-1)
-                       for p_ in (W_out, b_out, W_lin, b_lin)]
-            tab = pr.bwd_table(tgt[0].reshape(C, C), tgt[1], tgt[2].reshape(C, C), tgt[3], cache=direct)
-            g4, x4 = g.reshape(rows, 1, 1, C), a2.contiguous().reshape(rows, 1, 1, C)
-            spec = wgrad_job(g4, x4, C, C, rows, 1, 1, 1, pr.M.view(C, C, 1), pr.dcol, ks, accumulate=False)
+                tgt = [torch.zeros(p_.shape, dtype=F32, device=g.device) for p_ in ps]
+            tw_out, tb_out, tw_lin, tb_lin = tgt
+            if rows >= _ATTN_SPLIT * C:
+                tab = pr.bwd_table(tw_out.view(C, C), tb_out, tw_lin.view(C, C), tb_lin, cache=direct)
+                g4, x4 = g.reshape(rows, 1, 1, C), a2.reshape(rows, 1, 1, C)
+                spec = wgrad_job(g4, x4, C, C, rows, 1, 1, 1, pr.M.view(C, C, 1), pr.dcol, ks, accumulate=False)
 
-            def reduce_job(g4=g4, x4=x4, ks=ks):
-                _wgrad(g4, x4, C, C, rows, 1, 1, 1, 1, 1, 1, dW=pr.M.view(C, C, 1), db=pr.dcol, accumulate=False,
-                       scale=ks)
+                def job(g4=g4, x4=x4, ks=ks):
+                    _wgrad(g4, x4, C, C, rows, 1, 1, 1, 1, 1, 1, dW=pr.M.view(C, C, 1), db=pr.dcol,
+                           accumulate=False, scale=ks)
 
-            if direct:
-                # M = ks dy^T a (+ colsum) as a grouped weight-gradient job, then the C x C split
-                # onto the two layers' gradients -- both on the weight-gradient stream, in order
-                SINK.submit(g.device, reduce_job, (g4, x4), (), spec=spec)
-                SINK.submit(g.device, tab.run, (), (W_out, b_out, W_lin, b_lin))
+                if direct:
+                    # M = ks dy^T a (+ colsum) as a grouped weight-gradient job, then the C x C split
+                    # onto the two layers' gradients -- both on the weight-gradient stream, in order
+                    SINK.submit(g.device, job, (g4, x4), (), spec=spec)
+                    SINK.submit(g.device, tab.run, (), ps)
+                else:
+                    job()
+                    tab.run()
+                    grads = tgt
             else:
-                reduce_job()
-                tab.run()
-                grads = [t.view(p_.shape) for t, p_ in zip(tgt, (W_out, b_out, W_lin, b_lin))]
+                def job(g=g, a2=a2, ks=ks):
+                    # the layers' intermediates, recomputed off the critical path
+                    o = torch.empty(rows, C, dtype=BF16, device=g.device)
+                    gemm_nt(bf16_weight(W_out), a2, o, C, rows, C, C, C, C, bias=b_out.detach())
+                    do = torch.empty(rows, C, dtype=BF16, device=g.device)
+                    gemm_nt(packed_weight(W_lin, True, 1), g, do, C, rows, C, C, C, C, alpha=ks)
+                    pairs = [(t_.reshape(rows, 1, 1, C), u_.reshape(rows, 1, 1, C), tw_.view(C, C, 1), tb_, sc_)
+                             for t_, u_, tw_, tb_, sc_ in ((g, o, tw_lin, tb_lin, ks), (do, a2, tw_out, tb_out, 1.0))]
+                    jobs = [wgrad_job(d4, x4, C, C, rows, 1, 1, 1, tw_, tb_, sc_) for d4, x4, tw_, tb_, sc_ in pairs]
+                    if all(j is not None for j in jobs):
+                        wgrad_group_run(jobs)
+                    else:
+                        for d4, x4, tw_, tb_, sc_ in pairs:
+                            _wgrad(d4, x4, C, C, rows, 1, 1, 1, 1, 1, 1, dW=tw_, db=tb_, accumulate=True, scale=sc_)
+
+                if direct:
+                    SINK.submit(g.device, job, (g, a2), ps)
+                else:
+                    job()
+                    grads = tgt
         dres = None
         if ctx.has_res and ctx.needs_input_grad[5] and (slot is None or not slot.deposit(g, ks)):
             assert ks == 1.0
@@ -1820,8 +1857,9 @@ def attn_out(a, W_out, b_out, W_lin, b_lin, residual=None, out_scale=1.0, res_sl
     backward (see _AttnPair).  ``a`` [N, L, C]."""
     _need_bf16(a, residual)
     C = a.shape[-1]
+    rows = a.numel() // C
     if C % 64 or W_lin.reshape(W_lin.shape[0], -1).shape != (C, C) or tuple(W_out.shape) != (C, C) or \
-            b_out is None or b_lin is None:
+            b_out is None or b_lin is None or (rows < _ATTN_SPLIT * C and not _ATTN_SMALL):
         o = linear(a, W_out, b_out)
         return linear(o, W_lin, b_lin, residual, out_scale, res_slot, None, gn_groups)
     if gn_groups and gn_img_ok(a.shape[1], C, int(gn_groups)):

@@ -210,14 +210,18 @@ def test_gn_whole_image(H, N, Hh, C, C1, mode, maxp):
             assert rel(a.grad, c.grad) < 3e-2, rel(a.grad, c.grad)
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("N,L,C", [(8, 256, 256), (16, 64, 512), (3, 100, 256)])
-def test_attn_out_merged(H, N, L, C):
+def test_attn_out_merged(H, N, L, C, split, monkeypatch):
     """AttnBlock output map out_proj -> 1x1 linear as ONE merged GEMM
     (hip_impl.attn_out: W = W_lin W_out, b = W_lin b_out + b_lin; input
-    gradient against W^T; weight gradients split from one dy^T a reduction)
-    against the fp32 two-layer composition: output and the gradients of a,
-    the residual and all four parameters; the merged operands follow an
-    in-place parameter update (version bump)."""
+    gradient against W^T; weight gradients from the recomputed intermediates
+    or -- split -- from one dy^T a reduction split by C x C products) against
+    the fp32 two-layer composition: output and the gradients of a, the
+    residual and all four parameters; the merged operands follow an in-place
+    parameter update (version bump)."""
+    monkeypatch.setattr(H, "_ATTN_SPLIT", 0 if split else 1 << 30)
+    monkeypatch.setattr(H, "_ATTN_SMALL", True)
     torch.manual_seed(23)
     a = torch.randn(N, L, C, device=DEV).to(BF)
     x = torch.randn(N, L, C, device=DEV).to(BF)
