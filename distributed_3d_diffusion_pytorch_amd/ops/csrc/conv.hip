@@ -2794,6 +2794,10 @@ extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias
                                 const void* res, void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW,
                                 int OC, int ldo, int stride, int trans, float scale, int res_nmod, int taps,
                                 float* gnp, int gn_groups, int* gn_done, hipStream_t st, void* O2);
+extern "C" int d3d_conv_hsm_try(const void* I, const void* Wp, const float* bias, const float* row_bias,
+                                const void* res, void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW,
+                                int OC, int ldo, int stride, int trans, float scale, int res_nmod, int taps,
+                                const float* gnp, const void* O2, hipStream_t st);
 // 64x64 no-split tiles (conv_small.hip) on grids of at most g_s64_maxb
 // 128x128 blocks (default 160): the 16x16 / 8x8 levels at 16 examples per GPU
 // and the 8x8 level at 32 (in-graph A/B: +1.1 % at bs16; the 16x16 level at
@@ -2937,6 +2941,9 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
   constexpr int BM = 128, BN = 128;
   if (nsplit < 1 || !ws || g_conv_impl < 1) nsplit = 1;
   if (g_conv_impl >= 2 && nsplit == 1 && s64_wanted(Mpix, OC, ICp, taps)) {
+    const int rh = d3d_conv_hsm_try(I, Wp, bias, row_bias, res, O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans,
+                                    scale, res_nmod, taps, gnp, O2, st);
+    if (rh != 0) return rh < 0 ? -rh : 0;
     const int r = d3d_conv_s64_try(I, Wp, bias, row_bias, res, O, N, IH, IW, IC, ICp, OH, OW, OC, ldo, stride, trans,
                                    scale, res_nmod, taps, gnp, gn_groups, gn_done, st, O2);
     if (r > 0 && silu_done) *silu_done = O2 ? 1 : 0;

@@ -315,6 +315,242 @@ conv_s64_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float*
   }
 }
 
+
+// ------------------------------------------------- small-image halo conv ----
+// Stride-1 3x3 conv (and its input gradient, TRANS) of 8- and 16-wide images
+// at small grids (the 8x8 / 16x16 levels at 16-32 examples per GPU), with the
+// halo staging of conv.hip's conv_halo_k at a 64-channel x 64/128-pixel tile.
+// Why: conv_s64_k above streams an im2col row per tap, 16 KiB per 64-deep
+// k-step for a 64 x 64 tile (32 FLOP/B), and LDS-DMA fills sustain only
+// ~26 B/clk per CU when every CU streams (rocprofv3: TCP->TCC latency ~300-370
+// cycles, 2.6k cycles per k-step, 12-16 % MFMA; profiles/r5/s64_diag.txt).
+// Here a block owns TR whole rows of one image (TR x OW = 64 or 128 pixels) x
+// 64 output channels over the whole K:
+//   * per 32-channel chunk the (TR + 2) x (OW + 2) halo (rows padded to a
+//     multiple of 8 pixels) is LDS-DMA'd ONCE and feeds the nine taps by
+//     address shift, so the input crosses L2 1.6-2.2x instead of 9x: 51-92
+//     FLOP per staged byte instead of 32;
+//   * the weights of one (tap, chunk) step (64 x 32, 4 KiB, one 1-KiB piece per
+//     wave) stream through a 4-slot LDS ring, the halo through two buffers
+//     filled one chunk ahead, one barrier per step with counted vmcnt waits
+//     (the wait/issue schedule of conv_halo_k);
+//   * 4 waves as 2 (channels) x 2 (pixels): 32 x (BN/2) each;
+//   * fragment swizzle as conv_halo_k (quarter ^ ((row >> 1) & 2)): the halo
+//     row pitch is a multiple of 8 pixels, so every tap shift stays
+//     conflict-free;
+//   * epilogue: bias, per-image bias, residual (res_nmod broadcast), scale.
+//     No GroupNorm partials (the GroupNorms of these levels are whole-image
+//     kernels that make their own statistics) and no SiLU companion output:
+//     the launcher declines those calls.
+constexpr int HSM_CH = 32;
+
+template <int OWT, int TR>
+struct HsmGeom {
+  static constexpr int BN = TR * OWT;                  // pixels per tile
+  static constexpr int HW2 = (OWT + 2 + 7) / 8 * 8;    // halo row pitch (pixels)
+  static constexpr int HP = (TR + 2) * HW2;            // halo pixels
+  static constexpr int HPW = ((HP + 15) / 16 + 3) / 4; // 1-KiB pieces (16 pixels) per wave
+  static constexpr int HBUF = HPW * 4 * 16 * HSM_CH;   // elements per halo buffer
+  static constexpr int ABUF = 64 * HSM_CH;             // elements per weight slot
+};
+
+// one step's weight piece / one chunk's halo pieces (__device__ functions: a
+// buffer resource captured by a kernel lambda can suppress the host stub)
+__device__ __forceinline__ void hsm_issue_a(bf16* dst, const bf16* Wp, int w_bytes, int aoff, int soff) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, w_bytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)dst, 16, aoff, soff, 0, 0);
+}
+template <int HPW>
+__device__ __forceinline__ void hsm_issue_b(bf16* hb, const bf16* I, int in_bytes, const unsigned* hoff, int cbyte,
+                                            int wave) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  const __amdgpu_buffer_rsrc_t rI = __builtin_amdgcn_make_buffer_rsrc((void*)I, (short)0, in_bytes, 0x00020000);
+#pragma unroll
+  for (int k = 0; k < HPW; ++k)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rI, (lds_void*)(hb + (wave + 4 * k) * 16 * HSM_CH), 16,
+                                             hoff[k] + (unsigned)cbyte, 0, 0, 0);
+}
+
+// G wave groups (4 waves each) split the channel chunks round-robin (group g
+// takes chunks g, g + G, ...), each through its own halo buffers and weight
+// ring; groups 1.. hand their accumulators to group 0 through LDS, which sums
+// them in a fixed order and runs the epilogue.  With one 4-wave block per CU
+// (the grids here are 128-512 blocks) every SIMD held a single wave that
+// serialised DMA issue, barrier, fragment reads and MFMAs (~800 cycles per
+// 128-cycle MFMA step); G waves per SIMD overlap them.
+template <int OWT, int TR, bool TRANS, int G>
+__global__ void __launch_bounds__(256 * G, G == 1 ? 2 : 1)
+conv_hsm_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
+           const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
+           int w_bytes, int OH, int IC, int ICp, int OC, float scale, int res_nmod) {
+  typedef HsmGeom<OWT, TR> Gm;
+  constexpr int BN = Gm::BN, WN = BN / 2, TM = 2, TN = WN / 16;
+  constexpr int GLDS = 2 * Gm::HBUF + 4 * Gm::ABUF;     // elements per group
+  static_assert(G * GLDS * 2 <= 160 * 1024, "LDS");
+  static_assert(G == 1 || (G - 1) * 4 * TM * TN * 64 * 16 <= GLDS * 2 * (G - 1), "reduction area");
+  __shared__ __attribute__((aligned(16))) bf16 smem_all[G * GLDS];
+
+  const int lane = threadIdx.x & 63;
+  const int wave_g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wave_g >> 2, wave = wave_g & 3;
+  bf16* const sH = smem_all + grp * GLDS;
+  bf16* const sA = sH + 2 * Gm::HBUF;
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware order: consecutive tiles of one channel slab on one XCD (its L2
+  // keeps the slab's weight rows)
+  const int nbx = gridDim.x, nby = gridDim.y;
+  int bid = blockIdx.x + nbx * blockIdx.y;
+  {
+    const int T = nbx * nby, q = T / 8, r = T % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int tile = bid % nbx, m0 = (bid / nbx) * 64;
+  const int tpi = OH / TR;
+  const int img = tile / tpi, r0 = (tile - img * tpi) * TR;
+  const long n0 = ((long)img * OH + r0) * OWT;
+  const int Kp = 9 * ICp;
+
+  // weights: row = wave * 16 + (lane >> 2), source quarter = slot ^ ((row >> 1) & 2)
+  const int arow = wave * 16 + (lane >> 2);
+  const int aoff = ((m0 + arow) * Kp + (((lane & 3) ^ ((arow >> 1) & 2)) << 3)) * 2;
+  // halo pieces: flat halo pixel fi = (wave + 4k) * 16 + (lane >> 2)
+  unsigned hoff[Gm::HPW];
+#pragma unroll
+  for (int k = 0; k < Gm::HPW; ++k) {
+    const int fi = (wave + 4 * k) * 16 + (lane >> 2);
+    const int hr = fi / Gm::HW2, hc = fi - hr * Gm::HW2;
+    const int ih = r0 - 1 + hr, iw = hc - 1;
+    const bool ok = fi < Gm::HP && ih >= 0 && ih < OH && iw >= 0 && iw < OWT;
+    const int q = (lane & 3) ^ ((fi >> 1) & 2);
+    const unsigned o = (unsigned)((((img * OH + (ok ? ih : 0)) * OWT + (ok ? iw : 0)) * IC + q * 8) * 2);
+    hoff[k] = ok ? o : 0x80000000u;             // past every operand: the range check returns zeros
+  }
+  const int NCH = IC / HSM_CH;
+  const int J = (NCH + G - 1) / G;               // chunk iterations of every group (barriers stay matched)
+  // this group's k-th chunk (clamped: loads past the group's last chunk re-read valid data)
+  auto gchunk = [&](int k) {
+    const int c = grp + k * G;
+    return c < NCH ? c : NCH - 1;
+  };
+  auto issue_a = [&](int s) {                   // group-local step s = 9 k + t
+    const int k = s / 9, t = s - k * 9;
+    hsm_issue_a(sA + (s & 3) * Gm::ABUF + wave * 16 * HSM_CH, Wp, w_bytes, aoff,
+                (t * ICp + gchunk(k) * HSM_CH) * 2);
+  };
+  auto issue_b = [&](int k) {
+    hsm_issue_b<Gm::HPW>(sH + (k & 1) * Gm::HBUF, I, in_bytes, hoff, gchunk(k) * HSM_CH * 2, wave);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  int bo[3][TN], ao[TM];                        // B offsets per kw (a kh shift adds whole pitches), A offsets
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int p = wn * WN + j * 16 + fr;
+    const int hp0 = (p / OWT) * Gm::HW2 + (p % OWT);
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int hp = hp0 + kw;
+      bo[kw][j] = hp * HSM_CH + ((fq ^ ((hp >> 1) & 2)) << 3);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int row = wm * 32 + i * 16 + fr;
+    ao[i] = row * HSM_CH + ((fq ^ ((row >> 1) & 2)) << 3);
+  }
+
+  issue_b(0);
+  issue_a(0);
+  issue_a(1);
+  issue_a(2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int k = 0; k < J; ++k) {
+    const bf16* hb = sH + (k & 1) * Gm::HBUF;
+    const bool live = grp + k * G < NCH;         // wave-uniform
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int s = k * 9 + t;
+      // this step's weights landed (and at t == 0 this chunk's halo); newer loads stay in flight
+      if (t >= 1 && t <= 3) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + Gm::HPW) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      issue_a(s + 3);
+      if (t == 0) issue_b(k + 1);
+      if (!live) continue;
+      const bf16* a = sA + (s & 3) * Gm::ABUF;
+      const int kh = TRANS ? 2 - t / 3 : t / 3, kw = TRANS ? 2 - t % 3 : t % 3;
+      __builtin_amdgcn_s_setprio(1);
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(hb + kh * Gm::HW2 * HSM_CH + bo[kw][j]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a + ao[i]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // tail re-loads drained before exit / reuse
+
+  if constexpr (G > 1) {
+    // groups 1.. hand their accumulators to group 0 (area: the drained buffers of groups 1..)
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(smem_all + GLDS);     // [G - 1][4 waves][TM][TN][64 lanes]
+    if (grp > 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) red[((((grp - 1) * 4 + wave) * TM + i) * TN + j) * 64 + lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (grp > 0) return;
+#pragma unroll
+    for (int g = 1; g < G; ++g)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] += red[((((g - 1) * 4 + wave) * TM + i) * TN + j) * 64 + lane];
+  }
+
+  const int OHW = OH * OWT;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int co = m0 + wm * 32 + i * 16 + fq * 4;
+    float cb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cb[e] = (bias ? bias[co + e] : 0.f) + (row_bias ? row_bias[(long)img * OC + co + e] : 0.f);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const long pix = n0 + wn * WN + j * 16 + fr;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + cb[e];
+      if (res) {
+        const long rpix = res_nmod > 0 ? (long)(img % res_nmod) * OHW + (pix - (long)img * OHW) : pix;
+        const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + rpix * OC + co);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+      }
+      bf16x4 o4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o4[e] = (bf16)(v[e] * scale);
+      *reinterpret_cast<bf16x4*>(O + pix * OC + co) = o4;
+    }
+  }
+}
+
 }  // namespace
 
 // 0: wave groups by grid size; 1: one group (the 4-wave form); 2 / 4: 2 / 4
@@ -363,6 +599,52 @@ extern "C" int d3d_conv_s64_try(const void* I, const void* Wp, const float* bias
 #undef S64G
 #undef S64
   if (gn_done) *gn_done = gnp ? 1 : 0;
+  const int e = (int)hipGetLastError();
+  return e ? -e : 1;
+}
+
+// Small-image halo conv (conv_hsm_k) when it applies: stride 1, 3x3, 8- or
+// 16-wide images with 8 | OH, IC % 32 == 0, OC % 64 == 0, contiguous output,
+// no GroupNorm partials / SiLU companion requested, and a grid of at least
+// 128 blocks.  Returns 1 if launched, 0 if not applicable, < 0 on a launch error.
+// 0: off; 1: on, wave groups by image width (default); 2 / 3 / 4: 1 / 2 / 4 (8-wide) or 3 (16-wide)
+// groups (A/B knob D3D_CONV_HSM)
+static int g_hsm = 1;
+D3D_API void d3d_conv_hsm_cfg(int v) { g_hsm = v; }
+extern "C" int d3d_conv_hsm_try(const void* I, const void* Wp, const float* bias, const float* row_bias,
+                                const void* res, void* O, int N, int IH, int IW, int IC, int ICp, int OH, int OW,
+                                int OC, int ldo, int stride, int trans, float scale, int res_nmod, int taps,
+                                const float* gnp, const void* O2, hipStream_t st) {
+  if (!g_hsm || taps != 9 || stride != 1 || IH != OH || IW != OW || ldo != OC || gnp || O2) return 0;
+  if ((OW != 8 && OW != 16) || OH % 8 || OC % 64 || IC % HSM_CH || ICp < IC || ICp % HSM_CH) return 0;
+  const long in_bytes = (long)N * IH * IW * IC * 2;
+  const long w_bytes = (long)((OC + 127) / 128 * 128) * 9 * ICp * 2;
+  if (in_bytes >= (1L << 31) || w_bytes >= (1L << 31)) return 0;
+  const long tiles = (long)N * (OH / 8);
+  if (tiles * (OC / 64) < 128 || tiles >= (1L << 24)) return 0;
+  dim3 grid((unsigned)tiles, (unsigned)(OC / 64), 1);
+  // auto: 4 (8-wide) / 3 (16-wide) groups on grids of one block per CU, else 2
+  // (tools/kbench_s64.py --hsm 2,3,4: 8x8x512 at 32 frames 26.4 -> 24.1 us with
+  // 4 groups, at 64 frames 30.2 -> 33.3 us)
+  const int gmax = OW == 8 ? 4 : 3;
+  int g = g_hsm == 2 ? 1 : g_hsm == 3 ? 2 : g_hsm == 4 ? gmax : (tiles * (OC / 64) <= 320 ? gmax : 2);
+#define HSM(OWv, TRv, Gv)                                                                                        \
+  hipLaunchKernelGGL((conv_hsm_k<OWv, 8, TRv, Gv>), grid, dim3(256 * Gv), 0, st, (const bf16*)I, (const bf16*)Wp, \
+                     bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, OH, IC, ICp, OC,     \
+                     scale, res_nmod)
+#define HSMG(OWv, TRv, G3)                                                                                       \
+  do {                                                                                                          \
+    if (g == 1) HSM(OWv, TRv, 1);                                                                               \
+    else if (g == 2) HSM(OWv, TRv, 2);                                                                          \
+    else HSM(OWv, TRv, G3);                                                                                     \
+  } while (0)
+  if (OW == 8) {
+    if (trans) HSMG(8, true, 4); else HSMG(8, false, 4);
+  } else {
+    if (trans) HSMG(16, true, 3); else HSMG(16, false, 3);
+  }
+#undef HSMG
+#undef HSM
   const int e = (int)hipGetLastError();
   return e ? -e : 1;
 }

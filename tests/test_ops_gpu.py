@@ -293,6 +293,39 @@ def test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale):
         assert rel(a, c) < 3e-2, (names[i], rel(a, c))
 
 
+HSM_SHAPES = [
+    # the 8x8 / 16x16 levels at 16 examples per GPU: small-image halo conv (conv_hsm_k)
+    (32, 8, 8, 512, 512, 1, True, True, 1 / math.sqrt(2)),
+    (32, 16, 16, 256, 256, 1, True, False, 1 / math.sqrt(2)),
+    (32, 8, 8, 1024, 512, 1, False, True, 1.0),                 # decoder concat input
+    (32, 16, 16, 512, 256, 1, False, False, 1.0),
+    (32, 16, 16, 96, 128, 1, True, False, 0.5),                 # IC < ICp (padded K), 128 blocks
+    (64, 8, 8, 512, 512, 1, True, False, 1.0),                  # bs32 share: 512 blocks
+]
+
+
+@pytest.mark.parametrize("N,Hh,W,Ci,Co,s,res,rb,scale", HSM_SHAPES)
+def test_conv3x3_small_halo(H, N, Hh, W, Ci, Co, s, res, rb, scale):
+    """conv_hsm_k (fwd and input gradient) against fp32, and every wave-group
+    form against the 64 x 64 im2col kernel it replaces (D3D_CONV_HSM=0)."""
+    test_conv3x3(H, N, Hh, W, Ci, Co, s, res, rb, scale)
+    torch.manual_seed(5)
+    x = torch.randn(N, Hh, W, Ci, device=DEV).to(BF)
+    w = torch.randn(Co, Ci, 3, 3, device=DEV) / math.sqrt(9 * Ci)
+    b = torch.randn(Co, device=DEV) * 0.1
+    ys = {}
+    with torch.no_grad():
+        try:
+            for cfg in (0, 1, 2, 3, 4):          # off, auto, 1 / 2 / 3-4 wave groups
+                H._lib.d3d_conv_hsm_cfg(cfg)
+                ys[cfg] = H.conv3x3(x, w, b)
+        finally:
+            H._lib.d3d_conv_hsm_cfg(1)
+    for cfg in (1, 2, 3, 4):
+        assert rel(ys[cfg], ys[0]) < 1e-2, (cfg, rel(ys[cfg], ys[0]))
+    assert torch.equal(ys[1], ys[3] if N * (Hh // 8) * (Co // 64) > 320 else ys[4])   # auto form, deterministic
+
+
 W8_SHAPES = [
     # large grids (>= 256 blocks of 256 pixels): the 8-wave conv_w8_k path
     (32, 64, 64, 128, 128, 1, True, False, 1 / math.sqrt(2)),     # BM=128 (w8w: 128x512 tiles)

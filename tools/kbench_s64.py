@@ -29,24 +29,54 @@ def timeit(fn, iters=30):
     return ts[len(ts) // 2]
 
 
+SHAPES = ((32, 8, 512, 512), (32, 16, 256, 256), (32, 8, 1024, 512), (32, 16, 512, 256), (64, 8, 512, 512))
+
+
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="0,1,2,3,4", help="indices into SHAPES (N, H, IC, OC)")
+    ap.add_argument("--cfgs", default="1,2,3,4,0")
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--dgrad", action="store_true", help="also time the input gradient (TRANS)")
+    ap.add_argument("--hsm", default="0", help="small-image halo conv settings to run (0 off, 1 auto, 2/3/4: 1/2/3-4 wave groups)")
+    a = ap.parse_args()
     torch.manual_seed(0)
-    for N, Hh, C in ((32, 8, 512), (32, 16, 256), (64, 8, 512), (32, 8, 1024)):
-        x = torch.randn(N, Hh, Hh, C, device="cuda").to(BF)
-        w = torch.randn(C, C, 3, 3, device="cuda") * 0.03
-        fl = 2.0 * N * Hh * Hh * C * C * 9
+    for si in [int(v) for v in a.shapes.split(",")]:
+        N, Hh, IC, OC = SHAPES[si]
+        x = torch.randn(N, Hh, Hh, IC, device="cuda").to(BF)
+        w = torch.randn(OC, IC, 3, 3, device="cuda") * 0.03
+        g = torch.randn(N, Hh, Hh, OC, device="cuda").to(BF)
+        fl = 2.0 * N * Hh * Hh * IC * OC * 9
+        wpf, wpt = H.packed_weight(w, False), H.packed_weight(w, True)
+        # packed operands are flat: [OCp128][9][ICp64] and (transposed) [ICp128][9][OCp64]
+        ICp, OCp = (IC + 63) // 64 * 64, (OC + 63) // 64 * 64
+        assert wpf.numel() == (OC + 127) // 128 * 128 * 9 * ICp, wpf.shape
+        assert wpt.numel() == (IC + 127) // 128 * 128 * 9 * OCp, wpt.shape
+        y = torch.empty(N, Hh, Hh, OC, device="cuda", dtype=BF)
+        dx = torch.empty(N, Hh, Hh, IC, device="cuda", dtype=BF)
+
+        def fwd():
+            H._conv_fwd(x, wpf, None, None, None, y, N, Hh, Hh, IC, ICp, Hh, Hh, OC, OC, 1, False, 1.0)
+
+        def bwd():
+            H._conv_fwd(g, wpt, None, None, None, dx, N, Hh, Hh, OC, OCp, Hh, Hh, IC, IC, 1, True, 1.0)
+
         ref = None
-        for cfg in (1, 2, 3, 4, 0):
+        for hsm, cfg in [(int(h), int(v)) for h in a.hsm.split(",") for v in a.cfgs.split(",")]:
+            H._lib.d3d_conv_hsm_cfg(hsm)
             H._lib.d3d_conv_s64_cfg(cfg)
-            with torch.no_grad():
-                y = H.conv3x3(x, w, None)
-                if ref is None:
-                    ref = y.float()
-                err = ((y.float() - ref).norm() / ref.norm()).item()
-                us = timeit(lambda: H.conv3x3(x, w, None))
-            print(f"{N}x{Hh}x{Hh}x{C} fwd cfg{cfg}: {us:7.1f} us {fl / us / 1e6:6.1f} TF/s  rel-vs-cfg1 {err:.1e}",
-                  flush=True)
+            for name, fn, out in (("fwd", fwd, y), ("dgrad", bwd, dx))[: 2 if a.dgrad else 1]:
+                fn()
+                torch.cuda.synchronize()
+                if ref is None or name not in ref:
+                    ref = dict(ref or {}, **{name: out.float().clone()})
+                err = ((out.float() - ref[name]).norm() / ref[name].norm()).item()
+                us = timeit(fn, a.iters)
+                print(f"{N}x{Hh}x{Hh} {IC}->{OC} {name} hsm{hsm} cfg{cfg}: {us:7.1f} us {fl / us / 1e6:6.1f} TF/s  "
+                      f"rel-vs-first {err:.1e}", flush=True)
         H._lib.d3d_conv_s64_cfg(0)
+        H._lib.d3d_conv_hsm_cfg(1)
 
 
 if __name__ == "__main__":
