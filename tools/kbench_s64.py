@@ -13,23 +13,37 @@ from distributed_3d_diffusion_pytorch_amd.ops import hip_impl as H
 BF = torch.bfloat16
 
 
-def timeit(fn, iters=30):
+def timeit(fn, iters=30, reps=20):
+    """Median device time of one call: ``reps`` calls captured into a HIP graph
+    and replayed (host launch overhead out of the measurement -- event pairs
+    around a single eager call include ~10 us of host time per call)."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
     ts = []
     for _ in range(iters):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        fn()
+        a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
         e.record()
         torch.cuda.synchronize()
-        ts.append(s.elapsed_time(e) * 1e3)
+        ts.append(a.elapsed_time(e) * 1e3 / reps)
     ts.sort()
     return ts[len(ts) // 2]
 
 
-SHAPES = ((32, 8, 512, 512), (32, 16, 256, 256), (32, 8, 1024, 512), (32, 16, 512, 256), (64, 8, 512, 512))
+SHAPES = ((32, 8, 512, 512), (32, 16, 256, 256), (32, 8, 1024, 512), (32, 16, 512, 256), (64, 8, 512, 512),
+          (16, 8, 512, 512), (24, 8, 512, 512), (31, 8, 512, 512), (33, 8, 512, 512), (40, 8, 512, 512))
 
 
 def main():
