@@ -296,16 +296,23 @@ class GradSink:
             self._wait_compute(torch.cuda.current_stream(idx), idx)
 
     @contextlib.contextmanager
-    def collective(self):
+    def collective(self, main=None):
         """Issue a collective over deposited gradients: from behind the side
         stream (which first catches up with the compute stream), so it reads
-        both streams' gradients without stalling the compute stream."""
+        both streams' gradients without stalling the compute stream.
+        ``main``: the stream the backward started on (GradReducer.reset):
+        waited for too when the collective is issued from another stream's
+        context (a flush from the conditioning stream's backward), so a bucket
+        never narrows a gradient that the trunk stream still writes."""
         if not self._forked:
             yield
             return
         idx = torch.cuda.current_device()
         side = self._side(idx)
-        side.wait_stream(torch.cuda.current_stream(idx))
+        cur = torch.cuda.current_stream(idx)
+        side.wait_stream(cur)
+        if main is not None and main.cuda_stream != cur.cuda_stream and main.cuda_stream != side.cuda_stream:
+            side.wait_stream(main)
         self._wait_compute(side, idx)       # deposits made from the other compute stream(s)
         with torch.cuda.stream(side):
             yield

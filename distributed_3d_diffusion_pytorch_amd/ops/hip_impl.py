@@ -721,8 +721,6 @@ class _GNFiLM(torch.autograd.Function):
             holder, off = ctx.slot
             dss = holder.grad_slice(off, x.shape[-1])
         dx, dss, dg, db = _gn_bwd(2, x, dy.contiguous(), ss, stats, w, b, G, p, seed, dss=dss, ssld=ld)
-        if ctx.slot is not None and ctx.needs_input_grad[3] and ctx.slot[0].width == ld:
-            ctx.slot[0].deposited(ctx.slot[1])
         return dx, dg, db, dss, None, None, None, None, None
 
 
@@ -1403,77 +1401,18 @@ def _film_wgrad_product(dy: torch.Tensor, x2: torch.Tensor):
 
 class _FiLMSlot:
     """Shared gradient buffer of one level-batched FiLM projection: each
-    GN-FiLM backward deposits its d(scale|shift) into its column slice.
-
-    Early weight gradient: the backward deposits the level's decoder blocks
-    (a column suffix: film_batch lists a level's encoder blocks first) long
-    before its encoder blocks.  Once a deposited suffix covers at least half
-    the columns its weight gradient is queued on the weight-gradient stream
-    right away (``early``, set by the forward), overlapped with the rest of
-    the backward; the FiLM backward then covers the remaining prefix only.
-    Without it the level-0 FiLM weight gradient (a [P, 1792] x [P, 1024]
-    reduction at bs16) ran alone after the trunk's last kernel."""
+    GN-FiLM backward deposits its d(scale|shift) into its column slice."""
 
     def __init__(self, shape, width, device, want_events=False):
         self.shape, self.width, self.device = tuple(shape), width, device
         self.buf = None
         self.want_events = want_events      # forward: one GEMM + ready event per block (film_batch)
         self.events = []
-        self.early = None                   # (block offsets + [S], fire(k) -> bool)
-        self.dep = set()
-        self.early_k = None                 # first block whose weight gradient went out early
 
     def grad_slice(self, off: int, C: int) -> torch.Tensor:
         if self.buf is None:
             self.buf = torch.empty(*self.shape, self.width, dtype=BF16, device=self.device)
         return self.buf[..., off: off + 2 * C]
-
-    def deposited(self, off: int) -> None:
-        if self.early is None or self.early_k is not None:
-            return
-        self.dep.add(off)
-        offs, fire = self.early
-        n = len(offs) - 1
-        k = n
-        while k > 0 and offs[k - 1] in self.dep:
-            k -= 1
-        if 0 < k < n and 2 * (offs[n] - offs[k]) >= offs[n] and fire(k):
-            self.early_k = k
-
-
-_FILM_EARLY = os.environ.get("D3D_FILM_EARLY", "1") != "0"
-
-
-def _film_wgrad_early(slot, x2, Ws, Bs, offs, k) -> bool:
-    """Queue the weight gradient of FiLM blocks k.. (a deposited column
-    suffix of the level's d(scale|shift) buffer) on the weight-gradient stream
-    now; False when it cannot go (no sink targets, no split-K plan)."""
-    n = len(Ws)
-    Wk, Bk = Ws[k:], Bs[k:]
-    tw = [SINK.target(w) for w in Wk]
-    tb = [SINK.target(b) for b in Bk]
-    if slot.buf is None or not all(t is not None for t in tw + tb):
-        return False
-    S = offs[n]
-    c0 = offs[k]
-    dy = slot.buf.view(-1, S)[:, c0:]
-    rows, K = x2.shape
-    _ensure_impl()
-    sp = _lib.d3d_wgrad_tn_plan(S - c0, K, rows, S, K)
-    if sp <= 0:
-        return False
-    m = n - k
-    row0s = [o - c0 for o in offs[k:n]]
-
-    def job():
-        row0 = (ctypes.c_int * m)(*row0s)
-        wd = (ctypes.c_void_p * m)(*[t.data_ptr() for t in tw])
-        bd = (ctypes.c_void_p * m)(*[t.data_ptr() for t in tb])
-        ws, bws, used = wgrad_tn(dy, x2, sp)
-        _chk(_lib.d3d_wgrad_scatter(ws.data_ptr(), S - c0, K, used, 1, bws.data_ptr(), bws.shape[0], m, row0, wd, bd,
-                                    _st()), "film_wgrad_scatter")
-    SINK.submit(x2.device, job, (dy, x2), [p for wb in zip(Wk, Bk) for p in wb])
-    return True
 
 
 class _FiLMBatch(torch.autograd.Function):
@@ -1524,11 +1463,6 @@ class _FiLMBatch(torch.autograd.Function):
         ctx.n, ctx.slot, ctx.shp = n, slot, shp
         ctx.params = (Ws, Bs)
         ctx.widths = [w.shape[0] for w in Ws]
-        if _FILM_EARLY and _FILM_WGRAD == "tn" and n > 1 and all(ctx.needs_input_grad[4: 4 + 2 * n]):
-            offs = [0]
-            for wd in ctx.widths:
-                offs.append(offs[-1] + wd)
-            slot.early = (offs, lambda k: _film_wgrad_early(slot, x2, Ws, Bs, offs, k))
         for i, (w, b) in enumerate(zip(Ws, Bs)):
             SINK.use(w, ctx.needs_input_grad[4 + i])
             SINK.use(b, ctx.needs_input_grad[4 + n + i])
@@ -1566,8 +1500,6 @@ class _FiLMBatch(torch.autograd.Function):
                 if g is not None:
                     dy[:, o: o + wd].copy_(g.reshape(-1, wd))
         slot.buf = None
-        nw = slot.early_k if slot.early_k is not None else n     # blocks [nw, n) went out early
-        slot.early, slot.early_k, slot.dep = None, None, set()
         rows, K = x2.shape
         dx = None
         if ctx.needs_input_grad[0]:
@@ -1583,10 +1515,6 @@ class _FiLMBatch(torch.autograd.Function):
         grads_w, grads_b = [None] * n, [None] * n
         need_w = any(ctx.needs_input_grad[4: 4 + n])
         if need_w:
-            if nw < n:
-                Ws, Bs, n = Ws[:nw], Bs[:nw], nw
-                S = offs[nw]
-                dy = dy[:, :S]
             tw = [SINK.target(w) for w in Ws]
             tb = [SINK.target(b) for b in Bs]
             direct = all(t is not None for t in tw + tb)
@@ -1594,9 +1522,7 @@ class _FiLMBatch(torch.autograd.Function):
                 tw = [torch.zeros(w.shape, dtype=F32, device=x2.device) for w in Ws]
                 tb = [torch.zeros(b.shape, dtype=F32, device=x2.device) for b in Bs]
             _ensure_impl()
-            sp_tn = _lib.d3d_wgrad_tn_plan(S, K, rows, dy.stride(0), K) if _FILM_WGRAD == "tn" else 0
-            if not sp_tn and dy.stride(0) != S:
-                dy = dy.contiguous()
+            sp_tn = _lib.d3d_wgrad_tn_plan(S, K, rows, S, K) if _FILM_WGRAD == "tn" else 0
 
             def job():
                 row0 = (ctypes.c_int * n)(*offs[:n])

@@ -83,6 +83,8 @@ class GradReducer:
 
     # ------------------------------------------------------------------
     def reset(self) -> None:
+        # the stream this step's backward runs its trunk on (the capture stream inside a graph capture)
+        self.main_stream = torch.cuda.current_stream() if self.flat.grad.is_cuda else None
         for b, bk in enumerate(self.buckets):
             self._pending[b] = sum(1 for i in bk["params"] if self.flat.params[i].requires_grad)
             self._launched[b] = False
@@ -111,7 +113,7 @@ class GradReducer:
         self._launched[b] = True
         bk = self.buckets[b]
         view = self.flat.grad[bk["start"]: bk["end"]]
-        ctx = self.sink.collective() if self.sink is not None else contextlib.nullcontext()
+        ctx = self.sink.collective(self.main_stream) if self.sink is not None else contextlib.nullcontext()
         with ctx:       # behind the sink's weight-gradient stream (ops/gradsink.py)
             if self.mirror is None:
                 self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))

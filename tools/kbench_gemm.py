@@ -29,6 +29,11 @@ SHAPES = [
     ("nin fwd P524288 256->128", 128, 524288, 256),
     ("nin fwd P131072 512->256", 256, 131072, 512),
     ("out fwd P32768 512->512", 512, 32768, 512),
+    ("res proj P262144 256->256", 256, 262144, 256),
+    ("res proj P65536 256->256", 256, 65536, 256),
+    ("res proj P65536 512->512", 512, 65536, 512),
+    ("res proj P16384 512->512", 512, 16384, 512),
+    ("res nin P1048576 256->128", 128, 1048576, 256),
 ]
 
 
@@ -50,6 +55,7 @@ def main():
     ap.add_argument("--vers", default="1", help="comma list of tile configs timed interleaved (1 = by size, 8 / 4 / 2 forced)")
     ap.add_argument("--gm", type=int, default=0, help="tile-group width (d3d_gemm_tune gm; 0 = default)")
     ap.add_argument("--nobias", action="store_true")
+    ap.add_argument("--res", action="store_true", help="with a residual operand R [N, M] (F_RES epilogue)")
     args = ap.parse_args()
     H._ensure_impl()
     lib = H._lib
@@ -61,21 +67,23 @@ def main():
         x = (torch.rand(N, K, device="cuda") * 2 - 1).to(BF)
         bias = None if args.nobias else torch.randn(M, device="cuda")
         y = torch.empty(N, M, dtype=BF, device="cuda")
+        r = (torch.rand(N, M, device="cuda") * 2 - 1).to(BF) if args.res else None
         st = H._st()
 
         def ours(v=None):
             if v is not None:
                 lib.d3d_gemm_tune(v, args.gm, 0)
-            rc = lib.d3d_gemm_nt(w.data_ptr(), x.data_ptr(), y.data_ptr(), H._ptr(bias), None, M, N, K, K, K, M,
-                                 M, 1.0, 1.0, st)
+            rc = lib.d3d_gemm_nt(w.data_ptr(), x.data_ptr(), y.data_ptr(), H._ptr(bias), H._ptr(r), M, N, K, K, K,
+                                 M, M, 1.0, 1.0, st)
             assert rc == 0, rc
 
         def blas():
-            return torch.addmm(bias.to(BF), x, w.t()) if bias is not None else torch.mm(x, w.t())
+            o = torch.addmm(bias.to(BF), x, w.t()) if bias is not None else torch.mm(x, w.t())
+            return o.add_(r) if r is not None else o
 
         vers = [int(v) for v in args.vers.split(",")]
         rows = torch.randint(0, N, (256,), device="cuda")
-        ref = x[rows].float() @ w.float().t() + (bias if bias is not None else 0)
+        ref = x[rows].float() @ w.float().t() + (bias if bias is not None else 0) + (r[rows].float() if r is not None else 0)
         errs = {}
         for v in vers:
             y.zero_()
