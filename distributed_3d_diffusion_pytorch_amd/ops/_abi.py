@@ -33,6 +33,7 @@ SIGNATURES = {
     "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P, F, P, F, P],
     "d3d_conv_s64_cfg": [I],
     "d3d_conv_hsm_cfg": [I],
+    "d3d_gemm_small_k": [I],
     "d3d_conv_halo_cfg": [I],
     "d3d_conv_res_cfg": [I],
     # elementwise.hip

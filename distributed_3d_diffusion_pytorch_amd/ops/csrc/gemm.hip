@@ -461,9 +461,18 @@ D3D_API void d3d_gemm_tune(int cfg, int gm, int grid) {
 
 // Tile configuration for a problem: the 256 x 256 tile when it gives the chip
 // most of a wave of tiles, smaller tiles (more blocks per CU) otherwise.
-static int g_cfg(int M, int N) {
+// Short-K projections (K <= 512, 256-768 output channels: the attention /
+// NIN / 1x1 maps and their residual forms) are bandwidth-bound with one
+// 256 x 256 block per CU -- its epilogue (residual read, output write) runs
+// with nothing else in flight; two 128 x 128 blocks per CU overlap one's
+// epilogue with the other's loads (tools/kbench_gemm.py: residual 256->256
+// over 262144 pixels 55.9 -> 51.3 us, 512->256 NIN 42.2 -> 40.2 us).
+static int g_small_k_w4 = 1;
+D3D_API void d3d_gemm_small_k(int on) { g_small_k_w4 = on; }
+static int g_cfg(int M, int N, int K) {
   if (g_cfg_force) return g_cfg_force;
   const long cus = g_cus();
+  if (g_small_k_w4 && K <= 512 && M >= 256 && M <= 768 && (long)cdiv(M, 128) * cdiv(N, 128) >= cus) return 4;
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256);
   if (t256 >= cus * 3 / 4) return 8;
   const long t128 = (long)cdiv(M, 128) * cdiv(N, 128);
@@ -502,7 +511,7 @@ D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, i
   if (ldo % 8 || ldo < M || (R && (ldr % 4 || ldr < M || ((uintptr_t)R & 7)))) return -1;
   if (epi == 1 && (!R || bias_ || gnp)) return -1;
   if (gnp && bias_ && bias_bf16) return -1;
-  int W = g_cfg(M, N);
+  int W = g_cfg(M, N, K);
   if (gnp) {
     const int cg = G > 0 ? M / G : 0;
     if (G <= 0 || M % G || hw <= 0 || hw % 64 || N % hw || !(cg == 4 || cg == 8 || cg == 16 || cg == 32)) return -1;

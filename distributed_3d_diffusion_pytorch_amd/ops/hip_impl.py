@@ -738,6 +738,8 @@ if os.environ.get("D3D_GEMM_TUNE"):     # A/B knob "cfg,gm,grid" (gemm.hip d3d_g
     _lib.d3d_gemm_tune(*[int(v) for v in os.environ["D3D_GEMM_TUNE"].split(",")])
 if os.environ.get("D3D_HALO_AU"):        # A/B knob: halo conv with unrolled taps / precomputed offsets (1) or not (0)
     _lib.d3d_conv_halo_cfg(int(os.environ["D3D_HALO_AU"]))
+if os.environ.get("D3D_GEMM_SMALL_K"):   # A/B knob: 128x128 tiles for short-K 256-768-channel GEMMs (1) or not (0)
+    _lib.d3d_gemm_small_k(int(os.environ["D3D_GEMM_SMALL_K"]))
 if os.environ.get("D3D_CONV_HSM"):      # A/B knob: small-image halo conv (conv_small.hip conv_hsm_k) on (1) / off (0)
     _lib.d3d_conv_hsm_cfg(int(os.environ["D3D_CONV_HSM"]))
 if os.environ.get("D3D_GN_CFG"):        # A/B knob "blocks,red_u,app_u": GroupNorm launch shapes

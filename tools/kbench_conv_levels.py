@@ -17,18 +17,31 @@ from distributed_3d_diffusion_pytorch_amd.ops import hip_impl as H
 BF = torch.bfloat16
 
 
-def timeit(fn, iters=25):
-    for _ in range(4):
+def timeit(fn, iters=25, reps=10):
+    """Median device time of one call: ``reps`` calls captured into a HIP graph
+    and replayed (an event pair around one eager call also counts ~10 us of
+    host launch time -- the round-4 numbers of this tool carried it)."""
+    for _ in range(3):
         fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(g, stream=st):
+            for _ in range(reps):
+                fn()
+    torch.cuda.current_stream().wait_stream(st)
+    g.replay()
     torch.cuda.synchronize()
     ts = []
     for _ in range(iters):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        fn()
+        g.replay()
         e.record()
         torch.cuda.synchronize()
-        ts.append(s.elapsed_time(e) * 1e3)
+        ts.append(s.elapsed_time(e) * 1e3 / reps)
     ts.sort()
     return ts[len(ts) // 2]
 
@@ -53,15 +66,19 @@ def main():
             with torch.no_grad():
                 f1 = timeit(lambda: H.conv3x3(x, w, b, gn_groups=32))
                 f2 = timeit(lambda: H.conv3x3(x, w, b, residual=r, out_scale=0.7071, gn_groups=32))
-            xr = x.clone().requires_grad_(True)
-            y = H.conv3x3(xr, w, None)
-            g = torch.randn_like(y)
-            d = timeit(lambda: torch.autograd.grad(y, xr, g, retain_graph=True))
+            # input gradient: the transposed-weight conv the backward launches
+            g = torch.randn(N, Hh, Hh, OC, device="cuda").to(BF)
+            wpt = H.packed_weight(w, True)
+            OCp = (OC + 63) // 64 * 64
+            assert wpt.numel() == (C + 127) // 128 * 128 * 9 * OCp
+            dx = torch.empty(N, Hh, Hh, C, device="cuda", dtype=BF)
+            d = timeit(lambda: H._conv_fwd(g, wpt, None, None, None, dx, N, Hh, Hh, OC, OCp, Hh, Hh, C, C, 1, True,
+                                           1.0))
             print(json.dumps({"res_always": os.environ.get("D3D_CONV_RES_ALWAYS", "0"), "N": N, "level": f"{Hh}x{Hh}x{C}->{OC}", "fwd_us": round(f1, 1),
                               "fwd_tfs": round(fl / f1 / 1e6, 1), "fwd_res_us": round(f2, 1),
                               "fwd_res_tfs": round(fl / f2 / 1e6, 1), "dgrad_us": round(d, 1),
                               "dgrad_tfs": round(fl / d / 1e6, 1)}), flush=True)
-            del x, r, xr, y, g
+            del x, r, g, dx
             torch.cuda.empty_cache()
 
 

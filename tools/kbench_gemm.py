@@ -6,7 +6,10 @@ an fp32 product, then interleaved timing rounds in one process.
 """
 import argparse
 import json
+import os
+import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 from distributed_3d_diffusion_pytorch_amd.ops import hip_impl as H
