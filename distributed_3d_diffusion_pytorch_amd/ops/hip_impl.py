@@ -32,6 +32,8 @@ _ZERO_PAGE: Dict[int, torch.Tensor] = {}
 # separate bias sums + segment scatter; profiles/ab_film_wgrad.txt) or "seg"
 # (the 1x1 conv weight-gradient kernel)
 _FILM_WGRAD = "tn"
+# level-batched FiLM forward of the big levels on hipBLASLt (plain GEMM + bias)
+_FILM_BLAS = os.environ.get("D3D_FILM_BLAS", "1") != "0"
 
 
 def set_conv_impl(impl: str) -> None:
@@ -1456,6 +1458,11 @@ class _FiLMBatch(torch.autograd.Function):
                 ev.record()
                 slot.events.append(ev)
                 off += wd
+        elif _FILM_BLAS and P * S * K >= (1 << 37) and x2.is_contiguous():
+            # the big level projections (a plain GEMM + bias): hipBLASLt's
+            # kernels run these 8-17 % faster than gemm_fw_k's 256 x 256 tile
+            # (tools/kbench_gemm.py "film fwd"; profiles/r5/ab_gemm_small_k.txt)
+            torch.addmm(bcat, x2, wcat.t(), out=y)
         elif _gemm_ok(S, P, K, K, K, x2):
             gemm_nt(wcat, x2, y, S, P, K, K, K, S, bias=bcat)
         else:
