@@ -55,3 +55,62 @@ D3D_API int d3d_colsum(const float* in, long R, int Cc, float* part, float* out,
                      accumulate);
   return (int)hipGetLastError();
 }
+
+// Batched column sums: up to 16 independent [R][Cc] reductions (the
+// whole-image GroupNorm's per-image dgamma/dbeta rows of one weight-gradient
+// flush) in ONE launch, a block per 256 columns of a job, each column summed
+// over its rows in order (deterministic).  Interleaved pairs go to out0 (even
+// columns) and out1 (odd columns), accumulated or stored.  Replaces the two
+// launches per GroupNorm of d3d_colsum on the weight-gradient stream.
+struct ColJob {
+  const float* in;
+  float* out0;
+  float* out1;
+  int R, Cc, acc, blk0;
+};
+constexpr int kMaxColJobs = 16;
+struct ColJobs {
+  ColJob j[kMaxColJobs];
+  int n;
+};
+
+namespace {
+__global__ void __launch_bounds__(256) colsum_jobs_k(ColJobs t) {
+  int k = 0;
+#pragma unroll 1
+  while (k + 1 < t.n && (int)blockIdx.x >= t.j[k + 1].blk0) ++k;
+  const ColJob& J = t.j[k];
+  const int c = ((int)blockIdx.x - J.blk0) * 256 + (int)threadIdx.x;
+  if (c >= J.Cc) return;
+  const float* p = J.in + c;
+  const long ld = J.Cc;
+  float s = 0.f;
+  int r = 0;
+  for (; r + 8 <= J.R; r += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(long)(r + u) * ld];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; r < J.R; ++r) s += p[(long)r * ld];
+  float* dst = (c & 1) ? J.out1 : J.out0;
+  const int idx = c >> 1;
+  dst[idx] = J.acc ? dst[idx] + s : s;
+}
+}  // namespace
+
+D3D_API int d3d_colsum_jobs(const ColJob* jobs, int njobs, hipStream_t st) {
+  if (njobs < 1 || njobs > kMaxColJobs) return (int)hipErrorInvalidValue;
+  ColJobs t{};
+  t.n = njobs;
+  int blk = 0;
+  for (int i = 0; i < njobs; ++i) {
+    t.j[i] = jobs[i];
+    if (t.j[i].Cc % 2 || t.j[i].R < 1 || !t.j[i].in || !t.j[i].out0 || !t.j[i].out1) return (int)hipErrorInvalidValue;
+    t.j[i].blk0 = blk;
+    blk += (t.j[i].Cc + 255) / 256;
+  }
+  hipLaunchKernelGGL(colsum_jobs_k, dim3(blk), dim3(256), 0, st, t);
+  return (int)hipGetLastError();
+}

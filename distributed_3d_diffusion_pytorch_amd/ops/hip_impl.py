@@ -524,7 +524,9 @@ def _gn_bwd_img(mode, x, dy, ss, stats, w, b, G, p, seed, dss, ssld, x2, dres, d
         def job():
             _chk(_lib.d3d_colsum(chan.data_ptr(), N, 2 * C, ws.data_ptr(), tg.data_ptr(), tb.data_ptr(), 1, _st()),
                  "gn_img_dgb")
-        SINK.submit(dev, job, (chan,), (w, b))
+        # the column sums of a flush run as one batched launch (sink_group_run)
+        spec = _ColJob(chan.data_ptr(), tg.data_ptr(), tb.data_ptr(), N, 2 * C, 1, 0) if _COLSUM_GROUP else None
+        SINK.submit(dev, job, (chan,), (w, b), spec=spec)
         return dx, dss, None, None
     dg = torch.empty(C, dtype=F32, device=dev)
     db = torch.empty(C, dtype=F32, device=dev)
@@ -876,7 +878,48 @@ def wgrad_group_run(jobs) -> None:
         go(batch)
 
 
-SINK.group_fn = wgrad_group_run
+class _ColJob(ctypes.Structure):
+    """reduce.hip ColJob: one [R][Cc] column sum (interleaved pairs -> two outputs)."""
+    _fields_ = [("inp", ctypes.c_void_p), ("out0", ctypes.c_void_p), ("out1", ctypes.c_void_p), ("R", ctypes.c_int),
+                ("Cc", ctypes.c_int), ("acc", ctypes.c_int), ("blk0", ctypes.c_int)]
+
+
+assert ctypes.sizeof(_ColJob) == 40
+_COLSUM_GROUP = os.environ.get("D3D_COLSUM_GROUP", "1") != "0"
+
+
+def colsum_group_run(jobs) -> None:
+    """Run batched column-sum jobs on the current stream, 16 per launch, never
+    two accumulating into the same output in one launch."""
+    batch, seen = [], set()
+
+    def go(b):
+        arr = (_ColJob * len(b))(*b)
+        _chk(_lib.d3d_colsum_jobs(arr, len(b), _st()), "colsum_jobs")
+
+    for j in jobs:
+        keys = {j.out0, j.out1}
+        if len(batch) == 16 or keys & seen:
+            go(batch)
+            batch, seen = [], set()
+        batch.append(j)
+        seen |= keys
+    if batch:
+        go(batch)
+
+
+def sink_group_run(specs) -> None:
+    """The sink's grouped launch: weight-gradient specs as grouped wgrad
+    launches, column-sum specs as batched column sums (issue order kept per kind)."""
+    wg = [s_ for s_ in specs if not isinstance(s_, _ColJob)]
+    cs = [s_ for s_ in specs if isinstance(s_, _ColJob)]
+    if wg:
+        wgrad_group_run(wg)
+    if cs:
+        colsum_group_run(cs)
+
+
+SINK.group_fn = sink_group_run
 
 
 def _chansum(g, per_image: bool):

@@ -1819,3 +1819,38 @@ def test_conv_operands_beyond_2gib(H):
     assert rel(dW.reshape(C2, C2, 3, 3), ref) < 1e-3, rel(dW.reshape(C2, C2, 3, 3), ref)
     rb = g2.float().sum((0, 1, 2))
     assert (db - rb).abs().max().item() <= 1e-3 * rb.abs().max().item() + 1e-2
+
+
+def test_colsum_jobs_batched(H):
+    """Batched column sums (reduce.hip colsum_jobs_k): 20 jobs of mixed row
+    counts / widths (two launches, one output accumulated twice across
+    them) against torch sums; interleaved pairs split into two outputs."""
+    torch.manual_seed(7)
+    specs, refs, outs = [], [], []
+    shared0 = torch.randn(256, device=DEV)
+    shared1 = torch.randn(256, device=DEV)
+    base0, base1 = shared0.clone(), shared1.clone()
+    acc0, acc1 = torch.zeros(256, device=DEV), torch.zeros(256, device=DEV)
+    for i in range(20):
+        R, C = (32, 256) if i % 3 else (256, 512 if i % 2 else 128)
+        x = torch.randn(R, 2 * C, device=DEV)
+        if i in (3, 17):            # two jobs accumulate into one shared output pair (C = 256)
+            x = torch.randn(R, 512, device=DEV)
+            o0, o1 = shared0, shared1
+            acc0 += x[:, 0::2].sum(0)
+            acc1 += x[:, 1::2].sum(0)
+            specs.append(H._ColJob(x.data_ptr(), o0.data_ptr(), o1.data_ptr(), R, 512, 1, 0))
+            outs.append(x)
+            continue
+        o0 = torch.full((C,), 5.0, device=DEV)
+        o1 = torch.full((C,), 5.0, device=DEV)
+        specs.append(H._ColJob(x.data_ptr(), o0.data_ptr(), o1.data_ptr(), R, 2 * C, 0, 0))
+        refs.append((o0, o1, x[:, 0::2].sum(0), x[:, 1::2].sum(0)))
+        outs.append(x)
+    H.colsum_group_run(specs)
+    torch.cuda.synchronize()
+    for o0, o1, r0, r1 in refs:
+        assert torch.allclose(o0, r0, rtol=1e-5, atol=1e-4)
+        assert torch.allclose(o1, r1, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(shared0, base0 + acc0, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(shared1, base1 + acc1, rtol=1e-5, atol=1e-4)
