@@ -81,6 +81,9 @@ def main() -> None:
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--bucket_mb", type=float, default=64.0)
     ap.add_argument("--grad_dtype", default="fp32")
+    ap.add_argument("--force_comm", action="store_true",
+                    help="1-GPU rehearsal of the multi-GPU step: a 1-rank RCCL group with the bucketed reducer and "
+                         "its collectives on (D3D_GRAPH_COMM=0 / D3D_GRAPH_SEG=0 select the fallback modes)")
     ap.add_argument("--graph", default="auto",
                     help="1: replay the step from captured HIP graphs; auto: when the per-GPU micro-batch is "
                          "<= 32 (there the eager step is host-launch-bound, so any host jitter shows up in the "
@@ -110,6 +113,13 @@ def main() -> None:
 
     ctx = init_distributed("auto", timeout_s=900, use_gpu=False if args.device == "cpu" else None)
     N = ctx.world
+    if args.force_comm and N == 1 and ctx.device.type == "cuda":
+        import datetime
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=ctx.device,
+                                timeout=datetime.timedelta(seconds=300))
     if args.gpus and args.gpus != N and ctx.rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={N}", file=sys.stderr)
     if args.per_gpu_batch:
@@ -134,7 +144,7 @@ def main() -> None:
                              "global_batch": global_batch, "micro_batch": mb, "data.synthetic": True,
                              "backend": args.backend, "dtype": args.dtype, "log_every": 0, "ckpt_every": 0,
                              "dist.bucket_mb": args.bucket_mb, "dist.grad_dtype": args.grad_dtype,
-                             "graph": graph})
+                             "dist.force_comm": bool(args.force_comm), "graph": graph})
     trainer = Trainer(cfg, ctx)
     data = SyntheticBatches(local, args.imgsize, ctx.device, seed=1234 + ctx.rank)
     pool = [next(data) for _ in range(4)]
@@ -246,6 +256,7 @@ def comm_diagnostics(trainer, pool, ctx) -> dict:
             info["step"] = "graph"
             info["comm_mode"] = g.comm_mode
             info["probe_ok"] = g.comm_mode == "graph"
+            info["segments"] = len(g.segs) if g.segs else None
             ms = g.measure_comm(3)
         else:
             info["step"] = "eager"

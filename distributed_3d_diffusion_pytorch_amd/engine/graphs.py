@@ -24,16 +24,29 @@ Layout of one step (MI355X, one process per GPU):
       payload (dist.grad_dtype) narrows each bucket into a persistent bf16
       mirror on the collective's stream and widens it back inside the graph.
       ``dist.force_comm`` runs this topology on a 1-rank RCCL group (tests).
-  [world > 1, comm_mode "post"] fallback when a probe capture of an RCCL
-      collective fails (or D3D_GRAPH_COMM=0, or gloo): eager all-reduce of the
-      flat gradient after graph A in 4 async chunks, each chunk's Adam
-      launched as soon as its collective lands; bf16 payload by default
-      (dist.post_grad_dtype: the reduction is exposed here, so half the bytes
-      is half the exposed time).  (Overlapping it with the replay's backward
-      would need a signal out of the running graph: external event-record
-      nodes are refused by this stack -- torch's Event(external=True) on ROCm
-      and hipEventRecordWithFlags(hipEventRecordExternal) inside a capture,
-      hipErrorInvalidValue on the box, which also invalidates the capture.)
+  [world > 1, comm_mode "seg"] fallback when a probe capture of an RCCL
+      collective fails (or D3D_GRAPH_COMM=0): graph A is captured as a CHAIN
+      of segment graphs cut at bucket boundaries.  The same gradient hooks /
+      sink notifications that issue the collectives in the eager step mark
+      the cut points: once >= D3D_GRAPH_SEG MiB of buckets are complete the
+      capture stream joins every stream (the weight-gradient stream, the
+      conditioning stream), ends its graph and begins the next one in the
+      same memory pool, re-forking the conditioning stream into it.  A step
+      replays segment k, then issues the eager all-reduces of the buckets
+      completed in it on RCCL's stream, then replays segment k + 1: bucket k's
+      reduction overlaps the backward of the layers below it, as in the
+      captured mode, without any collective inside a graph; only the buckets
+      of the last segment are exposed.  The deferred update is kept.
+  [world > 1, comm_mode "post"] last resort (the segmented capture failed, or
+      D3D_GRAPH_SEG=0, or gloo): eager all-reduce of the flat gradient after
+      graph A in 4 async chunks, each chunk's Adam launched as soon as its
+      collective lands; bf16 payload by default (dist.post_grad_dtype: the
+      reduction is exposed here, so half the bytes is half the exposed time).
+      (Overlap by a signal out of ONE running graph was tried: external
+      event-record nodes are refused by this stack -- torch's
+      Event(external=True) on ROCm and hipEventRecordWithFlags(
+      hipEventRecordExternal) inside a capture, hipErrorInvalidValue on the
+      box, which also invalidates the capture.)
   graph B: fused Adam reading its per-step hyper-parameters from a device
       block (lr warmup / bias correction change every step; the 1/world
       gradient average is folded in) -> batched weight repack -> gradient /
@@ -122,6 +135,13 @@ _DEFER_UPDATE = os.environ.get("D3D_DEFER_UPDATE", "1") != "0"
 _NOOP_HP = [1.0, 1.0, 1.0, 0.0, 0.0, 1.0, 0.0, 0.0]
 
 
+def _seg_mb() -> float:
+    """comm_mode "seg": cut the capture once this many MiB of gradient buckets
+    are complete (D3D_GRAPH_SEG; 0: no segmented mode, the post-graph
+    reduction is the fallback).  Read per GraphedTrainStep."""
+    return float(os.environ.get("D3D_GRAPH_SEG", "64"))
+
+
 class GraphCaptureError(RuntimeError):
     """The training step could not be captured (on this rank or any other):
     the trainer falls back to the eager step on every rank."""
@@ -155,7 +175,14 @@ class GraphedTrainStep:
             # fp32 and bf16 payloads alike (the bf16 mirror is persistent, see
             # parallel/ddp.py): the collectives are captured inside graph A
             want = os.environ.get("D3D_GRAPH_COMM", "1") != "0"
-            self.comm_mode = "graph" if (want and probe_graph_collective(dev)) else "post"
+            if want and probe_graph_collective(dev):
+                self.comm_mode = "graph"
+            elif _seg_mb() > 0 and dist.get_backend() == "nccl":
+                self.comm_mode = "seg"
+            else:
+                self.comm_mode = "post"
+        self.segs: Optional[list] = None        # comm_mode "seg": segment graphs of the last micro-batch
+        self.seg_bk: Optional[list] = None      # ... and the buckets completed in each
         # post mode: a persistent narrow mirror of the flat gradient (bf16 payload)
         self.post_mirror = None
         if self.comm_mode == "post" and trainer.cfg.dist.post_grad_dtype == "bf16":
@@ -233,14 +260,34 @@ class GraphedTrainStep:
 
     def capture(self, nchunks: int = 1) -> None:
         """Capture the graphs; on failure (here or on any rank) raise
-        GraphCaptureError on every rank, so all ranks take the same path."""
+        GraphCaptureError on every rank, so all ranks take the same path.  A
+        failed SEGMENTED capture is retried once in comm_mode "post"."""
+        err = self._capture_agreed(nchunks)
+        if err is not None and self.comm_mode == "seg":
+            if self.tr.ctx.is_main:
+                print(f"[graphs] segmented capture failed ({type(err).__name__}: {err}); "
+                      "all-reduce runs after the graph", flush=True)
+            self.comm_mode = "post"
+            if self.tr.cfg.dist.post_grad_dtype == "bf16":
+                self.post_mirror = torch.empty(self.tr.flat.grad.numel(), dtype=torch.bfloat16,
+                                               device=self.tr.device)
+            self.defer = False
+            self.tr.flat.zero_grad()
+            self.loss_acc.zero_()
+            err = self._capture_agreed(nchunks)
+        if err is not None:
+            tr = self.tr
+            tr.flat.zero_grad()
+            self.loss_acc.zero_()
+            raise GraphCaptureError(f"{type(err).__name__}: {err}") from err
+
+    def _capture_agreed(self, nchunks: int):
         err = None
         try:
             self._capture(nchunks)
         except Exception as e:            # noqa: BLE001
             err = e
-            self.gA = self.gA0 = self.gB = None
-            self.H.set_device_seed(None)
+            self._drop()
             torch.cuda.synchronize()
         tr = self.tr
         if tr.ctx.world > 1 and dist.is_initialized():
@@ -248,11 +295,16 @@ class GraphedTrainStep:
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if flag.item() < 0.5 and err is None:
                 err = RuntimeError("graph capture failed on another rank")
-                self.gA = self.gA0 = self.gB = None
-        if err is not None:
-            tr.flat.zero_grad()
-            self.loss_acc.zero_()
-            raise GraphCaptureError(f"{type(err).__name__}: {err}") from err
+                self._drop()
+        return err
+
+    def _drop(self) -> None:
+        self.gA = self.gA0 = self.gB = None
+        self.segs = self.seg_bk = None
+        self.H.set_device_seed(None)
+        red = self.tr.reducer
+        if red is not None:
+            red.seg_cut = None
 
     def _capture(self, nchunks: int = 1) -> None:
         tr = self.tr
@@ -260,6 +312,7 @@ class GraphedTrainStep:
         tr.model.set_dropout_seed(0)             # baked; the per-step part is self.seed
         self.H.set_device_seed(self.seed)
         comm = self.comm_mode == "graph"
+        seg = self.comm_mode == "seg"
         self.img.normal_()
         self.R.copy_(torch.eye(3, device=self.R.device).expand_as(self.R))
         self.K.copy_(torch.eye(3, device=self.K.device).expand_as(self.K))
@@ -271,7 +324,7 @@ class GraphedTrainStep:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                self._body(comm)
+                self._body(comm or seg)
         torch.cuda.current_stream().wait_stream(s)
         self.H.refresh_weights()                 # descriptor table final before capture
         # RCCL's watchdog thread keeps polling the events of the warm-up's eager
@@ -288,19 +341,26 @@ class GraphedTrainStep:
         if self.defer:
             self.H.prepare_update_parts(tr.flat, self.parts)
         torch.cuda.synchronize()
-        mode = "thread_local" if comm else "global"     # RCCL's watchdog thread keeps querying events
+        # RCCL's watchdog thread keeps querying events: thread_local with
+        # collectives in play.  The segmented capture is cut (one capture
+        # ended, the next begun) from autograd's worker thread, which a
+        # thread_local capture refuses (hipErrorStreamCaptureWrongThread): relaxed.
+        mode = "relaxed" if seg else ("thread_local" if comm else "global")
         # graphs sharing a memory pool are captured in their replay order
         # (leading micro-batches first)
         with _gc_paused():
-            if comm and nchunks > 1:
+            if (comm or seg) and nchunks > 1:
                 self.gA0 = torch.cuda.CUDAGraph()
                 self.gA0.register_generator_state(tr.gen)
                 with torch.cuda.graph(self.gA0, pool=self.pool, capture_error_mode=mode):
                     self._body(False)
-            self.gA = torch.cuda.CUDAGraph()
-            self.gA.register_generator_state(tr.gen)
-            with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
-                self._body(comm, defer=self.defer)
+            if seg:
+                self._capture_segments(mode)
+            else:
+                self.gA = torch.cuda.CUDAGraph()
+                self.gA.register_generator_state(tr.gen)
+                with torch.cuda.graph(self.gA, pool=self.pool, capture_error_mode=mode):
+                    self._body(comm, defer=self.defer)
             self.gB = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.gB, pool=self.pool, capture_error_mode=mode):
                 self._update()
@@ -312,6 +372,87 @@ class GraphedTrainStep:
         # warm-up / capture left partial gradients behind
         tr.flat.zero_grad()
         self.loss_acc.zero_()
+
+    # ------------------------------------------------------------ "seg" mode
+    def _capture_segments(self, mode: str) -> None:
+        """Graph A of the last micro-batch as a chain of segment graphs, cut
+        where the gradient buckets complete (see the module doc)."""
+        tr = self.tr
+        red = tr.reducer
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+        self._cs, self._mode = cs, mode
+        self._seg_bytes = _seg_mb() * 2 ** 20
+        self._seg_acc = 0
+        g = torch.cuda.CUDAGraph()
+        g.register_generator_state(tr.gen)
+        self.segs, self.seg_bk = [g], [[]]
+        with torch.cuda.stream(cs):
+            g.capture_begin(pool=self.pool, capture_error_mode=mode)
+            red.seg_cut = self._cut
+            try:
+                self._body(True, defer=self.defer)
+            except BaseException:
+                try:
+                    self.segs[-1].capture_end()
+                except Exception:        # noqa: BLE001 -- the original error is the one to report
+                    pass
+                raise
+            finally:
+                red.seg_cut = None
+            self.segs[-1].capture_end()
+        torch.cuda.current_stream().wait_stream(cs)
+        self.gA = self.segs[-1]
+
+    def _cut(self, b: int, cut: bool) -> None:
+        """Bucket b is complete (called from backward, on whichever thread
+        runs it): record it in the current segment; cut the capture once the
+        segment holds >= D3D_GRAPH_SEG MiB of buckets."""
+        self.seg_bk[-1].append(b)
+        if not cut:
+            return
+        bk = self.tr.reducer.buckets[b]
+        self._seg_acc += (bk["end"] - bk["start"]) * 4
+        if self._seg_acc < self._seg_bytes:
+            return
+        self._seg_acc = 0
+        sink = self.tr.sink
+        with torch.cuda.stream(self._cs):
+            # every stream of the capture rejoins the capture stream (legal
+            # end), the next segment begins in the same pool, and the
+            # conditioning stream is forked into it again
+            sink.join()
+            self.segs[-1].capture_end()
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=self.pool, capture_error_mode=self._mode)
+            self.segs.append(g)
+            self.seg_bk.append([])
+            sink.refork(self._cs)
+
+    def _seg_issue(self, b: int, works: list) -> None:
+        """Eager all-reduce of bucket b on RCCL's stream (behind everything
+        replayed so far on the current stream), the reducer's payload."""
+        red = self.tr.reducer
+        bk = red.buckets[b]
+        view = self.tr.flat.grad[bk["start"]: bk["end"]]
+        if red.mirror is None:
+            works.append((dist.all_reduce(view, group=red.group, async_op=True), None, None))
+        else:
+            tmp = red.mirror[bk["start"]: bk["end"]]
+            tmp.copy_(view)
+            works.append((dist.all_reduce(tmp, group=red.group, async_op=True), tmp, view))
+
+    def _replay_segments(self, comm: bool = True) -> None:
+        works: list = []
+        for g, bks in zip(self.segs, self.seg_bk):
+            g.replay()
+            if comm:
+                for b in bks:
+                    self._seg_issue(b, works)
+        for w, tmp, view in works:
+            w.wait()                      # the current stream waits on RCCL's
+            if tmp is not None:
+                view.copy_(tmp)
 
     # ------------------------------------------------------------------
     def _reduce_update_chunked(self) -> None:
@@ -365,7 +506,10 @@ class GraphedTrainStep:
             self.T.copy_(T[s:s + mb])
             self.K.copy_(K[s:s + mb])
             last = ci == nchunks - 1
-            (self.gA if (last or self.gA0 is None) else self.gA0).replay()
+            if last and self.segs is not None:
+                self._replay_segments()
+            else:
+                (self.gA if (last or self.gA0 is None) else self.gA0).replay()
         loss = self.loss_acc.clone()
         world = tr.ctx.world
         o = tr.optim
@@ -424,6 +568,14 @@ class GraphedTrainStep:
         if self.comm_mode == "post":
             with_comm = dev_ms(lambda: (self.gA.replay(), self._reduce_update_chunked()))
             without = dev_ms(lambda: (self.gA.replay(), self._update()))
+            return max(0.0, with_comm - without)
+        if self.comm_mode == "seg":
+            # the segment chain with its eager bucket all-reduces against the
+            # same chain replayed without them
+            with_comm = dev_ms(self._replay_segments)
+            without = dev_ms(lambda: self._replay_segments(comm=False))
+            with_comm = min(with_comm, dev_ms(self._replay_segments))
+            tr.flat.zero_grad()
             return max(0.0, with_comm - without)
         g0 = torch.cuda.CUDAGraph()
         g0.register_generator_state(tr.gen)

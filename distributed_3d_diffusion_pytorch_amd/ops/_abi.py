@@ -92,6 +92,7 @@ SIGNATURES = {
     "d3d_mlp_mm": [P, P, I, I, I, I, I, I, P, P, P, P, P],
     "d3d_mlp_wgrad": [P, P, I, I, I, I, P, P, I, P],
     "d3d_gemm": [P, P, P, P, I, P, I, I, I, I, I, I, I, F, F, P, I, I, I, P],
+    "d3d_gemm_cat": [P, P, P, I, P, P, I, I, I, I, I, F, F, P],
     # small_gemm.hip
     "d3d_sgemm_strided": [P, P, P, I, I, I, I, L, L, L, L, L, L, L, L, L, F, F, P],
     # wgrad_gemm.hip

@@ -69,7 +69,10 @@ struct GCfg {
   static constexpr int NS = WI * WJ / 2;                 // epilogue stores per wave
 };
 
-enum : int { F_B32 = 1, F_B16 = 2, F_RES = 4, F_GN = 8, F_DSILU = 16 };
+// F_CAT: B is the virtual channel concat [B | B2] of two [N][ldb] tensors
+// split at K1 = ldb = K / 2 (the decoder's NIN skip over [h | skip]): one
+// GEMM over both halves instead of a GEMM plus a residual-accumulating one
+enum : int { F_B32 = 1, F_B16 = 2, F_RES = 4, F_GN = 8, F_DSILU = 16, F_CAT = 32 };
 
 // Epilogue parameters of one tile (32-bit offsets from the tile's row base).
 struct GEpi {
@@ -83,6 +86,23 @@ struct GEpi {
 };
 }  // namespace
 
+// Residual / pre-activation rows of fragment pair (ii, 2jp), (ii, 2jp + 1):
+// 8-byte reads through a range-checked descriptor (rows past the tile end and
+// channels past M read as zero without a branch).  Issued a whole fragment
+// row ahead of their use (g_epi_rows): each read-then-use pair waited for
+// every older vector-memory op -- the next tile's stage DMAs and the previous
+// pair's store -- once per pair, 32 serial round trips per 256 x 256 tile.
+typedef unsigned g_u2l __attribute__((ext_vector_type(2)));
+template <int WI, int WJ, int II, int JP>
+__device__ __forceinline__ void g_epi_rload(const GEpi& e, g_u2l& rx, g_u2l& ry) {
+  const int fr = e.lane & 15, fq = e.lane >> 4;
+  const int cl = e.m0 + e.wm * 16 * WI + II * 16 + fq * 4;
+  const int px = e.wn * 16 * WJ + 2 * JP * 16 + fr;
+  const bool cok = cl < e.M;
+  rx = g_load8(e.R, e.rrec, cok ? (px * e.ldr + cl) * 2 : (int)0x80000000);
+  ry = g_load8(e.R, e.rrec, cok ? ((px + 16) * e.ldr + cl) * 2 : (int)0x80000000);
+}
+
 // Fragment pair (ii, 2jp), (ii, 2jp + 1) -> one 16-byte store per lane.  Before
 // the swap lane (fq, fr) holds channels fq*4..+3 of pixels P(2jp, fr) /
 // P(2jp+1, fr); v_permlane16_swap (odd rows of X <-> even rows of Y) leaves it
@@ -90,7 +110,8 @@ struct GEpi {
 // cb: this lane's 4 bias values (already times scale).
 template <int F, int WI, int WJ, int II, int JP>
 __device__ __forceinline__ void g_epi_pair(const f32x4 (&acc)[WI][WJ], const GEpi& e, const f32x4& cb,
-                                           float (&gs)[WI][2], float (&gq)[WI][2]) {
+                                           float (&gs)[WI][2], float (&gq)[WI][2], const g_u2l& rx2,
+                                           const g_u2l& ry2) {
 #pragma clang fp contract(off)      // explicit fmas: every instantiation rounds alike
   const int fr = e.lane & 15, fq = e.lane >> 4;
   // accumulators leave the AGPRs here, one pair at a time (plain reads were
@@ -104,14 +125,9 @@ __device__ __forceinline__ void g_epi_pair(const f32x4 (&acc)[WI][WJ], const GEp
   const int cl = e.m0 + e.wm * 16 * WI + II * 16 + fq * 4;        // channel (pre-swap)
   const int px = e.wn * 16 * WJ + 2 * JP * 16 + fr;               // tile-local pixel (pre-swap)
   float vx[4], vy[4];
+  (void)cl;
+  (void)px;
   if constexpr ((F & F_RES) || (F & F_DSILU)) {
-    // 8-byte reads through a range-checked descriptor: rows past the tile end and
-    // channels past M read as zero without a branch
-    typedef unsigned u2l __attribute__((ext_vector_type(2)));
-    const bool cok = cl < e.M;
-    const int ox = cok ? (px * e.ldr + cl) * 2 : (int)0x80000000;
-    const int oy = cok ? ((px + 16) * e.ldr + cl) * 2 : (int)0x80000000;
-    const u2l rx2 = g_load8(e.R, e.rrec, ox), ry2 = g_load8(e.R, e.rrec, oy);
     const bf16x4 rx = __builtin_bit_cast(bf16x4, rx2), ry = __builtin_bit_cast(bf16x4, ry2);
     if constexpr (F & F_DSILU) {
 #pragma unroll
@@ -166,7 +182,8 @@ template <int WI, int WJ, int F, int NST = 2>
 __global__ void __launch_bounds__(256, 1)
 gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ O, const float* __restrict__ bias,
           const bf16* __restrict__ R, int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha,
-          float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw) {
+          float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw,
+          const bf16* __restrict__ B2, int K1) {
   constexpr bool BIAS = (F & (F_B32 | F_B16)) != 0, BBF = (F & F_B16) != 0;
   using C = GCfg<WI, WJ, NST>;
   // 4 bias slots: the loader may run at most 3 tiles ahead -- NST 4 needs K >= 128 (host)
@@ -225,7 +242,8 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   struct Ops {                               // one tile's operand panels: descriptor bases / sizes
     const bf16* a;
     const bf16* b;
-    int ra, rb;
+    const bf16* b2;                          // F_CAT: second half, based K1 elements early (K offsets run on)
+    int ra, rb, rb2;
     long m0;
   };
   Ops lo, no;
@@ -240,6 +258,16 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
     o.b = B + n0 * ldb;
     o.ra = v ? (int)((arows - 1) * lda + K) * 2 : 0;
     o.rb = v ? (int)((brows - 1) * ldb + K) * 2 : 0;
+    if constexpr ((F & F_CAT) != 0) {
+      // each half ends exactly at its last valid row: rows past N read zeros
+      // (ldb = K1 < K, so the plain range would reach into the next rows)
+      o.b2 = B2 + n0 * ldb - K1;
+      o.rb = v ? (int)(brows * ldb) * 2 : 0;
+      o.rb2 = v ? (int)(brows * ldb + K1) * 2 : 0;
+    } else {
+      o.b2 = nullptr;
+      o.rb2 = 0;
+    }
     o.m0 = v ? m0 : -1;
     return o;
   };
@@ -268,7 +296,12 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
     if (d < C::DA)
       g_dma(lo.a, lo.ra, smem + st * C::STAGE + (wave * (C::BM / 4) + d * 8) * G_PK,
             d ? piece_off(aoff, d * astep) : aoff, lkb);
-    else
+    else if constexpr ((F & F_CAT) != 0) {
+      const bool hi = lkb >= 2 * K1;         // K-stages never straddle the split (K1 % 64 == 0)
+      g_dma(hi ? lo.b2 : lo.b, hi ? lo.rb2 : lo.rb,
+            smem + st * C::STAGE + (C::BM + wave * (C::BN / 4) + (d - C::DA) * 8) * G_PK,
+            d > C::DA ? piece_off(boff, (d - C::DA) * bstep) : boff, lkb);
+    } else
       g_dma(lo.b, lo.rb, smem + st * C::STAGE + (C::BM + wave * (C::BN / 4) + (d - C::DA) * 8) * G_PK,
             d > C::DA ? piece_off(boff, (d - C::DA) * bstep) : boff, lkb);
   };
@@ -395,8 +428,30 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
 #pragma unroll
       for (int i = 0; i < WI; ++i) gs[i][0] = gq[i][0] = gs[i][1] = gq[i][1] = 0.f;
       const bf16* sb = smem + C::BIAS + (ti & 3) * 512;
+      // residual rows: fragment row ii + 1's reads are issued before row ii's
+      // pairs (two row buffers, compile-time indexed)
+#ifdef D3D_GEMM_EPI_SERIAL
+      constexpr bool RD = false;                 // A/B build: each pair reads its rows right before use
+      constexpr bool RS = (F & (F_RES | F_DSILU)) != 0;
+#else
+      constexpr bool RD = (F & (F_RES | F_DSILU)) != 0;
+      constexpr bool RS = false;
+#endif
+      g_u2l rbuf[2][WJ / 2][2];
+      if constexpr (RD) {
+        g_for(std::make_integer_sequence<int, WJ / 2>{}, [&](auto jc) {
+          g_epi_rload<WI, WJ, 0, decltype(jc)::value>(e, rbuf[0][decltype(jc)::value][0],
+                                                       rbuf[0][decltype(jc)::value][1]);
+        });
+      }
       g_for(std::make_integer_sequence<int, WI>{}, [&](auto ic) {
         constexpr int ii = decltype(ic)::value;
+        if constexpr (RD && ii + 1 < WI) {
+          g_for(std::make_integer_sequence<int, WJ / 2>{}, [&](auto jc) {
+            g_epi_rload<WI, WJ, ii + 1, decltype(jc)::value>(e, rbuf[(ii + 1) & 1][decltype(jc)::value][0],
+                                                              rbuf[(ii + 1) & 1][decltype(jc)::value][1]);
+          });
+        }
         f32x4 cb = {0.f, 0.f, 0.f, 0.f};
         const int cl = wm * 16 * WI + ii * 16 + (ln >> 4) * 4;       // tile-local channel of the lane
         if constexpr (F & F_B32) {
@@ -409,7 +464,9 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
 #pragma unroll
         for (int k = 0; k < 4; ++k) cb[k] *= scale;
         g_for(std::make_integer_sequence<int, WJ / 2>{}, [&](auto jc) {
-          g_epi_pair<F, WI, WJ, ii, decltype(jc)::value>(acc, e, cb, gs, gq);
+          constexpr int jp = decltype(jc)::value;
+          if constexpr (RS) g_epi_rload<WI, WJ, ii, jp>(e, rbuf[ii & 1][jp][0], rbuf[ii & 1][jp][1]);
+          g_epi_pair<F, WI, WJ, ii, jp>(acc, e, cb, gs, gq, rbuf[ii & 1][jp][0], rbuf[ii & 1][jp][1]);
         });
       });
       if constexpr ((F & F_GN) && WJ >= 4) {
@@ -493,10 +550,10 @@ D3D_API int d3d_gemm_nt_ok(int M, int N, int K, int lda, int ldb) {
 template <int W, int F, int NST = 2>
 static void g_launch(int G_, hipStream_t st, const void* A, const void* B, void* O, const void* bias, const void* R,
                      int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha, float scale, int mt, int nt,
-                     int gm, float* gnp, int G, int hw) {
+                     int gm, float* gnp, int G, int hw, const void* B2 = nullptr, int K1 = 0) {
   hipLaunchKernelGGL((gemm_fw_k<W, W, F, NST>), dim3(G_), dim3(256), 0, st, (const bf16*)A, (const bf16*)B,
                      (bf16*)O, (const float*)bias, (const bf16*)R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, mt, nt,
-                     gm, gnp, G, hw);
+                     gm, gnp, G, hw, (const bf16*)B2, K1);
 }
 
 // epi 0: O = (alpha * A.B^T + bias + R) * scale (+ GroupNorm partials gnp:
@@ -560,4 +617,39 @@ D3D_API int d3d_gemm_nt_gn(const void* A, const void* B, void* O, const float* b
 D3D_API int d3d_gemm_nt(const void* A, const void* B, void* O, const float* bias, const void* R, int M, int N, int K,
                         int lda, int ldb, int ldo, int ldr, float alpha, float scale, hipStream_t st) {
   return d3d_gemm(A, B, O, bias, 0, R, M, N, K, lda, ldb, ldo, ldr, alpha, scale, nullptr, 0, 0, 0, st);
+}
+
+// Decoder NIN skip over the virtual concat [B | B2] (two [N][K1] tensors,
+// K = 2 K1): O = (alpha * A.[B|B2]^T + bias) * scale as ONE GEMM (fp32 bias or
+// none).  Returns -1 for shapes it does not take (the caller runs two GEMMs).
+D3D_API int d3d_gemm_cat(const void* A, const void* B, const void* B2, int K1, void* O, const float* bias, int M,
+                         int N, int K, int lda, int ldo, float alpha, float scale, hipStream_t st) {
+  const int ldb = K1;
+  if (M <= 0 || N <= 0 || K1 < 64 || K1 % 64 || K != 2 * K1 || M % 8 || lda % 8 || lda < K) return -1;
+  if (256L * lda * 2 >= (1L << 31) || 256L * ldb * 2 + 4L * K1 >= (1L << 31)) return -1;   // per-tile offsets
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)B2 | (uintptr_t)O) & 15) return -1;
+  if (ldo % 8 || ldo < M || 256L * ldo * 2 >= (1L << 31)) return -1;
+  const int W = g_cfg(M, N, K);
+  const int BT = 32 * W;
+  const int mt = cdiv(M, BT), nt = cdiv(N, BT);
+  const long tiles = (long)mt * nt;
+  if (tiles >= (1L << 31)) return -1;
+  const bool deep = g_deep && W != 8 && tiles <= (long)g_cus() * (W == 4 ? 1 : 2);
+  const int per_cu = W == 8 ? 1 : W == 4 ? 2 : 4;
+  const int G_ = (int)std::min<long>(tiles, g_grid > 0 ? g_grid : (long)g_cus() * per_cu);
+  const int gm = std::max(1, std::min(mt, g_gm));
+#define G_CAT(W_, F_)                                                                                        \
+  if (W == W_ && (bias ? F_B32 | F_CAT : F_CAT) == (F_)) {                                                   \
+    if (W_ != 8 && deep)                                                                                     \
+      g_launch<W_, F_, (W_ != 8 ? 4 : 2)>(G_, st, A, B, O, bias, nullptr, M, N, K, lda, ldb, ldo, ldo, alpha,  \
+                                          scale, mt, nt, gm, nullptr, 0, 0, B2, K1);                         \
+    else                                                                                                     \
+      g_launch<W_, F_>(G_, st, A, B, O, bias, nullptr, M, N, K, lda, ldb, ldo, ldo, alpha, scale, mt, nt, gm,  \
+                       nullptr, 0, 0, B2, K1);                                                                \
+    return (int)hipGetLastError();                                                                           \
+  }
+  G_CAT(8, F_CAT) G_CAT(8, F_B32 | F_CAT) G_CAT(4, F_CAT) G_CAT(4, F_B32 | F_CAT) G_CAT(2, F_CAT)
+  G_CAT(2, F_B32 | F_CAT)
+#undef G_CAT
+  return -1;
 }

@@ -295,6 +295,19 @@ class GradSink:
             idx = torch.cuda.current_device()
             self._wait_compute(torch.cuda.current_stream(idx), idx)
 
+    def refork(self, st) -> None:
+        """Make the registered compute streams wait on ``st``: after a
+        segmented capture was cut (engine/graphs.py comm_mode "seg", the
+        capture stream joined every stream, ended its graph and began the
+        next one), a compute stream that still has backward work to issue
+        must be part of the NEW capture before it launches anything --
+        autograd issues same-stream successors without a cross-stream wait.
+        (The weight-gradient stream needs none: every flush forks it anew.)"""
+        idx = torch.cuda.current_device()
+        for c in self._compute:
+            if c.device.index == idx and c.cuda_stream != st.cuda_stream:
+                c.wait_stream(st)
+
     @contextlib.contextmanager
     def collective(self, main=None):
         """Issue a collective over deposited gradients: from behind the side

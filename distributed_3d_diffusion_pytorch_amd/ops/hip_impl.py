@@ -565,6 +565,11 @@ class _GroupNorm(torch.autograd.Function):
 
 
 
+# decoder NIN skip as ONE GEMM over [h | skip] when both halves have the same
+# width (12 of the 16 decoder blocks); D3D_CAT_GEMM=0: two GEMMs
+_CAT_GEMM = os.environ.get("D3D_CAT_GEMM", "1") != "0"
+
+
 class _CatGNDense(torch.autograd.Function):
     """Decoder ResnetBlock entry on the virtual concat x = [h | skip]
     (`xunet.py:521-531` + `xunet.py:139-150`): returns silu(GN0(x)) and the
@@ -583,7 +588,18 @@ class _CatGNDense(torch.autograd.Function):
         OC = wb.shape[0]
         a2, b2 = a.reshape(-1, C1), b.reshape(-1, C2)
         C = C1 + C2
-        if _gemm_ok(OC, a2.shape[0], C1, C, C1, a2, wb) and _gemm_ok(OC, b2.shape[0], C2, C, C2, b2, wb[:, C1:]):
+        skip = None
+        if C1 == C2 and _CAT_GEMM:
+            # one GEMM over the virtual concat (gemm.hip F_CAT: the B operand
+            # switches tensors at K = C1)
+            skip = torch.empty(a2.shape[0], OC, dtype=BF16, device=a.device)
+            bias = db.detach() if db is not None else None
+            if _lib.d3d_gemm_cat(wb.data_ptr(), a2.data_ptr(), b2.data_ptr(), C1, skip.data_ptr(), _ptr(bias), OC,
+                                 a2.shape[0], C, C, OC, 1.0, 1.0, _st()) < 0:
+                skip = None
+        if skip is not None:
+            pass
+        elif _gemm_ok(OC, a2.shape[0], C1, C, C1, a2, wb) and _gemm_ok(OC, b2.shape[0], C2, C, C2, b2, wb[:, C1:]):
             # two GEMMs over the halves; the second accumulates through its residual epilogue
             skip = torch.empty(a2.shape[0], OC, dtype=BF16, device=a.device)
             gemm_nt(wb, a2, skip, OC, a2.shape[0], C1, C, C1, OC, bias=db.detach() if db is not None else None)

@@ -71,6 +71,11 @@ class GradReducer:
             for i in bk["params"]:
                 self.param_bucket[i] = b
         self.sink = None            # ops.gradsink.GradSink delivering kernel-deposited grads
+        # segmented graph capture (engine/graphs.py comm_mode "seg"): a ready
+        # bucket is handed to seg_cut(b, cut) instead of being reduced here --
+        # the capture is split at that point and the bucket's collective is
+        # issued eagerly between the segment replays
+        self.seg_cut = None
         self._pending = [0] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
         self._works: List = []
@@ -111,6 +116,9 @@ class GradReducer:
         if self._launched[b]:
             return
         self._launched[b] = True
+        if self.seg_cut is not None:
+            self.seg_cut(b, True)
+            return
         bk = self.buckets[b]
         view = self.flat.grad[bk["start"]: bk["end"]]
         ctx = self.sink.collective(self.main_stream) if self.sink is not None else contextlib.nullcontext()
@@ -128,6 +136,14 @@ class GradReducer:
         if self.sink is not None:
             self.sink.join()
         if not self.active or not self.enabled:
+            self.reset()
+            return
+        if self.seg_cut is not None:
+            # the remaining buckets belong to the last segment (no cut after it)
+            for b in range(len(self.buckets)):
+                if not self._launched[b]:
+                    self._launched[b] = True
+                    self.seg_cut(b, False)
             self.reset()
             return
         for b in range(len(self.buckets)):

@@ -1078,6 +1078,42 @@ def test_cat_gn_silu_dense(H, C1, C2, OC, Hh):
         assert rel(x, r) < 3e-2, (n, rel(x, r))
 
 
+@pytest.mark.parametrize("C,OC,N,Hh", [(128, 128, 3, 10), (256, 256, 2, 16), (512, 512, 5, 8), (128, 256, 1, 64),
+                                       (256, 512, 3, 7)])
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_cat_gemm_one_launch(H, C, OC, N, Hh, with_bias):
+    """Decoder NIN skip over [h | skip] with equal halves as ONE GEMM
+    (gemm.hip F_CAT: the B operand switches tensors at K = C) == the fp32
+    dense of the materialised concat and == the two-GEMM form; pixel counts
+    that leave partial 256 / 128 / 64-row tiles (rows past the end read
+    zeros through each half's own descriptor range); the decoder op takes
+    the one-GEMM path for equal halves."""
+    from distributed_3d_diffusion_pytorch_amd.ops import hip_impl as HI
+    torch.manual_seed(5)
+    P = N * Hh * Hh
+    a = torch.randn(P, C, device=DEV).to(BF)
+    b = (torch.randn(P, C, device=DEV) * 2).to(BF)
+    w = (torch.randn(OC, 2 * C, device=DEV) / 20).to(BF)
+    db = torch.randn(OC, device=DEV) * 0.1 if with_bias else None
+    ref = torch.cat([a, b], -1).float() @ w.float().t()
+    if with_bias:
+        ref = ref + db
+    one = torch.full((P, OC), float("nan"), device=DEV, dtype=BF)
+    rc = HI._lib.d3d_gemm_cat(w.data_ptr(), a.data_ptr(), b.data_ptr(), C, one.data_ptr(), HI._ptr(db), OC, P,
+                              2 * C, 2 * C, OC, 1.0, 1.0, HI._st())
+    assert rc == 0, rc
+    two = torch.empty(P, OC, device=DEV, dtype=BF)
+    HI.gemm_nt(w, a, two, OC, P, C, 2 * C, C, OC, bias=db)
+    HI.gemm_nt(w[:, C:], b, two, OC, P, C, 2 * C, C, OC, res=two)
+    torch.cuda.synchronize()
+    assert rel(one.float(), ref) < 1e-2, rel(one.float(), ref)
+    assert rel(two.float(), ref) < 1e-2, rel(two.float(), ref)
+    assert rel(one.float(), two.float()) < 1e-2
+    # unequal halves are refused (the op falls back to two GEMMs)
+    assert HI._lib.d3d_gemm_cat(w.data_ptr(), a.data_ptr(), b.data_ptr(), C // 2, one.data_ptr(), HI._ptr(db), OC,
+                                P, 2 * C, 2 * C, OC, 1.0, 1.0, HI._st()) < 0 or C // 2 < 64
+
+
 @pytest.mark.parametrize("OC,IC,taps", [(128, 128, 9), (256, 384, 9), (1024, 144, 9), (3, 128, 9),
                                         (2048, 1024, 1), (768, 256, 1), (128, 3, 9)])
 def test_batched_weight_refresh_matches_pack(H, OC, IC, taps):
@@ -1417,9 +1453,12 @@ def _graph_comm_1rank_worker(out_dir):
     # (payload, micro-batch): one micro-batch (deferred update) for both
     # payloads, and two micro-batches, where the leading one's graph gA0 is
     # captured next to the comm graph (thread_local, no watchdog wait)
+    # gc "0": no RCCL capture -> the segmented capture (comm_mode "seg"); "p":
+    # no segmented capture either (D3D_GRAPH_SEG=0) -> the post-graph reduction
     for gd, mb, gc in (("fp32", 0, "1"), ("bf16", 0, "1"), ("fp32", 2, "1"), ("fp32", 0, "0"), ("bf16", 0, "0"),
-                       ("fp32", 2, "0")):
-        os.environ["D3D_GRAPH_COMM"] = gc        # "0": no RCCL capture -> external-event comm mode
+                       ("fp32", 2, "0"), ("fp32", 0, "p"), ("bf16", 0, "p")):
+        os.environ["D3D_GRAPH_COMM"] = "1" if gc == "1" else "0"
+        os.environ["D3D_GRAPH_SEG"] = "0" if gc == "p" else "64"
         res = []
         for graph in (False, True):
             cfg = make_config(None, {"model.H": 32, "model.W": 32, "data.imgsize": 32, "global_batch": 4,
@@ -1431,6 +1470,8 @@ def _graph_comm_1rank_worker(out_dir):
             losses = [float(tr.train_step(*b)) for b in batches]
             g = tr._graphed
             mode = f"{g.comm_mode}/{int(g.defer)}/{int(g.gA0 is not None)}" if g is not None else "eager"
+            if g is not None and g.segs is not None:
+                mode += f"/{len(g.segs)}/{sum(len(b) for b in g.seg_bk)}/{len(tr.reducer.buckets)}"
             tr.sync()
             res.append((losses, tr.flat.data.clone(), mode))
             exposed = g.measure_comm(2) if g is not None else 0.0      # (changes the training state)
@@ -1439,6 +1480,7 @@ def _graph_comm_1rank_worker(out_dir):
         lines.append(f"{gd}/{mb}/{gc} {(pe - pg).abs().max().item()} {max(abs(a - b) for a, b in zip(le, lg))} "
                      f"{mode} {exposed}")
     os.environ.pop("D3D_GRAPH_COMM", None)
+    os.environ.pop("D3D_GRAPH_SEG", None)
     with open(os.path.join(out_dir, "gc1.txt"), "w") as f:
         f.write("\n".join(lines))
     cleanup()
@@ -1449,22 +1491,33 @@ def test_graph_step_captured_collectives_one_rank(tmp_path):
     group), deferred update on, fp32 and bf16 payloads, and a two-micro-batch
     step (leading graph gA0 captured too): comm_mode "graph", parameters equal
     to the eager bucketed step within 5e-4.  No sleep before any capture.
-    The same three with D3D_GRAPH_COMM=0: comm_mode "post" (chunked bf16
-    reduction after the replay, each chunk's Adam behind its collective), the
-    same parameters; measure_comm works in both modes."""
+    The same three with D3D_GRAPH_COMM=0: comm_mode "seg" (graph A captured
+    as a chain of segments cut every 64 MiB of complete buckets, each
+    segment's buckets all-reduced eagerly between the replays, deferred update
+    kept): more than one segment, every bucket issued exactly once, the same
+    parameters.  With D3D_GRAPH_SEG=0 as well: comm_mode "post" (chunked bf16
+    reduction after the replay, each chunk's Adam behind its collective).
+    measure_comm works in every mode."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from distributed_3d_diffusion_pytorch_amd.parallel import spawn
     import test_ops_gpu as me
     spawn(me._graph_comm_1rank_worker, 1, (str(tmp_path),))
     rows = open(tmp_path / "gc1.txt").read().split("\n")
-    assert [r.split()[0] for r in rows] == ["fp32/0/1", "bf16/0/1", "fp32/2/1", "fp32/0/0", "bf16/0/0", "fp32/2/0"]
+    assert [r.split()[0] for r in rows] == ["fp32/0/1", "bf16/0/1", "fp32/2/1", "fp32/0/0", "bf16/0/0", "fp32/2/0",
+                                            "fp32/0/p", "bf16/0/p"]
     for r in rows:
         gd, d, dl, mode, exp = r.split()
         if gd.endswith("/1"):
             assert mode == ("graph/0/1" if gd == "fp32/2/1" else "graph/1/0"), r
+        elif gd.endswith("/0"):
+            # no RCCL capture: segmented capture, deferred update with one micro-batch
+            m = mode.split("/")
+            assert m[:3] == (["seg", "0", "1"] if gd == "fp32/2/0" else ["seg", "1", "0"]), r
+            assert int(m[3]) > 1 and m[4] == m[5], r       # several segments; every bucket once
+            assert float(exp) >= 0.0, r
         else:
-            # no RCCL capture: the chunked post-graph reduction (bf16 payload), no deferred update
+            # no segmented capture either: the chunked post-graph reduction (bf16 payload), no deferred update
             assert mode == "post/0/0" and float(exp) >= 0.0, r
         assert float(d) < 5e-4 and float(dl) < 2e-3, r
 

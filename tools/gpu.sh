@@ -21,6 +21,8 @@
 #   envprof:<VAR=val>:<bs>     the same trace with an environment knob set
 #   pmc:<bs>                   step-level hardware counters (three --pmc passes) -> table_bs<bs>.txt
 #   kbench:<tool.py>[:args]    a tools/ kernel micro-benchmark (args: comma-separated)
+#   fc:<bs>:<graph|seg|post>[:<MiB>]  1-rank RCCL rehearsal of the multi-GPU step (bench --force_comm) in one comm
+#                              mode (seg: segment size) -> fc_<mode><MiB>_b<bs>.json with its comm record
 set -o pipefail
 OUT=${1:?usage: gpu.sh <out> <step>...}; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -113,6 +115,16 @@ for step in "$@"; do
           bench "env_base_b${bs}_$r" --global_batch "$bs" --steps "$st" --warmup 4
         done
       done ;;
+    fc)                          # fc:<bs>:<graph|seg|post>: 1-rank RCCL rehearsal of the multi-GPU step (bench --force_comm)
+      case $b in
+        graph) gcm=1; gsg=64 ;;
+        seg) gcm=0; gsg=${c:-64} ;;
+        post) gcm=0; gsg=0 ;;
+        *) die "fc mode $b" 2 ;;
+      esac
+      D3D_GRAPH_COMM=$gcm D3D_GRAPH_SEG=$gsg bench "fc_${b}${c}_b$a" --force_comm --global_batch "$a" \
+        --steps "$(steps_for "$a")" --warmup 4
+      python3 -c "import json;d=json.loads(open('$O/fc_${b}${c}_b$a.json').read().strip().splitlines()[-1]);print(d.get('comm'))" ;;
     prof) prof "$a" ;;
     envprof)                     # envprof:<VAR=val>:<bs>: a trace with the knob set (files get a _<VAR> suffix)
       var=${a%%=*}
