@@ -88,20 +88,32 @@ __global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, 
   const float sl2 = scale * LOG2E;
   const int qq = (lane & 15) >> 2, pc = lane & 3;
 
-  for (int kb = 0; kb < L; kb += 64) {
-    // cooperative K/V block load
-    constexpr int CH = D / 8;  // chunks per row
+  // cooperative K/V block loads, one block ahead: block kb + 64 is in flight
+  // in registers while block kb computes (was one HBM round trip per block)
+  constexpr int CH = D / 8;                  // chunks per row
+  constexpr int NKV = 64 * CH / 256;         // chunks per thread of each of K / V
+  bf16x8 kr[NKV], vr[NKV];
+  auto fetch = [&](int kb) {
 #pragma unroll
-    for (int i = 0; i < 64 * CH / 256; ++i) {
+    for (int i = 0; i < NKV; ++i) {
       int idx = tid + i * 256;
       int r = idx / CH, c = idx % CH;
       const bool kok = kb + r < L;
       const bf16* src = qkv + ((long)nkv * L + (kok ? kb + r : 0)) * C3 + h * D + c * 8;
-      bf16x8 kv = kok ? *reinterpret_cast<const bf16x8*>(src + C) : bf16x8{};
-      bf16x8 vv = kok ? *reinterpret_cast<const bf16x8*>(src + 2 * C) : bf16x8{};
-      *reinterpret_cast<bf16x8*>(Ks + swz<D>(r, c)) = kv;
-      *reinterpret_cast<bf16x8*>(Vs + r * VS + c * 8) = vv;
+      kr[i] = kok ? *reinterpret_cast<const bf16x8*>(src + C) : bf16x8{};
+      vr[i] = kok ? *reinterpret_cast<const bf16x8*>(src + 2 * C) : bf16x8{};
     }
+  };
+  fetch(0);
+  for (int kb = 0; kb < L; kb += 64) {
+#pragma unroll
+    for (int i = 0; i < NKV; ++i) {
+      int idx = tid + i * 256;
+      int r = idx / CH, c = idx % CH;
+      *reinterpret_cast<bf16x8*>(Ks + swz<D>(r, c)) = kr[i];
+      *reinterpret_cast<bf16x8*>(Vs + r * VS + c * 8) = vr[i];
+    }
+    if (kb + 64 < L) fetch(kb + 64);
     __syncthreads();
     f32x4 s[4];
 #pragma unroll
@@ -216,43 +228,70 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
   const float* lse_nh = lse + ((long)n * heads + h) * L;
   const bool direct_dq = L <= 64;                 // one key block: dQ is complete here
 
+  // the query tile (Q, dO rows) and the D-term operands (O, dO row parts) of
+  // tile q0 + 32 are loaded into registers while tile q0 computes: the loop
+  // was one HBM round trip per 32-query step with nothing to overlap it
+  // (7 % MFMA in the bs128 step counters)
+  constexpr int NQ = (32 * CH + 255) / 256;       // 16-byte chunks per thread of each of Q / dO
+  constexpr int PER = D / 8;                      // D-term elements per lane (8 or 16)
+  bf16x8 qr[NQ], dr[NQ], orr[PER / 8], drr[PER / 8];
+  float lse_r = 0.f;
+  bool lse_ok = false;
+  auto fetch = [&](int qb) {
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      int idx = tid + i * 256;
+      int r = idx / CH, c = idx % CH;
+      const bool ok = idx < 32 * CH && qb + r < L;
+      long row = (long)n * L + (ok ? qb + r : 0);
+      qr[i] = ok ? *reinterpret_cast<const bf16x8*>(qkv + row * C3 + h * D + c * 8) : bf16x8{};
+      dr[i] = ok ? *reinterpret_cast<const bf16x8*>(dout + row * C + h * D + c * 8) : bf16x8{};
+    }
+    {
+      const int r = tid >> 3, part = tid & 7;
+      const bool ok = qb + r < L;
+      const long row = (long)n * L + (ok ? qb + r : 0);
+#pragma unroll
+      for (int k = 0; k < PER / 8; ++k) {
+        orr[k] = ok ? *reinterpret_cast<const bf16x8*>(out + row * C + h * D + part * PER + 8 * k) : bf16x8{};
+        drr[k] = ok ? *reinterpret_cast<const bf16x8*>(dout + row * C + h * D + part * PER + 8 * k) : bf16x8{};
+      }
+    }
+    // unconditional load, used next step (a use inside a lane branch made
+    // the compiler wait for every prefetch above at the branch's end)
+    const int li = qb + (tid & 31);
+    lse_ok = tid < 32 && li < L;
+    lse_r = lse_nh[li < L ? li : 0];
+  };
+  fetch(0);
+
   for (int q0 = 0; q0 < L; q0 += 32) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < (32 * CH + 255) / 256; ++i) {
+    for (int i = 0; i < NQ; ++i) {
       int idx = tid + i * 256;
       if (idx < 32 * CH) {
         int r = idx / CH, c = idx % CH;
-        const bool ok = q0 + r < L;
-        long row = (long)n * L + (ok ? q0 + r : 0);
-        *reinterpret_cast<bf16x8*>(Qs + r * TS + c * 8) =
-            ok ? *reinterpret_cast<const bf16x8*>(qkv + row * C3 + h * D + c * 8) : bf16x8{};
-        *reinterpret_cast<bf16x8*>(dOs + r * TS + c * 8) =
-            ok ? *reinterpret_cast<const bf16x8*>(dout + row * C + h * D + c * 8) : bf16x8{};
+        *reinterpret_cast<bf16x8*>(Qs + r * TS + c * 8) = qr[i];
+        *reinterpret_cast<bf16x8*>(dOs + r * TS + c * 8) = dr[i];
       }
     }
     // query rows past L: lse = +inf makes their probabilities exactly 0
-    if (tid < 32) lse_s[tid] = q0 + tid < L ? lse_nh[q0 + tid] * LOG2E : INFINITY;
+    if (tid < 32) lse_s[tid] = lse_ok ? lse_r * LOG2E : INFINITY;
     {
       // D[q] = sum_d dO[q, d] O[q, d]: 8 adjacent lanes per query row
-      constexpr int PER = D / 8;                  // elements per lane (8 or 16)
       const int r = tid >> 3, part = tid & 7;
-      const bool ok = q0 + r < L;
-      const long row = (long)n * L + (ok ? q0 + r : 0);
-      const bf16* o = out + row * C + h * D + part * PER;
-      const bf16* d = dout + row * C + h * D + part * PER;
       float acc = 0.f;
 #pragma unroll
-      for (int k = 0; k < PER && ok; k += 8) {
-        const f32x8 a = ld8(o + k), b = ld8(d + k);
+      for (int k = 0; k < PER / 8; ++k)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc += a[j] * b[j];
-      }
+        for (int j = 0; j < 8; ++j) acc += (float)orr[k][j] * (float)drr[k][j];
       acc += __shfl_xor(acc, 1, 64);
       acc += __shfl_xor(acc, 2, 64);
       acc += __shfl_xor(acc, 4, 64);
       if (part == 0) D_s[r] = acc;
     }
+    if (q0 + 32 < L) fetch(q0 + 32);              // in flight during this tile's compute
     __syncthreads();
     f32x4 p[2], ds[2];
 #pragma unroll
