@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
   auto compute = [&](const bf16* s) {
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      bf16x8 af[4], bcur[1], bnext[1];
+      bf16x8 af[4], bq[3];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         gs16x4 lo = gw_tr_asm(s + la[i] + kk * 32 * GH_BM);
@@ -526,20 +526,44 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_k(GwTable tab) {
         gs16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[i] = __builtin_bit_cast(bf16x8, v);
       }
-      bcur[0] = rd_b(s, kk, 0);
-      gw_tr_wait<4, 1>(af, bcur);
+#ifdef D3D_WGRAD_HALO_AHEAD1
+      bq[0] = rd_b(s, kk, 0);
+      gw_tr_wait<4, 1>(af, *reinterpret_cast<bf16x8(*)[1]>(&bq[0]));
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        if (t < 8) bnext[0] = rd_b(s, kk, t + 1);
+        if (t < 8) bq[(t + 1) % 3] = rd_b(s, kk, t + 1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[0], acc[i][t], 0, 0, 0);
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bq[t % 3], acc[i][t], 0, 0, 0);
         if (t < 8) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          asm volatile("" : "+v"(bnext[0]));
-          bcur[0] = bnext[0];
+          asm volatile("" : "+v"(bq[(t + 1) % 3]));
         }
       }
+#else
+      // the window fragments of taps t + 1 AND t + 2 are in flight while tap
+      // t's MFMAs run (three rotating registers; LDS reads complete in order,
+      // so lgkmcnt(2) = everything but the newest fragment's two reads; no
+      // scalar loads are in flight inside this loop)
+      bq[0] = rd_b(s, kk, 0);
+      bq[1] = rd_b(s, kk, 1);
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(af[i]));
+      asm volatile("" : "+v"(bq[0]));
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t + 2 < 9) bq[(t + 2) % 3] = rd_b(s, kk, t + 2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bq[t % 3], acc[i][t], 0, 0, 0);
+        if (t + 1 < 9) {
+          if (t + 2 < 9) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+          else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          asm volatile("" : "+v"(bq[(t + 1) % 3]));
+        }
+      }
+#endif
       if (bias_wave) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
