@@ -139,6 +139,9 @@ class ResnetBlock(nn.Module):
                         self.groupnorm1.gn.num_groups, self.groupnorm1.gn.eps,
                         self.dropout_p, self.training, _next_seed(self), ss_map=ss_map)
         rslot = None
+        if skip is not None:
+            # decoder: conv2 deposits the skip's gradient in the NIN op's slot
+            rslot = skip.__dict__.get("_d3d_out_slot")
         if skip is None:
             if self.in_features != self.features:
                 skip = ops.linear(x, self.dense.weight, self.dense.bias, in_slot=slot)

@@ -568,6 +568,9 @@ class _GroupNorm(torch.autograd.Function):
 # decoder NIN skip as ONE GEMM over [h | skip] when both halves have the same
 # width (12 of the 16 decoder blocks); D3D_CAT_GEMM=0: two GEMMs
 _CAT_GEMM = os.environ.get("D3D_CAT_GEMM", "1") != "0"
+# conv2 hands the skip's gradient to the NIN op through a slot with its 1/sqrt2
+# (no scaled copy of dy per decoder block); D3D_SKIP_SLOT=0: returned scaled
+_SKIP_SLOT = os.environ.get("D3D_SKIP_SLOT", "1") != "0"
 
 
 class _CatGNDense(torch.autograd.Function):
@@ -620,7 +623,16 @@ class _CatGNDense(torch.autograd.Function):
         SINK.use(gb, ctx.needs_input_grad[3])
         SINK.use(dw, ctx.needs_input_grad[4])
         SINK.use(db, ctx.needs_input_grad[5])
-        return y, skip.view(N, H, W, OC)
+        # the skip's consumer (conv2's residual, out = s * (conv + skip)) may
+        # deposit its unscaled gradient and s here instead of returning a
+        # scaled copy (models.xunet.ResnetBlock); s rides on the GEMM alphas
+        # and the weight-gradient job
+        ctx.oslot = ResGradSlot() if _SKIP_SLOT else None
+        ctx.set_materialize_grads(False)
+        skip = skip.view(N, H, W, OC)
+        if ctx.oslot is not None:
+            skip._d3d_out_slot = ctx.oslot
+        return y, skip
 
     @staticmethod
     def backward(ctx, dy, dskip):
@@ -628,32 +640,54 @@ class _CatGNDense(torch.autograd.Function):
         G, has_db = ctx.cfg
         N, H, W, C1 = a.shape
         C2 = b.shape[-1]
+        dwp, dbp = ctx.params
+        OC = dwp.shape[0]
+        if dy is None:
+            dy = torch.zeros(N, H, W, C1 + C2, dtype=BF16, device=a.device)
         dy = dy.contiguous()
         (da, db_in), _, dgw, dgb = _gn_bwd(1, a, dy, None, stats, gw, gb, G, 0.0, 0, x2=b)
-        g = dskip.contiguous()
-        OC = g.shape[-1]
+        # the skip's gradient: returned by autograd, or deposited (unscaled,
+        # with its scale) by conv2's backward into the output slot
+        gs = 1.0
+        g = dskip
+        if ctx.oslot is not None:
+            d1, s1, d2, s2 = ctx.oslot.take()
+            if d1 is not None:
+                if d2 is not None:
+                    d1, s1 = (d1.float() * s1 + d2.float() * s2).to(BF16), 1.0
+                if g is not None:
+                    d1, s1 = (d1.float() * s1 + g.float()).to(BF16), 1.0
+                g, gs = d1, s1
+        if g is None:
+            g = torch.zeros(N, H, W, OC, dtype=BF16, device=a.device)
+        g = g.contiguous()
         g2 = g.reshape(-1, OC)
-        OCp = _up(OC, 64)
-        rows_ = g2.shape[0]
-        if g2.is_contiguous() and _gemm_ok(C1, rows_, OC, OCp, OC, g2, da, db_in) and \
-                _gemm_ok(C2, rows_, OC, OCp, OC, g2, da, db_in):
-            pk = packed_weight(dw, True, 1)                      # [ICp][OCp]: rows = input channels
-            d2a, d2b = da.view(-1, C1), db_in.view(-1, C2)
-            gemm_nt(pk, g2, d2a, C1, rows_, OC, OCp, OC, C1, res=d2a)
-            gemm_nt(pk[C1 * OCp:], g2, d2b, C2, rows_, OC, OCp, OC, C2, res=d2b)
-        else:
-            wb = bf16_weight(dw)
-            da.view(-1, C1).addmm_(g2, wb[:, :C1])
-            db_in.view(-1, C2).addmm_(g2, wb[:, C1:])
         rows = g2.shape[0]
         C = C1 + C2
-        dwp, dbp = ctx.params
         gW = gB = None
         tw = SINK.target(dwp)
         tb = SINK.target(dbp) if has_db else None
         direct = tw is not None and (not has_db or tb is not None)
         dWt = tw.view(OC, C) if direct else torch.zeros(OC, C, dtype=F32, device=g.device)
         dbt = (tb if direct else torch.zeros(OC, dtype=F32, device=g.device)) if has_db else None
+        spec = wgrad_job(g2, a, OC, C, rows, 1, 1, 1, dWt, dbt, gs, x2=b, C1=C1) if direct else None
+        if gs != 1.0 and spec is None:
+            # the per-job weight-gradient path takes no scale: a scaled copy
+            gsc = torch.empty_like(g2)
+            _chk(_lib.d3d_add_scale(g2.data_ptr(), None, gsc.data_ptr(), float(gs), g2.numel(), _st()), "scale")
+            g2, gs = gsc, 1.0
+        OCp = _up(OC, 64)
+        rows_ = g2.shape[0]
+        if g2.is_contiguous() and _gemm_ok(C1, rows_, OC, OCp, OC, g2, da, db_in) and \
+                _gemm_ok(C2, rows_, OC, OCp, OC, g2, da, db_in):
+            pk = packed_weight(dw, True, 1)                      # [ICp][OCp]: rows = input channels
+            d2a, d2b = da.view(-1, C1), db_in.view(-1, C2)
+            gemm_nt(pk, g2, d2a, C1, rows_, OC, OCp, OC, C1, res=d2a, alpha=gs)
+            gemm_nt(pk[C1 * OCp:], g2, d2b, C2, rows_, OC, OCp, OC, C2, res=d2b, alpha=gs)
+        else:
+            wb = bf16_weight(dw)
+            da.view(-1, C1).addmm_(g2, wb[:, :C1], alpha=gs)
+            db_in.view(-1, C2).addmm_(g2, wb[:, C1:], alpha=gs)
         # one weight-gradient GEMM over the virtual concat (the kernel picks
         # the source per 128-channel tile); two GEMMs when it cannot
         _ensure_impl()
@@ -674,7 +708,6 @@ class _CatGNDense(torch.autograd.Function):
             else:
                 _chk(rc, "wgrad_cat")
         if direct:
-            spec = wgrad_job(g2, a, OC, C, rows, 1, 1, 1, dWt, dbt, 1.0, x2=b, C1=C1)
             SINK.submit(g.device, job, (g2, a, b), (dwp, dbp if has_db else None), spec=spec)
         else:
             job()

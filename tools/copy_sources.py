@@ -28,7 +28,7 @@ def main():
     for _ in range(2):
         tr.train_step(*b)
     torch.cuda.synchronize()
-    wanted = set(a.ops.split(","))
+    wanted = set(a.ops.replace("+", ",").split(","))      # "+" also separates (tools/gpu.sh kbench args)
     with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU], with_stack=True) as prof:
         tr.train_step(*b)
         torch.cuda.synchronize()
