@@ -290,13 +290,41 @@ class GraphedTrainStep:
             self._drop()
             torch.cuda.synchronize()
         tr = self.tr
-        if tr.ctx.world > 1 and dist.is_initialized():
-            flag = torch.tensor([0.0 if err is not None else 1.0], device=tr.device)
+        # (also on a forced 1-rank group: the tests run this agreement path)
+        red = tr.reducer
+        if dist.is_initialized() and (tr.ctx.world > 1 or (red is not None and red.active)):
+            ok = 0.0 if err is not None else 1.0
+            # (comm_mode is agreed over the group: every rank runs this exchange or none does)
+            if self.comm_mode == "seg" and not self._segments_agree() and err is None:
+                ok = 0.0
+                err = RuntimeError("segmented capture: the ranks cut different segment layouts")
+                self._drop()
+            flag = torch.tensor([ok], device=tr.device)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if flag.item() < 0.5 and err is None:
                 err = RuntimeError("graph capture failed on another rank")
                 self._drop()
         return err
+
+    def _segments_agree(self) -> bool:
+        """Every rank must issue the eager bucket all-reduces of the segmented
+        step in the same sequence (else RCCL pairs different buckets and
+        hangs): compare the [bucket -> (segment, position)] layout over the
+        group (MIN == MAX)."""
+        nb = len(self.tr.reducer.buckets)
+        lay = torch.full((2 * nb + 1,), -1.0, device=self.tr.device)
+        lay[-1] = float(len(self.segs)) if self.segs is not None else -1.0
+        pos = 0
+        for si, bks in enumerate(self.seg_bk or []):
+            for b in bks:
+                if 0 <= b < nb:
+                    lay[2 * b] = float(si)
+                    lay[2 * b + 1] = float(pos)
+                pos += 1
+        hi, lo = lay.clone(), lay.clone()
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        return bool(torch.equal(hi, lo))
 
     def _drop(self) -> None:
         self.gA = self.gA0 = self.gB = None
