@@ -288,7 +288,10 @@ class GraphedTrainStep:
         except Exception as e:            # noqa: BLE001
             err = e
             self._drop()
-            torch.cuda.synchronize()
+            try:
+                torch.cuda.synchronize()
+            except Exception as e2:       # noqa: BLE001 -- a capture the failure left open
+                print(f"[graphs] synchronize after the failed capture: {type(e2).__name__}: {e2}", flush=True)
         tr = self.tr
         # (also on a forced 1-rank group: the tests run this agreement path)
         red = tr.reducer
