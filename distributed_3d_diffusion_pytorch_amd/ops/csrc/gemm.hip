@@ -428,8 +428,9 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
 #pragma unroll
       for (int i = 0; i < WI; ++i) gs[i][0] = gq[i][0] = gs[i][1] = gq[i][1] = 0.f;
       const bf16* sb = smem + C::BIAS + (ti & 3) * 512;
-      // residual rows: fragment row ii + 1's reads are issued before row ii's
-      // pairs (two row buffers, compile-time indexed)
+      // residual rows: fragment row ii + PD's reads are issued before row
+      // ii's pairs (PD + 1 row buffers, compile-time indexed): each row's
+      // reads get PD rows of epilogue work to land in
 #ifdef D3D_GEMM_EPI_SERIAL
       constexpr bool RD = false;                 // A/B build: each pair reads its rows right before use
       constexpr bool RS = (F & (F_RES | F_DSILU)) != 0;
@@ -437,19 +438,27 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
       constexpr bool RD = (F & (F_RES | F_DSILU)) != 0;
       constexpr bool RS = false;
 #endif
-      g_u2l rbuf[2][WJ / 2][2];
+#ifndef D3D_GEMM_EPI_PD
+#define D3D_GEMM_EPI_PD 1        // 3 rows ahead measured -0.4 % bs128 (profiles/r5/epi_pd/)
+#endif
+      constexpr int PD = D3D_GEMM_EPI_PD < WI - 1 ? D3D_GEMM_EPI_PD : (WI > 1 ? WI - 1 : 1);
+      constexpr int NB = PD + 1;
+      g_u2l rbuf[NB][WJ / 2][2];
       if constexpr (RD) {
-        g_for(std::make_integer_sequence<int, WJ / 2>{}, [&](auto jc) {
-          g_epi_rload<WI, WJ, 0, decltype(jc)::value>(e, rbuf[0][decltype(jc)::value][0],
-                                                       rbuf[0][decltype(jc)::value][1]);
+        g_for(std::make_integer_sequence<int, PD>{}, [&](auto rc) {
+          constexpr int r0 = decltype(rc)::value;
+          g_for(std::make_integer_sequence<int, WJ / 2>{}, [&](auto jc) {
+            g_epi_rload<WI, WJ, r0, decltype(jc)::value>(e, rbuf[r0 % NB][decltype(jc)::value][0],
+                                                          rbuf[r0 % NB][decltype(jc)::value][1]);
+          });
         });
       }
       g_for(std::make_integer_sequence<int, WI>{}, [&](auto ic) {
         constexpr int ii = decltype(ic)::value;
-        if constexpr (RD && ii + 1 < WI) {
+        if constexpr (RD && ii + PD < WI) {
           g_for(std::make_integer_sequence<int, WJ / 2>{}, [&](auto jc) {
-            g_epi_rload<WI, WJ, ii + 1, decltype(jc)::value>(e, rbuf[(ii + 1) & 1][decltype(jc)::value][0],
-                                                              rbuf[(ii + 1) & 1][decltype(jc)::value][1]);
+            g_epi_rload<WI, WJ, ii + PD, decltype(jc)::value>(e, rbuf[(ii + PD) % NB][decltype(jc)::value][0],
+                                                               rbuf[(ii + PD) % NB][decltype(jc)::value][1]);
           });
         }
         f32x4 cb = {0.f, 0.f, 0.f, 0.f};
@@ -465,8 +474,8 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
         for (int k = 0; k < 4; ++k) cb[k] *= scale;
         g_for(std::make_integer_sequence<int, WJ / 2>{}, [&](auto jc) {
           constexpr int jp = decltype(jc)::value;
-          if constexpr (RS) g_epi_rload<WI, WJ, ii, jp>(e, rbuf[ii & 1][jp][0], rbuf[ii & 1][jp][1]);
-          g_epi_pair<F, WI, WJ, ii, jp>(acc, e, cb, gs, gq, rbuf[ii & 1][jp][0], rbuf[ii & 1][jp][1]);
+          if constexpr (RS) g_epi_rload<WI, WJ, ii, jp>(e, rbuf[ii % NB][jp][0], rbuf[ii % NB][jp][1]);
+          g_epi_pair<F, WI, WJ, ii, jp>(acc, e, cb, gs, gq, rbuf[ii % NB][jp][0], rbuf[ii % NB][jp][1]);
         });
       });
       if constexpr ((F & F_GN) && WJ >= 4) {
