@@ -61,7 +61,8 @@ class GradSink:
         self.notify: Optional[Callable[[int], None]] = None
         self.stream_enabled = os.environ.get("D3D_WGRAD_STREAM", "1") != "0"
         self.graph_defer = True      # weight gradients on the side stream inside graph capture too
-        self.defer_batch = 8         # jobs per fork (4 measured 1.5 % slower at bs16)
+        # jobs per fork (4 measured 1.5 % slower at bs16; D3D_WGRAD_DEFER_BATCH for A/B)
+        self.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "8"))
         # eager steps: queue the grouped-kernel jobs too and flush them 8 at a
         # time (one grouped launch each) instead of one launch pair per job
         # (default "2": eager jobs run immediately, each as a one-job grouped
