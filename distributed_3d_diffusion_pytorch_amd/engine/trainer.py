@@ -86,12 +86,13 @@ class Trainer:
                 self.reducer.sink = SINK
             self.sink = SINK
             # weight-gradient jobs per side-stream fork: 64 when no collective
-            # waits on the reports (bs16 +1.7 %, profiles/r5/defer_batch/); 8
-            # when the bucketed all-reduces do -- a parameter is reported only
-            # when its job's batch is flushed, so big batches would start the
-            # buckets' reductions late (D3D_WGRAD_DEFER_BATCH overrides)
+            # waits on the reports (bs16 +1.7 %, profiles/r5/defer_batch/); 16
+            # when the bucketed all-reduces do (+0.7 % over 8 with the captured
+            # collectives) -- a parameter is reported only when its job's batch
+            # is flushed, so big batches would start the buckets' reductions
+            # late (D3D_WGRAD_DEFER_BATCH overrides)
             comm = self.reducer is not None and self.reducer.active
-            SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "8" if comm else "64"))
+            SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "16" if comm else "64"))
         oc = cfg.optim
         self.optim = FusedAdam(self.flat, oc.lr, oc.betas, oc.eps, oc.weight_decay,
                                ema_decay_for(cfg.global_batch, oc.ema_halflife_examples))
