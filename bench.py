@@ -86,8 +86,8 @@ def main() -> None:
                          "its collectives on (D3D_GRAPH_COMM=0 / D3D_GRAPH_SEG=0 select the fallback modes)")
     ap.add_argument("--graph", default="auto",
                     help="1: replay the step from captured HIP graphs; auto: when the per-GPU micro-batch is "
-                         "<= 32 (there the eager step is host-launch-bound, so any host jitter shows up in the "
-                         "step time; the replayed step is not)")
+                         "<= 64 (graph +2.2 %% at 64, -2.5 %% at 128: profiles/r5/graph_threshold/; at small "
+                         "batches the eager step is host-launch-bound)")
     ap.add_argument("--profile", default="", help="write a torch.profiler kernel table (text) here")
     ap.add_argument("--profile_stack", type=int, default=0, help="with --profile: also group by N stack frames")
     ap.add_argument("--mode", default="train", choices=["train", "sample"],
@@ -136,7 +136,7 @@ def main() -> None:
         # of 64, profiles/ab_bs128_modes_r2.txt); larger images split into 64s
         mb = 0 if local * args.imgsize * args.imgsize <= 128 * 64 * 64 else 64
     if args.graph == "auto":
-        graph = ctx.device.type == "cuda" and (mb or local) <= 32
+        graph = ctx.device.type == "cuda" and (mb or local) <= 64
     else:
         graph = bool(int(args.graph))
     cfg = make_config(None, {"model.H": args.imgsize, "model.W": args.imgsize, "data.imgsize": args.imgsize,
