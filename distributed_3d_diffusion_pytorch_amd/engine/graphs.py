@@ -142,6 +142,18 @@ def _seg_mb() -> float:
     return float(os.environ.get("D3D_GRAPH_SEG", "64"))
 
 
+def agree_switches(*flags: bool, device=None) -> tuple:
+    """Per-rank boolean switches (environment knobs) agreed over the group:
+    True only where every rank says True (MIN).  Used before any choice that
+    changes the collective sequence a rank runs."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return tuple(bool(f) for f in flags)
+    dev = device if (device is not None and dist.get_backend() == "nccl") else "cpu"
+    t = torch.tensor([float(bool(f)) for f in flags], device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return tuple(bool(v > 0.5) for v in t.tolist())
+
+
 class GraphCaptureError(RuntimeError):
     """The training step could not be captured (on this rank or any other):
     the trainer falls back to the eager step on every rank."""
@@ -173,11 +185,15 @@ class GraphedTrainStep:
         red = trainer.reducer
         if red is not None and red.active:
             # fp32 and bf16 payloads alike (the bf16 mirror is persistent, see
-            # parallel/ddp.py): the collectives are captured inside graph A
-            want = os.environ.get("D3D_GRAPH_COMM", "1") != "0"
+            # parallel/ddp.py): the collectives are captured inside graph A.
+            # The per-rank switches are agreed over the group first (MIN): a
+            # rank that probes or captures segments while another does not
+            # would run a different collective sequence and hang the job.
+            want, seg_ok = agree_switches(os.environ.get("D3D_GRAPH_COMM", "1") != "0",
+                                          _seg_mb() > 0 and dist.get_backend() == "nccl", device=dev)
             if want and probe_graph_collective(dev):
                 self.comm_mode = "graph"
-            elif _seg_mb() > 0 and dist.get_backend() == "nccl":
+            elif seg_ok:
                 self.comm_mode = "seg"
             else:
                 self.comm_mode = "post"
@@ -245,6 +261,12 @@ class GraphedTrainStep:
         self.loss_acc.add_(loss.detach() * self.frac)
         if red is not None and comm:
             red.finish()            # remaining buckets + the join of RCCL's stream (captured edges)
+        elif tr.sink is not None:
+            # the end-of-backward callback normally did this; explicit, so a
+            # weight-gradient job still queued can never be left out of the
+            # graph (a no-op when the callback ran)
+            tr.sink.flush()
+            tr.sink.join()
         if red is not None:
             red.enabled = False
 
@@ -302,6 +324,10 @@ class GraphedTrainStep:
                 ok = 0.0
                 err = RuntimeError("segmented capture: the ranks cut different segment layouts")
                 self._drop()
+            if self.comm_mode == "graph" and not self._issue_order_agrees() and err is None:
+                ok = 0.0
+                err = RuntimeError("captured collectives: the ranks recorded different bucket sequences")
+                self._drop()
             flag = torch.tensor([ok], device=tr.device)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if flag.item() < 0.5 and err is None:
@@ -324,6 +350,27 @@ class GraphedTrainStep:
                     lay[2 * b] = float(si)
                     lay[2 * b + 1] = float(pos)
                 pos += 1
+        hi, lo = lay.clone(), lay.clone()
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        return bool(torch.equal(hi, lo))
+
+    def _issue_order_agrees(self) -> bool:
+        """comm_mode "graph": the bucket all-reduces recorded into graph A must
+        come in the same sequence on every rank (RCCL pairs collectives by
+        issue order: a different sequence reduces mismatched buckets or hangs
+        at the first replay).  The capture's [bucket -> position] map is
+        compared over the group (MIN == MAX), as _segments_agree does for the
+        segmented capture.  An empty log (the capture failed) compares as
+        all -1 and the failure is reported through the capture flag."""
+        red = self.tr.reducer
+        nb = len(red.buckets)
+        lay = torch.full((nb + 1,), -1.0, device=self.tr.device)
+        log = red.issue_log if self.gA is not None else []
+        lay[-1] = float(len(log))
+        for pos, b in enumerate(log):
+            if 0 <= b < nb:
+                lay[b] = float(pos)
         hi, lo = lay.clone(), lay.clone()
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
@@ -466,12 +513,14 @@ class GraphedTrainStep:
         red = self.tr.reducer
         bk = red.buckets[b]
         view = self.tr.flat.grad[bk["start"]: bk["end"]]
+        src = red.probe_src(b, view)                 # (test-only race probe: a snapshot, result discarded)
+        back = view if src is view else None
         if red.mirror is None:
-            works.append((dist.all_reduce(view, group=red.group, async_op=True), None, None))
+            works.append((dist.all_reduce(src, group=red.group, async_op=True), None, None))
         else:
             tmp = red.mirror[bk["start"]: bk["end"]]
-            tmp.copy_(view)
-            works.append((dist.all_reduce(tmp, group=red.group, async_op=True), tmp, view))
+            tmp.copy_(src)
+            works.append((dist.all_reduce(tmp, group=red.group, async_op=True), tmp, back))
 
     def _replay_segments(self, comm: bool = True) -> None:
         works: list = []
@@ -482,8 +531,10 @@ class GraphedTrainStep:
                     self._seg_issue(b, works)
         for w, tmp, view in works:
             w.wait()                      # the current stream waits on RCCL's
-            if tmp is not None:
+            if tmp is not None and view is not None:
                 view.copy_(tmp)
+        if comm:
+            self.tr.reducer.probe_final()
 
     # ------------------------------------------------------------------
     def _reduce_update_chunked(self) -> None:

@@ -203,8 +203,11 @@ class GradSink:
         # (queueing does not depend on the side stream: with it off the flush
         # runs on the current stream, so the same jobs group the same way and
         # the gradients are bitwise those of the side-stream step)
+        # (eager grouping: a closure job submitted while grouped jobs are
+        # queued is queued behind them -- it may read what they produce, e.g.
+        # the attention block's C x C split of the queued M = dy^T a job)
         if dev.type == "cuda" and ((self.graph_defer and capturing) or
-                                   (self.eager_group and spec is not None and not capturing)):
+                                   (self.eager_group and (spec is not None or self._queue) and not capturing)):
             # the submitting stream travels with the job: its inputs were
             # produced there, and it need not be the stream that flushes
             # (conditioning-stream jobs are often flushed from the compute
@@ -318,23 +321,40 @@ class GradSink:
         waited for too when the collective is issued from another stream's
         context (a flush from the conditioning stream's backward), so a bucket
         never narrows a gradient that the trunk stream still writes."""
-        if not self._forked:
+        if not (torch.cuda.is_available() and torch.cuda.is_initialized()):
             yield
             return
         idx = torch.cuda.current_device()
-        side = self._side(idx)
         cur = torch.cuda.current_stream(idx)
+        others = [s for s in ([main] if main is not None else []) + [c for c in self._compute if c.device.index == idx]
+                  if s.cuda_stream != cur.cuda_stream]
+        if not self._forked and not others:
+            # every deposit so far was made on this stream: RCCL's stream waits for it
+            yield
+            return
+        # Behind the side stream, which waits for this stream, the backward's
+        # main stream and the registered compute streams -- also when nothing
+        # has forked yet (deposits on the conditioning stream, or the side
+        # stream off): a collective must never read a bucket that another
+        # stream still writes.
+        side = self._side(idx)
         side.wait_stream(cur)
-        if main is not None and main.cuda_stream != cur.cuda_stream and main.cuda_stream != side.cuda_stream:
-            side.wait_stream(main)
-        self._wait_compute(side, idx)       # deposits made from the other compute stream(s)
+        for s in others:
+            if s.cuda_stream != side.cuda_stream:
+                side.wait_stream(s)
+        self._forked.add(idx)               # the next join() rejoins it
         with torch.cuda.stream(side):
             yield
 
     def reset(self) -> None:
+        """Start of a step (before its backward).  Also clears the queued
+        end-of-backward flag: a backward that raised (e.g. a failed graph
+        capture) drops autograd's final callbacks, and a stale flag would stop
+        the next backward from queueing its flush + join."""
         self.uses = {}
         self.seen = set()
         self._queue = []
+        self._cb_queued = False
 
 
 SINK = GradSink()

@@ -1784,6 +1784,7 @@ class _AttnPair:
         self.M = self.dcol = None                                    # dy^T a, colsum dy (split backward)
         self.tok = None
         self.bwd = {}                                                # (grad target ptrs) -> _SgTable
+        self.scratch = None          # persistent gradient targets when the sink does not own the parameters
 
     def token(self):
         return (_EPOCH[0],) + tuple(p._version for p in self.params)
@@ -1905,11 +1906,21 @@ class _AttnOut(torch.autograd.Function):
             ps = (W_out, b_out, W_lin, b_lin)
             tgt = [SINK.target(p_) for p_ in ps]
             direct = all(t is not None for t in tgt)
-            if not direct:
+            split = rows >= _ATTN_SPLIT * C
+            if not direct and split:
+                # persistent targets: the split table (a device job table, built by
+                # a host-to-device copy) is built once for them, never per backward
+                # (nor inside a graph capture); the results leave as copies
+                if pr.scratch is None or pr.scratch[0].device != g.device:
+                    pr.scratch = [torch.zeros(p_.shape, dtype=F32, device=g.device) for p_ in ps]
+                tgt = pr.scratch
+                for t_ in tgt:
+                    t_.zero_()
+            elif not direct:
                 tgt = [torch.zeros(p_.shape, dtype=F32, device=g.device) for p_ in ps]
             tw_out, tb_out, tw_lin, tb_lin = tgt
-            if rows >= _ATTN_SPLIT * C:
-                tab = pr.bwd_table(tw_out.view(C, C), tb_out, tw_lin.view(C, C), tb_lin, cache=direct)
+            if split:
+                tab = pr.bwd_table(tw_out.view(C, C), tb_out, tw_lin.view(C, C), tb_lin)
                 g4, x4 = g.reshape(rows, 1, 1, C), a2.reshape(rows, 1, 1, C)
                 spec = wgrad_job(g4, x4, C, C, rows, 1, 1, 1, pr.M.view(C, C, 1), pr.dcol, ks, accumulate=False)
 
@@ -1925,7 +1936,7 @@ class _AttnOut(torch.autograd.Function):
                 else:
                     job()
                     tab.run()
-                    grads = tgt
+                    grads = [t_.clone() for t_ in tgt]
             else:
                 def job(g=g, a2=a2, ks=ks):
                     # the layers' intermediates, recomputed off the critical path

@@ -80,6 +80,11 @@ class GradReducer:
         self._launched = [False] * len(self.buckets)
         self._works: List = []
         self._tmp = {}
+        # bucket issue order of the last step (captured mode: compared over the
+        # group after the capture, engine/graphs.py)
+        self.issue_log: List[int] = []
+        # test-only race probe (1-rank groups, enable_race_probe): (snapshots, final)
+        self.race_probe = None
         self._hooks = []
         for i, p in enumerate(flat.params):
             if p.requires_grad:
@@ -94,6 +99,35 @@ class GradReducer:
             self._pending[b] = sum(1 for i in bk["params"] if self.flat.params[i].requires_grad)
             self._launched[b] = False
         self._works = []
+        self.issue_log = []
+
+    def enable_race_probe(self) -> None:
+        """Test-only (1-rank group): every collective reduces a SNAPSHOT of its
+        bucket taken on the collective's stream at issue time, and its result
+        is discarded (a 1-rank sum is the identity), so the real gradient is
+        never overwritten by the collective.  ``finish()`` copies the complete
+        gradient into ``race_probe[1]``: a collective issued before a deposit
+        into its bucket landed shows as a snapshot that differs from it, for
+        fp32 and bf16 payloads alike (with the in-place reduction a premature
+        read is invisible on one rank: the write-back restores what was read)."""
+        assert self.world == 1, "race probe: 1-rank groups only"
+        n = self.flat.grad.numel()
+        self.race_probe = (torch.zeros(n, device=self.flat.grad.device),
+                           torch.zeros(n, device=self.flat.grad.device))
+
+    def probe_src(self, b: int, view: torch.Tensor) -> torch.Tensor:
+        """The tensor bucket b's collective reduces: the bucket itself, or its
+        race-probe snapshot (copied on the current stream)."""
+        if self.race_probe is None:
+            return view
+        bk = self.buckets[b]
+        snap = self.race_probe[0][bk["start"]: bk["end"]]
+        snap.copy_(view)
+        return snap
+
+    def probe_final(self) -> None:
+        if self.race_probe is not None:
+            self.race_probe[1].copy_(self.flat.grad)
 
     def _make_hook(self, i: int):
         def hook(p):
@@ -119,16 +153,19 @@ class GradReducer:
         if self.seg_cut is not None:
             self.seg_cut(b, True)
             return
+        self.issue_log.append(b)
         bk = self.buckets[b]
         view = self.flat.grad[bk["start"]: bk["end"]]
         ctx = self.sink.collective(self.main_stream) if self.sink is not None else contextlib.nullcontext()
         with ctx:       # behind the sink's weight-gradient stream (ops/gradsink.py)
+            src = self.probe_src(b, view)
+            back = view if src is view else None                    # probe: the result is discarded
             if self.mirror is None:
-                self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+                self._works.append((dist.all_reduce(src, group=self.group, async_op=True), None, None))
             else:
                 tmp = self.mirror[bk["start"]: bk["end"]]
-                tmp.copy_(view)                                     # narrow on the collective's stream
-                self._works.append((dist.all_reduce(tmp, group=self.group, async_op=True), tmp, view))
+                tmp.copy_(src)                                      # narrow on the collective's stream
+                self._works.append((dist.all_reduce(tmp, group=self.group, async_op=True), tmp, back))
 
     def finish(self) -> None:
         """Launch any bucket whose gradients never arrived (unused params) and
@@ -149,11 +186,18 @@ class GradReducer:
         for b in range(len(self.buckets)):
             if not self._launched[b]:
                 self._launch(b)
+        if self.sink is not None:
+            # collectives issued above from behind the weight-gradient stream:
+            # rejoin it (also a graph capture's end-of-capture join)
+            self.sink.join()
         for w, tmp, view in self._works:
             w.wait()
-            if tmp is not None:
+            if tmp is not None and view is not None:
                 view.copy_(tmp)                                     # widen (persistent mirror: no recycling)
+        self.probe_final()
+        log = self.issue_log
         self.reset()
+        self.issue_log = log
 
     def describe(self) -> dict:
         """Bucket layout and payload, for benchmark / metrics records."""

@@ -201,3 +201,45 @@ def two_node_emulation(out_dir):
     with open(os.path.join(out_dir, f"node{ctx.rank}.txt"), "w") as f:
         f.write(f"{int(ok)} {int(same)} {int(ok2)}")
     cleanup()
+
+
+def capture_agreement(out_dir):
+    """8 gloo ranks: the cross-rank checks that guard the graph step's
+    collective sequence (engine/graphs.py) -- the captured bucket order
+    (comm_mode "graph"), the segment layout (comm_mode "seg") and the
+    agreement of per-rank environment switches -- on real reducer buckets."""
+    import types
+    from distributed_3d_diffusion_pytorch_amd.parallel import init_distributed, cleanup, FlatParams, GradReducer
+    from distributed_3d_diffusion_pytorch_amd.engine.graphs import GraphedTrainStep, agree_switches
+    from helpers import tiny_model, tiny_batch
+    ctx = init_distributed("gloo", 60, use_gpu=False)
+    r = ctx.rank
+    m = tiny_model(seed=0).eval()
+    flat = FlatParams(list(m.parameters()))
+    red = GradReducer(flat, bucket_mb=0.05, first_bucket_mb=0.01)
+    nb = len(red.buckets)
+    # the real issue order of an eager bucketed backward: the same on every rank
+    red.reset()
+    m(tiny_batch(2, seed=10 + r), cond_mask=torch.tensor([True, True])).square().mean().backward()
+    red.finish()
+    real = list(red.issue_log)
+    st = types.SimpleNamespace(tr=types.SimpleNamespace(reducer=red, device=torch.device("cpu")), gA=object())
+    res = [GraphedTrainStep._issue_order_agrees(st)]
+    red.issue_log = real[:2][::-1] + real[2:] if r == 3 else list(real)           # rank 3 swaps two buckets
+    res.append(GraphedTrainStep._issue_order_agrees(st))
+    red.issue_log = list(real)
+    st.gA = None if r == 5 else object()                                           # rank 5's capture failed
+    res.append(GraphedTrainStep._issue_order_agrees(st))
+    # segment layouts: equal, then rank 2 cuts one bucket later
+    half = nb // 2
+    st.segs = [None, None]
+    st.seg_bk = [real[:half], real[half:]]
+    res.append(GraphedTrainStep._segments_agree(st))
+    if r == 2:
+        st.seg_bk = [real[:half + 1], real[half + 1:]]
+    res.append(GraphedTrainStep._segments_agree(st))
+    # switches: rank 6 turns the captured collectives off, all keep segments on
+    res.append(agree_switches(r != 6, True) == (False, True))
+    with open(os.path.join(out_dir, f"agree{r}.txt"), "w") as f:
+        f.write(f"{nb} {len(real)} " + " ".join(str(int(x)) for x in res))
+    cleanup()

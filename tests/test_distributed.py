@@ -39,6 +39,20 @@ def test_four_ranks_two_node_layout_resume(tmp_path):
     assert res == ["1 1 1"] * 4, res
 
 
+def test_graph_step_sequence_agreement_eight_ranks(tmp_path):
+    """The graph step's cross-rank guards on 8 gloo ranks: the captured
+    bucket order (comm_mode "graph") and the segment layout (comm_mode "seg")
+    agree when every rank recorded the same sequence and disagree on EVERY
+    rank when one rank differs (so all ranks fall back together instead of
+    hanging in mismatched collectives); per-rank switches agree by MIN."""
+    spawn(W.capture_agreement, 8, (str(tmp_path),))
+    res = [open(tmp_path / f"agree{r}.txt").read().split() for r in range(8)]
+    for r in res:
+        nb, nissued, *flags = r
+        assert int(nb) > 3 and int(nissued) == int(nb), r          # every bucket issued once
+        assert flags == ["1", "0", "0", "1", "0", "1"], r
+
+
 @pytest.mark.parametrize("n,world", [(8, 1), (8, 3), (64, 8), (5, 8)])
 def test_sampler_chain_shards_disjoint_covering(n, world):
     from distributed_3d_diffusion_pytorch_amd.engine.sampler import shard_range

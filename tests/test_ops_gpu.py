@@ -917,6 +917,45 @@ def test_graph_train_step_matches_eager(micro):
     hip_impl.set_device_seed(None)
 
 
+def test_eager_grouped_wgrad_keeps_attention_split_order(monkeypatch):
+    """D3D_WGRAD_EAGER_GROUP=1 (eager weight-gradient jobs queued and flushed
+    as grouped launches) with the attention block's SPLIT backward: the C x C
+    split job reads M = dy^T a, which the queued grouped job produces, so it
+    must be queued behind it (GradSink.submit), never run ahead on a stale or
+    uninitialised M.  Parameters after 2 eager steps match the default mode
+    (one-job grouped launches, run at once)."""
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.parallel import DistContext
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    from distributed_3d_diffusion_pytorch_amd.ops.gradsink import SINK
+    from distributed_3d_diffusion_pytorch_amd.ops import hip_impl
+    monkeypatch.setattr(hip_impl, "_ATTN_SPLIT", 0)          # split backward at every attention block
+    ctx = DistContext(device=torch.device("cuda", 0))
+    data = SyntheticBatches(4, 32, "cuda", seed=7)
+    batches = [next(data) for _ in range(2)]
+    prev = (SINK.eager_group, SINK.eager_single)
+    res = []
+    try:
+        for grp, single in ((False, True), (True, False)):
+            SINK.eager_group, SINK.eager_single = grp, single
+            torch.manual_seed(0)
+            cfg = make_config(None, {"model.H": 32, "model.W": 32, "data.imgsize": 32, "global_batch": 4,
+                                     "data.synthetic": True, "log_every": 0, "ckpt_every": 0,
+                                     "optim.warmup_examples": 8})
+            tr = Trainer(cfg, ctx)
+            losses = [tr.train_step(*b).item() for b in batches]
+            torch.cuda.synchronize()
+            res.append((losses, tr.flat.data.clone()))
+            del tr
+    finally:
+        SINK.eager_group, SINK.eager_single = prev
+    (la, pa), (lb, pb) = res
+    assert all(math.isfinite(v) for v in la + lb), (la, lb)
+    assert max(abs(a - b) for a, b in zip(la, lb)) < 2e-3, (la, lb)
+    assert (pa - pb).abs().max().item() < 5e-4
+
+
 @pytest.mark.parametrize("N,Hh,C1,C2,OC", [(32, 64, 128, 0, 128), (12, 64, 256, 128, 128), (8, 128, 128, 0, 128)])
 def test_gn_silu_conv_composition(H, N, Hh, C1, C2, OC):
     """GN0 + SiLU -> conv1 (`xunet.py:139-140`; C2 > 0: the decoder's virtual
@@ -1394,9 +1433,12 @@ def test_rccl_allreduce_graph_capture_probe(tmp_path):
     assert be == "nccl" and ok == "1"
 
 
-def _graph_comm_worker(out_dir):
+def _graph_comm_worker(out_dir, graph_comm="1"):
     """world=2 RCCL: the graph step with the all-reduce captured inside graph
-    A must equal the eager bucketed step."""
+    A (graph_comm "1"), or captured as segments with eager bucket all-reduces
+    between the replays (graph_comm "0": comm_mode "seg"), must equal the
+    eager bucketed step, with identical parameters on both ranks."""
+    os.environ["D3D_GRAPH_COMM"] = graph_comm
     import torch.distributed as dist
     from distributed_3d_diffusion_pytorch_amd.config import make_config
     from distributed_3d_diffusion_pytorch_amd.engine import Trainer
@@ -1467,18 +1509,27 @@ def _graph_comm_1rank_worker(out_dir):
                                      "dist.grad_dtype": gd, "dist.force_comm": True})
             tr = Trainer(cfg, ctx)
             assert tr.reducer is not None and tr.reducer.active
-            losses = [float(tr.train_step(*b)) for b in batches]
+            # race probe: each collective reduces a snapshot of its bucket taken
+            # at issue time (result discarded: 1-rank identity); after every step
+            # the snapshots must equal the complete gradient bit for bit
+            tr.reducer.enable_race_probe()
+            losses, race = [], 0.0
+            for b in batches:
+                losses.append(float(tr.train_step(*b)))
+                snap, final = tr.reducer.race_probe
+                race = max(race, (snap - final).abs().max().item())
+                probed = final.abs().max().item() > 0
             g = tr._graphed
             mode = f"{g.comm_mode}/{int(g.defer)}/{int(g.gA0 is not None)}" if g is not None else "eager"
             if g is not None and g.segs is not None:
                 mode += f"/{len(g.segs)}/{sum(len(b) for b in g.seg_bk)}/{len(tr.reducer.buckets)}"
             tr.sync()
-            res.append((losses, tr.flat.data.clone(), mode))
+            res.append((losses, tr.flat.data.clone(), mode, race, probed))
             exposed = g.measure_comm(2) if g is not None else 0.0      # (changes the training state)
             del tr
-        (le, pe, _), (lg, pg, mode) = res
+        (le, pe, _, re_, pre), (lg, pg, mode, rg, prg) = res
         lines.append(f"{gd}/{mb}/{gc} {(pe - pg).abs().max().item()} {max(abs(a - b) for a, b in zip(le, lg))} "
-                     f"{mode} {exposed}")
+                     f"{mode} {exposed} {re_} {rg} {int(pre)}{int(prg)}")
     os.environ.pop("D3D_GRAPH_COMM", None)
     os.environ.pop("D3D_GRAPH_SEG", None)
     with open(os.path.join(out_dir, "gc1.txt"), "w") as f:
@@ -1497,7 +1548,10 @@ def test_graph_step_captured_collectives_one_rank(tmp_path):
     kept): more than one segment, every bucket issued exactly once, the same
     parameters.  With D3D_GRAPH_SEG=0 as well: comm_mode "post" (chunked bf16
     reduction after the replay, each chunk's Adam behind its collective).
-    measure_comm works in every mode."""
+    measure_comm works in every mode.  Every row runs the reducer's race probe
+    (GradReducer.enable_race_probe): a collective that read its bucket before
+    the last deposit landed -- invisible to a 1-rank in-place all-reduce --
+    fails the test."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from distributed_3d_diffusion_pytorch_amd.parallel import spawn
@@ -1507,7 +1561,11 @@ def test_graph_step_captured_collectives_one_rank(tmp_path):
     assert [r.split()[0] for r in rows] == ["fp32/0/1", "bf16/0/1", "fp32/2/1", "fp32/0/0", "bf16/0/0", "fp32/2/0",
                                             "fp32/0/p", "bf16/0/p"]
     for r in rows:
-        gd, d, dl, mode, exp = r.split()
+        gd, d, dl, mode, exp, race_e, race_g, probed = r.split()
+        # no collective read a bucket before its last deposit (eager step, and
+        # the captured / segmented steps; the post mode reduces after the replay)
+        assert float(race_e) == 0.0 and float(race_g) == 0.0, r
+        assert probed == ("10" if gd.endswith("/p") else "11"), r
         if gd.endswith("/1"):
             assert mode == ("graph/0/1" if gd == "fp32/2/1" else "graph/1/0"), r
         elif gd.endswith("/0"):
@@ -1523,15 +1581,20 @@ def test_graph_step_captured_collectives_one_rank(tmp_path):
 
 
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs 2 GPUs (RCCL: one rank per device)")
-def test_graph_step_rccl_captured_allreduce_two_gpus(tmp_path):
+@pytest.mark.parametrize("graph_comm,want", [("1", "graph"), ("0", "seg")])
+def test_graph_step_rccl_captured_allreduce_two_gpus(tmp_path, graph_comm, want):
+    """2 ranks on 2 GPUs: the captured-collective step and the segmented
+    fallback (the path taken whenever the RCCL capture probe fails: bucket
+    all-reduces issued eagerly between segment replays, agreed segment
+    layout) against the eager bucketed step; replicas identical."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from distributed_3d_diffusion_pytorch_amd.parallel import spawn
     import test_ops_gpu as me
-    spawn(me._graph_comm_worker, 2, (str(tmp_path),))
+    spawn(me._graph_comm_worker, 2, (str(tmp_path), graph_comm))
     for r in range(2):
         d, de, dg, dl, mode = open(tmp_path / f"gc{r}.txt").read().split()
-        assert mode == "graph"
+        assert mode == want
         assert float(de) == 0.0 and float(dg) == 0.0
         assert float(d) < 5e-4 and float(dl) < 2e-3
 

@@ -43,15 +43,26 @@ def build(force: bool = False, jobs: int = 8, debug: bool = False, verbose: bool
     SRC_, OUT_, OBJ_ = src, out, obj
     os.makedirs(OBJ_, exist_ok=True)
     cc = hipcc()
-    hdrs = [os.path.join(SRC_, f) for f in os.listdir(SRC_) if f.endswith(".h")]
-    hdr_mtime = max((os.path.getmtime(h) for h in hdrs), default=0)
+    def dep_mtime(path: str, seen=None) -> float:
+        """Newest mtime of a source and the local headers it includes (recursively)."""
+        seen = set() if seen is None else seen
+        if path in seen or not os.path.exists(path):
+            return 0.0
+        seen.add(path)
+        t = os.path.getmtime(path)
+        with open(path) as f:
+            for line in f:
+                line = line.strip()
+                if line.startswith("#include \""):
+                    t = max(t, dep_mtime(os.path.join(os.path.dirname(path), line.split('"')[1]), seen))
+        return t
     flags = ["-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
     flags += ["-O0", "-g"] if debug else ["-O3"]
     flags += os.environ.get("D3D_EXTRA_FLAGS", "").split()      # A/B builds (e.g. -DD3D_SIGMOID_IEEE)
 
     def compile_one(src: str) -> str:
         obj = os.path.join(OBJ_, os.path.basename(src)[:-4] + ".o")
-        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= dep_mtime(src):
             return obj
         cmd = [cc, *flags, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -19,11 +19,16 @@ BF = torch.bfloat16
 # (label, M = output channels, N = pixels, K = reduction)
 SHAPES = [
     ("sq8192", 8192, 8192, 8192),
+    ("film fwd P1048576 1024->2048", 2048, 1048576, 1024),
+    ("film fwd P262144 1024->4608", 4608, 262144, 1024),
+    ("film fwd P16384 1024->9216", 9216, 16384, 1024),
     ("film fwd P524288 1024->2048", 2048, 524288, 1024),
     ("film fwd P131072 1024->4608", 4608, 131072, 1024),
     ("film fwd P65536 1024->2048", 2048, 65536, 1024),
     ("film fwd P16384 1024->4608", 4608, 16384, 1024),
     ("k1024 M1024 P131072", 1024, 131072, 1024),
+    ("film dgrad P1048576 2048->1024", 1024, 1048576, 2048),
+    ("film dgrad P262144 4608->1024", 1024, 262144, 4608),
     ("film dgrad P524288 2048->1024", 1024, 524288, 2048),
     ("film dgrad P131072 4608->1024", 1024, 131072, 4608),
     ("film dgrad P16384 4608->1024", 1024, 16384, 4608),
@@ -59,6 +64,7 @@ def main():
     ap.add_argument("--gm", type=int, default=0, help="tile-group width (d3d_gemm_tune gm; 0 = default)")
     ap.add_argument("--nobias", action="store_true")
     ap.add_argument("--res", action="store_true", help="with a residual operand R [N, M] (F_RES epilogue)")
+    ap.add_argument("--mf_ab", action="store_true", help="also time the generic epilogue (d3d_gemm_mf(0)) as v0")
     args = ap.parse_args()
     H._ensure_impl()
     lib = H._lib
@@ -75,7 +81,8 @@ def main():
 
         def ours(v=None):
             if v is not None:
-                lib.d3d_gemm_tune(v, args.gm, 0)
+                lib.d3d_gemm_mf(0 if v == 0 else 1)
+                lib.d3d_gemm_tune(v if v else 1, args.gm, 0)
             rc = lib.d3d_gemm_nt(w.data_ptr(), x.data_ptr(), y.data_ptr(), H._ptr(bias), H._ptr(r), M, N, K, K, K,
                                  M, M, 1.0, 1.0, st)
             assert rc == 0, rc
@@ -84,7 +91,7 @@ def main():
             o = torch.addmm(bias.to(BF), x, w.t()) if bias is not None else torch.mm(x, w.t())
             return o.add_(r) if r is not None else o
 
-        vers = [int(v) for v in args.vers.split(",")]
+        vers = [int(v) for v in args.vers.split(",")] + ([0] if args.mf_ab else [])
         rows = torch.randint(0, N, (256,), device="cuda")
         ref = x[rows].float() @ w.float().t() + (bias if bias is not None else 0) + (r[rows].float() if r is not None else 0)
         errs = {}
@@ -100,8 +107,10 @@ def main():
         t_o, t_b = {v: [] for v in vers}, []
         for _ in range(args.rounds):
             for v in vers:
-                lib.d3d_gemm_tune(v, args.gm, 0)
+                lib.d3d_gemm_mf(0 if v == 0 else 1)
+                lib.d3d_gemm_tune(v if v else 1, args.gm, 0)
                 t_o[v].append(timeit(ours, args.iters))
+            lib.d3d_gemm_mf(1)
             t_b.append(timeit(blas, args.iters))
         fl = 2.0 * M * N * K
         b = min(t_b)
