@@ -1342,9 +1342,32 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
       cb[i][e] = t;
     }
   }
+  // The output tile leaves through LDS (free after the K loop; the tile,
+  // BN x 128 bf16 = at most 128 KiB, fits): each lane parks its bf16x4
+  // fragments in a [pixel][128 ch] image (16-byte chunks XOR-swizzled by
+  // pixel & 15), then the block streams it out as whole 256-byte pixel rows,
+  // 16 bytes per lane.  The direct form stored 8 bytes per lane into 16
+  // different pixel rows per instruction (32-byte pieces), twice with the
+  // SiLU output: store-issue-bound at ~3 B/clk/CU -- the level-0
+  // conditioning conv (K = 576, 1024 + 1024 output channels per pixel) ran
+  // at 20 % MFMA, ~1.5 TB/s of writes.  D3D_HALO_EPI_DIRECT: the old form
+  // (A/B build).
+#ifdef D3D_HALO_EPI_DIRECT
+  constexpr bool LEPI = false;
+#else
+  constexpr bool LEPI = true;
+#endif
+  static_assert(2 * Gm::HBUF + (P2 ? 8 : 4) * Gm::ABUF >= BN * 128, "output tile must fit the LDS");
+  const bool lepi = LEPI && (OC % 8) == 0;
+  bf16* const sT = smem;                       // [BN][128] bf16, swizzled
+  if (lepi) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();              // every wave is done reading the K loop's LDS
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const long pix = n0 + wn * WN + j * 16 + fr;
+    const int pl = wn * WN + j * 16 + fr;      // tile-local pixel
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int co = m0 + wm * WM + i * 16 + fq * 4;
@@ -1366,11 +1389,36 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
         gs[i][j / 4] += y;
         gq[i][j / 4] += y * y;
       }
-      *reinterpret_cast<bf16x4*>(O + pix * OC + co) = o4;
-      if (O2) silu_store4(O2, pix * OC + co, o4);
+      if (lepi) {
+        const int cl = wm * WM + i * 16 + fq * 4;          // tile-local channel (0..127)
+        *reinterpret_cast<bf16x4*>(sT + pl * 128 + (((cl >> 3) ^ (pl & 15)) << 3) + (cl & 4)) = o4;
+      } else {
+        *reinterpret_cast<bf16x4*>(O + pix * OC + co) = o4;
+        if (O2) silu_store4(O2, pix * OC + co, o4);
+      }
     }
   }
   if (gnp) gn_part_store<TM, NH>(gs, gq, lane, m0 + wm * WM, n0 + wn * WN, OC, gn_groups, OHW, Mpix, gnp);
+  if (lepi) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // 16 lanes per 256-byte pixel row (channel chunks past OC skipped)
+#pragma unroll 4
+    for (int idx = tid; idx < BN * 16; idx += 512) {
+      const int pl = idx >> 4, c = idx & 15;
+      const int co = m0 + c * 8;
+      if (co >= OC) continue;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(sT + pl * 128 + ((c ^ (pl & 15)) << 3));
+      const long off = (n0 + pl) * OC + co;
+      *reinterpret_cast<bf16x8*>(O + off) = v;
+      if (O2) {
+        bf16x8 s8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s8[e] = (bf16)siluf_((float)v[e]);
+        *reinterpret_cast<bf16x8*>(O2 + off) = s8;
+      }
+    }
+  }
 }
 
 // split-K epilogue: O[pix][co] = (sum_s part[s][pix][co] + bias + row_bias

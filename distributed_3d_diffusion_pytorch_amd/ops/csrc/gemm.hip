@@ -37,7 +37,16 @@ static int g_small_k_w4 = 1;
 static int g_mf = 1;
 D3D_API void d3d_gemm_mf(int on) { g_mf = on; }
 D3D_API void d3d_gemm_small_k(int on) { g_small_k_w4 = on; }
+// the 256 x 256 tile on 8 waves (two per SIMD: one wave's LDS-DMA issue and
+// waits overlap the other's MFMAs) instead of 4 waves of 128 x 128
+static int g_w8_waves = 4;           // 8 measured 3-8 % slower on the FiLM shapes (profiles/r6/gemm_waves.txt)
+D3D_API void d3d_gemm_w8_waves(int nw) { g_w8_waves = nw == 4 ? 4 : 8; }
+static int g_cfg8(int M, int N, int K);
 static int g_cfg(int M, int N, int K) {
+  const int w = g_cfg8(M, N, K);
+  return w == 8 && g_w8_waves == 8 ? 9 : w;
+}
+static int g_cfg8(int M, int N, int K) {
   if (g_cfg_force) return g_cfg_force;
   const long cus = g_cus();
   if (g_small_k_w4 && K <= 512 && M >= 256 && M <= 768 && (long)cdiv(M, 128) * cdiv(N, 128) >= cus) return 4;
@@ -76,16 +85,16 @@ D3D_API int d3d_gemm(const void* A, const void* B, void* O, const void* bias_, i
     if (G <= 0 || M % G || hw <= 0 || hw % 64 || N % hw || !(cg == 4 || cg == 8 || cg == 16 || cg == 32)) return -1;
     if (W == 2) W = 4;                         // the partials need whole 64-pixel parts per wave
   }
-  const int BT = 32 * W;
+  const int BT = W == 9 ? 256 : 32 * W;
   if (256L * ldo * 2 >= (1L << 31) || (R && 256L * ldr * 2 >= (1L << 31)) || (long)M * 2 >= (1L << 31)) return -1;
   const int mt = cdiv(M, BT), nt = cdiv(N, BT);
   const long tiles = (long)mt * nt;
   if (tiles >= (1L << 31)) return -1;
   // deep ring (68 KB / 130 KB of LDS: 2 / 1 blocks per CU) when those
   // resident blocks hold every tile -- the latency-bound small problems
-  const bool deep = g_deep && W != 8 && tiles <= (long)g_cus() * (W == 4 ? 1 : 2);
+  const bool deep = g_deep && W < 8 && tiles <= (long)g_cus() * (W == 4 ? 1 : 2);
   // (an 8-stage ring for one 64-tile block per CU measured no gain, profiles/r4/gemm_deep8/: removed)
-  const int per_cu = W == 8 ? 1 : W == 4 ? 2 : 4;
+  const int per_cu = W >= 8 ? 1 : W == 4 ? 2 : 4;
   const int G_ = (int)std::min<long>(tiles, g_grid > 0 ? g_grid : (long)g_cus() * per_cu);
   const int gm = std::max(1, std::min(mt, g_gm));
   const int F = (epi == 1 ? F_DSILU
@@ -118,12 +127,12 @@ D3D_API int d3d_gemm_cat(const void* A, const void* B, const void* B2, int K1, v
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)B2 | (uintptr_t)O) & 15) return -1;
   if (ldo % 8 || ldo < M || 256L * ldo * 2 >= (1L << 31)) return -1;
   const int W = g_cfg(M, N, K);
-  const int BT = 32 * W;
+  const int BT = W == 9 ? 256 : 32 * W;
   const int mt = cdiv(M, BT), nt = cdiv(N, BT);
   const long tiles = (long)mt * nt;
   if (tiles >= (1L << 31)) return -1;
-  const bool deep = g_deep && W != 8 && tiles <= (long)g_cus() * (W == 4 ? 1 : 2);
-  const int per_cu = W == 8 ? 1 : W == 4 ? 2 : 4;
+  const bool deep = g_deep && W < 8 && tiles <= (long)g_cus() * (W == 4 ? 1 : 2);
+  const int per_cu = W >= 8 ? 1 : W == 4 ? 2 : 4;
   const int G_ = (int)std::min<long>(tiles, g_grid > 0 ? g_grid : (long)g_cus() * per_cu);
   const int gm = std::max(1, std::min(mt, g_gm));
   const int F = (bias ? F_B32 | F_CAT : F_CAT) | (g_mf && M % BT == 0 ? F_MF : 0);

@@ -62,13 +62,16 @@ constexpr int G_PK = 64;         // K per LDS stage (two steps): 128-byte rows, 
 // ds_read_b128 lane groups read 16 rows at one chunk: conflict-free)
 __device__ __forceinline__ int g_swz(int row, int chunk) { return row * G_PK + ((chunk ^ (row & 7)) << 3); }
 
-template <int WI, int WJ, int NST = 2>
+template <int WI, int WJ, int NST = 2, int NW = 4>
 struct GCfg {
-  static constexpr int BM = 32 * WI, BN = 32 * WJ;       // 2 x 2 waves of 16*WI x 16*WJ
+  // NW waves as 2 (M) x NW/2 (N), each 16*WI x 16*WJ outputs
+  static constexpr int WGN = NW / 2;
+  static constexpr int BM = 32 * WI, BN = 16 * WJ * WGN;
   static constexpr int STAGE = (BM + BN) * G_PK;         // bf16 per stage (two K-steps)
   static constexpr int BIAS = NST * STAGE;               // 4 slots of 256 fp32
   static constexpr int LDS = BIAS + 4 * 512;
-  static constexpr int DA = BM / 32, DB = BN / 32;       // DMA pieces (8 rows x 128 B) per wave and stage
+  static constexpr int RA = BM / NW, RB = BN / NW;       // operand rows each wave DMAs per stage
+  static constexpr int DA = RA / 8, DB = RB / 8;         // DMA pieces (8 rows x 128 B) per wave and stage
   static constexpr int ND = DA + DB;
   static constexpr int NM = WI * WJ;                     // MFMAs per wave and K-tile
   static constexpr int NR = WI + WJ;                     // fragment reads
@@ -240,20 +243,20 @@ __device__ __forceinline__ void g_epi_pair_mf(const f32x4 (&acc)[WI][WJ], bf16* 
 // (one or two tiles per CU, K <= 1024: attention / NIN projections and their
 // input gradients at 8x8 .. 32x32) are latency-bound with two stages -- each
 // stage waits a whole HBM round trip for 8 MFMAs -- so they take 4.
-template <int WI, int WJ, int F, int NST = 2>
-__global__ void __launch_bounds__(256, 1)
+template <int WI, int WJ, int F, int NST = 2, int NW = 4>
+__global__ void __launch_bounds__(64 * NW, 1)
 gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ O, const float* __restrict__ bias,
           const bf16* __restrict__ R, int M, int N, int K, int lda, int ldb, int ldo, int ldr, float alpha,
           float scale, int mt, int nt, int gm, float* __restrict__ gnp, int gn_groups, int gn_hw,
           const bf16* __restrict__ B2, int K1) {
   constexpr bool BIAS = (F & (F_B32 | F_B16)) != 0, BBF = (F & F_B16) != 0;
-  using C = GCfg<WI, WJ, NST>;
+  using C = GCfg<WI, WJ, NST, NW>;
   // 4 bias slots: the loader may run at most 3 tiles ahead -- NST 4 needs K >= 128 (host)
   static_assert(NST == 2 || NST == 4, "stage ring of 2 or 4");
   __shared__ __attribute__((aligned(16))) bf16 smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
   const int G = gridDim.x;
   int rb = blockIdx.x;
   {
@@ -285,8 +288,8 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   int aoff, boff;
   {
     const int chunk = (lane & 7) ^ (lane >> 3);
-    aoff = ((wave * (C::BM / 4) + (lane >> 3)) * lda + chunk * 8) * 2;
-    boff = ((wave * (C::BN / 4) + (lane >> 3)) * ldb + chunk * 8) * 2;
+    aoff = ((wave * C::RA + (lane >> 3)) * lda + chunk * 8) * 2;
+    boff = ((wave * C::RB + (lane >> 3)) * ldb + chunk * 8) * 2;
   }
   const int astep = 8 * lda * 2, bstep = 8 * ldb * 2;
   auto piece_off = [](int base, int step) { return g_vadd(base, step); };
@@ -356,16 +359,25 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
   };
   auto dma = [&](int st, int d) {            // piece d (< DA: A, else B) into stage st
     if (d < C::DA)
-      g_dma(lo.a, lo.ra, smem + st * C::STAGE + (wave * (C::BM / 4) + d * 8) * G_PK,
+      g_dma(lo.a, lo.ra, smem + st * C::STAGE + (wave * C::RA + d * 8) * G_PK,
             d ? piece_off(aoff, d * astep) : aoff, lkb);
     else if constexpr ((F & F_CAT) != 0) {
       const bool hi = lkb >= 2 * K1;         // K-stages never straddle the split (K1 % 64 == 0)
       g_dma(hi ? lo.b2 : lo.b, hi ? lo.rb2 : lo.rb,
-            smem + st * C::STAGE + (C::BM + wave * (C::BN / 4) + (d - C::DA) * 8) * G_PK,
+            smem + st * C::STAGE + (C::BM + wave * C::RB + (d - C::DA) * 8) * G_PK,
             d > C::DA ? piece_off(boff, (d - C::DA) * bstep) : boff, lkb);
-    } else
-      g_dma(lo.b, lo.rb, smem + st * C::STAGE + (C::BM + wave * (C::BN / 4) + (d - C::DA) * 8) * G_PK,
+    } else {
+#if defined(D3D_GEMM_X_SKIPB)        // timing-only builds (wrong results): B's DMA not issued / ...
+      return;
+#endif
+#if defined(D3D_GEMM_X_ZEROB)        // ... issued against an empty descriptor (no traffic)
+      g_dma(lo.b, 0, smem + st * C::STAGE + (C::BM + wave * C::RB + (d - C::DA) * 8) * G_PK,
             d > C::DA ? piece_off(boff, (d - C::DA) * bstep) : boff, lkb);
+#else
+      g_dma(lo.b, lo.rb, smem + st * C::STAGE + (C::BM + wave * C::RB + (d - C::DA) * 8) * G_PK,
+            d > C::DA ? piece_off(boff, (d - C::DA) * bstep) : boff, lkb);
+#endif
+    }
   };
 
   bf16x8 a0[WI], b0[WJ], a1[WI], b1[WJ];
@@ -636,11 +648,14 @@ struct GArgs {
   int K1;
 };
 
+// W: 8 / 4 / 2 = 4 waves of W x W fragments (tile 32W x 32W); 9 = 8 waves of
+// 8 x 4 fragments (256 x 256 tile, two waves per SIMD)
 template <int W, int F, int NST>
 static int g_run(const GArgs& a) {
-  hipLaunchKernelGGL((gemm_fw_k<W, W, F, NST>), dim3(a.G_), dim3(256), 0, a.st, (const bf16*)a.A, (const bf16*)a.B,
-                     (bf16*)a.O, (const float*)a.bias, (const bf16*)a.R, a.M, a.N, a.K, a.lda, a.ldb, a.ldo, a.ldr,
-                     a.alpha, a.scale, a.mt, a.nt, a.gm, a.gnp, a.G, a.hw, (const bf16*)a.B2, a.K1);
+  constexpr int WI = W == 9 ? 8 : W, WJ = W == 9 ? 4 : W, NW = W == 9 ? 8 : 4;
+  hipLaunchKernelGGL((gemm_fw_k<WI, WJ, F, NST, NW>), dim3(a.G_), dim3(64 * NW), 0, a.st, (const bf16*)a.A,
+                     (const bf16*)a.B, (bf16*)a.O, (const float*)a.bias, (const bf16*)a.R, a.M, a.N, a.K, a.lda, a.ldb,
+                     a.ldo, a.ldr, a.alpha, a.scale, a.mt, a.nt, a.gm, a.gnp, a.G, a.hw, (const bf16*)a.B2, a.K1);
   return (int)hipGetLastError();
 }
 
@@ -657,12 +672,12 @@ using GFlagsGN = GFlags<F_GN, F_B32 | F_GN, F_RES | F_GN, F_B32 | F_RES | F_GN>;
 template <int W, int... Fs>
 static int g_dispatch(int F, bool deep, const GArgs& a, GFlags<Fs...>) {
   int rc = -2;
-  (void)((F == Fs ? (rc = (W != 8 && deep) ? g_run<W, Fs, (W != 8 ? 4 : 2)>(a) : g_run<W, Fs, 2>(a), true)
+  (void)((F == Fs ? (rc = (W < 8 && deep) ? g_run<W, Fs, (W < 8 ? 4 : 2)>(a) : g_run<W, Fs, 2>(a), true)
                   : false) || ...);
   return rc;
 }
 
-// Instantiation units (gemm_w*.hip): tile size W (8 / 4 / 2), flag list L
+// Instantiation units (gemm_w*.hip): tile size W (8 / 4 / 2; 9 = the 8-wave 256 x 256 tile), flag list L
 // (0 plain + concat, 1 F_MF, 2 GroupNorm partials); -2 when F is not in L.
 int gemm_dispatch_w8_0(int F, bool deep, const GArgs& a);
 int gemm_dispatch_w8_1(int F, bool deep, const GArgs& a);
@@ -670,6 +685,9 @@ int gemm_dispatch_w8_2(int F, bool deep, const GArgs& a);
 int gemm_dispatch_w4_0(int F, bool deep, const GArgs& a);
 int gemm_dispatch_w4_1(int F, bool deep, const GArgs& a);
 int gemm_dispatch_w4_2(int F, bool deep, const GArgs& a);
+int gemm_dispatch_w9_0(int F, bool deep, const GArgs& a);
+int gemm_dispatch_w9_1(int F, bool deep, const GArgs& a);
+int gemm_dispatch_w9_2(int F, bool deep, const GArgs& a);
 int gemm_dispatch_w2_0(int F, bool deep, const GArgs& a);
 int gemm_dispatch_w2_1(int F, bool deep, const GArgs& a);
 
@@ -678,6 +696,9 @@ static int gemm_dispatch(int W, int F, bool deep, const GArgs& a) {
   if (W == 8) {
     if ((rc = gemm_dispatch_w8_0(F, deep, a)) == -2 && (rc = gemm_dispatch_w8_1(F, deep, a)) == -2)
       rc = gemm_dispatch_w8_2(F, deep, a);
+  } else if (W == 9) {
+    if ((rc = gemm_dispatch_w9_0(F, deep, a)) == -2 && (rc = gemm_dispatch_w9_1(F, deep, a)) == -2)
+      rc = gemm_dispatch_w9_2(F, deep, a);
   } else if (W == 4) {
     if ((rc = gemm_dispatch_w4_0(F, deep, a)) == -2 && (rc = gemm_dispatch_w4_1(F, deep, a)) == -2)
       rc = gemm_dispatch_w4_2(F, deep, a);

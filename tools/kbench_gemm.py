@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--nobias", action="store_true")
     ap.add_argument("--res", action="store_true", help="with a residual operand R [N, M] (F_RES epilogue)")
     ap.add_argument("--mf_ab", action="store_true", help="also time the generic epilogue (d3d_gemm_mf(0)) as v0")
+    ap.add_argument("--waves_ab", action="store_true", help="also time the 4-wave 256x256 tile (d3d_gemm_w8_waves(4)) as v0")
     args = ap.parse_args()
     H._ensure_impl()
     lib = H._lib
@@ -79,10 +80,15 @@ def main():
         r = (torch.rand(N, M, device="cuda") * 2 - 1).to(BF) if args.res else None
         st = H._st()
 
+        def sel(v):
+            # v0: the A/B side (--mf_ab: generic epilogue, --waves_ab: 4-wave 256 tile)
+            lib.d3d_gemm_mf(0 if (v == 0 and args.mf_ab) else 1)
+            lib.d3d_gemm_w8_waves(4 if (v == 0 and args.waves_ab) else 8)
+            lib.d3d_gemm_tune(v if v else 1, args.gm, 0)
+
         def ours(v=None):
             if v is not None:
-                lib.d3d_gemm_mf(0 if v == 0 else 1)
-                lib.d3d_gemm_tune(v if v else 1, args.gm, 0)
+                sel(v)
             rc = lib.d3d_gemm_nt(w.data_ptr(), x.data_ptr(), y.data_ptr(), H._ptr(bias), H._ptr(r), M, N, K, K, K,
                                  M, M, 1.0, 1.0, st)
             assert rc == 0, rc
@@ -91,7 +97,7 @@ def main():
             o = torch.addmm(bias.to(BF), x, w.t()) if bias is not None else torch.mm(x, w.t())
             return o.add_(r) if r is not None else o
 
-        vers = [int(v) for v in args.vers.split(",")] + ([0] if args.mf_ab else [])
+        vers = [int(v) for v in args.vers.split(",")] + ([0] if (args.mf_ab or args.waves_ab) else [])
         rows = torch.randint(0, N, (256,), device="cuda")
         ref = x[rows].float() @ w.float().t() + (bias if bias is not None else 0) + (r[rows].float() if r is not None else 0)
         errs = {}
@@ -107,10 +113,9 @@ def main():
         t_o, t_b = {v: [] for v in vers}, []
         for _ in range(args.rounds):
             for v in vers:
-                lib.d3d_gemm_mf(0 if v == 0 else 1)
-                lib.d3d_gemm_tune(v if v else 1, args.gm, 0)
+                sel(v)
                 t_o[v].append(timeit(ours, args.iters))
-            lib.d3d_gemm_mf(1)
+            sel(1)
             t_b.append(timeit(blas, args.iters))
         fl = 2.0 * M * N * K
         b = min(t_b)
