@@ -40,9 +40,18 @@ class FusedAdam(torch.optim.Optimizer):
         self.ema_decay = float(ema_decay)
         self.ema: Optional[torch.Tensor] = flat.data.clone() if ema_decay > 0 else None
         self.on_step = []          # callbacks run after each update (weight caches)
+        # the fused HIP update also zeroes the gradient (callers that always
+        # zero_grad() right after step(), e.g. engine.Trainer, turn this on)
+        self.zero_in_step = False
+        self._grad_zeroed = False
 
     # ------------------------------------------------------------------
     def zero_grad(self, set_to_none: bool = False) -> None:  # noqa: D401 - torch API
+        if self._grad_zeroed:
+            # the fused update of step() already left the gradient zeroed (one
+            # pass over the flat buffer instead of an extra 521 MiB fill)
+            self._grad_zeroed = False
+            return
         self.flat.zero_grad()
 
     def grad_norm(self, grad_scale: float = 1.0) -> torch.Tensor:
@@ -96,8 +105,10 @@ class FusedAdam(torch.optim.Optimizer):
                 hp = self.hparams_to(torch.empty(8, dtype=torch.float32, device=p.device), grad_scale)
                 if coef is not None:
                     hp[6:7].mul_(coef)
-                if FUSED_UPDATE:        # Adam + bf16 operand repack in one pass over the tiles
-                    hip_impl.adam_update_all(self.flat, self.exp_avg, self.exp_avg_sq, self.ema, hp)
+                if FUSED_UPDATE:        # Adam + bf16 operand repack (+ gradient zeroing) in one pass over the tiles
+                    hip_impl.adam_update_all(self.flat, self.exp_avg, self.exp_avg_sq, self.ema, hp,
+                                             zero_g=self.zero_in_step)
+                    self._grad_zeroed = self.zero_in_step
                 else:
                     hip_impl.adam_flat_dev(p, gr, self.exp_avg, self.exp_avg_sq, self.ema, hp)
             else:

@@ -96,6 +96,7 @@ class Trainer:
         oc = cfg.optim
         self.optim = FusedAdam(self.flat, oc.lr, oc.betas, oc.eps, oc.weight_decay,
                                ema_decay_for(cfg.global_batch, oc.ema_halflife_examples))
+        self.optim.zero_in_step = True        # train_step zeroes right after each update
         self.sched = None
         if oc.use_cosine:
             self.sched = torch.optim.lr_scheduler.CosineAnnealingLR(self.optim, T_max=oc.cosine_tmax)

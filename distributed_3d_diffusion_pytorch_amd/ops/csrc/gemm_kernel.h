@@ -320,7 +320,11 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
     const long arows = M - m0 < C::BM ? M - m0 : C::BM, brows = N - n0 < C::BN ? N - n0 : C::BN;
     Ops o;
     o.a = A + m0 * lda;
+#if defined(D3D_GEMM_X_L2B)            // timing-only build (wrong results): every tile reads B rows 0.. (L2-resident)
+    o.b = B;
+#else
     o.b = B + n0 * ldb;
+#endif
     o.ra = v ? (int)((arows - 1) * lda + K) * 2 : 0;
     o.rb = v ? (int)((brows - 1) * ldb + K) * 2 : 0;
     if constexpr ((F & F_CAT) != 0) {
