@@ -64,7 +64,7 @@ def main():
                 ref = out.float().clone()
             err = ((out.float() - ref).norm() / ref.norm()).item()
             us = timeit(fn)
-            print(f"N{N} cond conv {IC}->{OC} {impl:5s} silu_out={int(silu)}: {us:8.1f} us {fl / us / 1e6:7.1f} TF/s "
+            print(f"N{N} cond conv {IC}->{OC} {impl:8s} silu_out={int(silu)}: {us:8.1f} us {fl / us / 1e6:7.1f} TF/s "
                   f"rel {err:.1e}", flush=True)
     H.set_conv_impl("halo")
 
