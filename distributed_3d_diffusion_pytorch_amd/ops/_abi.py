@@ -36,6 +36,7 @@ SIGNATURES = {
     "d3d_gemm_small_k": [I],
     "d3d_gemm_mf": [I],
     "d3d_gemm_w8_waves": [I],
+    "d3d_attn_bwd_cfg": [I],
     "d3d_colsum_jobs": [P, I, P],
     "d3d_conv_halo_cfg": [I],
     "d3d_conv_res_cfg": [I],
@@ -106,6 +107,7 @@ SIGNATURES = {
     "d3d_gemm_nt": [P, P, P, P, P, I, I, I, I, I, I, I, F, F, P],
     "d3d_gemm_nt_gn": [P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, I, I, P],
     "d3d_attn_bwd": [P, P, P, P, P, P, I, I, I, I, I, F, P],
+    "d3d_attn_bwd_slabs": [I, I, I, I],
     # wgrad_group.hip (job tables: arrays of hip_impl._WgJob)
     "d3d_wgrad_group_cfg": [I, I, I],
     "d3d_wgrad_group_ok": [P],

@@ -179,17 +179,27 @@ __global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, 
 }
 
 // --------------------------------------------------------------- backward --
-template <int D>
-__global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                  const float* __restrict__ lse, const bf16* __restrict__ out,
-                                                  float* __restrict__ dq_acc, bf16* __restrict__ dqkv, int L, int C,
-                                                  int heads, int cross, float scale) {
+// KW keys per workgroup (KW / 16 waves of 16 keys).  KW = 64: four 64-key
+// blocks per (image, head) at L = 256, each writing its own fp32 dQ slab
+// (summed by dq_convert_k).  KW = 256: ONE workgroup owns every key of an
+// L <= 256 sequence (8 waves of 2 x 16 keys), so dQ = dS K is complete inside
+// it and leaves as bf16 directly: no slabs (4 x N x L x C fp32 written and
+// re-read at the 16x16 level: ~270 MB per call at 256 frames), no conversion
+// launch, and each query / dO tile is read once instead of once per key block.
+template <int D, int KW = 64>
+__global__ void __launch_bounds__(KW == 256 ? 512 : 256) attn_bwd_k(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                     const float* __restrict__ lse, const bf16* __restrict__ out,
+                                                     float* __restrict__ dq_acc, bf16* __restrict__ dqkv, int L, int C,
+                                                     int heads, int cross, float scale) {
   constexpr int KC = D / 32, DT = D / 16;
+  // waves (4, or 8 for KW = 256: 2 x 16-key groups per wave -- at 16 waves
+  // the 128-register budget spilled), threads, key groups per wave
+  constexpr int NWV = KW == 256 ? 8 : 4, NT = 64 * NWV, KG = KW / (16 * NWV);
   constexpr int TS = D + 16;      // padded rows: row reads + tr reads
-  constexpr int SS = 64 + 8;      // dS tile row stride (bf16)
+  constexpr int SS = KW + 8;      // dS tile row stride (bf16)
   __shared__ __attribute__((aligned(16))) bf16 Qs[32 * TS];
   __shared__ __attribute__((aligned(16))) bf16 dOs[32 * TS];
-  __shared__ __attribute__((aligned(16))) bf16 Kt[64 * TS];
+  __shared__ __attribute__((aligned(16))) bf16 Kt[KW * TS];
   __shared__ __attribute__((aligned(16))) bf16 dSs[32 * SS];
   __shared__ float lse_s[32], D_s[32];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -197,42 +207,47 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
   const int nkv = cross ? (n ^ 1) : n;
   const int g = lane >> 4, fr = lane & 15, qq = (lane & 15) >> 2, pc = lane & 3;
   const long C3 = 3L * C;
-  const int k0 = kblk * 64;
+  const int k0 = kblk * KW;
   const float sl2 = scale * LOG2E;
   constexpr int CH = D / 8;
 
   // K tile of the block (for dQ) and this wave's K / V fragments (B operands)
 #pragma unroll
-  for (int i = 0; i < 64 * CH / 256; ++i) {
-    int idx = tid + i * 256;
+  for (int i = 0; i < KW * CH / NT; ++i) {
+    int idx = tid + i * NT;
     int r = idx / CH, c = idx % CH;
     *reinterpret_cast<bf16x8*>(Kt + r * TS + c * 8) =
         k0 + r < L ? *reinterpret_cast<const bf16x8*>(qkv + ((long)nkv * L + k0 + r) * C3 + C + h * D + c * 8)
                    : bf16x8{};
   }
-  const int key = k0 + 16 * w + fr;
-  const bool kok = key < L;                       // ragged last key block (L % 64 != 0)
-  const bf16* krow = qkv + ((long)nkv * L + (kok ? key : 0)) * C3 + h * D;
-  bf16x8 kf[KC], vf[KC];
+  // key group kg of this wave: keys k0 + 16 (w + NWV kg) + 0..15
+  bool kok[KG];
+  bf16x8 kf[KG][KC], vf[KG][KC];
+  f32x4 dk[KG][DT], dv[KG][DT];
 #pragma unroll
-  for (int kc = 0; kc < KC; ++kc) {
-    kf[kc] = kok ? *reinterpret_cast<const bf16x8*>(krow + C + 32 * kc + 8 * g) : bf16x8{};
-    vf[kc] = kok ? *reinterpret_cast<const bf16x8*>(krow + 2 * C + 32 * kc + 8 * g) : bf16x8{};
-  }
-  f32x4 dk[DT], dv[DT];
+  for (int kg = 0; kg < KG; ++kg) {
+    const int key = k0 + 16 * (w + NWV * kg) + fr;
+    kok[kg] = key < L;                            // ragged last key block (L % 64 != 0)
+    const bf16* krow = qkv + ((long)nkv * L + (kok[kg] ? key : 0)) * C3 + h * D;
 #pragma unroll
-  for (int t = 0; t < DT; ++t) {
-    dk[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < KC; ++kc) {
+      kf[kg][kc] = kok[kg] ? *reinterpret_cast<const bf16x8*>(krow + C + 32 * kc + 8 * g) : bf16x8{};
+      vf[kg][kc] = kok[kg] ? *reinterpret_cast<const bf16x8*>(krow + 2 * C + 32 * kc + 8 * g) : bf16x8{};
+    }
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      dk[kg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[kg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
   const float* lse_nh = lse + ((long)n * heads + h) * L;
-  const bool direct_dq = L <= 64;                 // one key block: dQ is complete here
+  const bool direct_dq = L <= KW;                 // one key block: dQ is complete here
 
   // the query tile (Q, dO rows) and the D-term operands (O, dO row parts) of
   // tile q0 + 32 are loaded into registers while tile q0 computes: the loop
   // was one HBM round trip per 32-query step with nothing to overlap it
   // (7 % MFMA in the bs128 step counters)
-  constexpr int NQ = (32 * CH + 255) / 256;       // 16-byte chunks per thread of each of Q / dO
+  constexpr int NQ = (32 * CH + NT - 1) / NT;     // 16-byte chunks per thread of each of Q / dO
   constexpr int PER = D / 8;                      // D-term elements per lane (8 or 16)
   bf16x8 qr[NQ], dr[NQ], orr[PER / 8], drr[PER / 8];
   float lse_r = 0.f;
@@ -240,7 +255,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
   auto fetch = [&](int qb) {
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-      int idx = tid + i * 256;
+      int idx = tid + i * NT;
       int r = idx / CH, c = idx % CH;
       const bool ok = idx < 32 * CH && qb + r < L;
       long row = (long)n * L + (ok ? qb + r : 0);
@@ -248,8 +263,9 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
       dr[i] = ok ? *reinterpret_cast<const bf16x8*>(dout + row * C + h * D + c * 8) : bf16x8{};
     }
     {
+      // (threads past the first 256: row r >= 32, nothing to load)
       const int r = tid >> 3, part = tid & 7;
-      const bool ok = qb + r < L;
+      const bool ok = r < 32 && qb + r < L;
       const long row = (long)n * L + (ok ? qb + r : 0);
 #pragma unroll
       for (int k = 0; k < PER / 8; ++k) {
@@ -269,7 +285,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-      int idx = tid + i * 256;
+      int idx = tid + i * NT;
       if (idx < 32 * CH) {
         int r = idx / CH, c = idx % CH;
         *reinterpret_cast<bf16x8*>(Qs + r * TS + c * 8) = qr[i];
@@ -289,59 +305,62 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
       acc += __shfl_xor(acc, 1, 64);
       acc += __shfl_xor(acc, 2, 64);
       acc += __shfl_xor(acc, 4, 64);
-      if (part == 0) D_s[r] = acc;
+      if (part == 0 && r < 32) D_s[r] = acc;
     }
     if (q0 + 32 < L) fetch(q0 + 32);              // in flight during this tile's compute
     __syncthreads();
-    f32x4 p[2], ds[2];
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+    for (int kg = 0; kg < KG; ++kg) {
+      f32x4 p[2], ds[2];
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        bf16x8 a = *reinterpret_cast<const bf16x8*>(Qs + (16 * qt + fr) * TS + 32 * kc + 8 * g);
-        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, kf[kc], s, 0, 0, 0);
-        bf16x8 b = *reinterpret_cast<const bf16x8*>(dOs + (16 * qt + fr) * TS + 32 * kc + 8 * g);
-        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, vf[kc], dp, 0, 0, 0);
+      for (int qt = 0; qt < 2; ++qt) {
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          bf16x8 a = *reinterpret_cast<const bf16x8*>(Qs + (16 * qt + fr) * TS + 32 * kc + 8 * g);
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, kf[kg][kc], s, 0, 0, 0);
+          bf16x8 b = *reinterpret_cast<const bf16x8*>(dOs + (16 * qt + fr) * TS + 32 * kc + 8 * g);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, vf[kg][kc], dp, 0, 0, 0);
+        }
+        // rows: q = 16qt + 4g + i ; column (lane): key
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int qi = 16 * qt + 4 * g + i;
+          float pv = kok[kg] ? exp2f(s[i] * sl2 - lse_s[qi]) : 0.f;
+          p[qt][i] = pv;
+          ds[qt][i] = pv * (dp[i] - D_s[qi]);
+        }
       }
-      // rows: q = 16qt + 4g + i ; column (lane): key
+      // dV += P^T dO ; dK += dS^T Q  (k-slots permuted: q = {4g+j, 16+4g+j})
+      bf16x8 pa = pack8(p[0], p[1]);
+      bf16x8 dsa = pack8(ds[0], ds[1]);
+      int r1 = 4 * g + qq, r2 = 16 + 4 * g + qq;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int qi = 16 * qt + 4 * g + i;
-        float pv = kok ? exp2f(s[i] * sl2 - lse_s[qi]) : 0.f;
-        p[qt][i] = pv;
-        ds[qt][i] = pv * (dp[i] - D_s[qi]);
+      for (int t = 0; t < DT; ++t) {
+        bf16x8 bo = tr8(dOs, TS, r1, r2, 16 * t + 4 * pc);
+        dv[kg][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, bo, dv[kg][t], 0, 0, 0);
+        bf16x8 bq = tr8(Qs, TS, r1, r2, 16 * t + 4 * pc);
+        dk[kg][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsa, bq, dk[kg][t], 0, 0, 0);
       }
-    }
-    // dV += P^T dO ; dK += dS^T Q  (k-slots permuted: q = {4g+j, 16+4g+j})
-    bf16x8 pa = pack8(p[0], p[1]);
-    bf16x8 dsa = pack8(ds[0], ds[1]);
-    int r1 = 4 * g + qq, r2 = 16 + 4 * g + qq;
+      // dS -> LDS [32 q][KW keys] for dQ = dS K
+      // columns are stored in the permuted k-slot order of the tr-read K operand:
+      // key u of a 32-key chunk -> slot 8*(u/4)+u%4 (u<16), 8*((u-16)/4)+4+u%4
+      {
+        const int kl = 16 * (w + NWV * kg) + fr, u = kl & 31;
+        const int col = (kl & ~31) + (u < 16 ? 8 * (u >> 2) + (u & 3) : 8 * ((u - 16) >> 2) + 4 + (u & 3));
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      bf16x8 bo = tr8(dOs, TS, r1, r2, 16 * t + 4 * pc);
-      dv[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, bo, dv[t], 0, 0, 0);
-      bf16x8 bq = tr8(Qs, TS, r1, r2, 16 * t + 4 * pc);
-      dk[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsa, bq, dk[t], 0, 0, 0);
-    }
-    // dS -> LDS [32 q][64 keys] for dQ = dS K
-    // columns are stored in the permuted k-slot order of the tr-read K operand:
-    // key u of a 32-key chunk -> slot 8*(u/4)+u%4 (u<16), 8*((u-16)/4)+4+u%4
-    {
-      const int kl = 16 * w + fr, u = kl & 31;
-      const int col = (kl & 32) + (u < 16 ? 8 * (u >> 2) + (u & 3) : 8 * ((u - 16) >> 2) + 4 + (u & 3));
+        for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dSs[(16 * qt + 4 * g + i) * SS + col] = (bf16)ds[qt][i];
+          for (int i = 0; i < 4; ++i) dSs[(16 * qt + 4 * g + i) * SS + col] = (bf16)ds[qt][i];
+      }
     }
     __syncthreads();
-    // dQ tiles: 2 (q) x DT (d) tiles over 4 waves
-    for (int tt = w; tt < 2 * DT; tt += 4) {
+    // dQ tiles: 2 (q) x DT (d) tiles over the waves
+    for (int tt = w; tt < 2 * DT; tt += NWV) {
       int qt = tt / DT, t = tt % DT;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kc = 0; kc < 2; ++kc) {   // 64 keys = 2 x 32
+      for (int kc = 0; kc < KW / 32; ++kc) {   // KW keys = KW / 32 x 32
         bf16x8 a = *reinterpret_cast<const bf16x8*>(dSs + (16 * qt + fr) * SS + 32 * kc + 8 * g);
         bf16x8 b = tr8(Kt, TS, 32 * kc + 4 * g + qq, 32 * kc + 16 + 4 * g + qq, 16 * t + 4 * pc);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
@@ -368,16 +387,19 @@ __global__ void __launch_bounds__(256) attn_bwd_k(const bf16* __restrict__ qkv, 
       }
     }
   }
-  // write dK, dV for this wave's 16 keys: dk[t][i] = dK[key = 4g+i][d = 16t+fr]
+  // write dK, dV for this wave's keys: dk[kg][t][i] = dK[key = 16 (w + NWV kg) + 4g+i][d = 16t+fr]
 #pragma unroll
-  for (int t = 0; t < DT; ++t)
+  for (int kg = 0; kg < KG; ++kg)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (k0 + 16 * w + 4 * g + i >= L) continue;
-      long row = (long)nkv * L + k0 + 16 * w + 4 * g + i;
-      dqkv[row * C3 + C + h * D + 16 * t + fr] = (bf16)(dk[t][i] * scale);
-      dqkv[row * C3 + 2 * C + h * D + 16 * t + fr] = (bf16)dv[t][i];
-    }
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int kk = k0 + 16 * (w + NWV * kg) + 4 * g + i;
+        if (kk >= L) continue;
+        long row = (long)nkv * L + kk;
+        dqkv[row * C3 + C + h * D + 16 * t + fr] = (bf16)(dk[kg][t][i] * scale);
+        dqkv[row * C3 + 2 * C + h * D + 16 * t + fr] = (bf16)dv[kg][t][i];
+      }
 }
 
 // dQ = sum over the kb key-block slabs (fixed order) -> bf16 q-columns of dqkv
@@ -412,13 +434,34 @@ D3D_API int d3d_attn_fwd(const void* qkv, void* out, float* lse, int N, int L, i
   return (int)hipGetLastError();
 }
 
-// dq_acc: [ceil(L/64), N, L, C] fp32 workspace (one slab per key block, fully
-// written; unused and may be null when L == 64); dqkv: [N, L, 3C] bf16
-// output (every element written).
+// KW = 256 (one workgroup per (image, head), dQ written directly) for
+// head dim 64 and 64 < L <= 256 from g_attn_wide_min (image, head) pairs on
+// (default: always -- +0.6 % at bs16 and bs128, +1.1 % at bs32, even with
+// half the CUs busy at bs16's 128 pairs); else 64-key workgroups + fp32 dQ
+// slabs.
+static long g_attn_wide_min = 0;      // measured faster at bs16 / 32 / 128 (profiles/r6/attn_wide_bwd.txt)
+D3D_API void d3d_attn_bwd_cfg(int wide_min_pairs) { g_attn_wide_min = wide_min_pairs; }
+static bool attn_wide(int N, int L, int C, int heads) {
+  return heads > 0 && C / heads == 64 && L > 64 && L <= 256 && (long)N * heads >= g_attn_wide_min;
+}
+// fp32 dQ slabs d3d_attn_bwd needs for this shape (0: dQ is written directly)
+D3D_API int d3d_attn_bwd_slabs(int N, int L, int C, int heads) {
+  return (L <= 64 || attn_wide(N, L, C, heads)) ? 0 : (L + 63) / 64;
+}
+
+// dq_acc: [d3d_attn_bwd_slabs(...), N, L, C] fp32 workspace (one slab per
+// 64-key block, fully written; may be null when no slab is needed); dqkv:
+// [N, L, 3C] bf16 output (every element written).
 D3D_API int d3d_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* dq_acc,
                          void* dqkv, int N, int L, int C, int heads, int cross, float scale, hipStream_t st) {
   int D = C / heads;
-  if (L < 1 || (L > 64 && dq_acc == nullptr)) return (int)hipErrorInvalidValue;
+  const int slabs = d3d_attn_bwd_slabs(N, L, C, heads);
+  if (L < 1 || (slabs > 0 && dq_acc == nullptr)) return (int)hipErrorInvalidValue;
+  if (attn_wide(N, L, C, heads)) {
+    hipLaunchKernelGGL((attn_bwd_k<64, 256>), dim3(1, heads, N), dim3(512), 0, st, (const bf16*)qkv,
+                       (const bf16*)dout, lse, (const bf16*)out, dq_acc, (bf16*)dqkv, L, C, heads, cross, scale);
+    return (int)hipGetLastError();
+  }
   const int kblocks = (L + 63) / 64;
   dim3 grid(kblocks, heads, N);
   if (D == 64)

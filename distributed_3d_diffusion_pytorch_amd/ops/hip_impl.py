@@ -879,6 +879,8 @@ if os.environ.get("D3D_WGRAD_HALO"):                   # A/B knob "on[,blocks[,s
     _lib.d3d_wgrad_group_halo(_hv[0], _hv[1], _hv[2])
 if os.environ.get("D3D_WGRAD_HALO_BIG"):               # A/B knob "blocks,lg2": halo target of the big flushes
     _lib.d3d_wgrad_group_halo_big(*[int(v) for v in os.environ["D3D_WGRAD_HALO_BIG"].split(",")])
+if os.environ.get("D3D_ATTN_WIDE_MIN"):               # A/B knob: (image, head) pairs from which one workgroup owns
+    _lib.d3d_attn_bwd_cfg(int(os.environ["D3D_ATTN_WIDE_MIN"]))   # all keys of an attention backward (L <= 256)
 if os.environ.get("D3D_WGRAD_HALO_PK"):                # A/B knob: pixels per halo K-step (32 / 64, the latter at W >= 64)
     _lib.d3d_wgrad_group_halo_pk(int(os.environ["D3D_WGRAD_HALO_PK"]))
 
@@ -2017,9 +2019,12 @@ class _Attention(torch.autograd.Function):
         C = C3 // 3
         dout = dout.contiguous()
         # one fp32 dQ slab per 64-key block, summed in fixed order
-        # (deterministic); a single key block (L <= 64) writes dQ directly;
-        # a ragged last block (L % 64 != 0) is masked in the kernels
-        dq = torch.empty((L + 63) // 64, N, L, C, dtype=F32, device=qkv.device) if L > 64 else None
+        # (deterministic); a single key block (L <= 64), or one workgroup
+        # owning all keys (L <= 256 at head dim 64, enough (image, head)
+        # pairs), writes dQ directly; a ragged last block (L % 64 != 0) is
+        # masked in the kernels
+        slabs = _lib.d3d_attn_bwd_slabs(N, L, C, heads)
+        dq = torch.empty(slabs, N, L, C, dtype=F32, device=qkv.device) if slabs else None
         dqkv = torch.empty_like(qkv)
         _chk(_lib.d3d_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), _ptr(dq),
                                dqkv.data_ptr(), N, L, C, heads, int(cross), scale, _st()), "attn_bwd")

@@ -557,6 +557,33 @@ def test_attention(H, N, L, C, cross):
     assert rel(gh[0], gr[0]) < 4e-2
 
 
+@pytest.mark.parametrize("N,L,cross", [(4, 256, False), (4, 256, True), (2, 196, True), (2, 100, False),
+                                         (128, 256, True)])
+def test_attention_backward_one_workgroup_per_head(H, N, L, cross):
+    """Head dim 64, 64 < L <= 256: one 8-wave workgroup owns all keys of an
+    (image, head) and writes dQ directly (no fp32 slabs / conversion launch;
+    the default; d3d_attn_bwd_cfg(1 << 30) restores the 64-key path).
+    Gradients against fp32 and against the 64-key-workgroup + slab path."""
+    torch.manual_seed(8)
+    C = 256
+    qkv = torch.randn(N, L, 3 * C, device=DEV).to(BF)
+    go = torch.randn(N, L, C, device=DEV)
+    H._ensure_impl()
+    outs = []
+    try:
+        for wide_min in (0, 1 << 30):
+            H._lib.d3d_attn_bwd_cfg(wide_min)
+            assert (H._lib.d3d_attn_bwd_slabs(N, L, C, 4) == 0) == (wide_min == 0)
+            yh, yr, gh, gr = run_both(lambda q: H.attention(q, 4, cross), lambda q: T.attention(q, 4, cross), [qkv],
+                                      go)
+            assert rel(yh, yr) < 2e-2
+            assert rel(gh[0], gr[0]) < 4e-2, (wide_min, rel(gh[0], gr[0]))
+            outs.append(gh[0].float())
+    finally:
+        H._lib.d3d_attn_bwd_cfg(0)
+    assert rel(outs[0], outs[1]) < 1e-2
+
+
 def test_attention_spiky(H):
     """A key that dominates one query's softmax in a late key block forces the
     online-softmax rescale branch."""
