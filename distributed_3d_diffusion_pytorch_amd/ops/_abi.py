@@ -37,6 +37,7 @@ SIGNATURES = {
     "d3d_gemm_mf": [I],
     "d3d_gemm_w8_waves": [I],
     "d3d_attn_bwd_cfg": [I],
+    "d3d_attn_fwd_cfg": [I],
     "d3d_colsum_jobs": [P, I, P],
     "d3d_conv_halo_cfg": [I],
     "d3d_conv_res_cfg": [I],

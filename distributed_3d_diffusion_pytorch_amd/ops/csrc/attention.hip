@@ -25,8 +25,11 @@
 // into a per-key-block fp32 slab, and the slabs are summed in fixed order
 // (deterministic, no atomics).  The softmax-backward row term
 // D = rowsum(dO * O) is formed in the kernel while the query tile loads (no
-// preprocessing launch), and a single-key-block sequence (L = 64: the 8x8
-// level) writes bf16 dQ directly (no slab, no conversion launch).
+// preprocessing launch), and a sequence one workgroup covers (L = 64 with
+// 64-key workgroups; 64 < L <= 256 with the 8-wave 256-key workgroup that is
+// the default at head dim 64) writes bf16 dQ directly (no slab, no
+// conversion launch).  The forward likewise has a one-workgroup-per-(image,
+// head) form for 64 < L <= 256 with all of K / V resident in LDS.
 #include "common.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -59,21 +62,26 @@ __device__ __forceinline__ int swz(int row, int chunk) {
 }
 
 // ------------------------------------------------------------ forward ----
-template <int D>
-__global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                  float* __restrict__ lse, int L, int C, int heads, int cross,
-                                                  float scale) {
+// KALL: one workgroup per (image, head) for L <= 256 -- 16 waves, one per 16
+// queries, with the whole K / V of the sequence staged in LDS once (one
+// barrier); the 64-query workgroups each re-load every K / V block and wait
+// on it (prefetched one block ahead, still one round trip per block).
+template <int D, bool KALL = false>
+__global__ void __launch_bounds__(KALL ? 1024 : 256) attn_fwd_k(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                               float* __restrict__ lse, int L, int C, int heads,
+                                                               int cross, float scale) {
   constexpr int VS = D + 16;                 // padded V row (tr reads)
   constexpr int KC = D / 32;                 // 32-wide k chunks over head dim
   constexpr int DT = D / 16;                 // 16-wide dv tiles
-  __shared__ __attribute__((aligned(16))) bf16 Ks[64 * D];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[64 * VS];
+  constexpr int KR = KALL ? 256 : 64, NT = KALL ? 1024 : 256;     // staged key rows, threads
+  __shared__ __attribute__((aligned(16))) bf16 Ks[KR * D];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[KR * VS];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int qblk = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
   const int nkv = cross ? (n ^ 1) : n;
   const int g = lane >> 4, fr = lane & 15;
   const long C3 = 3L * C;
-  const int q = qblk * 64 + w * 16 + fr;
+  const int q = qblk * (NT / 4) + w * 16 + fr;
   const bool qok = q < L;                    // ragged last query block (L % 64 != 0)
   const bf16* qrow = qkv + ((long)n * L + (qok ? q : 0)) * C3 + h * D;
   bf16x8 qf[KC];
@@ -91,12 +99,12 @@ __global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, 
   // cooperative K/V block loads, one block ahead: block kb + 64 is in flight
   // in registers while block kb computes (was one HBM round trip per block)
   constexpr int CH = D / 8;                  // chunks per row
-  constexpr int NKV = 64 * CH / 256;         // chunks per thread of each of K / V
+  constexpr int NKV = KR * CH / NT;          // chunks per thread of each of K / V
   bf16x8 kr[NKV], vr[NKV];
   auto fetch = [&](int kb) {
 #pragma unroll
     for (int i = 0; i < NKV; ++i) {
-      int idx = tid + i * 256;
+      int idx = tid + i * NT;
       int r = idx / CH, c = idx % CH;
       const bool kok = kb + r < L;
       const bf16* src = qkv + ((long)nkv * L + (kok ? kb + r : 0)) * C3 + h * D + c * 8;
@@ -104,24 +112,37 @@ __global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, 
       vr[i] = kok ? *reinterpret_cast<const bf16x8*>(src + 2 * C) : bf16x8{};
     }
   };
-  fetch(0);
-  for (int kb = 0; kb < L; kb += 64) {
+  auto stage = [&]() {
 #pragma unroll
     for (int i = 0; i < NKV; ++i) {
-      int idx = tid + i * 256;
+      int idx = tid + i * NT;
       int r = idx / CH, c = idx % CH;
       *reinterpret_cast<bf16x8*>(Ks + swz<D>(r, c)) = kr[i];
       *reinterpret_cast<bf16x8*>(Vs + r * VS + c * 8) = vr[i];
     }
-    if (kb + 64 < L) fetch(kb + 64);
+  };
+  fetch(0);
+  if constexpr (KALL) {                      // every key of the sequence (rows past L zero), one barrier
+    stage();
     __syncthreads();
+    if (w * 16 >= L) return;                 // no queries for this wave (no barrier follows)
+  }
+  for (int kb = 0; kb < L; kb += 64) {
+    if constexpr (!KALL) {
+      stage();
+      if (kb + 64 < L) fetch(kb + 64);
+      __syncthreads();
+    }
+    // this key block's rows (the swizzle depends on row & 7 only)
+    const bf16* Kb = Ks + (KALL ? kb * D : 0);
+    const bf16* Vb = Vs + (KALL ? kb * VS : 0);
     f32x4 s[4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
-        bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + swz<D>(16 * kt + fr, 4 * kc + g));
+        bf16x8 a = *reinterpret_cast<const bf16x8*>(Kb + swz<D>(16 * kt + fr, 4 * kc + g));
         s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[kc], s[kt], 0, 0, 0);
       }
     }
@@ -159,11 +180,11 @@ __global__ void __launch_bounds__(256) attn_fwd_k(const bf16* __restrict__ qkv, 
       int r1 = 32 * kc2 + 4 * g + qq, r2 = 32 * kc2 + 16 + 4 * g + qq;
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
-        bf16x8 va = tr8(Vs, VS, r1, r2, 16 * t + 4 * pc);
+        bf16x8 va = tr8(Vb, VS, r1, r2, 16 * t + 4 * pc);
         o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[t], 0, 0, 0);
       }
     }
-    __syncthreads();
+    if constexpr (!KALL) __syncthreads();
   }
   if (!qok) return;
   const float inv = 1.f / l;
@@ -418,10 +439,20 @@ __global__ void dq_convert_k(const float* __restrict__ dq, bf16* __restrict__ dq
 
 // qkv: [N, L, 3C] bf16; out: [N, L, C] bf16; lse: [N, heads, L] fp32.
 // D = C/heads in {64, 128}; any L >= 1 (a ragged last 64-block is masked).
+// One 16-wave workgroup per (image, head) for 64 < L <= 256 at head dim 64 once
+// there are at least this many (image, head) pairs: bs128 (1024 pairs) +0.1%;
+// at bs16 (128 pairs, half the CUs idle) the 64-query workgroups win by 0.5%.
+static int g_attn_fwd_all_min = 512;
+D3D_API void d3d_attn_fwd_cfg(int min_pairs) { g_attn_fwd_all_min = min_pairs; }
 D3D_API int d3d_attn_fwd(const void* qkv, void* out, float* lse, int N, int L, int C, int heads, int cross,
                          float scale, hipStream_t st) {
   int D = C / heads;
   if (L < 1) return (int)hipErrorInvalidValue;
+  if (D == 64 && L > 64 && L <= 256 && N * heads >= g_attn_fwd_all_min) {
+    hipLaunchKernelGGL((attn_fwd_k<64, true>), dim3(1, heads, N), dim3(1024), 0, st, (const bf16*)qkv, (bf16*)out, lse,
+                       L, C, heads, cross, scale);
+    return (int)hipGetLastError();
+  }
   dim3 grid((L + 63) / 64, heads, N);
   if (D == 64)
     hipLaunchKernelGGL(attn_fwd_k<64>, grid, dim3(256), 0, st, (const bf16*)qkv, (bf16*)out, lse, L, C, heads, cross,

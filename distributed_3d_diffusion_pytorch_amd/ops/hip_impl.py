@@ -879,6 +879,8 @@ if os.environ.get("D3D_WGRAD_HALO"):                   # A/B knob "on[,blocks[,s
     _lib.d3d_wgrad_group_halo(_hv[0], _hv[1], _hv[2])
 if os.environ.get("D3D_WGRAD_HALO_BIG"):               # A/B knob "blocks,lg2": halo target of the big flushes
     _lib.d3d_wgrad_group_halo_big(*[int(v) for v in os.environ["D3D_WGRAD_HALO_BIG"].split(",")])
+if os.environ.get("D3D_ATTN_FWD_ALL_MIN"):             # A/B knob: min (image, head) pairs for the
+    _lib.d3d_attn_fwd_cfg(int(os.environ["D3D_ATTN_FWD_ALL_MIN"]))   # one-workgroup-per-head forward
 if os.environ.get("D3D_ATTN_WIDE_MIN"):               # A/B knob: (image, head) pairs from which one workgroup owns
     _lib.d3d_attn_bwd_cfg(int(os.environ["D3D_ATTN_WIDE_MIN"]))   # all keys of an attention backward (L <= 256)
 if os.environ.get("D3D_WGRAD_HALO_PK"):                # A/B knob: pixels per halo K-step (32 / 64, the latter at W >= 64)

@@ -584,6 +584,41 @@ def test_attention_backward_one_workgroup_per_head(H, N, L, cross):
     assert rel(outs[0], outs[1]) < 1e-2
 
 
+@pytest.mark.parametrize("N,L,cross", [(4, 256, False), (4, 256, True), (2, 196, True), (2, 100, False),
+                                         (2, 65, True)])
+def test_attention_forward_one_workgroup_per_head(H, N, L, cross):
+    """Head dim 64, 64 < L <= 256: one 16-wave workgroup per (image, head)
+    stages all K / V in LDS once (the default from 512 (image, head) pairs;
+    d3d_attn_fwd_cfg(0) forces it, d3d_attn_fwd_cfg(1 << 30) the 64-query
+    workgroups).  Output and saved log-sum-exp against fp32 and
+    against the 64-query path."""
+    torch.manual_seed(9)
+    C = 256
+    qkv = torch.randn(N, L, 3 * C, device=DEV).to(BF)
+    H._ensure_impl()
+    outs = []
+    try:
+        for all_ in (0, 1 << 30):
+            H._lib.d3d_attn_fwd_cfg(all_)
+            yh = H.attention(qkv, 4, cross)
+            yr = T.attention(qkv.float(), 4, cross)
+            assert rel(yh, yr) < 2e-2, (all_, rel(yh, yr))
+            out = torch.empty(N, L, C, device=DEV, dtype=BF)
+            lse = torch.empty(N, 4, L, device=DEV)
+            assert H._lib.d3d_attn_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr(), N, L, C, 4, int(cross),
+                                       64 ** -0.5, H._st()) == 0
+            q, k = qkv[..., :C].float(), qkv[..., C:2 * C].float()
+            if cross:
+                k = k.view(N // 2, 2, L, C).flip(1).reshape(N, L, C)
+            s = torch.einsum("nqhd,nkhd->nhqk", q.view(N, L, 4, 64), k.view(N, L, 4, 64)) * 64 ** -0.5
+            assert rel(lse, torch.logsumexp(s, -1)) < 1e-3
+            outs.append((out.float(), lse))
+    finally:
+        H._lib.d3d_attn_fwd_cfg(512)
+    assert rel(outs[0][0], outs[1][0]) < 1e-2
+    assert rel(outs[0][1], outs[1][1]) < 1e-4
+
+
 def test_attention_spiky(H):
     """A key that dominates one query's softmax in a late key block forces the
     online-softmax rescale branch."""
