@@ -559,7 +559,8 @@ class XUNet(nn.Module):
                     if fence is not None and i == fence[0]:
                         cs.wait_event(fence[1])
                     outs = ops.film_batch(semb, [b.film.dense.weight for b in blocks],
-                                          [b.film.dense.bias for b in blocks], block_events=FILM_BLOCK_EVENTS)
+                                          [b.film.dense.bias for b in blocks], block_events=FILM_BLOCK_EVENTS,
+                                          split=len(self.xunetblocks[i]))
                     for o in outs:
                         o.record_stream(main)       # read by the trunk's GN-FiLM kernels
                     ev = torch.cuda.Event()
@@ -579,8 +580,10 @@ class XUNet(nn.Module):
             for i, blocks in enumerate(self._film_groups()):
                 if fence is not None and i == fence[0]:
                     torch.cuda.current_stream().wait_event(fence[1])
+                # (split: the encoder blocks lead the level's group, _film_groups;
+                # the decoder blocks' FiLM weight gradients can start early)
                 outs = ops.film_batch(sembs[i], [b.film.dense.weight for b in blocks],
-                                      [b.film.dense.bias for b in blocks])
+                                      [b.film.dense.bias for b in blocks], split=len(self.xunetblocks[i]))
                 for b, o in zip(blocks, outs):
                     b.__dict__["_ss"] = o
         xz = batch.get("xz")

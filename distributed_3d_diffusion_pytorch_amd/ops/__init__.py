@@ -122,11 +122,12 @@ def cat_gn_silu_dense(a, b, gw, gb, dw, db, groups: int = 32, eps: float = 1e-5)
     return _t.cat_gn_silu_dense(a, b, gw, gb, dw, db, groups, eps)
 
 
-def film_batch(emb, weights, biases, block_events: bool = False):
+def film_batch(emb, weights, biases, block_events: bool = False, split: int = 0):
     """``dense_i(silu(emb))`` for every FiLM projection of one level
-    (``block_events``, HIP path: one GEMM and ready event per block)."""
+    (``block_events``, HIP path: one GEMM and ready event per block;
+    ``split``: blocks ``[split:]`` get their own, earlier weight-gradient job)."""
     if use_hip(emb):
-        return _h().film_batch(emb, weights, biases, block_events)
+        return _h().film_batch(emb, weights, biases, block_events, split)
     return _t.film_batch(emb, weights, biases)
 
 

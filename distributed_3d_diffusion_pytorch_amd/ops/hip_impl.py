@@ -34,6 +34,18 @@ _ZERO_PAGE: Dict[int, torch.Tensor] = {}
 _FILM_WGRAD = "tn"
 # level-batched FiLM forward of the big levels on hipBLASLt (plain GEMM + bias)
 _FILM_BLAS = os.environ.get("D3D_FILM_BLAS", "1") != "0"
+# FiLM weight gradients of a level in two jobs: the decoder blocks' (complete
+# early in the backward) as soon as their GN-FiLM backwards have written their
+# d(scale|shift) columns, the encoder blocks' after the level's last block --
+# instead of one level-wide job after that last block (the first encoder
+# block: the 64x64 level's whole weight gradient, P = 1M rows, ran exposed at
+# the very end of the backward).  Measured (profiles/r6/film_early_wgrad.txt):
+# +0.7 % at bs16 (graph-captured step), -0.7 % at bs128 (eager step: its
+# weight-gradient stream is saturated, so the earlier job only delays the
+# conv weight gradients), and one job per BLOCK -3 % / -2 % (each re-reads the
+# level's [P, 1024] silu(e) operand).  D3D_FILM_EARLY_WGRAD: 1 (default)
+# graph-captured steps only, 2 always, 0 never.
+_FILM_EARLY = int(os.environ.get("D3D_FILM_EARLY_WGRAD", "1"))
 
 
 def set_conv_impl(impl: str) -> None:
@@ -766,7 +778,8 @@ class _GNFiLM(torch.autograd.Function):
         x, w, b, ss, stats = ctx.saved_tensors
         G, p, seed, ld = ctx.cfg
         dss = None
-        if ctx.slot is not None and ctx.needs_input_grad[3] and ctx.slot[0].width == ld:
+        into_slot = ctx.slot is not None and ctx.needs_input_grad[3] and ctx.slot[0].width == ld
+        if into_slot:
             # write d(scale|shift) straight into the level's shared dY buffer
             # so the batched FiLM backward runs one GEMM with no gather (the
             # kernel reads ss and writes dss with ONE row stride: only when
@@ -774,6 +787,8 @@ class _GNFiLM(torch.autograd.Function):
             holder, off = ctx.slot
             dss = holder.grad_slice(off, x.shape[-1])
         dx, dss, dg, db = _gn_bwd(2, x, dy.contiguous(), ss, stats, w, b, G, p, seed, dss=dss, ssld=ld)
+        if into_slot:
+            ctx.slot[0].block_ready(ctx.slot[1])      # this block's FiLM weight gradient can start
         return dx, dg, db, dss, None, None, None, None, None
 
 
@@ -1508,11 +1523,60 @@ class _FiLMSlot:
         self.buf = None
         self.want_events = want_events      # forward: one GEMM + ready event per block (film_batch)
         self.events = []
+        self.x2 = None                      # silu(e) [P, K]: the weight gradients' second operand
+        self.blocks = {}                    # column offset -> (weight, bias, width): early weight gradients
+        self.groups = []                    # block offsets per weight-gradient job (contiguous columns)
+        self.ready = set()                  # offsets whose d(scale|shift) is written
+        self.early = set()                  # offsets whose weight gradient is submitted
 
     def grad_slice(self, off: int, C: int) -> torch.Tensor:
         if self.buf is None:
             self.buf = torch.empty(*self.shape, self.width, dtype=BF16, device=self.device)
         return self.buf[..., off: off + 2 * C]
+
+    def block_ready(self, off: int) -> None:
+        """The GN-FiLM backward of the block at column ``off`` has written its
+        d(scale|shift) slice of :attr:`buf`: once every block of its group
+        has, submit the group's weight gradient (it overlaps the rest of the
+        backward)."""
+        if off not in self.blocks or self.buf is None:
+            return
+        self.ready.add(off)
+        for grp in self.groups:
+            if grp[0] not in self.early and all(o in self.ready for o in grp):
+                if _film_group_wgrad(self.buf.view(-1, self.width), grp, self.blocks, self.x2):
+                    self.early.update(grp)
+
+
+def _film_group_wgrad(dy: torch.Tensor, grp, blocks, x2: torch.Tensor) -> bool:
+    """The weight / bias gradients of FiLM blocks ``grp`` (column offsets of
+    contiguous blocks of the level's [P, S] d(scale|shift) buffer ``dy``) as
+    ONE sink job: split-K MFMA GEMM over their columns against ``x2`` =
+    silu(e), then the reduction scatters rows into each block's gradients.
+    False when a parameter is not sink-managed or the GEMM cannot take the
+    shape (the level-wide job then covers the blocks)."""
+    ps = [blocks[o] for o in grp]
+    tw = [SINK.target(w) for w, _, _ in ps]
+    tb = [SINK.target(b) for _, b, _ in ps]
+    if any(t is None for t in tw + tb):
+        return False
+    c0, c1 = grp[0], grp[-1] + ps[-1][2]
+    cols = dy[:, c0:c1]
+    rows, K = x2.shape
+    sp = _lib.d3d_wgrad_tn_plan(c1 - c0, K, rows, cols.stride(0), K)
+    if sp <= 0:
+        return False
+    n = len(grp)
+
+    def job(cols=cols, x2=x2, tw=tw, tb=tb, sp=sp):
+        ws, bws, used = wgrad_tn(cols, x2, sp)
+        row0 = (ctypes.c_int * n)(*[o - c0 for o in grp])
+        wdst = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tw])
+        bdst = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tb])
+        _chk(_lib.d3d_wgrad_scatter(ws.data_ptr(), c1 - c0, K, used, 1, bws.data_ptr(), bws.shape[0], n, row0, wdst,
+                                    bdst, _st()), "film_group_wgrad")
+    SINK.submit(x2.device, job, (cols, x2), [p for w, b, _ in ps for p in (w, b)])
+    return True
 
 
 class _FiLMBatch(torch.autograd.Function):
@@ -1526,7 +1590,7 @@ class _FiLMBatch(torch.autograd.Function):
     reduction scatters rows into each block's parameter gradient."""
 
     @staticmethod
-    def forward(ctx, e, slot, n, se, *wb):
+    def forward(ctx, e, slot, n, se, split, *wb):
         Ws, Bs = wb[:n], wb[n:]
         shp = e.shape
         K = shp[-1]
@@ -1568,9 +1632,18 @@ class _FiLMBatch(torch.autograd.Function):
         ctx.n, ctx.slot, ctx.shp = n, slot, shp
         ctx.params = (Ws, Bs)
         ctx.widths = [w.shape[0] for w in Ws]
+        early_on = _FILM_EARLY == 2 or (_FILM_EARLY == 1 and torch.cuda.is_current_stream_capturing())
+        if early_on and _FILM_WGRAD == "tn" and 0 < split < n and all(ctx.needs_input_grad[5:5 + 2 * n]) and \
+                all(SINK.managed(p) for p in wb):
+            slot.x2 = x2
+            offs = [0]
+            for w, b, wd in zip(Ws, Bs, ctx.widths):
+                slot.blocks[offs[-1]] = (w, b, wd)
+                offs.append(offs[-1] + wd)
+            slot.groups = [offs[:split], offs[split:n]]
         for i, (w, b) in enumerate(zip(Ws, Bs)):
-            SINK.use(w, ctx.needs_input_grad[4 + i])
-            SINK.use(b, ctx.needs_input_grad[4 + n + i])
+            SINK.use(w, ctx.needs_input_grad[5 + i])
+            SINK.use(b, ctx.needs_input_grad[5 + n + i])
         y = y.view(*shp[:-1], S)
         outs, off = [], 0
         for wd in ctx.widths:
@@ -1604,7 +1677,8 @@ class _FiLMBatch(torch.autograd.Function):
             for g, o, wd in zip(gs, offs, ctx.widths):
                 if g is not None:
                     dy[:, o: o + wd].copy_(g.reshape(-1, wd))
-        slot.buf = None
+        early, blocks, groups = slot.early, slot.blocks, slot.groups
+        slot.buf, slot.x2, slot.blocks, slot.groups, slot.ready, slot.early = None, None, {}, [], set(), set()
         rows, K = x2.shape
         dx = None
         if ctx.needs_input_grad[0]:
@@ -1618,7 +1692,14 @@ class _FiLMBatch(torch.autograd.Function):
                 _chk(_lib.d3d_dsilu(e2.data_ptr(), ds.data_ptr(), dx.data_ptr(), dx.numel(), _st()), "dsilu")
             dx = dx.view(shp)
         grads_w, grads_b = [None] * n, [None] * n
-        need_w = any(ctx.needs_input_grad[4: 4 + n])
+        need_w = any(ctx.needs_input_grad[5: 5 + n])
+        if need_w and early:
+            # a group's weight gradients were submitted by its GN-FiLM
+            # backwards (_FiLMSlot.block_ready); the rest go one job per group
+            for grp in groups:
+                if grp[0] not in early and not _film_group_wgrad(dy, grp, blocks, x2):
+                    raise RuntimeError("FiLM weight gradient: early and level-wide jobs mixed")
+            need_w = False
         if need_w:
             tw = [SINK.target(w) for w in Ws]
             tb = [SINK.target(b) for b in Bs]
@@ -1661,15 +1742,18 @@ class _FiLMBatch(torch.autograd.Function):
                 job()
                 grads_w = [t.view(w.shape) for t, w in zip(tw, Ws)]
                 grads_b = tb
-        return (dx, None, None, None, *grads_w, *grads_b)
+        return (dx, None, None, None, None, *grads_w, *grads_b)
 
 
-def film_batch(emb, weights, biases, block_events=False):
+def film_batch(emb, weights, biases, block_events=False, split=0):
     """Level-batched FiLM projections ``dense_i(silu(emb))`` of the per-level
     pre-activation embedding -> tuple of ``[N,H,W,2C_i]`` modulations (column
     slices of one GEMM output; GN-FiLM reads them strided).  ``block_events``:
     one GEMM per block with a ready event attached to each output as
-    ``_d3d_ready`` (consumers on another stream wait per block)."""
+    ``_d3d_ready`` (consumers on another stream wait per block).  ``split``:
+    the weight gradients of blocks ``[split:]`` (the decoder's, done first in
+    the backward) run as their own job as soon as those blocks' backwards
+    are through; 0: one job for the level."""
     _need_bf16(emb)
     K = emb.shape[-1]
     widths = [w.shape[0] for w in weights]
@@ -1681,7 +1765,7 @@ def film_batch(emb, weights, biases, block_events=False):
     se = getattr(emb, "_d3d_silu", None)          # silu(emb) written by the conditioning conv (cond_conv)
     if se is not None and (se.shape != emb.shape or not se.is_contiguous() or not emb.is_contiguous()):
         se = None
-    outs = _FiLMBatch.apply(emb.contiguous(), slot, len(weights), se, *weights, *biases)
+    outs = _FiLMBatch.apply(emb.contiguous(), slot, len(weights), se, int(split), *weights, *biases)
     off = 0
     for i, (o, wd) in enumerate(zip(outs, widths)):
         o._d3d_slot = (slot, off)

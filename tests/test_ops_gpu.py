@@ -812,6 +812,48 @@ def test_film_batch_with_gn_film(H, chans, N, Hh, mode):
         assert rel(a, b) < 3e-2, rel(a, b)
 
 
+def test_film_early_weight_gradients(H, monkeypatch):
+    """Training step with sink-managed parameters: each level's FiLM weight
+    gradients run as two jobs -- the decoder blocks' submitted by the GN-FiLM
+    backward that completes them (overlapping the rest of the backward), the
+    encoder blocks' after -- instead of one level-wide job after the level's
+    last block; the flat gradient matches the level-wide path."""
+    from distributed_3d_diffusion_pytorch_amd.config import make_config
+    from distributed_3d_diffusion_pytorch_amd.engine import Trainer
+    from distributed_3d_diffusion_pytorch_amd.parallel import DistContext
+    from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
+    ctx = DistContext(device=torch.device("cuda", 0))
+    batch = next(SyntheticBatches(8, 64, "cuda", seed=5))
+    calls = []
+    orig = H._film_group_wgrad
+
+    def counting(*a):
+        r = orig(*a)
+        calls.append(r)
+        return r
+
+    monkeypatch.setattr(H, "_film_group_wgrad", counting)
+    grads, nblocks = [], 0
+    for early in (True, False):
+        monkeypatch.setattr(H, "_FILM_EARLY", 2 if early else 0)
+        torch.manual_seed(0)
+        cfg = make_config(None, {"model.H": 64, "model.W": 64, "data.imgsize": 64, "global_batch": 8,
+                                 "micro_batch": 0, "data.synthetic": True, "log_every": 0, "ckpt_every": 0,
+                                 "graph": False, "optim.warmup_examples": 0})
+        tr = Trainer(cfg, ctx)
+        tr.optim.zero_in_step = False          # keep the step's gradient for the comparison
+        tr.train_step(*batch)
+        torch.cuda.synchronize()
+        grads.append(tr.flat.grad.clone())
+        if early:
+            nblocks = 2 * len(tr.model._film_groups())        # two jobs per level
+            assert len(calls) == nblocks and all(calls), (len(calls), nblocks)
+        del tr
+    assert len(calls) == nblocks                # the level-wide run submitted no per-block job
+    assert torch.isfinite(grads[0]).all()
+    assert rel(grads[0], grads[1]) < 1e-4, rel(grads[0], grads[1])
+
+
 @pytest.mark.parametrize("P,M,N,ldy,splits", [(16384, 2048, 1024, 2048, 0), (8192, 4608, 1024, 4608, 0),
                                                (256, 200, 136, 200, 1), (1024, 264, 520, 384, 2),
                                                (4096, 512, 256, 512, 3), (128, 256, 256, 256, 1)])
