@@ -93,6 +93,11 @@ class Trainer:
             # late (D3D_WGRAD_DEFER_BATCH overrides)
             comm = self.reducer is not None and self.reducer.active
             SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "16" if comm else "64"))
+            # bucket-aware flushing (opt-in): a queued job that completes a
+            # bucket flushes the queue at once, so batches can be big without
+            # delaying any bucket's reduction (profiles/r6/bucket_flush.txt)
+            SINK.bucket_flush = self.reducer.completes_bucket if comm and \
+                os.environ.get("D3D_WGRAD_BUCKET_FLUSH", "0") == "1" else None
         oc = cfg.optim
         self.optim = FusedAdam(self.flat, oc.lr, oc.betas, oc.eps, oc.weight_decay,
                                ema_decay_for(cfg.global_batch, oc.ema_halflife_examples))

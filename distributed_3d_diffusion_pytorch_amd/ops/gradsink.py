@@ -48,6 +48,10 @@ import torch
 
 
 _PRIO = 0          # HIP stream priority of the weight-gradient stream (higher measured slower)
+# diagnostic switch (never set in training): collectives wait only for the
+# issuing stream, as before the round-5 / round-6 ordering fixes -- used to
+# confirm what the race probe catches (tools/diag_bucket_flush_race.py)
+_DIAG_NO_STREAM_WAITS = os.environ.get("D3D_DIAG_SINK_NO_STREAM_WAITS", "0") == "1"
 
 
 class GradSink:
@@ -81,6 +85,12 @@ class GradSink:
         # grouped weight-gradient launcher (set by ops.hip_impl): runs a
         # flush's job descriptors as one launch + one slab reduce
         self.group_fn: Optional[Callable[[list], None]] = None
+        # bucket-aware flushing (set by the trainer, D3D_WGRAD_BUCKET_FLUSH):
+        # called with the parameter indices a flush of the queue would
+        # complete; True = that completes an all-reduce bucket, flush now
+        # instead of waiting for defer_batch jobs
+        self.bucket_flush: Optional[Callable[[list], bool]] = None
+        self._qcount: Dict[int, int] = {}
 
     def attach(self, params, views, notify: Optional[Callable[[int], None]] = None) -> None:
         # the parameter objects themselves are kept: a key is only trusted
@@ -215,7 +225,7 @@ class GradSink:
             self._queue.append((fn, tuple(t for t in keep if t is not None), tuple(p for p in done if p is not None),
                                 torch.cuda.current_stream(dev.index if dev.index is not None else None), spec))
             self._queue_end_callback()
-            if len(self._queue) >= self.defer_batch:
+            if len(self._queue) >= self.defer_batch or self._completes_bucket(done):
                 self.flush()
             return
         with self.producer(dev, *keep):
@@ -227,9 +237,22 @@ class GradSink:
             if p is not None:
                 self.done(p)
 
+    def _completes_bucket(self, done) -> bool:
+        """Bucket-aware flushing: would reporting the queued jobs' parameters
+        complete an all-reduce bucket?  (A parameter completes when the queue
+        holds all of its remaining uses.)"""
+        if self.bucket_flush is None:
+            return False
+        for p in done:
+            if p is not None and self.managed(p):
+                self._qcount[id(p)] = self._qcount.get(id(p), 0) + 1
+        full = [self.index[k] for k, c in self._qcount.items() if self.uses.get(k, 0) == c]
+        return bool(full) and self.bucket_flush(full)
+
     def flush(self) -> None:
         """Issue the queued weight-gradient jobs on the side stream behind ONE
         wait on the compute stream, then report their parameters."""
+        self._qcount = {}
         if not self._queue:
             return
         q, self._queue = self._queue, []
@@ -328,6 +351,8 @@ class GradSink:
         cur = torch.cuda.current_stream(idx)
         others = [s for s in ([main] if main is not None else []) + [c for c in self._compute if c.device.index == idx]
                   if s.cuda_stream != cur.cuda_stream]
+        if _DIAG_NO_STREAM_WAITS:
+            others = []                     # diagnostic only: the round-5 ordering (tools/diag_bucket_flush_race.py)
         if not self._forked and not others:
             # every deposit so far was made on this stream: RCCL's stream waits for it
             yield
@@ -351,6 +376,7 @@ class GradSink:
         end-of-backward flag: a backward that raised (e.g. a failed graph
         capture) drops autograd's final callbacks, and a stale flag would stop
         the next backward from queueing its flush + join."""
+        self._qcount = {}
         self.uses = {}
         self.seen = set()
         self._queue = []

@@ -146,6 +146,17 @@ class GradReducer:
         if self._pending[b] == 0:
             self._launch(b)
 
+    def completes_bucket(self, params) -> bool:
+        """True when reporting parameters ``params`` (indices) would complete
+        a bucket not yet launched (the sink's bucket-aware flush)."""
+        if not self.enabled or not self.active:
+            return False
+        cnt = {}
+        for i in params:
+            b = self.param_bucket[i]
+            cnt[b] = cnt.get(b, 0) + 1
+        return any(not self._launched[b] and self._pending[b] <= c for b, c in cnt.items())
+
     def _launch(self, b: int) -> None:
         if self._launched[b]:
             return

@@ -1575,7 +1575,7 @@ def _graph_comm_worker(out_dir, graph_comm="1"):
     cleanup()
 
 
-def _graph_comm_1rank_worker(out_dir):
+def _graph_comm_1rank_worker(out_dir, bucket_flush=False):
     """The multi-GPU step topology on ONE GPU: a 1-rank RCCL group with the
     bucketed reducer forced on (dist.force_comm), so graph A is captured with
     the real bucket all-reduces, the sink's collective flushes, the
@@ -1589,6 +1589,10 @@ def _graph_comm_1rank_worker(out_dir):
     from distributed_3d_diffusion_pytorch_amd.parallel.dist import rccl_env_defaults
     from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
     rccl_env_defaults()
+    if bucket_flush:
+        # bucket-aware sink flushing with big batches (the round-5 NaN variant)
+        os.environ["D3D_WGRAD_BUCKET_FLUSH"] = "1"
+        os.environ["D3D_WGRAD_DEFER_BATCH"] = "64"
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, timeout=datetime.timedelta(seconds=120))
@@ -1613,6 +1617,7 @@ def _graph_comm_1rank_worker(out_dir):
                                      "dist.grad_dtype": gd, "dist.force_comm": True})
             tr = Trainer(cfg, ctx)
             assert tr.reducer is not None and tr.reducer.active
+            assert (tr.sink.bucket_flush is not None) == bucket_flush
             # race probe: each collective reduces a snapshot of its bucket taken
             # at issue time (result discarded: 1-rank identity); after every step
             # the snapshots must equal the complete gradient bit for bit
@@ -1641,7 +1646,8 @@ def _graph_comm_1rank_worker(out_dir):
     cleanup()
 
 
-def test_graph_step_captured_collectives_one_rank(tmp_path):
+@pytest.mark.parametrize("bucket_flush", [False, True])
+def test_graph_step_captured_collectives_one_rank(tmp_path, bucket_flush):
     """Graph A captured with the real bucketed RCCL all-reduces (1-rank
     group), deferred update on, fp32 and bf16 payloads, and a two-micro-batch
     step (leading graph gA0 captured too): comm_mode "graph", parameters equal
@@ -1655,12 +1661,14 @@ def test_graph_step_captured_collectives_one_rank(tmp_path):
     measure_comm works in every mode.  Every row runs the reducer's race probe
     (GradReducer.enable_race_probe): a collective that read its bucket before
     the last deposit landed -- invisible to a 1-rank in-place all-reduce --
-    fails the test."""
+    fails the test.  ``bucket_flush``: the same with bucket-aware weight-
+    gradient flushing and 64-job batches (D3D_WGRAD_BUCKET_FLUSH=1: a queued
+    job that completes a bucket flushes the queue at once)."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from distributed_3d_diffusion_pytorch_amd.parallel import spawn
     import test_ops_gpu as me
-    spawn(me._graph_comm_1rank_worker, 1, (str(tmp_path),))
+    spawn(me._graph_comm_1rank_worker, 1, (str(tmp_path), bucket_flush))
     rows = open(tmp_path / "gc1.txt").read().split("\n")
     assert [r.split()[0] for r in rows] == ["fp32/0/1", "bf16/0/1", "fp32/2/1", "fp32/0/0", "bf16/0/0", "fp32/2/0",
                                             "fp32/0/p", "bf16/0/p"]

@@ -19,6 +19,7 @@
 #   prof:<bs>                  rocprofv3 kernel trace of the step + rpstats (stats, grid, busy, gaps,
 #                              solo, families)
 #   envprof:<VAR=val>:<bs>     the same trace with an environment knob set
+#   envfc:<V=x[+V2=y]>:<bs>:<graph|seg>  same-box A/B of knobs on the 1-rank RCCL rehearsal (bench --force_comm)
 #   pmc:<bs>                   step-level hardware counters (three --pmc passes) -> table_bs<bs>.txt
 #   kbench:<tool.py>[:args]    a tools/ kernel micro-benchmark (args: comma-separated)
 #   fc:<bs>:<graph|seg|post>[:<MiB>]  1-rank RCCL rehearsal of the multi-GPU step (bench --force_comm) in one comm
@@ -125,6 +126,15 @@ for step in "$@"; do
       D3D_GRAPH_COMM=$gcm D3D_GRAPH_SEG=$gsg bench "fc_${b}${c}_b$a" --force_comm --global_batch "$a" \
         --steps "$(steps_for "$a")" --warmup 4
       python3 -c "import json;d=json.loads(open('$O/fc_${b}${c}_b$a.json').read().strip().splitlines()[-1]);print(d.get('comm'))" ;;
+    envfc)                       # envfc:<V=x[+V2=y]>:<bs>:<graph|seg>: fc rehearsal with knobs vs without, interleaved x2
+      case $c in graph) gcm=1 ;; seg) gcm=0 ;; *) die "envfc mode $c" 2 ;; esac
+      for r in 1 2; do
+        (for kv in ${a//+/ }; do export "${kv?}"; done
+         D3D_GRAPH_COMM=$gcm D3D_GRAPH_SEG=64 bench "envfc_${c}_b${b}_$r" --force_comm --global_batch "$b" \
+           --steps "$(steps_for "$b")" --warmup 4) || exit $?
+        D3D_GRAPH_COMM=$gcm D3D_GRAPH_SEG=64 bench "envfc_base_${c}_b${b}_$r" --force_comm --global_batch "$b" \
+          --steps "$(steps_for "$b")" --warmup 4
+      done ;;
     prof) prof "$a" ;;
     envprof)                     # envprof:<VAR=val>:<bs>: a trace with the knob set (files get a _<VAR> suffix)
       var=${a%%=*}
