@@ -105,6 +105,7 @@ class ResnetBlock(nn.Module):
 
     def forward(self, x, semb: torch.Tensor) -> torch.Tensor:
         skip = slot = None
+        fused = None
         if isinstance(x, tuple):
             # decoder: x is the skip concatenation [h | hs] (xunet.py:521-531),
             # never materialised -- GN0 and the 1x1 skip read both halves
@@ -122,10 +123,18 @@ class ResnetBlock(nn.Module):
             if slot is not None:
                 # a decoder skip concat that also reads x deposits its gradient here (ops _CatGNDense)
                 x._d3d_res_slot = slot
-            h = self.groupnorm0(x, silu=True, res_slot=slot)
-        # the conv epilogues also emit the partial statistics of the GroupNorm
-        # that reads their output (GN1 here; the next block's GN0 below)
-        h = ops.conv3x3(h, self.conv1.weight, self.conv1.bias, gn_groups=self.groupnorm1.gn.num_groups)
+            # GN0 + SiLU inside conv1's input staging where the HIP conv takes it
+            fused = ops.gn_silu_conv3x3(x, self.groupnorm0.gn.weight, self.groupnorm0.gn.bias, self.conv1.weight,
+                                        self.conv1.bias, self.groupnorm0.gn.num_groups, self.groupnorm0.gn.eps,
+                                        gn1_groups=self.groupnorm1.gn.num_groups, res_slot=slot)
+            if fused is None:
+                h = self.groupnorm0(x, silu=True, res_slot=slot)
+        if fused is not None:
+            h = fused
+        else:
+            # the conv epilogues also emit the partial statistics of the GroupNorm
+            # that reads their output (GN1 here; the next block's GN0 below)
+            h = ops.conv3x3(h, self.conv1.weight, self.conv1.bias, gn_groups=self.groupnorm1.gn.num_groups)
         ss = self.__dict__.pop("_ss", None)     # precomputed by the level-batched FiLM
         ev = self.__dict__.pop("_ss_event", None)
         if ev is not None:                      # ... on the conditioning stream: first read here

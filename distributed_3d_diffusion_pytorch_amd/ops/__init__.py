@@ -198,6 +198,15 @@ __all__ = ["diffusion_inputs", "diff_loss_nhwc", "group_norm", "gn_film", "conv3
            "use_hip", "load_library", "library_error", "lib_path"]
 
 
+def gn_silu_conv3x3(x, gw, gb, cw, cb, groups: int = 32, eps: float = 1e-5, gn1_groups: int = 0, res_slot=None):
+    """``conv3x3(silu(group_norm(x)))``: HIP path with the GroupNorm + SiLU in
+    the conv's input staging when the shape allows it (``None`` otherwise:
+    the caller runs the two ops)."""
+    if use_hip(x) and _h().gn_silu_conv_ok(x, cw.shape[0], groups):
+        return _h().gn_silu_conv3x3(x, gw, gb, cw, cb, groups, eps, gn1_groups, res_slot)
+    return None
+
+
 def res_slot(x: torch.Tensor):
     """A residual-gradient hand-off slot for x (HIP path), else None."""
     if use_hip(x):

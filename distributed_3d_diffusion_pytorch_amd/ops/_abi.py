@@ -26,6 +26,8 @@ SIGNATURES = {
     "d3d_gn_apply2": [I, P, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, I, P, P],
     "d3d_set_words64": [P, I, C.c_longlong, C.c_longlong, C.c_longlong, P],
     "d3d_sgemm_jobs": [P, I, I, P],
+    "d3d_gn_ab": [P, P, P, P, P, I, I, I, I, F, I, P],
+    "d3d_gn_ab_silu": [P, P, P, I, I, I, P],
     "d3d_gn_img_cfg": [I],
     "d3d_gn_img_ok": [I, I, I],
     "d3d_gn_img_fwd": [I, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, P, P],
@@ -69,6 +71,8 @@ SIGNATURES = {
     "d3d_pack_conv_weight": [P, P, I, I, I, I, I, P],
     "d3d_conv": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P],
     "d3d_conv2": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P],
+    "d3d_conv3_gn_ok": [I, I, I, I, I],
+    "d3d_conv3_gn": [P, P, P, P, I, I, I, I, I, I, P, I, IP, P, P],
     "d3d_conv3": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, I, P, I, IP, P, IP, P],
     "d3d_conv_plan": [I, I, I, I, I, I],
     "d3d_set_conv_korder": [I],

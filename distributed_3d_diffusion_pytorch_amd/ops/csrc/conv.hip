@@ -993,12 +993,25 @@ __device__ __forceinline__ void halo_issue_b(bf16* sH, const bf16* I, int in_byt
 // P2 (with AU): one barrier per PAIR of taps over an 8-slot weight ring (the
 // LDS budget of the 64-wide tile: 2 x 48 KB halo + 64 KB ring = all 160 KB);
 // halves the per-MFMA barrier / wait cost.  Needs an even chunk count.
-template <int OWT, bool TRANS, int BNT = 512, bool PF = false, bool RES = true, bool AU = false, bool P2 = false>
+// GNA (with AU, forward, single taps per barrier): the input is the
+// PRE-GroupNorm tensor x and the conv runs on silu(x * A + B) -- the
+// ResnetBlock's GN0 + SiLU folded into the halo staging (gab [Nimg][IC][2] =
+// (A, B) per image and channel, norm.hip gn_ab_k; the image's rows of it sit
+// in LDS).  Each lane transforms the 16-byte pieces it DMA'd itself (its 8
+// channels are fixed per lane: quarter (lane & 3) ^ ((lane >> 3) & 2)), once
+// per chunk, at the step after the chunk's wait, before the barrier that
+// publishes it; pads stay zero.  (Not on the tap-pair schedule: its 160 KB of
+// LDS leave no room for the table, and the 16 (A, B) registers it would hold
+// instead spill it.)
+template <int OWT, bool TRANS, int BNT = 512, bool PF = false, bool RES = true, bool AU = false, bool P2 = false,
+          bool GNA = false>
 __global__ void __launch_bounds__(512, 1)
 conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float* __restrict__ bias,
             const float* __restrict__ row_bias, const bf16* __restrict__ res, bf16* __restrict__ O, int in_bytes,
             int w_bytes, int Nimg, int OH, int IC, int ICp, int OC, float scale, int res_nmod,
-            float* __restrict__ gnp, int gn_groups, bf16* __restrict__ O2) {
+            float* __restrict__ gnp, int gn_groups, bf16* __restrict__ O2, const float* __restrict__ gab) {
+  static_assert(!GNA || (AU && !P2 && !TRANS && !PF), "GroupNorm staging: forward, unrolled single-tap schedule");
+  __shared__ __attribute__((aligned(16))) float sG[GNA ? 2 * 512 : 4];
   typedef HaloGeom<OWT, BNT> Gm;
   constexpr int BM = 128, BN = BNT, WM = 64, WN = BN / 4, TM = 4, TN = WN / 16;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * Gm::HBUF + (P2 ? 8 : 4) * Gm::ABUF];
@@ -1038,6 +1051,37 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     const unsigned o = (unsigned)((((img * IH + (ok ? ih : 0)) * IW + (ok ? iw : 0)) * IC + q * 8) * 2);
     hoff[k] = ok ? o : 0x80000000u;            // past every operand: the range check returns zeros
   }
+  // GNA: the in-LDS transform of this lane's own landed pieces of chunk c
+  const int gnq = (lane & 3) ^ ((lane >> 3) & 2);
+  auto gn_apply = [&](bf16* hb, int c) {
+    if constexpr (GNA) {
+      // 4 channels at a time, (A, B) re-read from LDS per half piece: few live
+      // registers beside the 128 accumulators (holding all 16 spilled)
+      // (opaque lane offsets: per-piece addresses hoisted out of the K loop
+      // held ~24 registers through it and spilled)
+      int lo = lane * 8 + wave * 16 * HALO_CH, to = (c * HALO_CH + gnq * 8) * 2;
+      asm volatile("" : "+v"(lo), "+v"(to));
+      const f32x4* t = reinterpret_cast<const f32x4*>(sG + to);
+#pragma unroll
+      for (int k = 0; k < Gm::HPW; ++k) {
+        // image border / past the halo: stays zero (a select, not a branch:
+        // a divergent region here made the allocator spill the K loop)
+        const bool ok = hoff[k] != 0x80000000u;
+        bf16x2* q = reinterpret_cast<bf16x2*>(hb + lo + 8 * k * 16 * HALO_CH);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const f32x4 a = t[h];                             // (A, B) of channels 2h, 2h + 1
+          const bf16x2 v = q[h];
+          bf16x2 o;
+          o[0] = (bf16)siluf_(__builtin_fmaf((float)v[0], a[0], a[1]));
+          o[1] = (bf16)siluf_(__builtin_fmaf((float)v[1], a[2], a[3]));
+          q[h] = ok ? o : v;
+          __builtin_amdgcn_sched_barrier(0);              // one channel pair at a time: few live registers
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // written before the publishing barrier
+    }
+  };
 
   const int NCH = IC / HALO_CH, S = 9 * NCH;
   auto a_soff = [&](int s) {
@@ -1212,11 +1256,28 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
     }
   }
   } else if constexpr (AU) {
+  float gt[GNA ? 2 : 1];
+  if constexpr (GNA) {                         // this image's (A, B) rows: into LDS behind the prologue DMAs
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = tid + 512 * i;
+      gt[i] = j < 2 * IC ? gab[(long)img * IC * 2 + j] : 0.f;
+    }
+  }
   halo_issue_b<Gm::HPW>(sH, I, in_bytes, hoff, 0, wave);
   halo_issue_a(sAr, Wp, w_bytes, aoff, a_soff(0), wave);
   halo_issue_a(sAr + Gm::ABUF, Wp, w_bytes, aoff, a_soff(1), wave);
   halo_issue_a(sAr + 2 * Gm::ABUF, Wp, w_bytes, aoff, a_soff(2), wave);
+  if constexpr (GNA) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) sG[tid + 512 * i] = gt[i];
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (GNA) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();              // the table is complete
+    gn_apply(sH, 0);
+  }
   int bo[3][TN], ao[TM];                       // per kw; the kh shift is a constant (HW2 % 8 == 0)
 #pragma unroll
   for (int kw = 0; kw < 3; ++kw)
@@ -1246,6 +1307,8 @@ conv_halo_k(const bf16* __restrict__ I, const bf16* __restrict__ Wp, const float
         const int cn = c + 1 < NCH ? c + 1 : NCH - 1;
         halo_issue_b<Gm::HPW>(sH + ((c + 1) & 1) * Gm::HBUF, I, in_bytes, hoff, cn * HALO_CH * 2, wave);
       }
+      // chunk c + 1 landed at step 4's wait: this lane's pieces, before step 5's barrier
+      if (t == 4) gn_apply(sH + ((c + 1) & 1) * Gm::HBUF, c + 1 < NCH ? c + 1 : NCH - 1);
       const bf16* a = sAr + (s & 3) * Gm::ABUF;
       __builtin_amdgcn_s_setprio(1);
       bf16x8 af[TM], bfr[TN];
@@ -3009,7 +3072,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
 #define HALO3(OWv, TR, RS, AUv, P2v)                                                                              \
   hipLaunchKernelGGL((conv_halo_k<OWv, TR, 512, false, RS, AUv, (P2v && OWv != 128)>), gh, dim3(512), 0, st, (const bf16*)I,     \
                      (const bf16*)Wp, bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, \
-                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2)
+                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, (const float*)nullptr)
 #define HALO2(OWv, TR, RS, AUv) HALO3(OWv, TR, RS, AUv, false)
 #define HALO(OWv, TR, RS)                                                                                          \
   do {                                                                                                            \
@@ -3041,7 +3104,7 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
 #define HALOS(OWv, TR, RS)                                                                                         \
   hipLaunchKernelGGL((conv_halo_k<OWv, TR, 256, false, RS, true>), gh, dim3(512), 0, st, (const bf16*)I,           \
                      (const bf16*)Wp, bias, row_bias, (const bf16*)res, (bf16*)O, (int)in_bytes, (int)w_bytes, N, OH, \
-                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2)
+                     IC, ICp, OC, scale, res_nmod, gnp, gn_groups, (bf16*)O2, (const float*)nullptr)
       if (OW == 16) {
         if (trans) { if (res || g_conv_res_always) HALOS(16, true, true); else HALOS(16, true, false); }
         else if (res || g_conv_res_always) HALOS(16, false, true); else HALOS(16, false, false);
@@ -3177,6 +3240,56 @@ D3D_API int d3d_conv3(const void* I, const void* Wp, const float* bias, const fl
     if (trans) LAUNCH(true, 1); else LAUNCH(false, 1);
   }
 #undef LAUNCH
+  return (int)hipGetLastError();
+}
+
+// ResnetBlock conv1 with GN0 + SiLU folded into the halo staging (conv_halo_k
+// GNA): I is the PRE-GroupNorm input x, gab [N][IC][2] the per-(image,
+// channel) affine (norm.hip d3d_gn_ab).  Only the halo tiles' forward
+// schedules take it; returns -2 (nothing launched) when this shape would run
+// another kernel, so the caller keeps the separate GroupNorm pass.
+static int conv3_gn_shape(int N, int H, int W, int IC, int OC, int* tile) {
+  const long in_bytes = (long)N * H * W * IC * 2, w_bytes = (long)((OC + 127) / 128 * 128) * 9 * ((IC + 63) / 64 * 64) * 2;
+  if (g_conv_impl != 8 || !g_halo_au || IC % HALO_CH || OC % 128 || (W != 32 && W != 64) || in_bytes >= (1L << 31) ||
+      w_bytes >= (1L << 31) || IC > 512)
+    return 0;
+  auto nblk = [&](int bn) { return H % (bn / W) ? 0L : (long)N * (H / (bn / W)) * (OC / 128); };
+  // (the 512-pixel tiles run the conv without the staging: with it their
+  // unrolled-tap schedules need ~20 registers more than the 256 a wave has
+  // at two waves per SIMD, and the spill reloads -- counted by vmcnt -- would
+  // serialise the DMA pipeline)
+  if ((W != 32 || g_halo_w32) && nblk(512) >= 256) return 0;
+  if (W == 32 && g_halo_w32s && nblk(256) >= 256) {
+    *tile = 256;
+    return 1;
+  }
+  return 0;
+}
+
+D3D_API int d3d_conv3_gn_ok(int N, int H, int W, int IC, int OC) {
+  int t = 0;
+  return conv3_gn_shape(N, H, W, IC, OC, &t);
+}
+
+D3D_API int d3d_conv3_gn(const void* I, const void* Wp, const float* bias, void* O, int N, int H, int W, int IC,
+                         int ICp, int OC, float* gnp, int gn_groups, int* gn_done, const float* gab, hipStream_t st) {
+  int tile = 0;
+  if (gn_done) *gn_done = 0;
+  if (!conv3_gn_shape(N, H, W, IC, OC, &tile) || ICp != (IC + 63) / 64 * 64) return -2;
+  if (gnp) {
+    const int Cg = gn_groups > 0 && OC % gn_groups == 0 ? OC / gn_groups : 0;
+    if (!((Cg == 4 || Cg == 8 || Cg == 16 || Cg == 32) && (H * W) % 64 == 0)) gnp = nullptr;
+  }
+  const long in_bytes = (long)N * H * W * IC * 2, w_bytes = (long)((OC + 127) / 128 * 128) * 9 * ICp * 2;
+  dim3 gh((unsigned)(N * (H / (tile / W))), (unsigned)(OC / 128), 1);
+#define GNL(OWv, BNv, P2v)                                                                                          \
+  hipLaunchKernelGGL((conv_halo_k<OWv, false, BNv, false, false, true, P2v, true>), gh, dim3(512), 0, st,            \
+                     (const bf16*)I, (const bf16*)Wp, bias, (const float*)nullptr, (const bf16*)nullptr, (bf16*)O,    \
+                     (int)in_bytes, (int)w_bytes, N, H, IC, ICp, OC, 1.f, 0, gnp, gn_groups, (bf16*)nullptr, gab)
+  GNL(32, 256, false);
+  (void)tile;
+#undef GNL
+  if (gn_done && gnp) *gn_done = 1;
   return (int)hipGetLastError();
 }
 

@@ -354,6 +354,43 @@ __device__ __forceinline__ void merge_image_stats(const float* __restrict__ part
   __syncthreads();
 }
 
+// GN0 folded into the next conv's halo staging (conv.hip conv_halo_k GNA):
+// per image the statistics, merged exactly as gn_apply2_k merges them (and
+// published for the backward), and the apply's per-channel affine
+// ab[n][c] = (A, B), A = rstd * gamma, B = beta - mean * A.
+__global__ void __launch_bounds__(NT) gn_ab_k(const float* __restrict__ part, float* __restrict__ stats_out,
+                                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                                              float* __restrict__ ab, int P, int C, int G, int rows, int nchunks,
+                                              float eps, int conv_parts) {
+  __shared__ float s_st[2 * 1024];
+  const int n = blockIdx.x, Cg = C / G;
+  merge_image_stats(part, n, nchunks, G, P, rows, Cg, eps, s_st, stats_out, true, conv_parts);
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const int g = c / Cg;
+    const float A = s_st[g * 2 + 1] * gamma[c];
+    const float B = beta[c] - s_st[g * 2] * A;
+    ab[((long)n * C + c) * 2 + 0] = A;
+    ab[((long)n * C + c) * 2 + 1] = B;
+  }
+}
+
+// h = silu(x * A + B) from that table -- the conv's weight-gradient operand,
+// rematerialised in the backward with the staging's exact arithmetic
+__global__ void gn_ab_silu_k(const bf16* __restrict__ x, const float* __restrict__ ab, bf16* __restrict__ y,
+                             long nvec, int C, long PC) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    const long e = i * 8;
+    const int c0 = (int)(e % C);
+    const long n = e / PC;
+    const f32x8 xv = ld8(x + e);
+    const float* p = ab + (n * C + c0) * 2;
+    f32x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (float)(bf16)siluf_(__builtin_fmaf(xv[j], p[2 * j], p[2 * j + 1]));
+    st8(y + e, o);
+  }
+}
+
 // Sum the backward's per-chunk group partials of image n (grp_part
 // [N][nchunks][G] x 2) with every thread of the block (batched loads, fixed
 // merge order): out[g] = (sum a, sum b).
@@ -1160,6 +1197,25 @@ D3D_API int d3d_gn_apply2(int mode, const void* x, const float* part, float* sta
   else if (mode == 1) AP(1);
   else AP(2);
 #undef AP
+  return (int)hipGetLastError();
+}
+
+// GN0 statistics + per-(image, channel) affine for conv_halo_k's GroupNorm
+// staging (part / conv_parts as d3d_gn_apply2's); stats_out for the backward.
+D3D_API int d3d_gn_ab(const float* part, float* stats_out, const float* gamma, const float* beta, float* ab, int N,
+                      int P, int C, int G, float eps, int conv_parts, hipStream_t st) {
+  if (G > 1024) return (int)hipErrorInvalidValue;
+  Plan p = make_plan(N, P, C);
+  hipLaunchKernelGGL(gn_ab_k, dim3(N), dim3(NT), 0, st, part, stats_out, gamma, beta, ab, P, C, G, p.rows, p.nchunks,
+                     eps, conv_parts);
+  return (int)hipGetLastError();
+}
+
+D3D_API int d3d_gn_ab_silu(const void* x, const float* ab, void* y, int N, int P, int C, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long nvec = (long)N * P * C / 8;
+  hipLaunchKernelGGL(gn_ab_silu_k, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, ab, (bf16*)y, nvec, C,
+                     (long)P * C);
   return (int)hipGetLastError();
 }
 

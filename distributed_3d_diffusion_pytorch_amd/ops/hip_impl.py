@@ -1104,6 +1104,129 @@ class _Conv(torch.autograd.Function):
         return dx, dW, db, None, dres, None, drb, None, None, None, None
 
 
+# ResnetBlock GN0 + SiLU folded into conv1's halo staging (conv.hip
+# conv_halo_k GNA) where that conv runs on the 256-pixel halo tiles (the
+# 32x32 level at 16 examples per GPU).  Measured -1.1 % at bs16
+# (profiles/r6/gn_conv_fusion.txt), so off by default; D3D_GN_CONV=1 enables it.
+_GN_CONV = os.environ.get("D3D_GN_CONV", "0") == "1"
+
+
+def gn_silu_conv_ok(x: torch.Tensor, OC: int, groups: int) -> bool:
+    """True when :func:`gn_silu_conv3x3` takes this shape (chunked GroupNorm
+    and the halo conv's 256-pixel tiles)."""
+    if not _GN_CONV or x.dtype != BF16 or x.dim() != 4:
+        return False
+    _ensure_impl()
+    N, H, W, C = x.shape
+    return not gn_img_ok(H * W, C, groups) and bool(_lib.d3d_conv3_gn_ok(N, H, W, C, OC))
+
+
+class _GNSiLUConv(torch.autograd.Function):
+    """conv3x3(silu(GroupNorm(x))) with the GroupNorm + SiLU applied to the
+    conv's input halo in LDS (`xunet.py:114-131`'s GN0 -> SiLU -> conv1): the
+    normalised activation h is never written in the forward.  Backward: the
+    conv's input gradient dh as usual, the GroupNorm backward on (x, dh) (with
+    the residual-gradient hand-off of x's other consumer), and the conv's
+    weight gradient on h rematerialised from x by the same arithmetic, inside
+    the weight-gradient job (side stream)."""
+
+    @staticmethod
+    def forward(ctx, x, gw, gb, cw, cb, groups, eps, gn1_groups, slot, info):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        OC = cw.shape[0]
+        P = H * W
+        fused = getattr(x, "_d3d_gnpart", None)
+        if fused is not None and fused[1] == groups:
+            part, conv_parts = fused[0], fused[2]
+        else:
+            nch, _ = _gn_plan(N, P, C)
+            part = torch.empty(N * nch * groups * 2, dtype=F32, device=x.device)
+            conv_parts = 0
+            _chk(_lib.d3d_gn_stats(x.data_ptr(), N, P, C, groups, eps, part.data_ptr(), None, None, C, _st()),
+                 "gn_stats")
+        stats = torch.empty(N * groups * 2, dtype=F32, device=x.device)
+        ab = torch.empty(N * C * 2, dtype=F32, device=x.device)
+        _chk(_lib.d3d_gn_ab(part.data_ptr(), stats.data_ptr(), gw.data_ptr(), gb.data_ptr(), ab.data_ptr(), N, P, C,
+                            groups, float(eps), int(conv_parts), _st()), "gn_ab")
+        wp = packed_weight(cw, False, 9)
+        out = torch.empty(N, H, W, OC, dtype=BF16, device=x.device)
+        gnp = torch.empty(N * gn1_groups * (P // 64) * 2, dtype=F32, device=x.device) \
+            if gn1_groups and P % 64 == 0 else None
+        done = ctypes.c_int(0)
+        rc = _lib.d3d_conv3_gn(x.data_ptr(), wp.data_ptr(), _ptr(cb), out.data_ptr(), N, H, W, C, _up(C, 64), OC,
+                               _ptr(gnp), int(gn1_groups), ctypes.byref(done), ab.data_ptr(), _st())
+        if rc == -2:
+            raise RuntimeError("gn_silu_conv3x3: shape not taken (check gn_silu_conv_ok first)")
+        _chk(rc, "conv3_gn")
+        ctx.save_for_backward(x, gw, gb, stats, ab, cw)
+        ctx.cfg = (groups, cb is not None)
+        ctx.slot = slot
+        ctx.cb = cb
+        if done.value:
+            info["part"] = (gnp, P // 64)
+        for i, p_ in ((1, gw), (2, gb), (3, cw), (4, cb)):
+            SINK.use(p_, ctx.needs_input_grad[i])
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gw, gb, stats, ab, cw = ctx.saved_tensors
+        G, has_b = ctx.cfg
+        cb = ctx.cb
+        N, H, W, C = x.shape
+        OC = cw.shape[0]
+        dy = dy.contiguous()
+        dev = x.device
+        # conv input gradient dh
+        wt = packed_weight(cw, True, 9)
+        dh = torch.empty_like(x)
+        _conv_fwd(dy, wt, None, None, None, dh, N, H, W, OC, _up(OC, 64), H, W, C, C, 1, True, 1.0, 0, 9)
+        # conv weight / bias gradients on h = silu(x * A + B), rematerialised
+        dW = dB = None
+        need_w, need_b = ctx.needs_input_grad[3], has_b and ctx.needs_input_grad[4]
+        if need_w or need_b:
+            tw = SINK.target(cw) if need_w else None
+            tb = SINK.target(cb) if need_b else None
+
+            def remat():
+                h = torch.empty_like(x)
+                _chk(_lib.d3d_gn_ab_silu(x.data_ptr(), ab.data_ptr(), h.data_ptr(), N, H * W, C, _st()), "gn_ab_silu")
+                return h
+            if need_w and tw is not None and (not need_b or tb is not None):
+                def job(dy=dy, tw=tw, tb=tb):
+                    _wgrad(dy, remat(), OC, C, N, H, W, H, W, 1, 9, dW=tw.view(OC, C, 9), db=tb, accumulate=True)
+                SINK.submit(dev, job, (dy, x, ab), (cw, cb if need_b else None))
+            else:
+                dW, dB = _wgrad(dy, remat(), OC, C, N, H, W, H, W, 1, 9, want_bias=need_b)
+                dW = dW.reshape(cw.shape) if need_w else None
+        # GroupNorm + SiLU backward on (x, dh), with x's other consumer's gradient
+        dres, rsc, dres2, rsc2 = ctx.slot.take() if ctx.slot is not None else (None, 1.0, None, 1.0)
+        if dres is not None:
+            dres = dres.reshape(x.shape).contiguous()
+        if dres2 is not None:
+            dres2 = dres2.reshape(x.shape).contiguous()
+        dx, _, dg, db = _gn_bwd(1, x, dh, None, stats, gw, gb, G, 0.0, 0, dres=dres, dres_scale=rsc, dres2=dres2,
+                                dres2_scale=rsc2)
+        return dx, dg, db, dW, dB, None, None, None, None, None
+
+
+def gn_silu_conv3x3(x, gw, gb, cw, cb, groups=32, eps=1e-5, gn1_groups=0, res_slot=None):
+    """``conv3x3(silu(group_norm(x)), cw, cb)`` with the GroupNorm + SiLU in
+    the conv's input staging (see :func:`gn_silu_conv_ok`).  ``gn1_groups``:
+    the output's GroupNorm partial statistics from the epilogue, as
+    :func:`conv3x3`'s ``gn_groups``."""
+    _need_bf16(x)
+    OC = cw.shape[0]
+    if gn1_groups and gn_img_ok(x.shape[1] * x.shape[2], OC, int(gn1_groups)):
+        gn1_groups = 0
+    info = {}
+    y = _GNSiLUConv.apply(x, gw, gb, cw, cb, int(groups), float(eps), int(gn1_groups), res_slot, info)
+    if "part" in info:
+        y._d3d_gnpart = (info["part"][0], int(gn1_groups), info["part"][1])
+    return y
+
+
 def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=None, res_period=0, gn_groups=0,
             res_slot=None, keep_pad=False):
     """3x3 conv.  gn_groups > 0: the output feeds a GroupNorm with that many

@@ -619,6 +619,53 @@ def test_attention_forward_one_workgroup_per_head(H, N, L, cross):
     assert rel(outs[0][1], outs[1][1]) < 1e-4
 
 
+@pytest.mark.parametrize("N,C,OC", [(32, 128, 256), (32, 256, 256)])
+def test_gn_silu_conv_fused(H, N, C, OC, monkeypatch):
+    """ResnetBlock GN0 + SiLU folded into conv1's halo staging (conv_halo_k
+    GNA, 32x32 images on 256-pixel tiles): output, the output's GroupNorm
+    partials and every gradient against the separate GroupNorm + conv ops
+    and against fp32; h is never written in the forward, and the weight
+    gradient runs on h rematerialised from x."""
+    torch.manual_seed(11)
+    Hh = 32
+    x = (torch.randn(N, Hh, Hh, C, device=DEV) * 1.5 + 0.3).to(BF)
+    gw = torch.rand(C, device=DEV) + 0.5
+    gb = torch.randn(C, device=DEV) * 0.2
+    cw = torch.randn(OC, C, 3, 3, device=DEV) / (3 * C ** 0.5)
+    cb = torch.randn(OC, device=DEV) * 0.1
+    go = torch.randn(N, Hh, Hh, OC, device=DEV)
+    monkeypatch.setattr(H, "_GN_CONV", True)          # (off by default: measured slower)
+    assert H.gn_silu_conv_ok(x, OC, 32)
+    # 512-pixel tiles (64 images) keep the separate GroupNorm pass
+    assert not H.gn_silu_conv_ok(torch.cat([x, x]), OC, 32)
+
+    def run(mode):
+        xs = leaf(x) if mode != "ref" else leaf(x, torch.float32)
+        ps = [leaf(t) for t in (gw, gb, cw, cb)]
+        if mode == "fused":
+            y = H.gn_silu_conv3x3(xs, *ps, 32, 1e-5, gn1_groups=32)
+        elif mode == "sep":
+            h = H.group_norm(xs, ps[0], ps[1], 32, 1e-5, silu=True)
+            y = H.conv3x3(h, ps[2], ps[3], gn_groups=32)
+        else:
+            h = T.group_norm(xs, ps[0], ps[1], 32, 1e-5, silu=True)
+            y = T.conv3x3(h, ps[2], ps[3])
+        (y.float() * go).sum().backward()
+        return y, [xs.grad] + [p_.grad for p_ in ps]
+
+    yf, gf = run("fused")
+    ys, gs = run("sep")
+    yr, gr = run("ref")
+    assert rel(yf, ys) < 1e-3, rel(yf, ys)
+    assert rel(yf, yr) < 2e-2
+    pf, ps_ = getattr(yf, "_d3d_gnpart", None), getattr(ys, "_d3d_gnpart", None)
+    assert pf is not None and ps_ is not None and pf[1:] == ps_[1:]
+    assert rel(pf[0], ps_[0]) < 1e-3
+    for a, b, c in zip(gf, gs, gr):
+        assert rel(a, b) < 1e-2, rel(a, b)
+        assert rel(a, c) < 4e-2, rel(a, c)
+
+
 def test_attention_spiky(H):
     """A key that dominates one query's softmax in a late key block forces the
     online-softmax rescale branch."""
