@@ -46,6 +46,14 @@ _FILM_BLAS = os.environ.get("D3D_FILM_BLAS", "1") != "0"
 # level's [P, 1024] silu(e) operand).  D3D_FILM_EARLY_WGRAD: 1 (default)
 # graph-captured steps only, 2 always, 0 never.
 _FILM_EARLY = int(os.environ.get("D3D_FILM_EARLY_WGRAD", "1"))
+# D3D_FILM_WGRAD_INLINE=1: the level's LAST FiLM weight-gradient job runs in
+# place, on the stream the level-batched FiLM backward runs on (the
+# conditioning stream), instead of queueing behind the conv weight gradients
+# on the side stream, where the 64x64 level's ran with nothing beside it
+# (bs128: ~4.6 ms/step of wgrad_tn_k "solo").  Measured -1.1 % at bs128 and
+# +0.4 % (noise) at bs16 -- overlapping it only slows the kernels it joins --
+# so off (profiles/r6/film_wgrad_inline.txt).
+_FILM_INLINE = os.environ.get("D3D_FILM_WGRAD_INLINE", "0") == "1"
 
 
 def set_conv_impl(impl: str) -> None:
@@ -1671,7 +1679,7 @@ class _FiLMSlot:
                     self.early.update(grp)
 
 
-def _film_group_wgrad(dy: torch.Tensor, grp, blocks, x2: torch.Tensor) -> bool:
+def _film_group_wgrad(dy: torch.Tensor, grp, blocks, x2: torch.Tensor, inline: bool = False) -> bool:
     """The weight / bias gradients of FiLM blocks ``grp`` (column offsets of
     contiguous blocks of the level's [P, S] d(scale|shift) buffer ``dy``) as
     ONE sink job: split-K MFMA GEMM over their columns against ``x2`` =
@@ -1698,7 +1706,13 @@ def _film_group_wgrad(dy: torch.Tensor, grp, blocks, x2: torch.Tensor) -> bool:
         bdst = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tb])
         _chk(_lib.d3d_wgrad_scatter(ws.data_ptr(), c1 - c0, K, used, 1, bws.data_ptr(), bws.shape[0], n, row0, wdst,
                                     bdst, _st()), "film_group_wgrad")
-    SINK.submit(x2.device, job, (cols, x2), [p for w, b, _ in ps for p in (w, b)])
+    params = [p for w, b, _ in ps for p in (w, b)]
+    if inline:
+        job()
+        for p_ in params:
+            SINK.done(p_)
+    else:
+        SINK.submit(x2.device, job, (cols, x2), params)
     return True
 
 
@@ -1820,7 +1834,7 @@ class _FiLMBatch(torch.autograd.Function):
             # a group's weight gradients were submitted by its GN-FiLM
             # backwards (_FiLMSlot.block_ready); the rest go one job per group
             for grp in groups:
-                if grp[0] not in early and not _film_group_wgrad(dy, grp, blocks, x2):
+                if grp[0] not in early and not _film_group_wgrad(dy, grp, blocks, x2, inline=_FILM_INLINE):
                     raise RuntimeError("FiLM weight gradient: early and level-wide jobs mixed")
             need_w = False
         if need_w:
@@ -1859,7 +1873,11 @@ class _FiLMBatch(torch.autograd.Function):
                     ws = torch.empty(sp.value * S * K + 2 * sp.value * S, dtype=F32, device=x2.device)
                     _chk(_lib.d3d_conv_wgrad_seg(dy.data_ptr(), x2.data_ptr(), ws.data_ptr(), rows, 1, 1, K, 1, 1, S,
                                                  1, sp.value, pps.value, 1, 1, n, row0, wd, bd, _st()), "film_wgrad")
-            if direct:
+            if direct and _FILM_INLINE:
+                job()
+                for p_ in [p for wb in zip(Ws, Bs) for p in wb]:
+                    SINK.done(p_)
+            elif direct:
                 SINK.submit(x2.device, job, (dy, x2), [p for wb in zip(Ws, Bs) for p in wb])
             else:
                 job()
