@@ -91,6 +91,12 @@ class GradSink:
         # instead of waiting for defer_batch jobs
         self.bucket_flush: Optional[Callable[[list], bool]] = None
         self._qcount: Dict[int, int] = {}
+        # work-based flushing: a queue holding at least this many weight-
+        # gradient FLOPs is flushed at once (0: by job count only), so a few
+        # big jobs (the 64x64 level's convs) start early while the many small
+        # ones still share forks and grouped launches
+        self.defer_work = float(os.environ.get("D3D_WGRAD_DEFER_GFLOP", "0")) * 1e9
+        self._qwork = 0.0
 
     def attach(self, params, views, notify: Optional[Callable[[int], None]] = None) -> None:
         # the parameter objects themselves are kept: a key is only trusted
@@ -201,14 +207,17 @@ class GradSink:
                 pass
 
     # ------------------------------------------------ weight-gradient jobs
-    def submit(self, dev: torch.device, fn: Callable[[], None], keep=(), done=(), spec=None) -> None:
+    def submit(self, dev: torch.device, fn: Callable[[], None], keep=(), done=(), spec=None,
+               work: float = 0.0) -> None:
         """Run one weight-gradient job: ``fn()`` launches kernels that deposit
         into sink targets, then the parameters in ``done`` are reported.
         Eager: now, on the side stream (:meth:`producer`).  Graph capture with
         deferral on: queued and flushed in batches behind one fork each.
         ``spec``: the same job as a grouped-kernel descriptor
         (hip_impl.wgrad_job); a flush runs all queued specs as ONE grouped
-        launch (:attr:`group_fn`) instead of their closures."""
+        launch (:attr:`group_fn`) instead of their closures.  ``work``: the
+        job's FLOPs for work-based flushing (taken from a weight-gradient
+        spec when not given)."""
         capturing = dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
         # (queueing does not depend on the side stream: with it off the flush
         # runs on the current stream, so the same jobs group the same way and
@@ -225,7 +234,12 @@ class GradSink:
             self._queue.append((fn, tuple(t for t in keep if t is not None), tuple(p for p in done if p is not None),
                                 torch.cuda.current_stream(dev.index if dev.index is not None else None), spec))
             self._queue_end_callback()
-            if len(self._queue) >= self.defer_batch or self._completes_bucket(done):
+            if self.defer_work > 0.0:
+                if not work and spec is not None and hasattr(spec, "taps"):
+                    work = 2.0 * spec.N * spec.H * spec.W * spec.OC * spec.IC * spec.taps
+                self._qwork += work
+            if len(self._queue) >= self.defer_batch or self._completes_bucket(done) or \
+                    (self.defer_work > 0.0 and self._qwork >= self.defer_work):
                 self.flush()
             return
         with self.producer(dev, *keep):
@@ -253,6 +267,7 @@ class GradSink:
         """Issue the queued weight-gradient jobs on the side stream behind ONE
         wait on the compute stream, then report their parameters."""
         self._qcount = {}
+        self._qwork = 0.0
         if not self._queue:
             return
         q, self._queue = self._queue, []
@@ -377,6 +392,7 @@ class GradSink:
         capture) drops autograd's final callbacks, and a stale flag would stop
         the next backward from queueing its flush + join."""
         self._qcount = {}
+        self._qwork = 0.0
         self.uses = {}
         self.seen = set()
         self._queue = []

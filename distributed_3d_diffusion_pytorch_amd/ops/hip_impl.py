@@ -1712,7 +1712,7 @@ def _film_group_wgrad(dy: torch.Tensor, grp, blocks, x2: torch.Tensor, inline: b
         for p_ in params:
             SINK.done(p_)
     else:
-        SINK.submit(x2.device, job, (cols, x2), params)
+        SINK.submit(x2.device, job, (cols, x2), params, work=2.0 * rows * (c1 - c0) * K)
     return True
 
 
@@ -1878,7 +1878,7 @@ class _FiLMBatch(torch.autograd.Function):
                 for p_ in [p for wb in zip(Ws, Bs) for p in wb]:
                     SINK.done(p_)
             elif direct:
-                SINK.submit(x2.device, job, (dy, x2), [p for wb in zip(Ws, Bs) for p in wb])
+                SINK.submit(x2.device, job, (dy, x2), [p for wb in zip(Ws, Bs) for p in wb], work=2.0 * rows * S * K)
             else:
                 job()
                 grads_w = [t.view(w.shape) for t, w in zip(tw, Ws)]
