@@ -85,14 +85,15 @@ class Trainer:
             if self.reducer is not None:
                 self.reducer.sink = SINK
             self.sink = SINK
-            # weight-gradient jobs per side-stream fork: 64 when no collective
-            # waits on the reports (bs16 +1.7 %, profiles/r5/defer_batch/); 16
-            # when the bucketed all-reduces do (+0.7 % over 8 with the captured
-            # collectives) -- a parameter is reported only when its job's batch
-            # is flushed, so big batches would start the buckets' reductions
-            # late (D3D_WGRAD_DEFER_BATCH overrides)
+            # weight-gradient jobs per side-stream fork in graph capture: 128
+            # when no collective waits on the reports (over 64: bs16 +2.9 %,
+            # bs64 +1.3 %, bs32 -0.2 %); 32 when the bucketed all-reduces do
+            # (over 16 in the 1-rank rehearsal: bs16 +2.9 %, bs32 +0.9 %) -- a
+            # parameter is reported only when its job's batch is flushed, so
+            # big batches would start the buckets' reductions late
+            # (profiles/r6/defer_batch.txt; D3D_WGRAD_DEFER_BATCH overrides)
             comm = self.reducer is not None and self.reducer.active
-            SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "16" if comm else "64"))
+            SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "32" if comm else "128"))
             # bucket-aware flushing (opt-in): a queued job that completes a
             # bucket flushes the queue at once, so batches can be big without
             # delaying any bucket's reduction (profiles/r6/bucket_flush.txt)
