@@ -87,13 +87,14 @@ class Trainer:
             self.sink = SINK
             # weight-gradient jobs per side-stream fork in graph capture: 128
             # when no collective waits on the reports (over 64: bs16 +2.9 %,
-            # bs64 +1.3 %, bs32 -0.2 %); 32 when the bucketed all-reduces do
-            # (over 16 in the 1-rank rehearsal: bs16 +2.9 %, bs32 +0.9 %) -- a
-            # parameter is reported only when its job's batch is flushed, so
-            # big batches would start the buckets' reductions late
-            # (profiles/r6/defer_batch.txt; D3D_WGRAD_DEFER_BATCH overrides)
+            # bs64 +1.3 %, bs32 -0.2 %); 16 when the bucketed all-reduces do
+            # -- a parameter is reported only when its job's batch is flushed,
+            # so big batches would start the buckets' reductions late.  (32
+            # measured +2.9 % in the 1-rank rehearsal but its captured step
+            # fails the 1-rank RCCL graph test -- NaN gradients -- so it is not
+            # used: profiles/r6/defer_batch.txt; D3D_WGRAD_DEFER_BATCH overrides)
             comm = self.reducer is not None and self.reducer.active
-            SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "32" if comm else "128"))
+            SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "16" if comm else "128"))
             # bucket-aware flushing (opt-in): a queued job that completes a
             # bucket flushes the queue at once, so batches can be big without
             # delaying any bucket's reduction (profiles/r6/bucket_flush.txt)
