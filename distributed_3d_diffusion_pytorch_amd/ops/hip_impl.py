@@ -43,9 +43,13 @@ _FILM_BLAS = os.environ.get("D3D_FILM_BLAS", "1") != "0"
 # +0.7 % at bs16 (graph-captured step), -0.7 % at bs128 (eager step: its
 # weight-gradient stream is saturated, so the earlier job only delays the
 # conv weight gradients), and one job per BLOCK -3 % / -2 % (each re-reads the
-# level's [P, 1024] silu(e) operand).  D3D_FILM_EARLY_WGRAD: 1 (default)
-# graph-captured steps only, 2 always, 0 never.
-_FILM_EARLY = int(os.environ.get("D3D_FILM_EARLY_WGRAD", "1"))
+# level's [P, 1024] silu(e) operand).  OFF by default: in the 1-rank RCCL
+# graph step with a 32-job flush batch the early jobs leave NaN gradients in
+# other parameters (4 of bucket 24 at the first replay; tools/
+# diag_flush_nan_bisect.sh isolates it to this switch) and the cause is not
+# found.  D3D_FILM_EARLY_WGRAD: 0 (default) never, 1 graph-captured steps,
+# 2 always.
+_FILM_EARLY = int(os.environ.get("D3D_FILM_EARLY_WGRAD", "0"))
 # D3D_FILM_WGRAD_INLINE=1: the level's LAST FiLM weight-gradient job runs in
 # place, on the stream the level-batched FiLM backward runs on (the
 # conditioning stream), instead of queueing behind the conv weight gradients
