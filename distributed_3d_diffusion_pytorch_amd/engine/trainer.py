@@ -95,11 +95,20 @@ class Trainer:
             # used: profiles/r6/defer_batch.txt; D3D_WGRAD_DEFER_BATCH overrides)
             comm = self.reducer is not None and self.reducer.active
             SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "16" if comm else "128"))
+            if comm and self.reducer.mirror is not None and SINK.defer_batch > 16:
+                # a bucket collective on the bf16 mirror in the captured step
+                # showed NaN at 48-128-job batches (1-rank RCCL rehearsal; not
+                # root-caused, profiles/r6/defer_batch.txt): keep such runs at 16
+                print(f"[trainer] bf16 gradient payload: weight-gradient flush batch {SINK.defer_batch} -> 16",
+                      flush=True)
+                SINK.defer_batch = 16
             # bucket-aware flushing (opt-in): a queued job that completes a
             # bucket flushes the queue at once, so batches can be big without
             # delaying any bucket's reduction (profiles/r6/bucket_flush.txt)
             SINK.bucket_flush = self.reducer.completes_bucket if comm and \
                 os.environ.get("D3D_WGRAD_BUCKET_FLUSH", "0") == "1" else None
+            if SINK.bucket_flush is not None and self.reducer.mirror is not None:
+                SINK.bucket_flush = None        # (same NaN with the bf16 mirror; see above)
         oc = cfg.optim
         self.optim = FusedAdam(self.flat, oc.lr, oc.betas, oc.eps, oc.weight_decay,
                                ema_decay_for(cfg.global_batch, oc.ema_halflife_examples))

@@ -4,7 +4,7 @@ every step which parameters' complete gradients (the reducer race probe's
 copy at finish()) hold non-finite values -- to locate the NaN that flush
 batch 32 produces (profiles/r6/defer_batch.txt).
 
-    D3D_WGRAD_DEFER_BATCH=32 python tools/diag_flush_nan.py [graph 0|1] [payload fp32|bf16]
+    D3D_WGRAD_DEFER_BATCH=32 python tools/diag_flush_nan.py [graph 0|1] [payload fp32|bf16] [comm|nocomm]
 """
 import datetime
 import os
@@ -13,7 +13,7 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
-def worker(graph, gd):
+def worker(graph, gd, comm=True):
     import torch
     import torch.distributed as dist
     from distributed_3d_diffusion_pytorch_amd.config import make_config
@@ -30,14 +30,29 @@ def worker(graph, gd):
     cfg = make_config(None, {"model.H": 32, "model.W": 32, "data.imgsize": 32, "global_batch": 4, "micro_batch": 0,
                              "data.synthetic": True, "log_every": 0, "ckpt_every": 0, "graph": bool(graph),
                              "optim.warmup_examples": 8, "dist.bucket_mb": 16.0, "dist.grad_dtype": gd,
-                             "dist.force_comm": True})
+                             "dist.force_comm": bool(comm)})
     tr = Trainer(cfg, ctx)
-    tr.reducer.enable_race_probe()
+    if not comm:
+        print("defer_batch", tr.sink.defer_batch, "(no collectives)", flush=True)
+        for step in range(5):
+            loss = float(tr.train_step(*next(data)))
+            torch.cuda.synchronize()
+            print(f"step {step} loss {loss:.5f} params finite {bool(torch.isfinite(tr.flat.data).all())}", flush=True)
+        tr.sync()
+        torch.cuda.synchronize()
+        print("after sync params finite", bool(torch.isfinite(tr.flat.data).all()), flush=True)
+        cleanup()
+        return
+    if os.environ.get("DIAG_NO_PROBE") != "1":
+        tr.reducer.enable_race_probe()
     names = [n for n, _ in tr.model.named_parameters()]
     print("defer_batch", tr.sink.defer_batch, "buckets", len(tr.reducer.buckets), flush=True)
     for step in range(4):
         loss = float(tr.train_step(*next(data)))
         torch.cuda.synchronize()
+        if tr.reducer.race_probe is None:
+            print(f"step {step} loss {loss:.5f} params finite {bool(torch.isfinite(tr.flat.data).all())}", flush=True)
+            continue
         snap, final = tr.reducer.race_probe
         bad = []
         for i in range(len(tr.flat.params)):
@@ -60,12 +75,13 @@ def worker(graph, gd):
 def main():
     from distributed_3d_diffusion_pytorch_amd.parallel import spawn
     graph = int(sys.argv[1]) if len(sys.argv) > 1 else 1
-    gd = sys.argv[2] if len(sys.argv) > 2 else "fp32"
-    spawn(_entry, 1, (graph, gd))
+    gd = os.environ.get("DIAG_PAYLOAD") or (sys.argv[2] if len(sys.argv) > 2 else "fp32")
+    comm = (sys.argv[3] if len(sys.argv) > 3 else "comm") != "nocomm"
+    spawn(_entry, 1, (graph, gd, comm))
 
 
-def _entry(graph, gd):
-    worker(graph, gd)
+def _entry(graph, gd, comm):
+    worker(graph, gd, comm)
 
 
 if __name__ == "__main__":
