@@ -95,7 +95,8 @@ class Trainer:
             # used: profiles/r6/defer_batch.txt; D3D_WGRAD_DEFER_BATCH overrides)
             comm = self.reducer is not None and self.reducer.active
             SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "16" if comm else "128"))
-            if comm and self.reducer.mirror is not None and SINK.defer_batch > 16:
+            if comm and self.reducer.mirror is not None and SINK.defer_batch > 16 and \
+                    os.environ.get("D3D_DIAG_BF16_ANY_BATCH", "0") != "1":
                 # a bucket collective on the bf16 mirror in the captured step
                 # showed NaN at 48-128-job batches (1-rank RCCL rehearsal; not
                 # root-caused, profiles/r6/defer_batch.txt): keep such runs at 16

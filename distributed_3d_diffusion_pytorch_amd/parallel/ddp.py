@@ -28,12 +28,18 @@ Design here (MI355X, 8 GPUs on xGMI, 7 point-to-point links per GPU):
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import List, Optional
 
 import torch
 import torch.distributed as dist
 
 from .flat import FlatParams
+
+
+# diagnostic (tools/diag_flush_nan.py): the race probe snapshots each bucket but
+# the collective reduces the bucket in place, as without the probe
+_PROBE_COPY_ONLY = os.environ.get("D3D_DIAG_PROBE_COPY_ONLY", "0") == "1"
 
 
 class GradReducer:
@@ -123,6 +129,8 @@ class GradReducer:
         bk = self.buckets[b]
         snap = self.race_probe[0][bk["start"]: bk["end"]]
         snap.copy_(view)
+        if _PROBE_COPY_ONLY:
+            return view         # diagnostic: snapshot taken, the collective still reduces in place
         return snap
 
     def probe_final(self) -> None:
