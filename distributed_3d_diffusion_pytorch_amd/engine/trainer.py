@@ -87,29 +87,26 @@ class Trainer:
             self.sink = SINK
             # weight-gradient jobs per side-stream fork in graph capture: 128
             # when no collective waits on the reports (over 64: bs16 +2.9 %,
-            # bs64 +1.3 %, bs32 -0.2 %); 16 when the bucketed all-reduces do
+            # bs64 +1.3 %, bs32 -0.2 %); 32 when the bucketed all-reduces do
+            # (over 16 in the 1-rank rehearsal: bs16 +2.4-2.9 %, bs32 +0.9 %)
             # -- a parameter is reported only when its job's batch is flushed,
-            # so big batches would start the buckets' reductions late.  (32
-            # measured +2.9 % in the 1-rank rehearsal but its captured step
-            # fails the 1-rank RCCL graph test -- NaN gradients -- so it is not
-            # used: profiles/r6/defer_batch.txt; D3D_WGRAD_DEFER_BATCH overrides)
+            # so big batches would start the buckets' reductions late; and the
+            # captured collective step is only known to be robust up to 32-job
+            # flushes (at >= 48 extra work on the collective path changed its
+            # results: profiles/r6/defer_batch.txt), so larger values are
+            # clamped there.  D3D_WGRAD_DEFER_BATCH overrides.
             comm = self.reducer is not None and self.reducer.active
-            SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "16" if comm else "128"))
-            if comm and self.reducer.mirror is not None and SINK.defer_batch > 16 and \
-                    os.environ.get("D3D_DIAG_BF16_ANY_BATCH", "0") != "1":
-                # a bucket collective on the bf16 mirror in the captured step
-                # showed NaN at 48-128-job batches (1-rank RCCL rehearsal; not
-                # root-caused, profiles/r6/defer_batch.txt): keep such runs at 16
-                print(f"[trainer] bf16 gradient payload: weight-gradient flush batch {SINK.defer_batch} -> 16",
-                      flush=True)
-                SINK.defer_batch = 16
+            SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "32" if comm else "128"))
+            if comm and SINK.defer_batch > 32 and os.environ.get("D3D_DIAG_BF16_ANY_BATCH", "0") != "1":
+                print(f"[trainer] collective step: weight-gradient flush batch {SINK.defer_batch} -> 32", flush=True)
+                SINK.defer_batch = 32
             # bucket-aware flushing (opt-in): a queued job that completes a
             # bucket flushes the queue at once, so batches can be big without
             # delaying any bucket's reduction (profiles/r6/bucket_flush.txt)
             SINK.bucket_flush = self.reducer.completes_bucket if comm and \
                 os.environ.get("D3D_WGRAD_BUCKET_FLUSH", "0") == "1" else None
             if SINK.bucket_flush is not None and self.reducer.mirror is not None:
-                SINK.bucket_flush = None        # (same NaN with the bf16 mirror; see above)
+                SINK.bucket_flush = None        # (NaN with the bf16 mirror: profiles/r6/bucket_flush.txt)
         oc = cfg.optim
         self.optim = FusedAdam(self.flat, oc.lr, oc.betas, oc.eps, oc.weight_decay,
                                ema_decay_for(cfg.global_batch, oc.ema_halflife_examples))

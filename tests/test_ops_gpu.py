@@ -1637,11 +1637,7 @@ def _graph_comm_1rank_worker(out_dir, bucket_flush=False):
     from distributed_3d_diffusion_pytorch_amd.data import SyntheticBatches
     rccl_env_defaults()
     if bucket_flush:
-        # bucket-aware sink flushing (the round-5 NaN variant) at the default
-        # 16-job batch.  (Larger batches: a collective on a separate buffer --
-        # the bf16 mirror, or this probe's snapshot -- leaves NaN in the
-        # captured step at some batch sizes, profiles/r6/defer_batch.txt; the
-        # trainer keeps such runs at 16.)
+        # bucket-aware sink flushing (the round-5 NaN variant; experimental)
         os.environ["D3D_WGRAD_BUCKET_FLUSH"] = "1"
         os.environ["D3D_WGRAD_DEFER_BATCH"] = "16"
     torch.cuda.set_device(0)
