@@ -29,7 +29,7 @@ def worker(graph, gd, comm=True):
     data = SyntheticBatches(4, 32, "cuda", seed=21)
     cfg = make_config(None, {"model.H": 32, "model.W": 32, "data.imgsize": 32, "global_batch": 4, "micro_batch": 0,
                              "data.synthetic": True, "log_every": 0, "ckpt_every": 0, "graph": bool(graph),
-                             "optim.warmup_examples": 8, "dist.bucket_mb": 16.0, "dist.grad_dtype": gd,
+                             "optim.warmup_examples": 8, "dist.bucket_mb": float(os.environ.get("DIAG_BUCKET_MB", "16")), "dist.grad_dtype": gd,
                              "dist.force_comm": bool(comm)})
     tr = Trainer(cfg, ctx)
     if not comm:
