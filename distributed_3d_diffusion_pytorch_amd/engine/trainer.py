@@ -87,17 +87,18 @@ class Trainer:
             self.sink = SINK
             # weight-gradient jobs per side-stream fork in graph capture: 128
             # when no collective waits on the reports (over 64: bs16 +2.9 %,
-            # bs64 +1.3 %, bs32 -0.2 %); 16 when the bucketed all-reduces do --
-            # a parameter is reported only when its job's batch is flushed, so
-            # big batches would start the buckets' reductions late, and the
-            # captured collective step is only known to be robust up to 32-job
-            # flushes (at >= 48 extra work on the collective path changed its
-            # results: profiles/r6/defer_batch.txt), so larger values are
-            # clamped to 32 there.  (32 measured +2.4-2.9 % at bs16 in the
-            # 1-rank rehearsal; 16 keeps a margin below the unexplained
-            # threshold for the multi-GPU runs.)  D3D_WGRAD_DEFER_BATCH overrides.
+            # bs64 +1.3 %, bs32 -0.2 %); 32 when the bucketed all-reduces do
+            # (over 16 in the 1-rank rehearsal: bs16 +2.4-2.9 %, bs32 +0.9 %)
+            # -- a parameter is reported only when its job's batch is flushed,
+            # so big batches would start the buckets' reductions late.  The
+            # captured collective step misbehaved with MANY captured
+            # collectives (16 MiB buckets or smaller: ~30-170 per step) under
+            # extra work on the collective path; with the default 64 MiB
+            # buckets (9 per step) it stayed bit-exact even at 64-job flushes
+            # (profiles/r6/defer_batch.txt).  Values above 32 are clamped.
+            # D3D_WGRAD_DEFER_BATCH overrides.
             comm = self.reducer is not None and self.reducer.active
-            SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "16" if comm else "128"))
+            SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "32" if comm else "128"))
             if comm and SINK.defer_batch > 32 and os.environ.get("D3D_DIAG_BF16_ANY_BATCH", "0") != "1":
                 print(f"[trainer] collective step: weight-gradient flush batch {SINK.defer_batch} -> 32", flush=True)
                 SINK.defer_batch = 32
