@@ -99,6 +99,10 @@ class Trainer:
             # D3D_WGRAD_DEFER_BATCH overrides.
             comm = self.reducer is not None and self.reducer.active
             SINK.defer_batch = int(os.environ.get("D3D_WGRAD_DEFER_BATCH", "32" if comm else "128"))
+            if comm and cfg.graph and len(self.reducer.buckets) > 32:
+                print(f"[trainer] warning: {len(self.reducer.buckets)} all-reduce buckets per step; the captured "
+                      f"collective step was seen to go wrong with ~90+ collectives under extra collective-path "
+                      f"work (profiles/r6/defer_batch.txt) -- prefer dist.bucket_mb >= 32", flush=True)
             if comm and SINK.defer_batch > 32 and os.environ.get("D3D_DIAG_BF16_ANY_BATCH", "0") != "1":
                 print(f"[trainer] collective step: weight-gradient flush batch {SINK.defer_batch} -> 32", flush=True)
                 SINK.defer_batch = 32
