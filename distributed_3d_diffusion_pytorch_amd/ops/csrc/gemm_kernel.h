@@ -378,8 +378,11 @@ gemm_fw_k(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restri
       g_dma(lo.b, 0, smem + st * C::STAGE + (C::BM + wave * C::RB + (d - C::DA) * 8) * G_PK,
             d > C::DA ? piece_off(boff, (d - C::DA) * bstep) : boff, lkb);
 #else
-      g_dma(lo.b, lo.rb, smem + st * C::STAGE + (C::BM + wave * C::RB + (d - C::DA) * 8) * G_PK,
-            d > C::DA ? piece_off(boff, (d - C::DA) * bstep) : boff, lkb);
+#ifndef D3D_GEMM_B_CPOL
+#define D3D_GEMM_B_CPOL 0          // cache policy of the activation (B) stream: A/B build knob
+#endif
+      g_dma_cp<D3D_GEMM_B_CPOL>(lo.b, lo.rb, smem + st * C::STAGE + (C::BM + wave * C::RB + (d - C::DA) * 8) * G_PK,
+                                d > C::DA ? piece_off(boff, (d - C::DA) * bstep) : boff, lkb);
 #endif
     }
   };

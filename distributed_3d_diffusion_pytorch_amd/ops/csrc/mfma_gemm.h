@@ -34,6 +34,13 @@ __device__ __forceinline__ void g_dma(const void* base, int nrec, void* lds, int
   __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000),
                                            (lds_void*)lds, 16, voff, soff, 0, 0);
 }
+// the same with a cache policy (CPOL: 1 sc0, 2 nt, 16 sc1) -- the streamed operand of the dense GEMM
+template <int CPOL>
+__device__ __forceinline__ void g_dma_cp(const void* base, int nrec, void* lds, int voff, int soff) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000),
+                                           (lds_void*)lds, 16, voff, soff, 0, CPOL);
+}
 typedef unsigned g_u4 __attribute__((ext_vector_type(4)));
 typedef unsigned g_u2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ g_u2 g_load8(const void* base, int nrec, int off) {
