@@ -30,6 +30,8 @@ SIGNATURES = {
     "d3d_gn_ab_silu": [P, P, P, I, I, I, P],
     "d3d_gn_img_cfg": [I],
     "d3d_gn_img_ok": [I, I, I],
+    "d3d_gn_img_ok_n": [I, I, I, I],
+    "d3d_gn_img_wide_cfg": [I, I],
     "d3d_gn_img_fwd": [I, P, P, P, P, P, P, I, I, I, I, F, F, U64, I, P, P, I, P, P],
     "d3d_gn_img_bwd": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, I, P, P, P, I, P, F, P, F, P],
     "d3d_gn_bwd2": [I, P, P, P, P, P, P, I, I, I, I, F, U64, P, P, P, P, P, P, P, I, I, P, P, P, I, P, F, P, F, P],

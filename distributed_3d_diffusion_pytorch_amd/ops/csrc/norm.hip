@@ -1114,10 +1114,17 @@ struct ImgPlan {
   int ok, CS, NTI, U;
 };
 static int g_gn_img_maxp = 256;            // 0: whole-image kernels off (A/B knob, d3d_gn_img_cfg)
+// Batches of g_gn_img_wide_lo..hi images also take the 512-thread form at the
+// 32x32 level: measured +0.5..1.2 % of the step at 64 / 128 images, but
+// -2.0 % at 32 (too few blocks) and -0.9 % at 256 (the chunked kernels
+// stream better) -- profiles/r6/knob_sweep_b128.txt.  d3d_gn_img_wide_cfg.
+static int g_gn_img_wide_lo = 64, g_gn_img_wide_hi = 128;
 
-ImgPlan img_plan(int P, int C, int G) {
+ImgPlan img_plan(int P, int C, int G, int N = 0) {
   ImgPlan p{0, 0, 0, 0};
-  if (G <= 0 || C % G || C > 4096 || P < 1 || P > g_gn_img_maxp) return p;
+  int maxp = g_gn_img_maxp;
+  if (maxp > 0 && maxp < 1024 && N >= g_gn_img_wide_lo && N <= g_gn_img_wide_hi) maxp = 1024;
+  if (G <= 0 || C % G || C > 4096 || P < 1 || P > maxp) return p;
   const int Cg = C / G;
   if (Cg % 8) return p;
   int CS = C;
@@ -1302,7 +1309,13 @@ D3D_API int d3d_gn_img_cfg(int max_p) {
   return g_gn_img_maxp;
 }
 
+D3D_API int d3d_gn_img_wide_cfg(int lo, int hi) {
+  if (lo >= 0) { g_gn_img_wide_lo = lo; g_gn_img_wide_hi = hi; }
+  return g_gn_img_wide_lo;
+}
+
 D3D_API int d3d_gn_img_ok(int P, int C, int G) { return img_plan(P, C, G).ok; }
+D3D_API int d3d_gn_img_ok_n(int N, int P, int C, int G) { return img_plan(P, C, G, N).ok; }
 
 // Forward in one launch (statistics from the registers + apply); stats_out
 // [N][G] (mean, rstd).  mode 0 GN, 1 GN+SiLU, 2 GN+FiLM(+dropout).
@@ -1310,7 +1323,7 @@ D3D_API int d3d_gn_img_fwd(int mode, const void* x, float* stats_out, const floa
                            const void* ss, void* y, int N, int P, int C, int G, float eps, float p_drop,
                            unsigned long long seed, int ssld, const void* seed_dev, const void* x2, int C1,
                            const int* ss_map, hipStream_t st) {
-  const ImgPlan p = img_plan(P, C, G);
+  const ImgPlan p = img_plan(P, C, G, N);
   if (!p.ok) return (int)hipErrorInvalidValue;
   Cat cat{(const bf16*)x2, nullptr, C1};
   if (ssld == 0) ssld = 2 * C;
@@ -1340,7 +1353,7 @@ D3D_API int d3d_gn_img_bwd(int mode, const void* x, const void* dy, const void* 
                            unsigned long long seed, void* dx, void* dss, float* chan_out, int ssld,
                            const void* seed_dev, const void* x2, void* dx2, int C1, const void* dres,
                            float dres_scale, const void* dres2, float dres2_scale, hipStream_t st) {
-  const ImgPlan p = img_plan(P, C, G);
+  const ImgPlan p = img_plan(P, C, G, N);
   if (!p.ok) return (int)hipErrorInvalidValue;
   Cat cat{(const bf16*)x2, (bf16*)dx2, C1};
   if (ssld == 0) ssld = 2 * C;

@@ -396,17 +396,26 @@ def _gn_stats(x, G, eps):
 # Whole-image GroupNorm kernels (norm.hip gn_img_*): images of at most this
 # many pixels (the 16x16 / 8x8 levels) run each GroupNorm pass as ONE launch
 # that keeps an (image, channel slab) in registers -- statistics and backward
-# reductions inside the block.  D3D_GN_IMG=<max pixels> (0: off).
+# reductions inside the block.  D3D_GN_IMG=<max pixels> (0: off).  Batches
+# of 64..128 images also take it at the 32x32 level (norm.hip img_plan;
+# D3D_GN_IMG_WIDE=<lo>:<hi> images, "0" off).
 if os.environ.get("D3D_GN_IMG"):
     _lib.d3d_gn_img_cfg(int(os.environ["D3D_GN_IMG"]))
-_GN_IMG_OK: Dict[Tuple[int, int, int, int], bool] = {}
+if os.environ.get("D3D_GN_IMG_WIDE"):
+    _w = os.environ["D3D_GN_IMG_WIDE"]
+    _lo, _hi = (int(v) for v in _w.split(":")) if ":" in _w else (1 << 30, 0)
+    _lib.d3d_gn_img_wide_cfg(_lo, _hi)
+_GN_IMG_OK: Dict[Tuple[int, ...], bool] = {}
 
 
-def gn_img_ok(P: int, C: int, G: int) -> bool:
-    key = (P, C, G, _lib.d3d_gn_img_cfg(-1))
+def gn_img_ok(P: int, C: int, G: int, N: int = 0) -> bool:
+    """True when a GroupNorm over N images of P pixels runs on the
+    whole-image kernels (the same answer for its forward, backward and the
+    producer that would otherwise emit its statistics)."""
+    key = (P, C, G, N, _lib.d3d_gn_img_cfg(-1), _lib.d3d_gn_img_wide_cfg(-1, 0))
     v = _GN_IMG_OK.get(key)
     if v is None:
-        v = _GN_IMG_OK[key] = bool(_lib.d3d_gn_img_ok(P, C, G))
+        v = _GN_IMG_OK[key] = bool(_lib.d3d_gn_img_ok_n(N, P, C, G))
     return v
 
 
@@ -420,7 +429,7 @@ def _gn_fwd(mode, x, w, b, G, eps, ss=None, ssld=0, p=0.0, seed=0, x2=None, ss_m
     C = C1 + (x2.shape[-1] if x2 is not None else 0)
     P = H * W
     stats = torch.empty(N * G * 2, dtype=F32, device=x.device)
-    if gn_img_ok(P, C, G):
+    if gn_img_ok(P, C, G, N):
         y = torch.empty(N, H, W, C, dtype=x.dtype, device=x.device)
         _chk(_lib.d3d_gn_img_fwd(mode, x.data_ptr(), stats.data_ptr(), w.data_ptr(), b.data_ptr(), _ptr(ss),
                                  y.data_ptr(), N, P, C, G, float(eps), float(p), int(seed), int(ssld),
@@ -490,7 +499,7 @@ def _gn_bwd(mode, x, dy, ss, stats, w, b, G, p, seed, dss=None, ssld=0, x2=None,
     N, H, W, C1 = x.shape
     C = C1 + (x2.shape[-1] if x2 is not None else 0)
     P = H * W
-    if gn_img_ok(P, C, G):
+    if gn_img_ok(P, C, G, N):
         return _gn_bwd_img(mode, x, dy, ss, stats, w, b, G, p, seed, dss, ssld, x2, dres, dres_scale, dres2,
                            dres2_scale)
     nch, _ = _gn_plan(N, P, C)
@@ -1130,7 +1139,7 @@ def gn_silu_conv_ok(x: torch.Tensor, OC: int, groups: int) -> bool:
         return False
     _ensure_impl()
     N, H, W, C = x.shape
-    return not gn_img_ok(H * W, C, groups) and bool(_lib.d3d_conv3_gn_ok(N, H, W, C, OC))
+    return not gn_img_ok(H * W, C, groups, N) and bool(_lib.d3d_conv3_gn_ok(N, H, W, C, OC))
 
 
 class _GNSiLUConv(torch.autograd.Function):
@@ -1230,7 +1239,7 @@ def gn_silu_conv3x3(x, gw, gb, cw, cb, groups=32, eps=1e-5, gn1_groups=0, res_sl
     :func:`conv3x3`'s ``gn_groups``."""
     _need_bf16(x)
     OC = cw.shape[0]
-    if gn1_groups and gn_img_ok(x.shape[1] * x.shape[2], OC, int(gn1_groups)):
+    if gn1_groups and gn_img_ok(x.shape[1] * x.shape[2], OC, int(gn1_groups), x.shape[0]):
         gn1_groups = 0
     info = {}
     y = _GNSiLUConv.apply(x, gw, gb, cw, cb, int(groups), float(eps), int(gn1_groups), res_slot, info)
@@ -1250,7 +1259,7 @@ def conv3x3(x, weight, bias, stride=1, residual=None, out_scale=1.0, row_bias=No
     if IC % 8 == 0 and OC % 8 == 0:
         if gn_groups:
             OH, OW = (x.shape[1] - 1) // stride + 1, (x.shape[2] - 1) // stride + 1
-            if gn_img_ok(OH * OW, OC, int(gn_groups)):
+            if gn_img_ok(OH * OW, OC, int(gn_groups), x.shape[0]):
                 gn_groups = 0           # the consumer's whole-image kernel makes its own statistics
         gn = {"groups": int(gn_groups)} if gn_groups else None
         y = _Conv.apply(x, weight, bias, stride, residual, out_scale, row_bias, res_period, 9, gn, res_slot)
@@ -1932,7 +1941,7 @@ def linear(x, weight, bias, residual=None, out_scale=1.0, res_slot=None, in_slot
     statistics of the GroupNorm that reads the output (attached as
     ``_d3d_gnpart``; see :func:`carry_gn_stats` across reshapes)."""
     _need_bf16(x, residual)
-    if gn_groups and x.dim() == 3 and gn_img_ok(x.shape[1], weight.shape[0], int(gn_groups)):
+    if gn_groups and x.dim() == 3 and gn_img_ok(x.shape[1], weight.shape[0], int(gn_groups), x.shape[0]):
         gn_groups = 0                   # the consumer's whole-image kernel makes its own statistics
     gn = {"groups": int(gn_groups)} if (gn_groups and _EPI_GN_STATS) else None
     y = _Linear.apply(x, weight, bias, residual, out_scale, res_slot, in_slot, gn)
@@ -2209,7 +2218,7 @@ def attn_out(a, W_out, b_out, W_lin, b_lin, residual=None, out_scale=1.0, res_sl
             b_out is None or b_lin is None or (rows < _ATTN_SPLIT * C and not _ATTN_SMALL):
         o = linear(a, W_out, b_out)
         return linear(o, W_lin, b_lin, residual, out_scale, res_slot, None, gn_groups)
-    if gn_groups and gn_img_ok(a.shape[1], C, int(gn_groups)):
+    if gn_groups and gn_img_ok(a.shape[1], C, int(gn_groups), a.shape[0]):
         gn_groups = 0                   # the consumer's whole-image kernel makes its own statistics
     gn = {"groups": int(gn_groups)} if (gn_groups and _EPI_GN_STATS) else None
     y = _AttnOut.apply(a.contiguous(), W_out, b_out, W_lin, b_lin, residual, out_scale, res_slot, gn)

@@ -148,6 +148,23 @@ def test_gn_film_dropout(H):
     assert torch.equal(dshift == 0, dropped)
 
 
+def test_gn_whole_image_batch_rule(H):
+    """The 32x32 level takes the whole-image kernels only for batches of
+    64..128 images (norm.hip img_plan; measured per batch size), and every
+    caller sees the same answer for one shape."""
+    assert H._lib.d3d_gn_img_cfg(-1) == 256
+    assert H.gn_img_ok(256, 256, 32, 32) and H.gn_img_ok(256, 256, 32)
+    for n, want in ((32, False), (64, True), (128, True), (256, False), (0, False)):
+        assert H.gn_img_ok(1024, 256, 32, n) == want, n
+    lo = H._lib.d3d_gn_img_wide_cfg(-1, 0)
+    try:
+        H._lib.d3d_gn_img_wide_cfg(1 << 30, 0)
+        assert not H.gn_img_ok(1024, 256, 32, 64)
+    finally:
+        H._lib.d3d_gn_img_wide_cfg(lo, 128)
+    assert H.gn_img_ok(1024, 256, 32, 64)
+
+
 @pytest.mark.parametrize("N,Hh,C,C1,mode,maxp", [
     (32, 8, 512, 0, 1, 256), (32, 16, 256, 0, 2, 256), (32, 8, 512, 0, 0, 256), (5, 16, 768, 512, 1, 256),
     (4, 8, 1024, 512, 1, 256), (3, 8, 768, 256, 1, 256), (6, 4, 256, 0, 2, 256), (4, 32, 256, 0, 1, 1024),
