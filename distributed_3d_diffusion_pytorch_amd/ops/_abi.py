@@ -16,6 +16,7 @@ SIGNATURES = {
     # norm.hip
     "d3d_gn_plan": [I, I, I, IP, IP],
     "d3d_gn_cfg": [I, I, I],
+    "d3d_gn_cfg_small": [I, I],
     "d3d_gn_stats": [P, I, I, I, I, F, P, P, P, I, P],
     "d3d_gn_apply": [P, P, P, P, P, I, I, I, I, I, P],
     "d3d_gn_film": [P, P, P, P, P, P, I, I, I, I, F, U64, I, P, P],

@@ -31,14 +31,18 @@ struct Plan {
 // rows; profiles/ab_gn_target.txt)
 static int g_gn_blocks = 1024;
 static int g_gn_red_u = 1, g_gn_app_u = 2;    // rows in flight per thread: backward reduce / apply
-static int gn_target_blocks() { return g_gn_blocks; }
+// ... except for batches of at most g_gn_small_n images, where 512 measured
+// +0.6 % of the bs16 step (32 images) in round 6 and 1024 stays ahead from 64
+// images (profiles/r6/knob_sweep_b128.txt; d3d_gn_cfg_small, 0 off)
+static int g_gn_small_n = 32, g_gn_small_blocks = 512;
+static int gn_target_blocks(int N) { return N <= g_gn_small_n ? g_gn_small_blocks : g_gn_blocks; }
 
 Plan make_plan(int N, int P, int C) {
   Plan p;
   p.tpr = C / 8;
   p.rpi = NT / p.tpr;
   if (p.rpi < 1) p.rpi = 1;
-  int target_blocks = gn_target_blocks();
+  int target_blocks = gn_target_blocks(N);
   int nch = (target_blocks + N - 1) / N;
   int maxch = (P + p.rpi - 1) / p.rpi;
   if (nch > maxch) nch = maxch;
@@ -1162,6 +1166,11 @@ D3D_API int d3d_gn_cfg(int blocks, int red_u, int app_u) {
   if (red_u > 0) g_gn_red_u = red_u;
   if (app_u > 0) g_gn_app_u = app_u;
   return 0;
+}
+
+D3D_API int d3d_gn_cfg_small(int max_n, int blocks) {
+  if (max_n >= 0) { g_gn_small_n = max_n; g_gn_small_blocks = blocks; }
+  return g_gn_small_n;
 }
 
 D3D_API int d3d_gn_plan(int N, int P, int C, int* nchunks, int* rows) {

@@ -833,6 +833,8 @@ if os.environ.get("D3D_CONV_HSM"):      # A/B knob: small-image halo conv (conv_
     _lib.d3d_conv_hsm_cfg(int(os.environ["D3D_CONV_HSM"]))
 if os.environ.get("D3D_GN_CFG"):        # A/B knob "blocks,red_u,app_u": GroupNorm launch shapes
     _lib.d3d_gn_cfg(*[int(v) for v in os.environ["D3D_GN_CFG"].split(",")])
+if os.environ.get("D3D_GN_CFG_SMALL"):  # "max_images,blocks": blocks per launch for small batches ("0,0" off)
+    _lib.d3d_gn_cfg_small(*[int(v) for v in os.environ["D3D_GN_CFG_SMALL"].split(",")])
 
 
 def _conv_fwd(x, wp, bias, row_bias, res, out, N, H, W, IC, ICp, OH, OW, OC, ldo, stride, trans, scale, res_nmod=0,
