@@ -18,6 +18,7 @@
 #   env:<VAR=val>:<bs,bs..>    same-box A/B of an environment knob against the default
 #   prof:<bs>                  rocprofv3 kernel trace of the step + rpstats (stats, grid, busy, gaps,
 #                              solo, families)
+#   env128px:<VAR=val>:<bs>    the env A/B at 128x128 (bench --imgsize 128)
 #   envprof:<VAR=val>:<bs>     the same trace with an environment knob set
 #   envfc:<V=x[+V2=y]>:<bs>:<graph|seg>  same-box A/B of knobs on the 1-rank RCCL rehearsal (bench --force_comm)
 #   pmc:<bs>                   step-level hardware counters (three --pmc passes) -> table_bs<bs>.txt
@@ -115,6 +116,14 @@ for step in "$@"; do
           unset "$var"
           bench "env_base_b${bs}_$r" --global_batch "$bs" --steps "$st" --warmup 4
         done
+      done ;;
+    env128px)                    # env128px:<VAR=val>:<bs>: the env A/B on the 128x128 config
+      var=${a%%=*}
+      for r in 1 2; do
+        export "${a?}"
+        bench "env128_${var}_b${b}_$r" --imgsize 128 --global_batch "$b" --steps 10 --warmup 3
+        unset "$var"
+        bench "env128_base_b${b}_$r" --imgsize 128 --global_batch "$b" --steps 10 --warmup 3
       done ;;
     fc)                          # fc:<bs>:<graph|seg|post>: 1-rank RCCL rehearsal of the multi-GPU step (bench --force_comm)
       case $b in
