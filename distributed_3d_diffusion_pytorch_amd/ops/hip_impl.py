@@ -2071,6 +2071,10 @@ _ATTN_SPLIT = int(os.environ.get("D3D_ATTN_SPLIT", "64"))
 # below that, merge with the recomputing backward (measured neutral at bs16) or
 # keep the two layers (default)
 _ATTN_SMALL = os.environ.get("D3D_ATTN_MERGE_SMALL", "0") == "1"
+# ... except from this many rows per channel (the 8x8 level at 256 images:
+# +0.2 % bs128, where the merge at 128 images is -1.6 % bs64;
+# profiles/r6/knob_sweep_b128.txt)
+_ATTN_SMALL_MIN = int(os.environ.get("D3D_ATTN_MERGE_SMALL_MIN", "32"))
 _ATTN_PAIRS: Dict[Tuple[int, int], _AttnPair] = {}
 _ATTN_TABLE = [None, -1]         # forward-refresh table over every registered pair, its registry size
 
@@ -2217,7 +2221,8 @@ def attn_out(a, W_out, b_out, W_lin, b_lin, residual=None, out_scale=1.0, res_sl
     C = a.shape[-1]
     rows = a.numel() // C
     if C % 64 or W_lin.reshape(W_lin.shape[0], -1).shape != (C, C) or tuple(W_out.shape) != (C, C) or \
-            b_out is None or b_lin is None or (rows < _ATTN_SPLIT * C and not _ATTN_SMALL):
+            b_out is None or b_lin is None or \
+            (rows < _ATTN_SPLIT * C and not _ATTN_SMALL and rows < _ATTN_SMALL_MIN * C):
         o = linear(a, W_out, b_out)
         return linear(o, W_lin, b_lin, residual, out_scale, res_slot, None, gn_groups)
     if gn_groups and gn_img_ok(a.shape[1], C, int(gn_groups), a.shape[0]):
