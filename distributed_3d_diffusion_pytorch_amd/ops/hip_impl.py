@@ -2071,10 +2071,10 @@ _ATTN_SPLIT = int(os.environ.get("D3D_ATTN_SPLIT", "64"))
 # below that, merge with the recomputing backward (measured neutral at bs16) or
 # keep the two layers (default)
 _ATTN_SMALL = os.environ.get("D3D_ATTN_MERGE_SMALL", "0") == "1"
-# ... except from this many rows per channel (the 8x8 level at 256 images:
-# +0.2 % bs128, where the merge at 128 images is -1.6 % bs64;
-# profiles/r6/knob_sweep_b128.txt)
-_ATTN_SMALL_MIN = int(os.environ.get("D3D_ATTN_MERGE_SMALL_MIN", "32"))
+# ... or from this many rows per channel (32: the 8x8 level at 256 images,
+# measured +0.2-0.3 % at bs128 -- the size of the A/A ordering bias of the
+# same runs, so off by default; profiles/r6/knob_sweep_b128.txt)
+_ATTN_SMALL_MIN = int(os.environ.get("D3D_ATTN_MERGE_SMALL_MIN", str(1 << 30)))
 _ATTN_PAIRS: Dict[Tuple[int, int], _AttnPair] = {}
 _ATTN_TABLE = [None, -1]         # forward-refresh table over every registered pair, its registry size
 
